@@ -1,0 +1,113 @@
+"""Seeded synthetic detection/embedding streams for the association benchmarks.
+
+This is the build's own scene generator (SURVEY.md §8(d) "Synthetic inputs"): ``n_obj``
+constant-velocity boxes over a 1920x1080 frame, each detected with probability ``p_det`` per
+frame, jittered box corners, confidences U(conf_lo, conf_hi), class 0, and per-identity unit
+embeddings perturbed by 0.1*N(0,1)/sqrt(F) and renormalised.
+
+Every frame is generated from its own ``numpy.random.default_rng([seed, frame])`` stream, so a
+frame can be produced independently of the frames before it (bench shards, GPU-side staging and
+the golden-fixture script all regenerate identical inputs from ``(seed, frame)``).
+
+Two layouts:
+* ``grid``   — objects on a regular grid, little overlap (the survey's C2/C3/C4 scene);
+* ``crowded``— uniformly random centres with heavy overlap: many non-trivial LAP components and
+  near-threshold costs (the stress variant §8(d) asks for).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+__all__ = ["SyntheticScene", "load_mot_dets"]
+
+
+@dataclass
+class SyntheticScene:
+    n_obj: int
+    seed: int = 0
+    emb_dim: int = 0
+    layout: str = "grid"
+    p_det: float = 0.5
+    conf_lo: float = 0.65
+    conf_hi: float = 1.0
+    jitter: float = 0.5
+    width: float = 1920.0
+    height: float = 1080.0
+    emb_dtype: type = np.float32
+
+    def __post_init__(self):
+        rng = np.random.default_rng([self.seed, 0x5CE7E])
+        n = self.n_obj
+        if self.layout == "grid":
+            cols = max(1, math.ceil(math.sqrt(n * self.width / self.height)))
+            rows = max(1, math.ceil(n / cols))
+            cw, ch = self.width / cols, self.height / rows
+            idx = np.arange(n)
+            cx = (idx % cols + 0.5) * cw
+            cy = (idx // cols + 0.5) * ch
+            w = 0.45 * cw * rng.uniform(0.8, 1.2, n)
+            h = 0.80 * ch * rng.uniform(0.8, 1.2, n)
+        elif self.layout == "crowded":
+            cx = rng.uniform(0.1, 0.9, n) * self.width
+            cy = rng.uniform(0.1, 0.9, n) * self.height
+            w = rng.uniform(30.0, 90.0, n)
+            h = w * rng.uniform(1.5, 3.0, n)
+        else:
+            raise ValueError(f"unknown layout {self.layout!r}")
+        self.c0 = np.stack([cx, cy], 1)
+        self.size = np.stack([w, h], 1)
+        self.vel = rng.uniform(-0.5, 0.5, (n, 2))
+        if self.emb_dim:
+            base = rng.standard_normal((n, self.emb_dim))
+            self.base_emb = base / np.linalg.norm(base, axis=1, keepdims=True)
+        else:
+            self.base_emb = None
+
+    def frame(self, t: int):
+        """Detections of frame ``t`` (1-based like the reference's frame counter).
+
+        Returns ``(dets[N,6] float64 (x1,y1,x2,y2,conf,cls), embs[N,F] or None, ids[N])``.
+        """
+        rng = np.random.default_rng([self.seed, int(t)])
+        n = self.n_obj
+        seen = rng.random(n) < self.p_det
+        ids = np.flatnonzero(seen)
+        rng.shuffle(ids)
+        m = ids.size
+        c = self.c0[ids] + self.vel[ids] * float(t)
+        half = self.size[ids] * 0.5
+        box = np.concatenate([c - half, c + half], 1) + rng.normal(0.0, self.jitter, (m, 4))
+        conf = rng.uniform(self.conf_lo, self.conf_hi, m)
+        dets = np.zeros((m, 6), np.float64)
+        dets[:, :4] = box
+        dets[:, 4] = conf
+        embs = None
+        if self.base_emb is not None:
+            e = self.base_emb[ids] + 0.1 * rng.standard_normal((m, self.emb_dim)) / math.sqrt(
+                self.emb_dim
+            )
+            e /= np.linalg.norm(e, axis=1, keepdims=True)
+            embs = e.astype(self.emb_dtype)
+        return dets, embs, ids
+
+
+def load_mot_dets(path):
+    """MOT17 ``det.txt`` (``frame,-1,x,y,w,h,conf``) → {frame: dets[N,6] xyxy,conf,cls=0}.
+
+    Mirrors how the survey fed MOT17-mini public detections to the trackers (§8(c)).
+    """
+    raw = np.loadtxt(path, delimiter=",", dtype=np.float64, ndmin=2)
+    out = {}
+    for f in np.unique(raw[:, 0]).astype(int):
+        r = raw[raw[:, 0] == f]
+        d = np.zeros((r.shape[0], 6), np.float64)
+        d[:, 0] = r[:, 2]
+        d[:, 1] = r[:, 3]
+        d[:, 2] = r[:, 2] + r[:, 4]
+        d[:, 3] = r[:, 3] + r[:, 5]
+        d[:, 4] = r[:, 6]
+        out[int(f)] = d
+    return out

@@ -1,0 +1,69 @@
+/*
+ * bxo — CPU restatement (fp64, plain C) of the BoxMOT per-frame association path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the oracle the HIP engine (libbxassoc.so) is checked
+ * against, and the "port" CPU baseline bench.py times beside it.  Nothing in boxmot_amd/ links,
+ * loads or calls it; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg do.
+ *
+ * Parity pinning: every function here is checked against golden vectors captured from the Python
+ * reference (tests/golden/make_golden.py, which imports /root/reference through an import shim)
+ * by tests/test_oracle.py.  lapx (the reference's JV dependency, 0.5.11.post1) is absent from the
+ * image; bxo_linear_assignment restates its wrapper semantics over a dense Jonker-Volgenant solve
+ * of the same (n_r+n_c)^2 extended matrix.
+ */
+#ifndef BXO_H
+#define BXO_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { BXO_KF_XYAH = 0, BXO_KF_XYWH = 1 };
+
+/* utils/iou.py:50-67  AssociationFunction.iou_batch  (a[na,4], b[nb,4] xyxy → out[na,nb]) */
+void bxo_iou_batch(const double *a, int na, const double *b, int nb, double *out);
+/* utils/matching.py:488-555  enhanced_fuse_score, in place on cost[nr,nc] */
+void bxo_fuse_score(double *cost, int nr, int nc, const double *confs);
+/* utils/matching.py:230-316  enhanced_embedding_distance (float32 features, scipy cosine) */
+void bxo_embedding_distance(const float *trk, int nt, const float *det, int nd, int f,
+                            double *out);
+/* numpy float32 np.linalg.norm(x, axis=1): pairwise summation of x*x, float32 sqrt */
+float bxo_np_norm_f32(const float *x, int n);
+
+/* motion/kalman_filters/aabb/base_kalman_filter.py:43-194 + xyah_kf.py / xywh_kf.py */
+void bxo_kf_initiate(int kind, const double *meas, double *mean, double *cov);
+void bxo_kf_multi_predict(int kind, int n, double *mean, double *cov);
+void bxo_kf_update(int kind, double *mean, double *cov, const double *z, double conf);
+void bxo_kf_gating_distance(int kind, const double *mean, const double *cov, const double *z,
+                            int nz, double *out);
+
+/* Dense square JV (Jonker & Volgenant 1987): x[row]→col, y[col]→row.  Returns 0 on success. */
+int bxo_lapjv(int n, const double *cost, int *x, int *y);
+/* utils/matching.py:30-141  linear_assignment(cost, thresh) with lapx extend_cost+cost_limit
+ * semantics.  matches: 2*min(nr,nc) ints (row, col) in row order. */
+int bxo_linear_assignment(const double *cost, int nr, int nc, double thresh, int *matches,
+                          int *n_matches, int *ua, int *n_ua, int *ub, int *n_ub);
+
+/* ----------------------------------------------------------------------------------------- */
+/* Trackers: ByteTrack (trackers/bytetrack/bytetrack.py:119-302) and BoT-SORT                */
+/* (trackers/botsort/botsort.py:27-411) per-frame update with the reference's list semantics. */
+typedef struct bxo_tracker bxo_tracker;
+
+bxo_tracker *bxo_bytetrack_new(double min_conf, double track_thresh, double match_thresh,
+                               int track_buffer, int frame_rate);
+bxo_tracker *bxo_botsort_new(double track_high_thresh, double track_low_thresh,
+                             double new_track_thresh, int track_buffer, double match_thresh,
+                             double proximity_thresh, double appearance_thresh, int frame_rate,
+                             int fuse_first_associate, int with_reid);
+/* dets[n,6] (x1,y1,x2,y2,conf,cls); embs[n,emb_dim] float32 (emb_is_f64=0) or float64;
+ * warp[6] = 2x3 CMC affine (NULL = identity).  Writes out[M,8] and returns M (or <0 on error,
+ * -2 when out_cap is too small). */
+int bxo_update(bxo_tracker *t, const double *dets, int n, const void *embs, int emb_dim,
+               int emb_is_f64, const double *warp, double *out, int out_cap);
+int bxo_id_count(const bxo_tracker *t);
+int bxo_frame_count(const bxo_tracker *t);
+void bxo_free(bxo_tracker *t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,495 @@
+/*
+ * bxo_ops.c — oracle kernels: box conversions, IoU, score fusion, cosine distance, Kalman
+ * filters and the lapx-semantics linear assignment.  TEST INFRASTRUCTURE ONLY (see bxo.h).
+ *
+ * Elementwise arithmetic follows numpy's operation order one-for-one and is compiled with
+ * -ffp-contract=off so products and sums round exactly as numpy's do.  Only the BLAS/LAPACK
+ * contractions inside the Kalman update (cho_factor / cho_solve / multi_dot) have an order the
+ * reference does not pin; those are restated straightforwardly and compared with a tolerance.
+ */
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "bxo.h"
+#include "bxo_internal.h"
+
+/* ------------------------------------------------------------------------------------------ */
+/* utils/ops.py:10-150 box conversions (numpy op order)                                        */
+
+void bxo_xyxy2xywh(const double *x, double *y) { /* ops.py:10-24 */
+    y[0] = (x[0] + x[2]) / 2;
+    y[1] = (x[1] + x[3]) / 2;
+    y[2] = x[2] - x[0];
+    y[3] = x[3] - x[1];
+}
+
+void bxo_xywh2xyxy(const double *x, double *y) { /* ops.py:27-43 */
+    double r[4];
+    r[0] = x[0] - x[2] / 2;
+    r[1] = x[1] - x[3] / 2;
+    r[2] = x[0] + x[2] / 2;
+    r[3] = x[1] + x[3] / 2;
+    memcpy(y, r, sizeof r);
+}
+
+void bxo_xywh2tlwh(const double *x, double *y) { /* ops.py:46-58 */
+    double r[4] = {x[0] - x[2] / 2, x[1] - x[3] / 2, x[2], x[3]};
+    memcpy(y, r, sizeof r);
+}
+
+void bxo_tlwh2xyah(const double *x, double *y) { /* ops.py:89-103 */
+    double r[4] = {x[0] + x[2] / 2, x[1] + x[3] / 2, x[2] / x[3], x[3]};
+    memcpy(y, r, sizeof r);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* utils/iou.py:50-67 iou_batch                                                                */
+
+double bxo_iou_pair(const double *b1, const double *b2) {
+    double xx1 = fmax(b1[0], b2[0]);
+    double yy1 = fmax(b1[1], b2[1]);
+    double xx2 = fmin(b1[2], b2[2]);
+    double yy2 = fmin(b1[3], b2[3]);
+    double w = fmax(0.0, xx2 - xx1);
+    double h = fmax(0.0, yy2 - yy1);
+    double wh = w * h;
+    return wh / ((b1[2] - b1[0]) * (b1[3] - b1[1]) + (b2[2] - b2[0]) * (b2[3] - b2[1]) - wh);
+}
+
+void bxo_iou_batch(const double *a, int na, const double *b, int nb, double *out) {
+    for (int i = 0; i < na; i++)
+        for (int j = 0; j < nb; j++) out[(size_t)i * nb + j] = bxo_iou_pair(a + 4 * i, b + 4 * j);
+}
+
+/* utils/matching.py:520-544: sim = 1-cost; w = conf>0.7 ? 1.2*conf : conf; mask conf>=0.5;
+ * fuse = 1 - sim*w*mask; ×2 where conf < 0.5 */
+double bxo_fuse_one(double cost, double conf) {
+    double sim = 1 - cost;
+    double w = conf > 0.7 ? conf * 1.2 : conf;
+    double mask = conf >= 0.5 ? 1.0 : 0.0;
+    double fuse = 1 - sim * w * mask;
+    return conf < 0.5 ? fuse * 2.0 : fuse;
+}
+
+void bxo_fuse_score(double *cost, int nr, int nc, const double *confs) {
+    for (int i = 0; i < nr; i++)
+        for (int j = 0; j < nc; j++)
+            cost[(size_t)i * nc + j] = bxo_fuse_one(cost[(size_t)i * nc + j], confs[j]);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* numpy float32 pairwise summation (numpy/core/src/umath/loops_utils.h pairwise_sum, PW_BLOCKSIZE
+ * 128, 8 accumulators) as used by np.add.reduce inside np.linalg.norm(x, axis=1).            */
+static float pairwise_sum_f32(const float *x, int n) {
+    if (n < 8) {
+        float res = 0.0f;
+        for (int i = 0; i < n; i++) res += x[i];
+        return res;
+    }
+    if (n <= 128) {
+        float r[8];
+        for (int k = 0; k < 8; k++) r[k] = x[k];
+        int i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int k = 0; k < 8; k++) r[k] += x[i + k];
+        float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += x[i];
+        return res;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return pairwise_sum_f32(x, n2) + pairwise_sum_f32(x + n2, n - n2);
+}
+
+float bxo_np_norm_f32(const float *x, int n) {
+    float *sq = (float *)malloc(sizeof(float) * (n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) sq[i] = x[i] * x[i];
+    float s = pairwise_sum_f32(sq, n);
+    free(sq);
+    return sqrtf(s);
+}
+
+/* scipy cdist 'cosine' inner product: two interleaved accumulators, remainder added last. */
+static double dot2(const double *u, const double *v, int n) {
+    double a0 = 0.0, a1 = 0.0;
+    int i = 0;
+    for (; i + 2 <= n; i += 2) {
+        a0 += u[i] * v[i];
+        a1 += u[i + 1] * v[i + 1];
+    }
+    double s = a0 + a1;
+    if (i < n) s += u[i] * v[i];
+    return s;
+}
+
+/* matching.py:279-287: cast float32, x/(||x||+1e-8) in float32, max(0, cdist cosine). */
+void bxo_embedding_distance(const float *trk, int nt, const float *det, int nd, int f,
+                            double *out) {
+    double *A = (double *)malloc(sizeof(double) * (size_t)(nt > 0 ? nt : 1) * f);
+    double *B = (double *)malloc(sizeof(double) * (size_t)(nd > 0 ? nd : 1) * f);
+    double *na = (double *)malloc(sizeof(double) * (nt > 0 ? nt : 1));
+    double *nb = (double *)malloc(sizeof(double) * (nd > 0 ? nd : 1));
+    for (int i = 0; i < nt; i++) {
+        float dn = bxo_np_norm_f32(trk + (size_t)i * f, f) + 1e-8f;
+        for (int k = 0; k < f; k++) A[(size_t)i * f + k] = (double)(trk[(size_t)i * f + k] / dn);
+        na[i] = sqrt(dot2(A + (size_t)i * f, A + (size_t)i * f, f));
+    }
+    for (int j = 0; j < nd; j++) {
+        float dn = bxo_np_norm_f32(det + (size_t)j * f, f) + 1e-8f;
+        for (int k = 0; k < f; k++) B[(size_t)j * f + k] = (double)(det[(size_t)j * f + k] / dn);
+        nb[j] = sqrt(dot2(B + (size_t)j * f, B + (size_t)j * f, f));
+    }
+    for (int i = 0; i < nt; i++)
+        for (int j = 0; j < nd; j++) {
+            double c = dot2(A + (size_t)i * f, B + (size_t)j * f, f) / (na[i] * nb[j]);
+            if (fabs(c) > 1.0) c = copysign(1.0, c);
+            double d = 1.0 - c;
+            out[(size_t)i * nd + j] = d < 0.0 ? 0.0 : d;
+        }
+    free(A);
+    free(B);
+    free(na);
+    free(nb);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Kalman filters.  State [x,y,a|w,h,vx,vy,va|vw,vh], dt=1 (base_kalman_filter.py:29-41).      */
+
+static const double STD_POS = 1.0 / 20, STD_VEL = 1.0 / 160;
+
+void bxo_kf_initiate(int kind, const double *m, double *mean, double *cov) {
+    double std[8];
+    if (kind == BXO_KF_XYAH) { /* xyah_kf.py:16-28 */
+        std[0] = 2 * STD_POS * m[3];
+        std[1] = 2 * STD_POS * m[3];
+        std[2] = 1e-2;
+        std[3] = 2 * STD_POS * m[3];
+        std[4] = 10 * STD_VEL * m[3];
+        std[5] = 10 * STD_VEL * m[3];
+        std[6] = 1e-5;
+        std[7] = 10 * STD_VEL * m[3];
+    } else { /* xywh_kf.py:16-26 */
+        std[0] = 2 * STD_POS * m[2];
+        std[1] = 2 * STD_POS * m[3];
+        std[2] = 2 * STD_POS * m[2];
+        std[3] = 2 * STD_POS * m[3];
+        std[4] = 10 * STD_VEL * m[2];
+        std[5] = 10 * STD_VEL * m[3];
+        std[6] = 10 * STD_VEL * m[2];
+        std[7] = 10 * STD_VEL * m[3];
+    }
+    for (int k = 0; k < 4; k++) mean[k] = m[k], mean[4 + k] = 0.0;
+    memset(cov, 0, sizeof(double) * 64);
+    for (int k = 0; k < 8; k++) cov[9 * k] = std[k] * std[k];
+}
+
+static void process_noise(int kind, const double *mean, double *q) {
+    double s[8];
+    if (kind == BXO_KF_XYAH) { /* xyah_kf.py:58-73 */
+        s[0] = STD_POS * mean[3];
+        s[1] = STD_POS * mean[3];
+        s[2] = 1e-2;
+        s[3] = STD_POS * mean[3];
+        s[4] = STD_VEL * mean[3];
+        s[5] = STD_VEL * mean[3];
+        s[6] = 1e-5;
+        s[7] = STD_VEL * mean[3];
+    } else { /* xywh_kf.py:40-54 */
+        s[0] = STD_POS * mean[2];
+        s[1] = STD_POS * mean[3];
+        s[2] = STD_POS * mean[2];
+        s[3] = STD_POS * mean[3];
+        s[4] = STD_VEL * mean[2];
+        s[5] = STD_VEL * mean[3];
+        s[6] = STD_VEL * mean[2];
+        s[7] = STD_VEL * mean[3];
+    }
+    for (int k = 0; k < 8; k++) q[k] = s[k] * s[k];
+}
+
+/* base_kalman_filter.py:111-127.  F has two non-zero terms per row/column, so np.dot's sums
+ * reduce to single roundings whatever BLAS order: cov' = (P_ij+P_i+4,j)+(P_i,j+4+P_i+4,j+4). */
+void bxo_kf_multi_predict(int kind, int n, double *mean, double *cov) {
+    for (int t = 0; t < n; t++) {
+        double *m = mean + 8 * t, *P = cov + 64 * t, q[8], FP[64];
+        process_noise(kind, m, q);
+        for (int k = 0; k < 4; k++) m[k] = m[k] + m[k + 4];
+        for (int i = 0; i < 8; i++)
+            for (int j = 0; j < 8; j++)
+                FP[8 * i + j] = i < 4 ? P[8 * i + j] + P[8 * (i + 4) + j] : P[8 * i + j];
+        for (int i = 0; i < 8; i++)
+            for (int j = 0; j < 8; j++) {
+                double v = j < 4 ? FP[8 * i + j] + FP[8 * i + j + 4] : FP[8 * i + j];
+                P[8 * i + j] = i == j ? v + q[i] : v;
+            }
+    }
+}
+
+static void meas_noise(int kind, const double *mean, double conf, double *r) {
+    double s[4];
+    if (kind == BXO_KF_XYAH) { /* xyah_kf.py:75-87 */
+        s[0] = STD_POS * mean[3];
+        s[1] = STD_POS * mean[3];
+        s[2] = 1e-1;
+        s[3] = STD_POS * mean[3];
+    } else { /* xywh_kf.py:56-63 */
+        s[0] = STD_POS * mean[2];
+        s[1] = STD_POS * mean[3];
+        s[2] = STD_POS * mean[2];
+        s[3] = STD_POS * mean[3];
+    }
+    for (int k = 0; k < 4; k++) {
+        double v = (1 - conf) * s[k]; /* base_kalman_filter.py:101 NSA scaling */
+        r[k] = v * v;
+    }
+}
+
+/* base_kalman_filter.py:86-109 project: S = P[:4,:4] + diag(R). */
+static void project(int kind, const double *mean, const double *P, double conf, double *S) {
+    double r[4];
+    meas_noise(kind, mean, conf, r);
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) S[4 * i + j] = P[8 * i + j] + (i == j ? r[i] : 0.0);
+}
+
+static int chol4(const double *S, double *L) {
+    memset(L, 0, sizeof(double) * 16);
+    for (int j = 0; j < 4; j++) {
+        double d = S[4 * j + j];
+        for (int k = 0; k < j; k++) d -= L[4 * j + k] * L[4 * j + k];
+        if (!(d > 0.0)) return -1;
+        d = sqrt(d);
+        L[4 * j + j] = d;
+        for (int i = j + 1; i < 4; i++) {
+            double s = S[4 * i + j];
+            for (int k = 0; k < j; k++) s -= L[4 * i + k] * L[4 * j + k];
+            L[4 * i + j] = s / d;
+        }
+    }
+    return 0;
+}
+
+/* base_kalman_filter.py:129-155 */
+void bxo_kf_update(int kind, double *mean, double *cov, const double *z, double conf) {
+    double S[16], L[16], K[32], PHt[32];
+    project(kind, mean, cov, conf, S);
+    if (chol4(S, L)) return;
+    for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 4; j++) PHt[4 * i + j] = cov[8 * i + j];
+    /* K^T = S^{-1} (P H^T)^T : solve L L^T X = B column by column (B = PHt^T, 4 x 8) */
+    for (int c = 0; c < 8; c++) {
+        double y[4], x[4];
+        for (int i = 0; i < 4; i++) {
+            double s = PHt[4 * c + i];
+            for (int k = 0; k < i; k++) s -= L[4 * i + k] * y[k];
+            y[i] = s / L[4 * i + i];
+        }
+        for (int i = 3; i >= 0; i--) {
+            double s = y[i];
+            for (int k = i + 1; k < 4; k++) s -= L[4 * k + i] * x[k];
+            x[i] = s / L[4 * i + i];
+        }
+        for (int i = 0; i < 4; i++) K[4 * c + i] = x[i]; /* K[c][i] (8 x 4) */
+    }
+    double innov[4];
+    for (int k = 0; k < 4; k++) innov[k] = z[k] - mean[k];
+    for (int i = 0; i < 8; i++) {
+        double s = 0.0;
+        for (int k = 0; k < 4; k++) s += innov[k] * K[4 * i + k];
+        mean[i] = mean[i] + s;
+    }
+    double KS[32];
+    for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 4; j++) {
+            double s = 0.0;
+            for (int k = 0; k < 4; k++) s += K[4 * i + k] * S[4 * k + j];
+            KS[4 * i + j] = s;
+        }
+    for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 8; j++) {
+            double s = 0.0;
+            for (int k = 0; k < 4; k++) s += KS[4 * i + k] * K[4 * j + k];
+            cov[8 * i + j] = cov[8 * i + j] - s;
+        }
+}
+
+/* base_kalman_filter.py:166-194 (metric 'maha', all 4 dims) */
+void bxo_kf_gating_distance(int kind, const double *mean, const double *cov, const double *z,
+                            int nz, double *out) {
+    double S[16], L[16];
+    project(kind, mean, cov, 0.0, S);
+    if (chol4(S, L)) {
+        for (int k = 0; k < nz; k++) out[k] = NAN;
+        return;
+    }
+    for (int k = 0; k < nz; k++) {
+        double d[4], y[4], s2 = 0.0;
+        for (int i = 0; i < 4; i++) d[i] = z[4 * k + i] - mean[i];
+        for (int i = 0; i < 4; i++) {
+            double s = d[i];
+            for (int j = 0; j < i; j++) s -= L[4 * i + j] * y[j];
+            y[i] = s / L[4 * i + i];
+            s2 += y[i] * y[i];
+        }
+        out[k] = s2;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Dense Jonker-Volgenant: column reduction + reduction transfer + shortest augmenting paths.  */
+
+int bxo_lapjv(int n, const double *c, int *x, int *y) {
+    if (n <= 0) return 0;
+    double *v = (double *)malloc(sizeof(double) * n), *d = (double *)malloc(sizeof(double) * n);
+    int *matches = (int *)calloc(n, sizeof(int)), *freer = (int *)malloc(sizeof(int) * n);
+    int *pred = (int *)malloc(sizeof(int) * n), *col = (int *)malloc(sizeof(int) * n);
+    for (int i = 0; i < n; i++) x[i] = -1;
+    for (int j = n - 1; j >= 0; j--) { /* column reduction */
+        double mn = c[j];
+        int imin = 0;
+        for (int i = 1; i < n; i++)
+            if (c[(size_t)i * n + j] < mn) mn = c[(size_t)i * n + j], imin = i;
+        v[j] = mn;
+        if (++matches[imin] == 1) {
+            x[imin] = j;
+            y[j] = imin;
+        } else if (v[j] < v[x[imin]]) {
+            int j1 = x[imin];
+            x[imin] = j;
+            y[j] = imin;
+            y[j1] = -1;
+        } else {
+            y[j] = -1;
+        }
+    }
+    int nfree = 0;
+    for (int i = 0; i < n; i++) { /* reduction transfer */
+        if (matches[i] == 0) {
+            freer[nfree++] = i;
+        } else if (matches[i] == 1) {
+            int j1 = x[i];
+            double mn = DBL_MAX;
+            for (int j = 0; j < n; j++)
+                if (j != j1 && c[(size_t)i * n + j] - v[j] < mn) mn = c[(size_t)i * n + j] - v[j];
+            if (mn < DBL_MAX) v[j1] = v[j1] - mn;
+        }
+    }
+    for (int f = 0; f < nfree; f++) { /* augmentation */
+        int fr = freer[f], low = 0, up = 0, last = 0, endofpath = -1, found = 0;
+        double mn = 0.0;
+        for (int j = 0; j < n; j++) {
+            d[j] = c[(size_t)fr * n + j] - v[j];
+            pred[j] = fr;
+            col[j] = j;
+        }
+        do {
+            if (up == low) {
+                last = low - 1;
+                mn = d[col[up++]];
+                for (int k = up; k < n; k++) {
+                    int j = col[k];
+                    double h = d[j];
+                    if (h <= mn) {
+                        if (h < mn) {
+                            up = low;
+                            mn = h;
+                        }
+                        col[k] = col[up];
+                        col[up++] = j;
+                    }
+                }
+                for (int k = low; k < up; k++)
+                    if (y[col[k]] < 0) {
+                        endofpath = col[k];
+                        found = 1;
+                        break;
+                    }
+            }
+            if (!found) {
+                int j1 = col[low++];
+                int i = y[j1];
+                double h = c[(size_t)i * n + j1] - v[j1] - mn;
+                for (int k = up; k < n; k++) {
+                    int j = col[k];
+                    double v2 = c[(size_t)i * n + j] - v[j] - h;
+                    if (v2 < d[j]) {
+                        pred[j] = i;
+                        if (v2 == mn) {
+                            if (y[j] < 0) {
+                                endofpath = j;
+                                found = 1;
+                                break;
+                            }
+                            col[k] = col[up];
+                            col[up++] = j;
+                        }
+                        d[j] = v2;
+                    }
+                }
+            }
+        } while (!found);
+        for (int k = 0; k <= last; k++) {
+            int j1 = col[k];
+            v[j1] = v[j1] + d[j1] - mn;
+        }
+        int i;
+        do {
+            i = pred[endofpath];
+            y[endofpath] = i;
+            int j1 = endofpath;
+            endofpath = x[i];
+            x[i] = j1;
+        } while (i != fr);
+    }
+    free(v);
+    free(d);
+    free(matches);
+    free(freer);
+    free(pred);
+    free(col);
+    return 0;
+}
+
+/* matching.py:30-108 with lapx.lapjv(cost, extend_cost=True, cost_limit=thresh):
+ * (nr+nc)^2 matrix, off-diagonal blocks cost_limit/2, bottom-right 0. */
+int bxo_linear_assignment(const double *cost, int nr, int nc, double thresh, int *matches,
+                          int *n_matches, int *ua, int *n_ua, int *ub, int *n_ub) {
+    *n_matches = *n_ua = *n_ub = 0;
+    if (nr == 0 || nc == 0) { /* matching.py:42-47 */
+        for (int i = 0; i < nr; i++) ua[(*n_ua)++] = i;
+        for (int j = 0; j < nc; j++) ub[(*n_ub)++] = j;
+        return 0;
+    }
+    int n = nr + nc;
+    double *E = (double *)malloc(sizeof(double) * (size_t)n * n);
+    int *x = (int *)malloc(sizeof(int) * n), *y = (int *)malloc(sizeof(int) * n);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            double e;
+            if (i < nr && j < nc) e = cost[(size_t)i * nc + j];
+            else if (i >= nr && j >= nc) e = 0.0;
+            else e = thresh / 2.0;
+            E[(size_t)i * n + j] = e;
+        }
+    bxo_lapjv(n, E, x, y);
+    for (int i = 0; i < nr; i++) {
+        int j = x[i] >= nc ? -1 : x[i];
+        if (j >= 0) {
+            if (cost[(size_t)i * nc + j] <= thresh) {
+                matches[2 * *n_matches] = i;
+                matches[2 * *n_matches + 1] = j;
+                (*n_matches)++;
+            }
+        } else {
+            ua[(*n_ua)++] = i;
+        }
+    }
+    for (int j = 0; j < nc; j++)
+        if (y[j] >= nr) ub[(*n_ub)++] = j;
+    free(E);
+    free(x);
+    free(y);
+    return 0;
+}

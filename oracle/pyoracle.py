@@ -1,0 +1,198 @@
+"""ctypes binding of the C oracle (oracle/build/libbxoracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg — never by the product package boxmot_amd/.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "build" / "libbxoracle.so"
+
+_dp = C.POINTER(C.c_double)
+_fp = C.POINTER(C.c_float)
+_ip = C.POINTER(C.c_int)
+
+
+def build(force: bool = False) -> Path:
+    srcs = [HERE / n for n in ("bxo_ops.c", "bxo_track.c", "bxo.h", "bxo_internal.h")]
+    if force or not LIB_PATH.exists() or any(
+        s.stat().st_mtime > LIB_PATH.stat().st_mtime for s in srcs
+    ):
+        subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(str(LIB_PATH))
+        L.bxo_iou_batch.argtypes = [_dp, C.c_int, _dp, C.c_int, _dp]
+        L.bxo_fuse_score.argtypes = [_dp, C.c_int, C.c_int, _dp]
+        L.bxo_embedding_distance.argtypes = [_fp, C.c_int, _fp, C.c_int, C.c_int, _dp]
+        L.bxo_np_norm_f32.argtypes = [_fp, C.c_int]
+        L.bxo_np_norm_f32.restype = C.c_float
+        L.bxo_kf_initiate.argtypes = [C.c_int, _dp, _dp, _dp]
+        L.bxo_kf_multi_predict.argtypes = [C.c_int, C.c_int, _dp, _dp]
+        L.bxo_kf_update.argtypes = [C.c_int, _dp, _dp, _dp, C.c_double]
+        L.bxo_kf_gating_distance.argtypes = [C.c_int, _dp, _dp, _dp, C.c_int, _dp]
+        L.bxo_lapjv.argtypes = [C.c_int, _dp, _ip, _ip]
+        L.bxo_linear_assignment.argtypes = [_dp, C.c_int, C.c_int, C.c_double, _ip, _ip, _ip,
+                                            _ip, _ip, _ip]
+        L.bxo_bytetrack_new.argtypes = [C.c_double, C.c_double, C.c_double, C.c_int, C.c_int]
+        L.bxo_bytetrack_new.restype = C.c_void_p
+        L.bxo_botsort_new.argtypes = [C.c_double, C.c_double, C.c_double, C.c_int, C.c_double,
+                                      C.c_double, C.c_double, C.c_int, C.c_int, C.c_int]
+        L.bxo_botsort_new.restype = C.c_void_p
+        L.bxo_update.argtypes = [C.c_void_p, _dp, C.c_int, C.c_void_p, C.c_int, C.c_int, _dp,
+                                 _dp, C.c_int]
+        L.bxo_id_count.argtypes = [C.c_void_p]
+        L.bxo_frame_count.argtypes = [C.c_void_p]
+        L.bxo_free.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(_dp)
+
+
+def iou_batch(a, b):
+    a = np.ascontiguousarray(a, np.float64).reshape(-1, 4)
+    b = np.ascontiguousarray(b, np.float64).reshape(-1, 4)
+    out = np.zeros((a.shape[0], b.shape[0]))
+    lib().bxo_iou_batch(_d(a), a.shape[0], _d(b), b.shape[0], _d(out))
+    return out
+
+
+def fuse_score(cost, confs):
+    c = np.array(cost, np.float64, order="C", copy=True)
+    confs = np.ascontiguousarray(confs, np.float64)
+    lib().bxo_fuse_score(_d(c), c.shape[0], c.shape[1], _d(confs))
+    return c
+
+
+def embedding_distance(trk, det):
+    trk = np.ascontiguousarray(trk, np.float32)
+    det = np.ascontiguousarray(det, np.float32)
+    out = np.zeros((trk.shape[0], det.shape[0]))
+    lib().bxo_embedding_distance(trk.ctypes.data_as(_fp), trk.shape[0], det.ctypes.data_as(_fp),
+                                 det.shape[0], trk.shape[1], _d(out))
+    return out
+
+
+KF_KIND = {"xyah": 0, "xywh": 1}
+
+
+def kf_initiate(kind, meas):
+    meas = np.ascontiguousarray(meas, np.float64)
+    mean, cov = np.zeros(8), np.zeros((8, 8))
+    lib().bxo_kf_initiate(KF_KIND[kind], _d(meas), _d(mean), _d(cov))
+    return mean, cov
+
+
+def kf_multi_predict(kind, mean, cov):
+    mean = np.array(mean, np.float64, order="C", copy=True)
+    cov = np.array(cov, np.float64, order="C", copy=True)
+    lib().bxo_kf_multi_predict(KF_KIND[kind], mean.shape[0], _d(mean), _d(cov))
+    return mean, cov
+
+
+def kf_update(kind, mean, cov, z, conf=0.0):
+    mean = np.array(mean, np.float64, order="C", copy=True)
+    cov = np.array(cov, np.float64, order="C", copy=True)
+    z = np.ascontiguousarray(z, np.float64)
+    lib().bxo_kf_update(KF_KIND[kind], _d(mean), _d(cov), _d(z), float(conf))
+    return mean, cov
+
+
+def kf_gating_distance(kind, mean, cov, z):
+    mean = np.ascontiguousarray(mean, np.float64)
+    cov = np.ascontiguousarray(cov, np.float64)
+    z = np.ascontiguousarray(z, np.float64).reshape(-1, 4)
+    out = np.zeros(z.shape[0])
+    lib().bxo_kf_gating_distance(KF_KIND[kind], _d(mean), _d(cov), _d(z), z.shape[0], _d(out))
+    return out
+
+
+def linear_assignment(cost, thresh):
+    cost = np.ascontiguousarray(cost, np.float64)
+    nr, nc = cost.shape
+    k = max(1, min(nr, nc))
+    m = np.zeros(2 * k, np.int32)
+    ua = np.zeros(max(nr, 1), np.int32)
+    ub = np.zeros(max(nc, 1), np.int32)
+    nm, nua, nub = C.c_int(), C.c_int(), C.c_int()
+    ip = lambda a: a.ctypes.data_as(_ip)  # noqa: E731
+    lib().bxo_linear_assignment(_d(cost), nr, nc, float(thresh), ip(m), C.byref(nm), ip(ua),
+                                C.byref(nua), ip(ub), C.byref(nub))
+    return m[: 2 * nm.value].reshape(-1, 2), ua[: nua.value], ub[: nub.value]
+
+
+class OracleTracker:
+    """Per-sequence CPU oracle tracker with the reference ``update`` contract."""
+
+    def __init__(self, kind: str, **p):
+        L = lib()
+        self.kind = kind
+        if kind == "bytetrack":
+            self.h = L.bxo_bytetrack_new(
+                p.get("min_conf", 0.1), p.get("track_thresh", 0.45), p.get("match_thresh", 0.8),
+                int(p.get("track_buffer", 25)), int(p.get("frame_rate", 30)))
+        elif kind == "botsort":
+            self.h = L.bxo_botsort_new(
+                p.get("track_high_thresh", 0.5), p.get("track_low_thresh", 0.1),
+                p.get("new_track_thresh", 0.6), int(p.get("track_buffer", 30)),
+                p.get("match_thresh", 0.8), p.get("proximity_thresh", 0.5),
+                p.get("appearance_thresh", 0.25), int(p.get("frame_rate", 30)),
+                int(bool(p.get("fuse_first_associate", False))), int(bool(p.get("with_reid", True))))
+        else:
+            raise KeyError(kind)
+        self._cap = 1024
+
+    def update(self, dets, embs=None, warp=None):
+        dets = np.ascontiguousarray(np.asarray(dets, np.float64).reshape(-1, 6))
+        n = dets.shape[0]
+        e_ptr, f, is64 = None, 0, 0
+        if embs is not None and n:
+            embs = np.ascontiguousarray(embs)
+            if embs.dtype == np.float64:
+                is64 = 1
+            else:
+                embs = embs.astype(np.float32, copy=False)
+            f = embs.shape[1]
+            e_ptr = embs.ctypes.data_as(C.c_void_p)
+        w = None if warp is None else _d(np.ascontiguousarray(warp, np.float64).reshape(6))
+        while True:
+            cap = max(self._cap, n + 16)
+            out = np.zeros((cap, 8))
+            m = lib().bxo_update(self.h, _d(dets), n, e_ptr, f, is64, w, _d(out), cap)
+            if m == -2:
+                raise RuntimeError("oracle output buffer too small")
+            if m < 0:
+                raise RuntimeError(f"oracle update failed ({m})")
+            return out[:m].copy()
+
+    @property
+    def id_count(self):
+        return lib().bxo_id_count(self.h)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            lib().bxo_free(h)
+            self.h = None
+
+
+def set_threads(n: int = 1):
+    os.environ.setdefault("OMP_NUM_THREADS", str(n))

@@ -1,0 +1,30 @@
+"""Helpers to replay golden fixtures (tests only)."""
+import ast
+
+import numpy as np
+
+from boxmot_amd.synth import SyntheticScene
+
+
+def fixture_frames(fx):
+    """Yield (frame_no, dets[N,6], embs|None) for a tracker fixture."""
+    if "dets" in fx.files:
+        D = fx["dets"]
+        for f in np.unique(D[:, 0]).astype(int):
+            yield int(f), D[D[:, 0] == f][:, 1:], None
+    else:
+        sc = SyntheticScene(**ast.literal_eval(str(fx["scene"])))
+        for t in range(1, int(fx["n_frames"]) + 1):
+            d, e, _ = sc.frame(t)
+            yield t, d, e
+
+
+def fixture_tracker_args(fx):
+    return str(fx["kind"]), ast.literal_eval(str(fx["tracker_args"]))
+
+
+def compare_outputs(got, ref, box_atol=1e-6):
+    """Integer columns (frame, id, det_ind) and conf/cls bit-exact; boxes within box_atol."""
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    np.testing.assert_array_equal(got[:, [0, 5, 6, 7, 8]], ref[:, [0, 5, 6, 7, 8]])
+    np.testing.assert_allclose(got[:, 1:5], ref[:, 1:5], rtol=0, atol=box_atol)

@@ -1,0 +1,108 @@
+"""Pin the C oracle against golden vectors captured from the Python reference.
+
+Fixtures: tests/golden/make_golden.py (reference imported through an import shim; lapx semantics
+restated over scipy with a uniqueness check on every LAP call).
+"""
+import glob
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+from tests.golden_util import compare_outputs, fixture_frames, fixture_tracker_args
+
+
+@pytest.fixture(scope="module")
+def K(golden_dir):
+    return np.load(golden_dir / "kernels.npz")
+
+
+def test_iou_batch_exact(K):
+    np.testing.assert_array_equal(po.iou_batch(K["iou_a"], K["iou_b"]), K["iou_out"])
+
+
+def test_fuse_score_exact(K):
+    np.testing.assert_array_equal(po.fuse_score(K["fuse_cost_in"], K["fuse_conf"]), K["fuse_out"])
+
+
+def test_embedding_distance_exact(K):
+    np.testing.assert_array_equal(po.embedding_distance(K["emb_trk"], K["emb_det"]), K["emb_out"])
+
+
+def test_np_norm_f32_pairwise_exact():
+    rng = np.random.default_rng(0)
+    for f in (3, 8, 64, 96, 128, 130, 512, 2048):
+        x = rng.standard_normal((7, f)).astype(np.float32)
+        ref = np.linalg.norm(x, axis=1)
+        got = np.array([po.lib().bxo_np_norm_f32(r.ctypes.data_as(po._fp), f) for r in x],
+                       np.float32)
+        np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("kind", ["xyah", "xywh"])
+def test_kalman(K, kind):
+    for z, m0, c0 in zip(K[f"kf_{kind}_meas"], K[f"kf_{kind}_init_mean"], K[f"kf_{kind}_init_cov"]):
+        m, c = po.kf_initiate(kind, z)
+        np.testing.assert_array_equal(m, m0)
+        np.testing.assert_array_equal(c, c0)
+    pm, pc = po.kf_multi_predict(kind, K[f"kf_{kind}_pred_in_mean"], K[f"kf_{kind}_init_cov"])
+    np.testing.assert_array_equal(pm, K[f"kf_{kind}_pred_mean"])  # predict is order-free: exact
+    np.testing.assert_array_equal(pc, K[f"kf_{kind}_pred_cov"])
+    for i in range(pm.shape[0]):
+        um, uc = po.kf_update(kind, K[f"kf_{kind}_pred_mean"][i], K[f"kf_{kind}_pred_cov"][i],
+                              K[f"kf_{kind}_upd_z"][i], K[f"kf_{kind}_upd_conf"][i])
+        # LAPACK/BLAS contraction order is not pinned by the reference → tolerance
+        np.testing.assert_allclose(um, K[f"kf_{kind}_upd_mean"][i], rtol=1e-12, atol=1e-9)
+        np.testing.assert_allclose(uc, K[f"kf_{kind}_upd_cov"][i], rtol=1e-10, atol=1e-9)
+        g = po.kf_gating_distance(kind, K[f"kf_{kind}_pred_mean"][i], K[f"kf_{kind}_pred_cov"][i],
+                                  K[f"kf_{kind}_gate_z"])
+        np.testing.assert_allclose(g, K[f"kf_{kind}_gate_out"][i], rtol=1e-10)
+
+
+def test_linear_assignment(K):
+    assert int(K["lap_degenerate"]) == 0
+    for i in range(int(K["lap_count"])):
+        m, ua, ub = po.linear_assignment(K[f"lap{i}_cost"], float(K[f"lap{i}_thr"]))
+        np.testing.assert_array_equal(m, K[f"lap{i}_matches"].reshape(-1, 2))
+        np.testing.assert_array_equal(ua, K[f"lap{i}_ua"])
+        np.testing.assert_array_equal(ub, K[f"lap{i}_ub"])
+
+
+def test_lapjv_random_vs_scipy():
+    from scipy.optimize import linear_sum_assignment
+
+    rng = np.random.default_rng(7)
+    for n in (1, 2, 5, 17, 64):
+        for _ in range(5):
+            c = rng.uniform(0, 1, (n, n))
+            x = np.zeros(n, np.int32)
+            y = np.zeros(n, np.int32)
+            po.lib().bxo_lapjv(n, c.ctypes.data_as(po._dp), x.ctypes.data_as(po._ip),
+                               y.ctypes.data_as(po._ip))
+            r, k = linear_sum_assignment(c)
+            np.testing.assert_array_equal(x, k)
+            np.testing.assert_array_equal(y[x], np.arange(n))
+
+
+def test_linear_assignment_empty():
+    m, ua, ub = po.linear_assignment(np.zeros((0, 3)), 0.5)
+    assert m.shape == (0, 2) and ua.size == 0 and list(ub) == [0, 1, 2]
+    m, ua, ub = po.linear_assignment(np.zeros((2, 0)), 0.5)
+    assert m.shape == (0, 2) and list(ua) == [0, 1] and ub.size == 0
+    m, ua, ub = po.linear_assignment(np.full((3, 3), 0.9), 0.5)  # all above the limit
+    assert m.shape == (0, 2) and list(ua) == [0, 1, 2] and list(ub) == [0, 1, 2]
+
+
+@pytest.mark.parametrize(
+    "path", sorted(glob.glob(str(__import__("pathlib").Path(__file__).parent / "golden" / "trk_*.npz"))),
+    ids=lambda p: p.rsplit("/", 1)[-1][4:-4])
+def test_tracker_fixture(path):
+    fx = np.load(path)
+    assert int(fx["lap_degenerate"]) == 0
+    kind, args = fixture_tracker_args(fx)
+    tr = po.OracleTracker(kind, **args)
+    rows = []
+    for f, d, e in fixture_frames(fx):
+        o = tr.update(d, e)
+        rows.append(np.concatenate([np.full((o.shape[0], 1), f), o], 1))
+    compare_outputs(np.concatenate(rows, 0), fx["outputs"], box_atol=1e-9)
