@@ -1,0 +1,205 @@
+#!/usr/bin/env python
+"""Association-FPS benchmark (BASELINE.json metric) for the MI355X engine.
+
+A step = one frame of every sequence this rank holds, advanced by ONE launch of the fused frame
+kernel.  Workload (BASELINE.json configs[2], the north_star's 256-track x 128-det x 512-d
+target): BoT-SORT on synthetic grid scenes of 256 objects detected w.p. 0.5 (≈128 dets/frame,
+all above track_high_thresh) with 512-d float32 embeddings; `--config bytetrack` runs configs[1]
+(ByteTrack, IoU only).  Each rank holds `--seqs` independent sequences (weak scaling: the
+sequence count per GPU is fixed as N grows; no per-frame collective).  Inputs for every timed
+frame are generated on the GPU and resident in HBM before the timed region.
+
+Single process: `python bench.py`.  Multi-GPU: `torch.distributed.run --nproc-per-node N
+bench.py --gpus N` (RCCL is used only to gather per-rank frame counts/time: max over ranks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "association FPS (frames/sec) at N_tracks×N_dets×feat_dim, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    # name: (tracker, n_obj, emb_dim, tracker params (YAML defaults))
+    "botsort": ("botsort", 256, 512, dict(track_high_thresh=0.6, track_low_thresh=0.1,
+                                          new_track_thresh=0.7, track_buffer=30,
+                                          match_thresh=0.8, proximity_thresh=0.5,
+                                          appearance_thresh=0.25)),
+    "bytetrack": ("bytetrack", 256, 0, dict(min_conf=0.1, track_thresh=0.6, match_thresh=0.9,
+                                            track_buffer=30)),
+}
+
+
+def algorithmic_bytes_per_frame(T, D, F, K):
+    """B = 2·T·576 + D·48 + (T_f + D)·F·4 + K·F·4 (fp64 track state read +
+    write, det rows, track + det features, updated features); T_f = T when F > 0."""
+    b = 2 * T * 576 + D * 48
+    if F:
+        b += (T + D) * F * 4 + K * F * 4
+    return b
+
+
+def cpu_baseline(kind, n_obj, emb_dim, params, seconds=15.0, warm_frames=40):
+    """Time the C oracle (port of the reference semantics, 1 thread) on one sequence of the
+    same workload: frames/s over a bounded sample after `warm_frames` of warm-up."""
+    from boxmot_amd.synth import SyntheticScene
+    from oracle import pyoracle as po
+
+    sc = SyntheticScene(n_obj=n_obj, seed=12345, emb_dim=emb_dim)
+    tr = po.OracleTracker(kind, **params)
+    t = 0
+    for _ in range(warm_frames):
+        t += 1
+        d, e, _ = sc.frame(t)
+        tr.update(d, e)
+    frames, busy = 0, 0.0
+    while busy < seconds:
+        t += 1
+        d, e, _ = sc.frame(t)  # generation excluded from the timed work
+        t0 = time.perf_counter()
+        tr.update(d, e)
+        busy += time.perf_counter() - t0
+        frames += 1
+    return {"value": frames / busy, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"1 sequence, {n_obj} objects (~{n_obj // 2} dets/frame)"
+                      f"{f' x {emb_dim}-d' if emb_dim else ''}, frames {warm_frames + 1}.."
+                      f"{t} ({frames} timed, {busy:.1f}s single-thread; oracle/ C fp64 port)"}
+
+
+def load_traffic(config):
+    p = ROOT / "profiles" / f"pmc_{config}.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get("hbm_bytes_per_launch_corrected")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", choices=list(CONFIGS), default="botsort")
+    ap.add_argument("--seqs", type=int, default=1024, help="sequences per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from boxmot_amd.engine import Engine, EngineParams
+    from boxmot_amd.synth import TorchSceneBatch
+
+    kind, n_obj, F, params = CONFIGS[args.config]
+    S = args.seqs
+    D_cap = 256
+    eng = Engine(kind, n_seq=S, track_cap=512, det_cap=D_cap, emb_dim=F,
+                 params=EngineParams(**params))
+    gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev)
+    total = args.warmup + args.steps
+    frames = [gen.frame(t) for t in range(1, total + 1)]  # resident in HBM before timing
+    max_n = max(int(f[1][-1].item()) for f in frames)
+    out = torch.empty((max_n, 8), dtype=torch.float64, device=dev)
+    cnt = torch.empty(S, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+
+    def step(k):
+        d, off, e = frames[k]
+        eng.step(d, off, e, None, out, cnt, stream=stream.cuda_stream)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for k in range(args.warmup, total):
+        step(k)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one frame-kernel launch per step
+    if eng.status() != 0:
+        raise RuntimeError(f"engine status {eng.status()} (capacity overflow)")
+
+    dets_timed = sum(int(frames[k][1][-1].item()) for k in range(args.warmup, total))
+    stats = torch.tensor([wall, float(S * args.steps), float(dets_timed), kern_ms],
+                         dtype=torch.float64, device=dev)
+    if dist:
+        # RCCL over xGMI only to gather per-rank results (KB-scale), never per frame
+        gathered = [torch.zeros_like(stats) for _ in range(world)]
+        dist.all_gather(gathered, stats)
+        allst = torch.stack(gathered).cpu().numpy()
+    else:
+        allst = stats[None].cpu().numpy()
+    t_max = float(allst[:, 0].max())
+    total_frames = float(allst[:, 1].sum())
+    value = total_frames / t_max
+    if rank == 0:
+        mean_d = float(allst[:, 2].sum() / allst[:, 1].sum())
+        T_pool = n_obj
+        per_frame = algorithmic_bytes_per_frame(T_pool, mean_d, F, mean_d)
+        per_launch = per_frame * S
+        achieved = per_launch / (kern_ms * 1e-3) / 1e9
+        traffic = load_traffic(args.config)
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (GPU-generated grid scenes, resident in HBM before timing)",
+            "config": {"workload": f"{args.config}: {S} sequences/GPU x {n_obj} tracks x "
+                                   f"~{mean_d:.0f} dets" + (f" x {F}-d ReID" if F else ""),
+                       "tracker": kind, "n_seq_per_gpu": S, "n_tracks": n_obj,
+                       "n_dets_mean": round(mean_d, 1), "feat_dim": F, "emb_dtype": "f32",
+                       "parallelism": f"seq-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "kernel": f"frame_kernel<{kind}>",
+                         "kernel_ms": round(kern_ms, 4),
+                         "algorithmic_bytes_per_launch": int(per_launch)},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(kind, n_obj, F, params, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

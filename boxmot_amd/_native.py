@@ -1,0 +1,141 @@
+"""ctypes binding of libbxassoc.so (include/bxassoc.h).
+
+The HIP library is the product: there is no CPU fallback.  Importing this module never needs a
+GPU, but any call into the engine on a machine without the built library or without a HIP
+device raises ``NativeUnavailable`` — loudly, so a silent eager/CPU path can never stand in.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+REPO = PKG.parent
+CSRC = PKG / "csrc"
+LIB_DIR = PKG / "lib"
+LIB_PATH = LIB_DIR / "libbxassoc.so"
+HEADER = REPO / "include" / "bxassoc.h"
+
+HIPCC_FLAGS = [
+    "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+    # numpy-identical rounding: no FMA contraction, IEEE f32 division/sqrt
+    "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
+]
+SOURCES = ["bx_engine.hip", "bx_ops.hip"]
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile the HIP extension for gfx950 in-tree (boxmot_amd/lib/libbxassoc.so)."""
+    srcs = [CSRC / s for s in SOURCES] + [CSRC / "bx_device.h", HEADER]
+    if not force and LIB_PATH.exists():
+        t = LIB_PATH.stat().st_mtime
+        if all(s.stat().st_mtime <= t for s in srcs):
+            return LIB_PATH
+    LIB_DIR.mkdir(exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [hipcc, *HIPCC_FLAGS, "-o", str(tmp), *[str(CSRC / s) for s in SOURCES]]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed:\n{r.stderr}")
+    if verbose and r.stderr:
+        print(r.stderr)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+class BxConfig(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("n_seq", C.c_int32), ("track_cap", C.c_int32),
+        ("det_cap", C.c_int32), ("emb_dim", C.c_int32), ("emb_f64", C.c_int32),
+        ("min_conf", C.c_double), ("track_thresh", C.c_double), ("match_thresh", C.c_double),
+        ("track_buffer", C.c_int32), ("frame_rate", C.c_int32),
+        ("track_high_thresh", C.c_double), ("track_low_thresh", C.c_double),
+        ("new_track_thresh", C.c_double), ("proximity_thresh", C.c_double),
+        ("appearance_thresh", C.c_double),
+        ("fuse_first_associate", C.c_int32), ("with_reid", C.c_int32),
+    ]
+
+
+# every symbol include/bxassoc.h declares (checked by tests/test_native_abi.py)
+EXPORTS = [
+    "bx_last_error", "bx_device_count", "bx_engine_create", "bx_engine_destroy",
+    "bx_engine_reset", "bx_engine_step", "bx_engine_update_host", "bx_engine_status",
+    "bx_engine_counters_host", "bx_engine_set_id_count", "bx_engine_tracks_host",
+    "bx_iou_batch", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
+    "bx_kf_multi_predict", "bx_kf_update", "bx_kf_gating_distance", "bx_linear_assignment",
+]
+
+_vp, _ip, _dp, _fp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_float)
+
+_SIGS = {
+    "bx_last_error": ([], C.c_char_p),
+    "bx_device_count": ([_ip], C.c_int),
+    "bx_engine_create": ([C.POINTER(BxConfig), C.POINTER(C.c_void_p)], C.c_int),
+    "bx_engine_destroy": ([_vp], C.c_int),
+    "bx_engine_reset": ([_vp, C.c_int, C.c_int, _vp], C.c_int),
+    "bx_engine_step": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_engine_update_host": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp, _vp, _ip, _vp], C.c_int),
+    "bx_engine_status": ([_vp, _ip], C.c_int),
+    "bx_engine_counters_host": ([_vp, C.c_int, _ip, _ip, _ip, _ip], C.c_int),
+    "bx_engine_set_id_count": ([_vp, C.c_int, C.c_int, _vp], C.c_int),
+    "bx_engine_tracks_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip,
+                               _ip], C.c_int),
+    "bx_iou_batch": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp], C.c_int),
+    "bx_fuse_score": ([_vp, C.c_int, C.c_int, _vp, _vp], C.c_int),
+    "bx_embedding_distance": ([_vp, C.c_int, _vp, C.c_int, C.c_int, _vp, _vp], C.c_int),
+    "bx_kf_initiate": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_kf_multi_predict": ([C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
+    "bx_kf_update": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_kf_gating_distance": ([C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, _vp], C.c_int),
+    "bx_linear_assignment": ([_vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp], C.c_int),
+}
+
+_lib = None
+
+
+def load(path: Path | None = None):
+    """Load libbxassoc.so (raises NativeUnavailable when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise NativeUnavailable(
+            f"{p} is missing: build the HIP extension first (python -c 'import __graft_entry__ "
+            "as g; g.build()' or boxmot_amd._native.build())")
+    L = C.CDLL(str(p))
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+STATUS = {0: "ok", 1: "invalid argument", 2: "capacity exceeded", 3: "track slots exhausted",
+          4: "HIP error", 5: "no HIP device", 6: "shape mismatch"}
+
+
+def check(rc: int, what: str = ""):
+    if rc == 0:
+        return
+    msg = load().bx_last_error().decode(errors="replace")
+    text = f"{what}: {STATUS.get(rc, rc)} ({msg})"
+    if rc == 5:
+        raise NativeUnavailable(text)
+    if rc in (1, 2, 6):
+        raise ValueError(text)
+    raise RuntimeError(text)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    load().bx_device_count(C.byref(n))
+    return n.value

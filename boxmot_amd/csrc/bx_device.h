@@ -1,0 +1,508 @@
+// bx_device.h — device-side building blocks of the association engine (gfx950, wave64).
+//
+// All floating-point expressions restate the reference's numpy operation order one-for-one and
+// the library is compiled with -ffp-contract=off, so every product/sum rounds exactly as numpy's
+// (and as the C oracle's) do.  The Kalman update and the BLAS-ordered feature norms follow the
+// oracle's fixed order (the reference's BLAS/LAPACK order is not pinned), making the GPU path
+// bitwise identical to oracle/ and within ~1e-13 of the reference.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bx {
+
+constexpr int WG = 256;  // threads per workgroup: 4 waves of 64
+constexpr int WAVE = 64;
+constexpr double INF = __builtin_huge_val();
+
+enum : int { KIND_BYTE = 0, KIND_BOT = 1 };
+enum : uint32_t { ST_NEW = 0, ST_TRACKED = 1, ST_LOST = 2, ST_REMOVED = 3 };
+// per-slot persistent flag word
+enum : uint32_t { F_STATE = 0x7u, F_ACT = 0x8u, F_INREM = 0x10u, F_INUSE = 0x20u };
+
+__device__ __forceinline__ uint32_t st_of(uint32_t f) { return f & F_STATE; }
+
+// ------------------------------------------------------------------------------------------
+// utils/ops.py box conversions (numpy op order)
+__device__ __forceinline__ void xyxy2xywh(const double* x, double* y) {
+  double a = (x[0] + x[2]) / 2, b = (x[1] + x[3]) / 2, c = x[2] - x[0], d = x[3] - x[1];
+  y[0] = a; y[1] = b; y[2] = c; y[3] = d;
+}
+__device__ __forceinline__ void xywh2xyxy(const double* x, double* y) {
+  double a = x[0] - x[2] / 2, b = x[1] - x[3] / 2, c = x[0] + x[2] / 2, d = x[1] + x[3] / 2;
+  y[0] = a; y[1] = b; y[2] = c; y[3] = d;
+}
+__device__ __forceinline__ void xywh2tlwh(const double* x, double* y) {
+  double a = x[0] - x[2] / 2, b = x[1] - x[3] / 2, c = x[2], d = x[3];
+  y[0] = a; y[1] = b; y[2] = c; y[3] = d;
+}
+__device__ __forceinline__ void tlwh2xyah(const double* x, double* y) {
+  double a = x[0] + x[2] / 2, b = x[1] + x[3] / 2, c = x[2] / x[3], d = x[3];
+  y[0] = a; y[1] = b; y[2] = c; y[3] = d;
+}
+
+// utils/iou.py:50-67 (no epsilon in the denominator)
+__device__ __forceinline__ double iou_pair(const double* b1, const double* b2) {
+  double xx1 = fmax(b1[0], b2[0]);
+  double yy1 = fmax(b1[1], b2[1]);
+  double xx2 = fmin(b1[2], b2[2]);
+  double yy2 = fmin(b1[3], b2[3]);
+  double w = fmax(0.0, xx2 - xx1);
+  double h = fmax(0.0, yy2 - yy1);
+  double wh = w * h;
+  return wh / ((b1[2] - b1[0]) * (b1[3] - b1[1]) + (b2[2] - b2[0]) * (b2[3] - b2[1]) - wh);
+}
+// Positive-area intersection.  A pair that fails this has IoU exactly 0 (cost 1 or 2 after
+// fuse_score), which is never admissible for a cost_limit <= 1.
+__device__ __forceinline__ bool boxes_intersect(const double* b1, const double* b2) {
+  return fmin(b1[2], b2[2]) > fmax(b1[0], b2[0]) && fmin(b1[3], b2[3]) > fmax(b1[1], b2[1]);
+}
+
+// utils/matching.py:520-544 enhanced_fuse_score (fork semantics)
+__device__ __forceinline__ double fuse_one(double cost, double conf) {
+  double sim = 1 - cost;
+  double w = conf > 0.7 ? conf * 1.2 : conf;
+  double mask = conf >= 0.5 ? 1.0 : 0.0;
+  double fuse = 1 - sim * w * mask;
+  return conf < 0.5 ? fuse * 2.0 : fuse;
+}
+
+// ------------------------------------------------------------------------------------------
+// Kalman filters (base_kalman_filter.py; xyah_kf.py / xywh_kf.py).  dt = 1.
+constexpr double STD_POS = 1.0 / 20, STD_VEL = 1.0 / 160;
+
+__device__ inline void kf_initiate(int kind, const double* m, double* mean, double* cov) {
+  double std[8];
+  if (kind == KIND_BYTE) {
+    std[0] = 2 * STD_POS * m[3]; std[1] = 2 * STD_POS * m[3]; std[2] = 1e-2;
+    std[3] = 2 * STD_POS * m[3]; std[4] = 10 * STD_VEL * m[3]; std[5] = 10 * STD_VEL * m[3];
+    std[6] = 1e-5; std[7] = 10 * STD_VEL * m[3];
+  } else {
+    std[0] = 2 * STD_POS * m[2]; std[1] = 2 * STD_POS * m[3]; std[2] = 2 * STD_POS * m[2];
+    std[3] = 2 * STD_POS * m[3]; std[4] = 10 * STD_VEL * m[2]; std[5] = 10 * STD_VEL * m[3];
+    std[6] = 10 * STD_VEL * m[2]; std[7] = 10 * STD_VEL * m[3];
+  }
+  for (int k = 0; k < 4; k++) { mean[k] = m[k]; mean[4 + k] = 0.0; }
+  for (int k = 0; k < 64; k++) cov[k] = 0.0;
+  for (int k = 0; k < 8; k++) cov[9 * k] = std[k] * std[k];
+}
+
+__device__ inline void kf_process_noise(int kind, const double* mean, double* q) {
+  double s[8];
+  if (kind == KIND_BYTE) {
+    s[0] = STD_POS * mean[3]; s[1] = STD_POS * mean[3]; s[2] = 1e-2; s[3] = STD_POS * mean[3];
+    s[4] = STD_VEL * mean[3]; s[5] = STD_VEL * mean[3]; s[6] = 1e-5; s[7] = STD_VEL * mean[3];
+  } else {
+    s[0] = STD_POS * mean[2]; s[1] = STD_POS * mean[3]; s[2] = STD_POS * mean[2];
+    s[3] = STD_POS * mean[3]; s[4] = STD_VEL * mean[2]; s[5] = STD_VEL * mean[3];
+    s[6] = STD_VEL * mean[2]; s[7] = STD_VEL * mean[3];
+  }
+  for (int k = 0; k < 8; k++) q[k] = s[k] * s[k];
+}
+
+// multi_predict on one track held in an SoA slab: element e of track t at base[e*stride].
+// F has two non-zero terms per row/col: cov' = (P_ij + P_i+4,j) + (P_i,j+4 + P_i+4,j+4) + Q.
+__device__ inline void kf_predict_soa(int kind, double* mean, double* cov, int stride) {
+  double m[8], q[8];
+  for (int k = 0; k < 8; k++) m[k] = mean[k * stride];
+  kf_process_noise(kind, m, q);
+  for (int k = 0; k < 4; k++) mean[k * stride] = m[k] + m[k + 4];
+  // row-pair (i, i+4) at a time keeps the live set to two rows
+  for (int i = 0; i < 4; i++) {
+    double r0[8], r1[8], f0[8];
+    for (int j = 0; j < 8; j++) { r0[j] = cov[(8 * i + j) * stride]; r1[j] = cov[(8 * (i + 4) + j) * stride]; }
+    for (int j = 0; j < 8; j++) f0[j] = r0[j] + r1[j];  // (F P) row i
+    for (int j = 0; j < 8; j++) {
+      double v0 = j < 4 ? f0[j] + f0[j + 4] : f0[j];
+      double v1 = j < 4 ? r1[j] + r1[j + 4] : r1[j];  // (F P) row i+4 = P row i+4
+      cov[(8 * i + j) * stride] = (i == j) ? v0 + q[i] : v0;
+      cov[(8 * (i + 4) + j) * stride] = (i + 4 == j) ? v1 + q[i + 4] : v1;
+    }
+  }
+}
+
+__device__ inline void kf_meas_noise(int kind, const double* mean, double conf, double* r) {
+  double s[4];
+  if (kind == KIND_BYTE) {
+    s[0] = STD_POS * mean[3]; s[1] = STD_POS * mean[3]; s[2] = 1e-1; s[3] = STD_POS * mean[3];
+  } else {
+    s[0] = STD_POS * mean[2]; s[1] = STD_POS * mean[3]; s[2] = STD_POS * mean[2];
+    s[3] = STD_POS * mean[3];
+  }
+  for (int k = 0; k < 4; k++) { double v = (1 - conf) * s[k]; r[k] = v * v; }
+}
+
+__device__ inline bool chol4(const double* S, double* L) {
+  for (int k = 0; k < 16; k++) L[k] = 0.0;
+  for (int j = 0; j < 4; j++) {
+    double d = S[4 * j + j];
+    for (int k = 0; k < j; k++) d -= L[4 * j + k] * L[4 * j + k];
+    if (!(d > 0.0)) return false;
+    d = sqrt(d);
+    L[4 * j + j] = d;
+    for (int i = j + 1; i < 4; i++) {
+      double s = S[4 * i + j];
+      for (int k = 0; k < j; k++) s -= L[4 * i + k] * L[4 * j + k];
+      L[4 * i + j] = s / d;
+    }
+  }
+  return true;
+}
+
+// base_kalman_filter.py:129-155 on one SoA track (same loop order as oracle/bxo_ops.c).
+__device__ inline void kf_update_soa(int kind, double* mean, double* cov, int stride,
+                                     const double* z, double conf) {
+  double m[8], S[16], L[16], K[32];
+  for (int k = 0; k < 8; k++) m[k] = mean[k * stride];
+  double r[4];
+  kf_meas_noise(kind, m, conf, r);
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) S[4 * i + j] = cov[(8 * i + j) * stride] + (i == j ? r[i] : 0.0);
+  if (!chol4(S, L)) return;
+  for (int c = 0; c < 8; c++) {
+    double y[4], x[4];
+    for (int i = 0; i < 4; i++) {
+      double s = cov[(8 * c + i) * stride];
+      for (int k = 0; k < i; k++) s -= L[4 * i + k] * y[k];
+      y[i] = s / L[4 * i + i];
+    }
+    for (int i = 3; i >= 0; i--) {
+      double s = y[i];
+      for (int k = i + 1; k < 4; k++) s -= L[4 * k + i] * x[k];
+      x[i] = s / L[4 * i + i];
+    }
+    for (int i = 0; i < 4; i++) K[4 * c + i] = x[i];
+  }
+  double innov[4];
+  for (int k = 0; k < 4; k++) innov[k] = z[k] - m[k];
+  for (int i = 0; i < 8; i++) {
+    double s = 0.0;
+    for (int k = 0; k < 4; k++) s += innov[k] * K[4 * i + k];
+    mean[i * stride] = m[i] + s;
+  }
+  for (int i = 0; i < 8; i++) {
+    double ks[4];
+    for (int j = 0; j < 4; j++) {
+      double s = 0.0;
+      for (int k = 0; k < 4; k++) s += K[4 * i + k] * S[4 * k + j];
+      ks[j] = s;
+    }
+    for (int j = 0; j < 8; j++) {
+      double s = 0.0;
+      for (int k = 0; k < 4; k++) s += ks[k] * K[4 * j + k];
+      cov[(8 * i + j) * stride] = cov[(8 * i + j) * stride] - s;
+    }
+  }
+}
+
+// base_kalman_filter.py:166-194 (maha, 4 dims) for one state vs nz measurements
+__device__ inline void kf_gating_soa(int kind, const double* mean, const double* cov, int stride,
+                                     const double* z, int nz, double* out) {
+  double m[8], S[16], L[16], r[4];
+  for (int k = 0; k < 8; k++) m[k] = mean[k * stride];
+  kf_meas_noise(kind, m, 0.0, r);
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) S[4 * i + j] = cov[(8 * i + j) * stride] + (i == j ? r[i] : 0.0);
+  bool ok = chol4(S, L);
+  for (int q = 0; q < nz; q++) {
+    if (!ok) { out[q] = __builtin_nan(""); continue; }
+    double d[4], y[4], s2 = 0.0;
+    for (int i = 0; i < 4; i++) d[i] = z[4 * q + i] - m[i];
+    for (int i = 0; i < 4; i++) {
+      double s = d[i];
+      for (int j = 0; j < i; j++) s -= L[4 * i + j] * y[j];
+      y[i] = s / L[4 * i + i];
+      s2 += y[i] * y[i];
+    }
+    out[q] = s2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Feature numerics.
+// numpy float32 pairwise sum (PW_BLOCKSIZE 128, 8 accumulators) of x[i]*x[i], sequential in
+// one lane; the recursion (n2 = n/2 rounded down to a multiple of 8) unrolled with a stack.
+template <typename XT>
+__device__ inline float np_pairwise_sumsq_f32(const XT* xs, int n) {
+  struct {
+    const XT* p;
+    __device__ float operator[](int i) const { return (float)p[i]; }
+  } x{xs};
+  float acc[24];
+  int ap = 0;
+  // iterative post-order walk over the split tree: leaves (<=128) summed, nodes combined
+  int stk_off[24], stk_n[24], stk_state[24], top = 0;
+  stk_off[0] = 0; stk_n[0] = n; stk_state[0] = 0; top = 1;
+  while (top > 0) {
+    int t = top - 1;
+    int off = stk_off[t], m = stk_n[t];
+    if (m <= 128) {
+      float res;
+      if (m < 8) {
+        res = 0.0f;
+        for (int i = 0; i < m; i++) { float v = x[off + i]; res += v * v; }
+      } else {
+        float r[8];
+        for (int k = 0; k < 8; k++) { float v = x[off + k]; r[k] = v * v; }
+        int i;
+        for (i = 8; i < m - (m % 8); i += 8)
+          for (int k = 0; k < 8; k++) { float v = x[off + i + k]; r[k] += v * v; }
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < m; i++) { float v = x[off + i]; res += v * v; }
+      }
+      acc[ap++] = res;
+      top--;
+      continue;
+    }
+    int n2 = m / 2;
+    n2 -= n2 % 8;
+    if (stk_state[t] == 0) {  // descend left
+      stk_state[t] = 1;
+      stk_off[top] = off; stk_n[top] = n2; stk_state[top] = 0; top++;
+    } else if (stk_state[t] == 1) {  // descend right
+      stk_state[t] = 2;
+      stk_off[top] = off + n2; stk_n[top] = m - n2; stk_state[top] = 0; top++;
+    } else {  // combine
+      float b = acc[--ap], a = acc[--ap];
+      acc[ap++] = a + b;
+      top--;
+    }
+  }
+  return acc[0];
+}
+
+// scipy cdist-cosine inner product: two interleaved fp64 accumulators, remainder added last.
+template <typename A, typename B>
+__device__ inline double dot2(const A& a, const B& b, int n) {
+  double a0 = 0.0, a1 = 0.0;
+  int i = 0;
+  for (; i + 2 <= n; i += 2) { a0 += a(i) * b(i); a1 += a(i + 1) * b(i + 1); }
+  double s = a0 + a1;
+  if (i < n) s += a(i) * b(i);
+  return s;
+}
+
+// np.linalg.norm of a 1-D feature (BLAS dot; order fixed as the oracle's: sequential fp64).
+template <typename FT>
+__device__ inline FT blas_norm(const FT* x, int n) {
+  double s = 0.0;
+  for (int k = 0; k < n; k++) { double v = (double)x[k]; s += v * v; }
+  if constexpr (sizeof(FT) == 4) return sqrtf((float)s);
+  else return sqrt(s);
+}
+
+// ------------------------------------------------------------------------------------------
+// Block (256-thread) helpers.
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+// exclusive prefix of a 0/1 flag over the block in thread order; `tmp` >= 4 ints of LDS.
+__device__ inline int block_scan_flag(bool f, int* tmp, int& total) {
+  const int lane = lane_id(), w = wave_id();
+  unsigned long long m = __ballot(f);
+  int pre = __popcll(m & ((1ull << lane) - 1ull));
+  if (lane == 0) tmp[w] = __popcll(m);
+  __syncthreads();
+  int off = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) off += (k < w) ? tmp[k] : 0;
+  total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+  __syncthreads();
+  return off + pre;
+}
+
+// Order-preserving compaction: emit(k, pos) for every k < n with pred(k).  Returns the count.
+template <class P, class E>
+__device__ inline int block_compact(int n, P pred, E emit, int* tmp) {
+  int base = 0;
+  for (int c = 0; c < n; c += WG) {
+    int k = c + (int)threadIdx.x;
+    bool f = k < n && pred(k);
+    int tot;
+    int pos = block_scan_flag(f, tmp, tot);
+    if (f) emit(k, base + pos);
+    base += tot;
+  }
+  return base;
+}
+
+// exclusive scan of cnt[0..n) in place by wave 0 (returns total via *total_out, also cnt[n]).
+__device__ inline void wave0_exclusive_scan(int* cnt, int n) {
+  if (wave_id() != 0) return;
+  const int lane = lane_id();
+  int carry = 0;
+  for (int c = 0; c < n; c += WAVE) {
+    int k = c + lane;
+    int v = k < n ? cnt[k] : 0;
+    int x = v;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+      int y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    if (k < n) cnt[k] = carry + x - v;
+    carry += __shfl(x, WAVE - 1);
+  }
+  if (lane == 0) cnt[n] = carry;
+}
+
+// ------------------------------------------------------------------------------------------
+// Linear assignment with lapx `extend_cost=True, cost_limit=L` semantics on a sparse CSR of
+// admissible edges (cost < L).  lapx's (n_r+n_c)^2 extension with L/2 fillers is exactly a
+// max-gain partial matching with gains L - c, solved here by successive
+// shortest augmenting paths (Dijkstra with potentials; rectangular LSAP) where every row owns a
+// private zero-cost "dummy" column meaning "unmatched".  Run by ONE wave: relaxations are
+// lane-parallel over a row's edges and the argmin over the touched columns is a wave reduction.
+struct LapWS {
+  const int* row_ptr;     // [R+1] edge offsets
+  const uint16_t* ecol;   // edge columns (first elds in LDS, the rest in gcol)
+  const double* ecost;    // edge costs  (first elds in LDS, the rest in gcost)
+  const uint16_t* gcol;   // overflow edges in global memory
+  const double* gcost;
+  int elds;
+  int16_t* col4row;       // [R] out: column or -1
+  int16_t* row4col;       // [C] out: row or -1
+  double* u;              // [R] row potentials
+  double* v;              // [C] column potentials
+  double* spc;            // [C] shortest-path costs (INF between solves)
+  int16_t* path;          // [C]
+  uint8_t* colflag;       // [C] bit0 = in SC, bit1 = touched
+  uint16_t* touched;      // [C] touched column list
+  uint16_t* srlist;       // [R] rows visited (SR) except the root
+};
+
+__device__ __forceinline__ void lap_edge(const LapWS& w, int e, int& col, double& cost) {
+  if (e < w.elds) { col = w.ecol[e]; cost = w.ecost[e]; }
+  else { col = w.gcol[e - w.elds]; cost = w.gcost[e - w.elds]; }
+}
+
+// wave-wide argmin over (val, key); ties -> smaller key.  All lanes get the result.
+__device__ __forceinline__ void wave_argmin(double& val, int& key) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    double ov = __shfl_xor(val, d);
+    int ok = __shfl_xor(key, d);
+    if (ov < val || (ov == val && ok < key)) { val = ov; key = ok; }
+  }
+}
+
+// Called by all 64 lanes of one wave.  R rows, C columns, limit L.
+__device__ inline void lap_solve_wave(int R, int C, double L, const LapWS& w) {
+  const int lane = lane_id();
+  for (int k = lane; k < R; k += WAVE) { w.col4row[k] = -1; w.u[k] = 0.0; }
+  for (int k = lane; k < C; k += WAVE) {
+    w.row4col[k] = -1; w.v[k] = 0.0; w.spc[k] = INF; w.colflag[k] = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  for (int root = 0; root < R; root++) {
+    const int rb = w.row_ptr[root], re = w.row_ptr[root + 1];
+    if (rb == re) continue;  // no admissible edge: stays unmatched (its dummy)
+    double minVal = 0.0;
+    int i = root;
+    int ntouched = 0, nsr = 0;
+    double dummy_best = INF;
+    int dummy_row = -1;
+    int sink = -1;  // >=0 real column, -2 dummy of dummy_row
+    while (true) {
+      // relax row i
+      const double ui = w.u[i];
+      const int b = w.row_ptr[i], e = w.row_ptr[i + 1];
+      for (int base = b; base < e; base += WAVE) {
+        int eidx = base + lane;
+        bool newt = false;
+        int j = 0;
+        if (eidx < e) {
+          double c;
+          lap_edge(w, eidx, j, c);
+          if (!(w.colflag[j] & 1)) {
+            double r = minVal + (c - L) - ui - w.v[j];
+            if (r < w.spc[j]) {
+              w.spc[j] = r;
+              w.path[j] = (int16_t)i;
+              if (!(w.colflag[j] & 2)) { w.colflag[j] |= 2; newt = true; }
+            }
+          }
+        }
+        unsigned long long m = __ballot(newt);
+        if (newt) w.touched[ntouched + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)j;
+        ntouched += __popcll(m);
+      }
+      {  // dummy of row i: reduced cost 0 - u_i - 0 (its potential never moves)
+        double dv = minVal - ui;
+        if (dv < dummy_best) { dummy_best = dv; dummy_row = i; }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      // argmin over touched, not-yet-scanned columns
+      double bv = INF;
+      int bk = 0x7fffffff;
+      for (int k = lane; k < ntouched; k += WAVE) {
+        int j = w.touched[k];
+        if (!(w.colflag[j] & 1)) {
+          double s = w.spc[j];
+          if (s < bv) { bv = s; bk = k; }
+        }
+      }
+      wave_argmin(bv, bk);
+      if (dummy_best <= bv) {  // leave dummy_row unmatched (ties: stop early)
+        minVal = dummy_best;
+        sink = -2;
+        break;
+      }
+      const int j = w.touched[bk];
+      minVal = bv;
+      if (lane == 0) w.colflag[j] |= 1;
+      const int r4c = w.row4col[j];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (r4c < 0) { sink = j; break; }
+      i = r4c;
+      if (lane == 0) w.srlist[nsr] = (uint16_t)i;
+      nsr++;
+    }
+    // dual updates
+    if (lane == 0) w.u[root] += minVal;
+    for (int k = lane; k < nsr; k += WAVE) {
+      int r = w.srlist[k];
+      w.u[r] += minVal - w.spc[w.col4row[r]];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    for (int k = lane; k < ntouched; k += WAVE) {
+      int j = w.touched[k];
+      if (w.colflag[j] & 1) w.v[j] -= minVal - w.spc[j];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // augment (lane 0; path length <= nsr + 1)
+    if (lane == 0) {
+      int j;
+      if (sink == -2) {
+        j = w.col4row[dummy_row];
+        w.col4row[dummy_row] = -1;
+        if (dummy_row == root) j = -1;
+      } else {
+        j = sink;
+      }
+      while (j >= 0) {
+        int r = w.path[j];
+        w.row4col[j] = (int16_t)r;
+        int old = w.col4row[r];
+        w.col4row[r] = (int16_t)j;
+        if (r == root) break;
+        j = old;
+      }
+    }
+    // reset touched columns
+    for (int k = lane; k < ntouched; k += WAVE) {
+      int j = w.touched[k];
+      w.spc[j] = INF;
+      w.colflag[j] = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+}
+
+}  // namespace bx

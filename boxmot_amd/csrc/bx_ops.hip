@@ -1,0 +1,281 @@
+// bx_ops.hip — op-level kernels of the C ABI (stateless, device pointers).  They share the
+// device functions of the frame kernel (bx_device.h) and exist so every building block can be
+// parity-checked on its own against the oracle and the reference's golden vectors.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/bxassoc.h"
+#include "bx_device.h"
+
+using namespace bx;
+
+namespace {
+
+thread_local std::string g_op_err;
+int op_err(int code, const char* msg) {
+  g_op_err = msg;
+  return code;
+}
+#define OPCHK(x)                                                  \
+  do {                                                            \
+    hipError_t _e = (x);                                          \
+    if (_e != hipSuccess) return op_err(BX_ERR_HIP, hipGetErrorString(_e)); \
+  } while (0)
+
+__global__ void iou_kernel(const double* a, int na, const double* b, int nb, double* out) {
+  const size_t n = (size_t)na * nb;
+  for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n;
+       k += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(k / nb), j = (int)(k % nb);
+    out[k] = iou_pair(a + 4 * i, b + 4 * j);
+  }
+}
+
+__global__ void fuse_kernel(double* c, int nr, int nc, const double* conf) {
+  const size_t n = (size_t)nr * nc;
+  for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n;
+       k += (size_t)gridDim.x * blockDim.x)
+    c[k] = fuse_one(c[k], conf[k % nc]);
+}
+
+// per-row float32 norm (numpy pairwise) and the fp64 norm cdist computes of the normalised row
+__global__ void row_norms_kernel(const float* x, int n, int f, float* dn, double* nrm) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* r = x + (size_t)i * f;
+  float d = sqrtf(np_pairwise_sumsq_f32(r, f)) + 1e-8f;
+  struct V {
+    const float* p;
+    float d;
+    __device__ double operator()(int k) const { return (double)(p[k] / d); }
+  } A{r, d};
+  dn[i] = d;
+  nrm[i] = sqrt(dot2(A, A, f));
+}
+
+__global__ void cosine_kernel(const float* a, int na, const float* b, int nb, int f,
+                              const float* adn, const double* anr, const float* bdn,
+                              const double* bnr, double* out) {
+  const size_t n = (size_t)na * nb;
+  for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n;
+       k += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(k / nb), j = (int)(k % nb);
+    struct V {
+      const float* p;
+      float d;
+      __device__ double operator()(int q) const { return (double)(p[q] / d); }
+    } A{a + (size_t)i * f, adn[i]}, B{b + (size_t)j * f, bdn[j]};
+    double c = dot2(A, B, f) / (anr[i] * bnr[j]);
+    if (fabs(c) > 1.0) c = copysign(1.0, c);
+    double d = 1.0 - c;
+    out[k] = d < 0.0 ? 0.0 : d;
+  }
+}
+
+__global__ void kf_init_kernel(int kind, int n, const double* meas, double* mean, double* cov) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  kf_initiate(kind, meas + 4 * t, mean + 8 * t, cov + 64 * t);
+}
+__global__ void kf_predict_kernel(int kind, int n, double* mean, double* cov) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  double m[8], c[64];
+  for (int k = 0; k < 8; k++) m[k] = mean[8 * t + k];
+  for (int k = 0; k < 64; k++) c[k] = cov[64 * t + k];
+  kf_predict_soa(kind, m, c, 1);
+  for (int k = 0; k < 8; k++) mean[8 * t + k] = m[k];
+  for (int k = 0; k < 64; k++) cov[64 * t + k] = c[k];
+}
+__global__ void kf_update_kernel(int kind, int n, double* mean, double* cov, const double* z,
+                                 const double* conf) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  kf_update_soa(kind, mean + 8 * t, cov + 64 * t, 1, z + 4 * t, conf ? conf[t] : 0.0);
+}
+__global__ void kf_gate_kernel(int kind, int n, const double* mean, const double* cov,
+                               const double* z, int nz, double* out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  kf_gating_soa(kind, mean + 8 * t, cov + 64 * t, 1, z, nz, out + (size_t)t * nz);
+}
+
+// One dense problem: CSR of admissible edges (cost < thresh) in LDS, then the wave LAP.
+__global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int nr, int nc,
+                                                       double thr, int elds, uint16_t* gcol,
+                                                       double* gcost, int32_t* x, int32_t* y) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    unsigned char* p = smem + o;
+    o += (bytes + 15) & ~size_t(15);
+    return p;
+  };
+  double* u = (double*)take(8 * nr);
+  double* v = (double*)take(8 * nc);
+  double* spc = (double*)take(8 * nc);
+  double* ecost = (double*)take(8 * elds);
+  int* rowptr = (int*)take(4 * (nr + 1));
+  int16_t* c4r = (int16_t*)take(2 * nr);
+  uint16_t* srl = (uint16_t*)take(2 * nr);
+  int16_t* r4c = (int16_t*)take(2 * nc);
+  int16_t* path = (int16_t*)take(2 * nc);
+  uint16_t* touch = (uint16_t*)take(2 * nc);
+  uint16_t* ecol = (uint16_t*)take(2 * elds);
+  uint8_t* colf = (uint8_t*)take(nc);
+  const int tid = threadIdx.x;
+  for (int i = tid; i < nr; i += WG) {
+    int cnt = 0;
+    for (int j = 0; j < nc; j++) cnt += cost[(size_t)i * nc + j] < thr;
+    rowptr[i] = cnt;
+  }
+  __syncthreads();
+  wave0_exclusive_scan(rowptr, nr);
+  __syncthreads();
+  for (int i = tid; i < nr; i += WG) {
+    int e = rowptr[i];
+    for (int j = 0; j < nc; j++) {
+      double c = cost[(size_t)i * nc + j];
+      if (!(c < thr)) continue;
+      if (e < elds) { ecol[e] = (uint16_t)j; ecost[e] = c; }
+      else { gcol[e - elds] = (uint16_t)j; gcost[e - elds] = c; }
+      e++;
+    }
+  }
+  __syncthreads();
+  LapWS W;
+  W.row_ptr = rowptr; W.ecol = ecol; W.ecost = ecost; W.gcol = gcol; W.gcost = gcost;
+  W.elds = elds; W.col4row = c4r; W.row4col = r4c; W.u = u; W.v = v; W.spc = spc;
+  W.path = path; W.colflag = colf; W.touched = touch; W.srlist = srl;
+  if (wave_id() == 0) lap_solve_wave(nr, nc, thr, W);
+  __syncthreads();
+  for (int i = tid; i < nr; i += WG) x[i] = c4r[i];
+  for (int j = tid; j < nc; j += WG) y[j] = r4c[j];
+}
+
+int grid_for(size_t n) {
+  size_t g = (n + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+
+}  // namespace
+
+extern "C" {
+
+int bx_iou_batch(const double* a, int na, const double* b, int nb, double* out, void* stream) {
+  if (na < 0 || nb < 0) return op_err(BX_ERR_INVALID, "negative size");
+  if (!na || !nb) return BX_OK;
+  hipLaunchKernelGGL(iou_kernel, dim3(grid_for((size_t)na * nb)), dim3(256), 0,
+                     (hipStream_t)stream, a, na, b, nb, out);
+  OPCHK(hipGetLastError());
+  return BX_OK;
+}
+
+int bx_fuse_score(double* cost, int nr, int nc, const double* confs, void* stream) {
+  if (nr < 0 || nc < 0) return op_err(BX_ERR_INVALID, "negative size");
+  if (!nr || !nc) return BX_OK;
+  hipLaunchKernelGGL(fuse_kernel, dim3(grid_for((size_t)nr * nc)), dim3(256), 0,
+                     (hipStream_t)stream, cost, nr, nc, confs);
+  OPCHK(hipGetLastError());
+  return BX_OK;
+}
+
+int bx_embedding_distance(const float* trk, int nt, const float* det, int nd, int f, double* out,
+                          void* stream) {
+  if (nt < 0 || nd < 0 || f <= 0) return op_err(BX_ERR_INVALID, "bad sizes");
+  if (!nt || !nd) return BX_OK;
+  hipStream_t st = (hipStream_t)stream;
+  void* ws = nullptr;
+  const size_t bytes = (size_t)(nt + nd) * (sizeof(float) + sizeof(double)) + 64;
+  OPCHK(hipMallocAsync(&ws, bytes, st));
+  float* adn = (float*)ws;
+  float* bdn = adn + nt;
+  double* anr = (double*)(((uintptr_t)(bdn + nd) + 15) & ~uintptr_t(15));
+  double* bnr = anr + nt;
+  hipLaunchKernelGGL(row_norms_kernel, dim3((nt + 127) / 128), dim3(128), 0, st, trk, nt, f, adn,
+                     anr);
+  hipLaunchKernelGGL(row_norms_kernel, dim3((nd + 127) / 128), dim3(128), 0, st, det, nd, f, bdn,
+                     bnr);
+  hipLaunchKernelGGL(cosine_kernel, dim3(grid_for((size_t)nt * nd)), dim3(256), 0, st, trk, nt,
+                     det, nd, f, adn, anr, bdn, bnr, out);
+  OPCHK(hipGetLastError());
+  OPCHK(hipFreeAsync(ws, st));
+  return BX_OK;
+}
+
+int bx_kf_initiate(int kind, int n, const double* meas, double* mean, double* cov, void* stream) {
+  if ((kind != 0 && kind != 1) || n < 0) return op_err(BX_ERR_INVALID, "bad kind/size");
+  if (!n) return BX_OK;
+  hipLaunchKernelGGL(kf_init_kernel, dim3((n + 127) / 128), dim3(128), 0, (hipStream_t)stream,
+                     kind, n, meas, mean, cov);
+  OPCHK(hipGetLastError());
+  return BX_OK;
+}
+
+int bx_kf_multi_predict(int kind, int n, double* mean, double* cov, void* stream) {
+  if ((kind != 0 && kind != 1) || n < 0) return op_err(BX_ERR_INVALID, "bad kind/size");
+  if (!n) return BX_OK;
+  hipLaunchKernelGGL(kf_predict_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream,
+                     kind, n, mean, cov);
+  OPCHK(hipGetLastError());
+  return BX_OK;
+}
+
+int bx_kf_update(int kind, int n, double* mean, double* cov, const double* z, const double* conf,
+                 void* stream) {
+  if ((kind != 0 && kind != 1) || n < 0) return op_err(BX_ERR_INVALID, "bad kind/size");
+  if (!n) return BX_OK;
+  hipLaunchKernelGGL(kf_update_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream,
+                     kind, n, mean, cov, z, conf);
+  OPCHK(hipGetLastError());
+  return BX_OK;
+}
+
+int bx_kf_gating_distance(int kind, int n, const double* mean, const double* cov,
+                          const double* z, int nz, double* out, void* stream) {
+  if ((kind != 0 && kind != 1) || n < 0 || nz < 0) return op_err(BX_ERR_INVALID, "bad args");
+  if (!n || !nz) return BX_OK;
+  hipLaunchKernelGGL(kf_gate_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, kind,
+                     n, mean, cov, z, nz, out);
+  OPCHK(hipGetLastError());
+  return BX_OK;
+}
+
+int bx_linear_assignment(const double* cost, int nr, int nc, double thresh, int32_t* x,
+                         int32_t* y, void* stream) {
+  if (nr < 0 || nc < 0 || nr > 8192 || nc > 8192)
+    return op_err(BX_ERR_INVALID, "nr/nc out of range (0..8192)");
+  hipStream_t st = (hipStream_t)stream;
+  if (!nr || !nc) {
+    if (nr) OPCHK(hipMemsetAsync(x, 0xff, sizeof(int32_t) * nr, st));
+    if (nc) OPCHK(hipMemsetAsync(y, 0xff, sizeof(int32_t) * nc, st));
+    return BX_OK;
+  }
+  int elds = 2048;
+  auto lds_for = [&](int e) {
+    size_t o = 0;
+    auto take = [&](size_t b) { o += (b + 15) & ~size_t(15); };
+    take(8 * nr); take(8 * nc); take(8 * nc); take(8 * e); take(4 * (nr + 1)); take(2 * nr);
+    take(2 * nr); take(2 * nc); take(2 * nc); take(2 * nc); take(2 * e); take(nc);
+    return o;
+  };
+  while (elds > 0 && lds_for(elds) > 160 * 1024) elds /= 2;
+  const size_t lds = lds_for(elds);
+  if (lds > 160 * 1024) return op_err(BX_ERR_INVALID, "problem too large for LDS");
+  void* ws = nullptr;
+  const size_t ne = (size_t)nr * nc;
+  OPCHK(hipMallocAsync(&ws, ne * 10 + 64, st));
+  double* gcost = (double*)ws;
+  uint16_t* gcol = (uint16_t*)(gcost + ne);
+  if (lds > 65536)
+    OPCHK(hipFuncSetAttribute((const void*)lap_dense_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(lap_dense_kernel, dim3(1), dim3(WG), lds, st, cost, nr, nc, thresh, elds,
+                     gcol, gcost, x, y);
+  OPCHK(hipGetLastError());
+  OPCHK(hipFreeAsync(ws, st));
+  return BX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,174 @@
+"""Python handle over the native engine (``bx_engine_*`` in include/bxassoc.h).
+
+An ``Engine`` holds ``n_seq`` independent sequences resident in HBM.  ``step`` advances one frame
+of a contiguous range of sequences in a single kernel launch (device tensors in, device tensors
+out); ``update_host`` is the single-sequence numpy path the drop-in tracker classes use.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+
+KINDS = {"bytetrack": 0, "botsort": 1}
+
+
+@dataclass
+class EngineParams:
+    """Tracker parameters with the reference constructors' defaults."""
+
+    # ByteTrack (bytetrack.py:132-140)
+    min_conf: float = 0.1
+    track_thresh: float = 0.45
+    match_thresh: float = 0.8
+    track_buffer: int = 25
+    frame_rate: int = 30
+    # BoT-SORT (botsort.py:49-66)
+    track_high_thresh: float = 0.5
+    track_low_thresh: float = 0.1
+    new_track_thresh: float = 0.6
+    proximity_thresh: float = 0.5
+    appearance_thresh: float = 0.25
+    fuse_first_associate: bool = False
+    with_reid: bool = True
+
+
+class Engine:
+    def __init__(self, kind: str, n_seq: int = 1, track_cap: int = 1024, det_cap: int = 1024,
+                 emb_dim: int = 0, emb_f64: bool = False, params: EngineParams | None = None):
+        if kind not in KINDS:
+            raise KeyError(kind)
+        p = params or EngineParams()
+        self.kind, self.n_seq, self.track_cap, self.det_cap = kind, n_seq, track_cap, det_cap
+        self.emb_dim, self.emb_f64, self.params = emb_dim, bool(emb_f64), p
+        self.with_reid = kind == "botsort" and p.with_reid
+        cfg = N.BxConfig(
+            kind=KINDS[kind], n_seq=n_seq, track_cap=track_cap, det_cap=det_cap,
+            emb_dim=emb_dim if self.with_reid else 0, emb_f64=int(emb_f64),
+            min_conf=p.min_conf, track_thresh=p.track_thresh, match_thresh=p.match_thresh,
+            track_buffer=int(p.track_buffer), frame_rate=int(p.frame_rate),
+            track_high_thresh=p.track_high_thresh, track_low_thresh=p.track_low_thresh,
+            new_track_thresh=p.new_track_thresh, proximity_thresh=p.proximity_thresh,
+            appearance_thresh=p.appearance_thresh,
+            fuse_first_associate=int(bool(p.fuse_first_associate)), with_reid=int(self.with_reid))
+        self._L = N.load()
+        h = C.c_void_p()
+        N.check(self._L.bx_engine_create(C.byref(cfg), C.byref(h)), "bx_engine_create")
+        self._h = h
+
+    # ----------------------------------------------------------------------------- lifecycle
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.bx_engine_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, seq0: int = 0, nseq: int | None = None, stream: int | None = None):
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        N.check(self._L.bx_engine_reset(self._h, seq0, nseq, stream), "bx_engine_reset")
+
+    # ------------------------------------------------------------------------------- frames
+    def step(self, dets, det_off, embs=None, warps=None, out=None, out_count=None, seq0: int = 0,
+             nseq: int | None = None, stream=None):
+        """One frame for sequences [seq0, seq0+nseq): torch device tensors (or raw pointers).
+
+        dets [sum N,6] float32, det_off [nseq+1] int32, embs [sum N,F] float32/64 or None,
+        warps [nseq,6] float64 or None, out [sum N,8] float64, out_count [nseq] int32.
+        """
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        ptr = _ptr
+        if stream is None:
+            stream = _current_stream()
+        N.check(self._L.bx_engine_step(self._h, seq0, nseq, ptr(dets), ptr(det_off), ptr(embs),
+                                       ptr(warps), ptr(out), ptr(out_count), stream),
+                "bx_engine_step")
+
+    def update_host(self, seq: int, dets: np.ndarray, embs: np.ndarray | None = None,
+                    warp: np.ndarray | None = None) -> np.ndarray:
+        """One frame of one sequence from host arrays; returns float64 [M, 8]."""
+        d = np.ascontiguousarray(dets, dtype=np.float32).reshape(-1, 6)
+        n = d.shape[0]
+        e = None
+        if self.with_reid and n:
+            if embs is None:
+                raise ValueError("BoT-SORT with_reid needs embeddings (ReID inference is outside "
+                                 "the association engine)")
+            e = np.ascontiguousarray(embs, dtype=np.float64 if self.emb_f64 else np.float32)
+            if e.shape != (n, self.emb_dim):
+                raise ValueError(f"embs shape {e.shape} != ({n}, {self.emb_dim})")
+        w = None if warp is None else np.ascontiguousarray(warp, np.float64).reshape(6)
+        out = np.empty((max(n, 1), 8), np.float64)
+        m = C.c_int(0)
+        N.check(self._L.bx_engine_update_host(
+            self._h, seq, d.ctypes.data if n else None, n,
+            e.ctypes.data if e is not None else None, w.ctypes.data if w is not None else None,
+            out.ctypes.data, C.byref(m), None), "bx_engine_update_host")
+        return out[: m.value].copy()
+
+    # ---------------------------------------------------------------------------- state I/O
+    def status(self) -> int:
+        s = C.c_int(0)
+        N.check(self._L.bx_engine_status(self._h, C.byref(s)), "bx_engine_status")
+        return s.value
+
+    def counters(self, seq: int = 0) -> dict:
+        fc, idc, na, nl = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        N.check(self._L.bx_engine_counters_host(self._h, seq, C.byref(fc), C.byref(idc),
+                                                C.byref(na), C.byref(nl)), "counters")
+        return {"frame_count": fc.value, "id_count": idc.value, "n_active": na.value,
+                "n_lost": nl.value}
+
+    def set_id_count(self, seq: int, value: int):
+        N.check(self._L.bx_engine_set_id_count(self._h, seq, int(value), None), "set_id_count")
+
+    def tracks(self, seq: int = 0) -> dict:
+        """Host snapshot of the live tracks: active list then lost list."""
+        cap = self.track_cap
+        ids = np.zeros(cap, np.int32)
+        st = np.zeros(cap, np.int32)
+        act = np.zeros(cap, np.int32)
+        fid = np.zeros(cap, np.int32)
+        sf = np.zeros(cap, np.int32)
+        mean = np.zeros((cap, 8))
+        cov = np.zeros((cap, 8, 8))
+        na, nl = C.c_int(), C.c_int()
+        N.check(self._L.bx_engine_tracks_host(
+            self._h, seq, cap, ids.ctypes.data, st.ctypes.data, act.ctypes.data, fid.ctypes.data,
+            sf.ctypes.data, mean.ctypes.data, cov.ctypes.data, C.byref(na), C.byref(nl)),
+            "tracks")
+        n = na.value + nl.value
+        return {"n_active": na.value, "n_lost": nl.value, "id": ids[:n], "state": st[:n],
+                "is_activated": act[:n].astype(bool), "frame_id": fid[:n],
+                "start_frame": sf[:n], "mean": mean[:n], "covariance": cov[:n]}
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError(type(x))
+
+
+def _current_stream():
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            return torch.cuda.current_stream().cuda_stream
+    except Exception:
+        pass
+    return None

@@ -94,6 +94,73 @@ class SyntheticScene:
         return dets, embs, ids
 
 
+class TorchSceneBatch:
+    """The ``grid`` scene process for ``n_seq`` independent sequences, generated on the GPU.
+
+    Same geometry, motion, detection probability, jitter, confidence and embedding model as
+    ``SyntheticScene(layout="grid")``, but drawn with torch's device RNG so that thousands of
+    sequences × frames can be staged in HBM before a timed region (numbers differ from the numpy
+    generator; the distribution does not).  ``frame(t)`` returns packed
+    ``(dets[sum N,6] f32, det_off[n_seq+1] i32, embs[sum N,F] f32 | None)`` on ``device``.
+    """
+
+    def __init__(self, n_seq, n_obj, emb_dim=0, seed=0, device="cuda", p_det=0.5,
+                 conf_lo=0.65, conf_hi=1.0, jitter=0.5, width=1920.0, height=1080.0):
+        import torch
+
+        self.torch, self.n_seq, self.n_obj, self.emb_dim = torch, n_seq, n_obj, emb_dim
+        self.device, self.p_det, self.conf = device, p_det, (conf_lo, conf_hi)
+        self.jitter = jitter
+        g = torch.Generator(device=device)
+        g.manual_seed(int(seed) * 7919 + 17)
+        self.g = g
+        cols = max(1, math.ceil(math.sqrt(n_obj * width / height)))
+        rows = max(1, math.ceil(n_obj / cols))
+        cw, ch = width / cols, height / rows
+        idx = torch.arange(n_obj, device=device, dtype=torch.float64)
+        cx = ((idx % cols) + 0.5) * cw
+        cy = torch.div(idx, cols, rounding_mode="floor").add(0.5) * ch
+        u = lambda *s: torch.rand(*s, generator=g, device=device, dtype=torch.float64)  # noqa
+        w = 0.45 * cw * (0.8 + 0.4 * u(n_seq, n_obj))
+        h = 0.80 * ch * (0.8 + 0.4 * u(n_seq, n_obj))
+        self.c0 = torch.stack([cx.expand(n_seq, n_obj), cy.expand(n_seq, n_obj)], -1)
+        self.half = torch.stack([w, h], -1) * 0.5
+        self.vel = u(n_seq, n_obj, 2) - 0.5
+        if emb_dim:
+            b = torch.randn(n_seq, n_obj, emb_dim, generator=g, device=device)
+            self.base = b / b.norm(dim=-1, keepdim=True)
+
+    def frame(self, t):
+        torch = self.torch
+        g, dev, S, n = self.g, self.device, self.n_seq, self.n_obj
+        seen = torch.rand(S, n, generator=g, device=dev) < self.p_det
+        # random order of the detected objects inside each sequence
+        key = torch.rand(S, n, generator=g, device=dev) + (~seen).float() * 2.0
+        order = key.argsort(dim=1)
+        counts = seen.sum(1)
+        sel = torch.arange(n, device=dev).expand(S, n) < counts[:, None]
+        sidx = torch.arange(S, device=dev)[:, None].expand(S, n)[sel]
+        oidx = order[sel]
+        c = self.c0[sidx, oidx] + self.vel[sidx, oidx] * float(t)
+        hf = self.half[sidx, oidx]
+        m = sidx.numel()
+        box = torch.cat([c - hf, c + hf], 1) + self.jitter * torch.randn(
+            m, 4, generator=g, device=dev, dtype=torch.float64)
+        lo, hi = self.conf
+        conf = lo + (hi - lo) * torch.rand(m, generator=g, device=dev, dtype=torch.float64)
+        dets = torch.zeros(m, 6, device=dev, dtype=torch.float32)
+        dets[:, :4] = box.float()
+        dets[:, 4] = conf.float()
+        off = torch.zeros(S + 1, dtype=torch.int32, device=dev)
+        off[1:] = counts.cumsum(0).to(torch.int32)
+        embs = None
+        if self.emb_dim:
+            e = self.base[sidx, oidx] + 0.1 * torch.randn(
+                m, self.emb_dim, generator=g, device=dev) / math.sqrt(self.emb_dim)
+            embs = (e / e.norm(dim=-1, keepdim=True)).contiguous()
+        return dets, off, embs
+
+
 def load_mot_dets(path):
     """MOT17 ``det.txt`` (``frame,-1,x,y,w,h,conf``) → {frame: dets[N,6] xyxy,conf,cls=0}.
 

@@ -1,0 +1,123 @@
+"""Drop-in BaseTracker: the reference's plugin contract (trackers/basetracker.py:12-226) with the
+per-frame numerics delegated to the MI355X engine.
+
+Kept byte-compatible with the reference: ``update(dets, img, embs=None)`` → ``np.ndarray`` rows
+``[x1, y1, x2, y2, id, conf, cls, det_ind]``; the same input unwrapping (``.data``/memoryview →
+float32, basetracker.py:122-128 — which rounds every det to float32, including for plain numpy
+arrays since they expose ``.data``), the same AssertionErrors (check_inputs, :203-226), the same
+empty-input handling (:162-163) and the first-frame latch of image size.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+class TrackView:
+    """Read-only host view of one engine track (what ``active_tracks`` entries expose)."""
+
+    __slots__ = ("id", "state", "is_activated", "frame_id", "start_frame", "mean", "covariance",
+                 "_box_fn")
+
+    def __init__(self, tid, state, act, fid, sf, mean, cov, box_fn):
+        self.id, self.state, self.is_activated = int(tid), int(state), bool(act)
+        self.frame_id, self.start_frame = int(fid), int(sf)
+        self.mean, self.covariance, self._box_fn = mean, cov, box_fn
+
+    @property
+    def end_frame(self):
+        return self.frame_id
+
+    @property
+    def xyxy(self):
+        return self._box_fn(self.mean)
+
+    def __repr__(self):
+        return f"TrackView(id={self.id}, state={self.state}, activated={self.is_activated})"
+
+
+class BaseTracker:
+    def __init__(self, det_thresh: float = 0.3, max_age: int = 30, min_hits: int = 3,
+                 iou_threshold: float = 0.3, max_obs: int = 50, nr_classes: int = 80,
+                 per_class: bool = False, asso_func: str = "iou", is_obb: bool = False):
+        self.det_thresh = det_thresh
+        self.max_age = max_age
+        self.max_obs = max_obs
+        self.min_hits = min_hits
+        self.per_class = per_class
+        self.nr_classes = nr_classes
+        self.iou_threshold = iou_threshold
+        self.last_emb_size = None
+        self.asso_func_name = asso_func + "_obb" if is_obb else asso_func
+        self.is_obb = is_obb
+        self.frame_count = 0
+        self.per_class_active_tracks = None
+        self._first_frame_processed = False
+        self._first_dets_processed = False
+        if self.max_age >= self.max_obs:
+            self.max_obs = self.max_age + 5
+        if per_class:
+            # The reference swaps only `active_tracks` per class while lost/removed lists stay
+            # shared (basetracker.py:154-201); that mode is not yet on the engine.
+            raise NotImplementedError("per_class tracking is not implemented by boxmot_amd yet")
+
+    # -------------------------------------------------------------------- reference decorators
+    @staticmethod
+    def setup_decorator(method):
+        def wrapper(self, *args, **kwargs):
+            dets = args[0]
+            img = args[1] if len(args) > 1 else kwargs.get("img")
+            if hasattr(dets, "data"):
+                dets = dets.data
+            if isinstance(dets, memoryview):
+                dets = np.array(dets, dtype=np.float32)
+            if not self._first_dets_processed and dets is not None:
+                if dets.ndim == 2 and dets.shape[1] == 6:
+                    self.is_obb = False
+                    self._first_dets_processed = True
+                elif dets.ndim == 2 and dets.shape[1] == 7:
+                    self.is_obb = True
+                    self._first_dets_processed = True
+            if not self._first_frame_processed and img is not None:
+                self.h, self.w = img.shape[0:2]
+                self._first_frame_processed = True
+            rest = args[2:]
+            if "embs" in kwargs:
+                rest = (kwargs.pop("embs"),)
+            kwargs.pop("img", None)
+            return method(self, dets, img, *rest, **kwargs)
+
+        return wrapper
+
+    @staticmethod
+    def per_class_decorator(update_method):
+        def wrapper(self, dets, img, embs=None):
+            if dets is None or len(dets) == 0:
+                dets = np.empty((0, 6))
+            return update_method(self, dets=dets, img=img, embs=embs)
+
+        return wrapper
+
+    def check_inputs(self, dets, img, embs=None):
+        assert isinstance(dets, np.ndarray), (
+            f"Unsupported 'dets' input format '{type(dets)}', valid format is np.ndarray")
+        assert isinstance(img, np.ndarray), (
+            f"Unsupported 'img_numpy' input format '{type(img)}', valid format is np.ndarray")
+        assert len(dets.shape) == 2, "Unsupported 'dets' dimensions, valid number of dimensions is two"
+        if embs is not None:
+            assert dets.shape[0] == embs.shape[0], "Missmatch between detections and embeddings sizes"
+        if self.is_obb:
+            assert dets.shape[1] == 7, "Unsupported 'dets' 2nd dimension lenght, valid lenghts is 6 (cx,cy,w,h,angle,conf,cls)"
+        else:
+            assert dets.shape[1] == 6, "Unsupported 'dets' 2nd dimension lenght, valid lenghts is 6 (x1,y1,x2,y2,conf,cls)"
+
+    def update(self, dets: np.ndarray, img: np.ndarray, embs: np.ndarray = None) -> np.ndarray:
+        raise NotImplementedError
+
+    # ------------------------------------------------------------------------ engine helpers
+    def _track_views(self, engine, box_fn):
+        snap = engine.tracks(0)
+        views = [TrackView(snap["id"][k], snap["state"][k], snap["is_activated"][k],
+                           snap["frame_id"][k], snap["start_frame"][k], snap["mean"][k],
+                           snap["covariance"][k], box_fn)
+                 for k in range(snap["id"].shape[0])]
+        return views[: snap["n_active"]], views[snap["n_active"]:]
