@@ -24,7 +24,7 @@ class EngineParams:
     min_conf: float = 0.1
     track_thresh: float = 0.45
     match_thresh: float = 0.8
-    track_buffer: int = 25
+    track_buffer: int | None = None  # None → the tracker's own default: 25 ByteTrack, 30 BoT-SORT
     frame_rate: int = 30
     # BoT-SORT (botsort.py:49-66)
     track_high_thresh: float = 0.5
@@ -37,11 +37,13 @@ class EngineParams:
 
 
 class Engine:
-    def __init__(self, kind: str, n_seq: int = 1, track_cap: int = 1024, det_cap: int = 1024,
+    def __init__(self, kind: str, n_seq: int = 1, track_cap: int = 1024, det_cap: int = 512,
                  emb_dim: int = 0, emb_f64: bool = False, params: EngineParams | None = None):
         if kind not in KINDS:
             raise KeyError(kind)
         p = params or EngineParams()
+        if p.track_buffer is None:
+            p = EngineParams(**{**p.__dict__, "track_buffer": 25 if kind == "bytetrack" else 30})
         self.kind, self.n_seq, self.track_cap, self.det_cap = kind, n_seq, track_cap, det_cap
         self.emb_dim, self.emb_f64, self.params = emb_dim, bool(emb_f64), p
         self.with_reid = kind == "botsort" and p.with_reid
