@@ -105,7 +105,8 @@ def load(path: Path | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # BX_LIB_PATH: load a diagnostic build (e.g. the -DBX_PHASE_TIMING stamps library)
+    p = Path(path) if path else Path(os.environ.get("BX_LIB_PATH", LIB_PATH))
     if not p.exists():
         raise NativeUnavailable(
             f"{p} is missing: build the HIP extension first (python -c 'import __graft_entry__ "

@@ -282,13 +282,59 @@ __device__ inline double dot2(const A& a, const B& b, int n) {
   return s;
 }
 
-// np.linalg.norm of a 1-D feature (BLAS dot; order fixed as the oracle's: sequential fp64).
+// np.linalg.norm of a 1-D feature is a BLAS dot with an unpinned order; the engine fixes the
+// "wave order" (restated in oracle/bxo_track.c vnorm): lane l accumulates x[l], x[l+64], ...
+// sequentially in fp64, then an xor butterfly d = 32..1 (commutative: every lane ends with the
+// same bits).  Called by all 64 lanes of a wave.
 template <typename FT>
-__device__ inline FT blas_norm(const FT* x, int n) {
+__device__ inline double wave_sumsq(const FT* x, int n) {
+  const int lane = threadIdx.x & 63;
   double s = 0.0;
-  for (int k = 0; k < n; k++) { double v = (double)x[k]; s += v * v; }
+  for (int k = lane; k < n; k += 64) { double v = (double)x[k]; s += v * v; }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+  return s;
+}
+template <typename FT>
+__device__ inline FT wave_norm(const FT* x, int n) {
+  double s = wave_sumsq(x, n);
   if constexpr (sizeof(FT) == 4) return sqrtf((float)s);
   else return sqrt(s);
+}
+
+// numpy float32 pairwise sum of squares, wave-parallel and bit-identical to the sequential
+// recursion when n = 128 * 2^m (every split lands on a 128-element leaf): accumulator a (leaf
+// a/8, slot a%8) sums x[128*(a/8) + 8i + a%8]^2 over i in order; slots and leaves then combine
+// as balanced binary trees = xor butterflies.  Other n fall back to one lane's sequential walk.
+template <typename XT>
+__device__ inline float np_sumsq_wave(const XT* x, int n) {
+  const int lane = threadIdx.x & 63;
+  const int nleaf = n >> 7;
+  if ((n & 127) == 0 && nleaf > 0 && (nleaf & (nleaf - 1)) == 0 && nleaf <= 32) {
+    const int nacc = nleaf * 8;            // 8 .. 256 accumulators
+    const int regs = nacc > 64 ? nacc / 64 : 1;
+    float part[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      part[r] = 0.0f;
+      const int a = lane + 64 * r;
+      if (r < regs && a < nacc) {
+        const XT* p = x + 128 * (a >> 3) + (a & 7);
+        float acc = (float)p[0] * (float)p[0];
+        for (int i = 1; i < 16; i++) { float v = (float)p[8 * i]; acc += v * v; }
+        part[r] = acc;
+      }
+      const int width = nacc < 64 ? nacc : 64;
+      for (int d = 1; d < width; d <<= 1) part[r] += __shfl_xor(part[r], d);
+    }
+    // registers hold consecutive blocks of 8 leaves; combine them as a balanced tree
+    float res = regs == 1 ? part[0]
+                : regs == 2 ? part[0] + part[1]
+                            : (part[0] + part[1]) + (part[2] + part[3]);
+    return __shfl(res, 0);
+  }
+  float s = np_pairwise_sumsq_f32(x, n);
+  return __shfl(s, 0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -323,6 +369,7 @@ __device__ inline int block_compact(int n, P pred, E emit, int* tmp) {
     if (f) emit(k, base + pos);
     base += tot;
   }
+  __syncthreads();  // emitted entries are read by other threads right after
   return base;
 }
 
@@ -369,6 +416,7 @@ struct LapWS {
   uint8_t* colflag;       // [C] bit0 = in SC, bit1 = touched
   uint16_t* touched;      // [C] touched column list
   uint16_t* srlist;       // [R] rows visited (SR) except the root
+  int* coldeg;            // [C] finite-edge degree per column (single-edge-component fast path)
 };
 
 __device__ __forceinline__ void lap_edge(const LapWS& w, int e, int& col, double& cost) {
@@ -393,11 +441,42 @@ __device__ inline void lap_solve_wave(int R, int C, double L, const LapWS& w) {
   for (int k = lane; k < C; k += WAVE) {
     w.row4col[k] = -1; w.v[k] = 0.0; w.spc[k] = INF; w.colflag[k] = 0;
   }
+  // Single-edge components (a row whose only finite edge goes to a column no other row can
+  // reach) are matched directly: that is exactly the path SSP would find for them (gain L-c>0,
+  // potentials u = c-L, v = 0), and no other row can ever touch that row or column.
+  for (int k = lane; k < C; k += WAVE) w.coldeg[k] = 0;
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const int E = w.row_ptr[R];
+  for (int e = lane; e < E; e += WAVE) {
+    int j;
+    double c;
+    lap_edge(w, e, j, c);
+    if (c < INF) atomicAdd(&w.coldeg[j], 1);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  for (int r = lane; r < R; r += WAVE) {
+    int nf = 0, jj = -1;
+    double cc = 0.0;
+    for (int e = w.row_ptr[r]; e < w.row_ptr[r + 1]; e++) {
+      int j;
+      double c;
+      lap_edge(w, e, j, c);
+      if (c < INF) { nf++; jj = j; cc = c; }
+    }
+    if (nf == 1 && w.coldeg[jj] == 1) {
+      w.col4row[r] = (int16_t)jj;
+      w.row4col[jj] = (int16_t)r;
+      w.u[r] = cc - L;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   for (int root = 0; root < R; root++) {
     const int rb = w.row_ptr[root], re = w.row_ptr[root + 1];
     if (rb == re) continue;  // no admissible edge: stays unmatched (its dummy)
+    if (w.col4row[root] >= 0) continue;  // matched by the single-edge fast path
     double minVal = 0.0;
     int i = root;
     int ntouched = 0, nsr = 0;

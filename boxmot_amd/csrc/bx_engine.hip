@@ -26,7 +26,58 @@ using namespace bx;
 namespace {
 
 constexpr int CLS_HIST = 8;  // BoT-SORT per-track class-history entries (update_cls)
-constexpr int ELDS_DEFAULT = 2048;
+constexpr int ELDS_DEFAULT = 1024;  // LAP edges kept in LDS; the rest spill to global scratch
+constexpr int REG_F = 512;   // feature rows up to this width live in registers: 8 per lane
+constexpr int REG_EPL = REG_F / 64;
+
+// A feature row held by one wave, element q = lane + 64 r in v[r] (F <= REG_F).
+template <typename FT>
+struct RegRow {
+  FT v[REG_EPL];
+  __device__ void load(const FT* p, int F) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int r = 0; r < REG_EPL; r++) {
+      const int q = lane + 64 * r;
+      v[r] = q < F ? p[q] : FT(0);
+    }
+  }
+  template <typename OT>
+  __device__ void store(OT* p, int F) const {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int r = 0; r < REG_EPL; r++) {
+      const int q = lane + 64 * r;
+      if (q < F) p[q] = (OT)v[r];
+    }
+  }
+  // the engine's fixed BLAS-dot order (see wave_sumsq): lane-strided sequential, xor butterfly
+  __device__ FT norm(int F) const {
+    const int lane = threadIdx.x & 63;
+    double s = 0.0;
+#pragma unroll
+    for (int r = 0; r < REG_EPL; r++)
+      if (lane + 64 * r < F) { double d = (double)v[r]; s += d * d; }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+    if constexpr (sizeof(FT) == 4) return sqrtf((float)s);
+    else return sqrt(s);
+  }
+  __device__ void div(FT n) {
+#pragma unroll
+    for (int r = 0; r < REG_EPL; r++) v[r] = v[r] / n;
+  }
+  // numpy float32 norm of the float32-cast row (+1e-8 as embedding_distance adds it), staged
+  // through this wave's LDS row so lanes can read numpy's accumulator layout
+  __device__ float np_dn(float* wbuf, int F) const {
+    store(wbuf, F);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    float dn = sqrtf(np_sumsq_wave((const float*)wbuf, F)) + 1e-8f;
+    __builtin_amdgcn_wave_barrier();
+    return dn;
+  }
+};
 
 thread_local std::string g_err;
 int set_err(int code, const std::string& msg) {
@@ -63,8 +114,24 @@ struct Dev {
   uint16_t* gcol;     // [S][T*D] LAP edge overflow
   double* gcost;      // [S][T*D]
   void* df2;          // [S][D][F] frame scratch: detection features after STrack.__init__
+  float* dB;          // [S][D][F] frame scratch: det rows as embedding_distance normalises them
+  float* tA;          // [S][T][F] frame scratch: track rows as embedding_distance normalises them
   int* status;        // [1] latched engine status
+  unsigned long long* dbg;  // [S][32] phase stamps (diagnostic builds only, else null)
 };
+
+// Diagnostic phase stamps (build with -DBX_PHASE_TIMING; never in the shipped library).
+#ifdef BX_PHASE_TIMING
+#define BX_STAMP(k)                                                                   \
+  do {                                                                                \
+    __syncthreads();                                                                  \
+    if (threadIdx.x == 0 && P.dbg) P.dbg[(size_t)s * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define BX_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
 enum { SQ_NA = 0, SQ_NL = 1, SQ_FC = 2, SQ_IDC = 3, SQ_STATUS = 4, SQ_STRIDE = 8 };
 
@@ -73,8 +140,8 @@ struct Lds {
   size_t o_act, o_lost, o_tracked, o_unconf, o_pool, o_rtr, o_lostl, o_refind, o_fa, o_fl,
       o_newt, o_flags, o_fid, o_mark, o_rowptr, o_c4r, o_u, o_srl, o_r4c, o_v, o_spc, o_path,
       o_colf, o_touch, o_dbox, o_dconf, o_dkind, o_hd, o_sd, o_rem, o_ecol, o_ecost, o_tdn,
-      o_tna, o_ddn, o_dnb, o_ints, total;
-  __host__ __device__ Lds(int T, int D, int elds) {
+      o_tna, o_ddn, o_dnb, o_ints, o_cdeg, o_wbuf, o_tbox, o_dboxf, total;
+  __host__ __device__ Lds(int T, int D, int elds, int F) {
     size_t o = 0;
     auto take = [&](size_t bytes) {
       size_t r = o;
@@ -83,7 +150,9 @@ struct Lds {
     };
     int R = T > D ? T : D;  // assignment rows/cols never exceed these
     o_dbox = take(sizeof(double) * 4 * D);
+    o_tbox = take(sizeof(double) * 4 * T);  // row boxes of the current association / dedup
     o_dconf = take(sizeof(double) * D);
+    o_dboxf = take(sizeof(float) * 4 * D);  // outward-rounded fp32 copy for candidate tests
     o_u = take(sizeof(double) * T);
     o_v = take(sizeof(double) * D);
     o_spc = take(sizeof(double) * D);
@@ -93,8 +162,7 @@ struct Lds {
     o_flags = take(sizeof(uint32_t) * T);
     o_fid = take(sizeof(int) * T);
     o_rowptr = take(sizeof(int) * (T + 1));
-    o_tdn = take(sizeof(float) * T);
-    o_ddn = take(sizeof(float) * D);
+    o_tdn = o_ddn = 0;  // (unused: the norms are folded into the dB/tA rows)
     o_ints = take(sizeof(int) * 64);
     o_act = take(2 * T);
     o_lost = take(2 * T);
@@ -112,6 +180,9 @@ struct Lds {
     o_r4c = take(2 * D);
     o_path = take(2 * D);
     o_touch = take(2 * D);
+    o_cdeg = take(4 * D);
+    // per-wave float32 staging row for numpy's pairwise norm (register fast path, F <= 512)
+    o_wbuf = take(F > 0 && F <= REG_F ? sizeof(float) * 4 * F : 0);
     o_hd = take(2 * D);
     o_sd = take(2 * D);
     o_rem = take(2 * D);
@@ -146,18 +217,16 @@ struct NormF32View {
   __device__ double operator()(int i) const { return (double)((float)p[i] / dn); }
 };
 
-// matching.py:279-283 casts the features to float32 first, then takes numpy's float32 norm
-template <typename FT>
-__device__ inline float np_norm_of(const FT* x, int n) {
-  return sqrtf(np_pairwise_sumsq_f32(x, n));
-}
+struct F32Row {
+  const float* p;
+  __device__ double operator()(int i) const { return (double)p[i]; }
+};
 
-// cosine distance of matching.enhanced_embedding_distance for one (track, det) pair
-template <typename FT>
-__device__ inline double emb_cost_pair(const FT* a, float adn, double ana, const FT* b, float bdn,
-                                       double bnb, int F) {
-  NormF32View<FT> A{a, adn}, B{b, bdn};
-  double c = dot2(A, B, F) / (ana * bnb);
+// scipy cdist-cosine of two already-normalised float32 rows (matching.py:283-287), max(0, .)
+__device__ inline double cosine_rows(const float* a, double na, const float* b, double nb,
+                                     int F) {
+  F32Row A{a}, B{b};
+  double c = dot2(A, B, F) / (na * nb);
   if (fabs(c) > 1.0) c = copysign(1.0, c);
   double d = 1.0 - c;
   return d < 0.0 ? 0.0 : d;
@@ -173,7 +242,8 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
                                                    int* __restrict__ out_count) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int T = P.T, D = P.D, F = P.F;
-  const Lds Lo(T, D, P.elds);
+  const Lds Lo(T, D, P.elds, F);
+  float* s_wbuf = (float*)(smem + Lo.o_wbuf) + (size_t)wave_id() * (F <= REG_F ? F : 0);
   uint16_t* s_act = (uint16_t*)(smem + Lo.o_act);
   uint16_t* s_lost = (uint16_t*)(smem + Lo.o_lost);
   uint16_t* s_tracked = (uint16_t*)(smem + Lo.o_tracked);
@@ -199,6 +269,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   uint8_t* s_colf = (uint8_t*)(smem + Lo.o_colf);
   uint16_t* s_touch = (uint16_t*)(smem + Lo.o_touch);
   double* s_dbox = (double*)(smem + Lo.o_dbox);
+  float4* s_dboxf = (float4*)(smem + Lo.o_dboxf);
   double* s_dconf = (double*)(smem + Lo.o_dconf);
   uint8_t* s_dkind = (uint8_t*)(smem + Lo.o_dkind);
   uint16_t* s_hd = (uint16_t*)(smem + Lo.o_hd);
@@ -206,9 +277,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   uint16_t* s_rem = (uint16_t*)(smem + Lo.o_rem);
   uint16_t* s_ecol = (uint16_t*)(smem + Lo.o_ecol);
   double* s_ecost = (double*)(smem + Lo.o_ecost);
-  float* s_tdn = (float*)(smem + Lo.o_tdn);
   double* s_tna = (double*)(smem + Lo.o_tna);
-  float* s_ddn = (float*)(smem + Lo.o_ddn);
   double* s_dnb = (double*)(smem + Lo.o_dnb);
   int* I = (int*)(smem + Lo.o_ints);
   int* scan_tmp = I + I_SCAN;
@@ -239,6 +308,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   const float* fdets = dets + (size_t)d0 * 6;
   const FT* fembs = REID ? embs + (size_t)d0 * F : nullptr;
 
+  BX_STAMP(0);
   // ---------------- P0: sequence state → LDS
   if (tid == 0) {
     I[I_NA] = seq[SQ_NA];
@@ -271,6 +341,8 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
     xyxy2xywh(xyxy, xywh);
     xywh2xyxy(xywh, box);  // STrack.xyxy of a detection (mean is None)
     for (int q = 0; q < 4; q++) s_dbox[4 * k + q] = box[q];
+    s_dboxf[k] = make_float4(__double2float_rd(box[0]), __double2float_rd(box[1]),
+                             __double2float_ru(box[2]), __double2float_ru(box[3]));
     s_dconf[k] = conf;
     uint8_t kd = 0;
     if (conf > P.high) kd = 1;
@@ -286,21 +358,54 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   // BoT-SORT: STrack(det, feat) → update_features: f1 = f/|f|, f2 = f1/|f1| (curr == smooth),
   // plus the float32 norms embedding_distance will need for the det side.
   if (REID) {
-    for (int p = tid; p < Dh; p += WG) {
-      const int k = s_hd[p];
+    // one wave per detection row (lane-strided, coalesced)
+    if (F <= REG_F) {  // whole row in registers: one load, two stores; next row prefetched
+      const int lane = lane_id();
+      int p = wave_id();
+      RegRow<FT> x;
+      if (p < Dh) x.load(fembs + (size_t)s_hd[p] * F, F);
+      for (; p < Dh; p += WG / WAVE) {
+        const int k = s_hd[p], pn = p + WG / WAVE;
+        RegRow<FT> nx;
+        if (pn < Dh) nx.load(fembs + (size_t)s_hd[pn] * F, F);
+        x.div(x.norm(F));
+        x.div(x.norm(F));
+        x.store(g_df2 + (size_t)k * F, F);
+        const float dn = x.np_dn(s_wbuf, F);
+        float* Bk = P.dB + ((size_t)s * D + k) * F;
+#pragma unroll
+        for (int r = 0; r < REG_EPL; r++) {
+          const int q = lane + 64 * r;
+          if (q < F) Bk[q] = (float)x.v[r] / dn;
+        }
+        x = nx;
+      }
+    }
+    for (int p = wave_id(); p < (F <= REG_F ? 0 : Dh); p += WG / WAVE) {
+      const int k = s_hd[p], lane = lane_id();
       const FT* f = fembs + (size_t)k * F;
       FT* f2 = g_df2 + (size_t)k * F;
-      FT n1 = blas_norm(f, F);
-      for (int q = 0; q < F; q++) f2[q] = f[q] / n1;
-      FT n2 = blas_norm((const FT*)f2, F);
-      for (int q = 0; q < F; q++) f2[q] = f2[q] / n2;
-      float dn = np_norm_of(f2, F) + 1e-8f;
-      NormF32View<FT> B{f2, dn};
-      s_ddn[k] = dn;
+      const FT n1 = wave_norm(f, F);
+      for (int q = lane; q < F; q += WAVE) f2[q] = f[q] / n1;
+      const FT n2 = wave_norm((const FT*)f2, F);  // same lane mapping: reads own writes
+      for (int q = lane; q < F; q += WAVE) f2[q] = f2[q] / n2;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // other lanes read f2 next
+      const float dn = sqrtf(np_sumsq_wave(f2, F)) + 1e-8f;
+      float* Bk = P.dB + ((size_t)s * D + k) * F;
+      for (int q = lane; q < F; q += WAVE) Bk[q] = (float)f2[q] / dn;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __syncthreads();
+    // scipy cdist's norm of each normalised row: its own two-accumulator sequential order
+    for (int p = tid; p < Dh; p += WG) {
+      const int k = s_hd[p];
+      const float* Bk = P.dB + ((size_t)s * D + k) * F;
+      F32Row B{Bk};
       s_dnb[k] = sqrt(dot2(B, B, F));
     }
   }
 
+  BX_STAMP(1);
   // ---------------- P2: tracked / unconfirmed / strack_pool = joint(tracked, lost)
   const int ntr = block_compact(na, [&](int k) { return (s_flags[s_act[k]] & F_ACT) != 0; },
                                 [&](int k, int p) { s_tracked[p] = s_act[k]; }, scan_tmp);
@@ -316,6 +421,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   const int npool = ntr + npl;
   for (int k = tid; k < npool; k += WG) s_mark[s_pool[k]] &= ~M_POOL;
 
+  BX_STAMP(2);
   // ---------------- P3: multi_predict (+ BoT-SORT multi_gmc on pool and unconfirmed)
   const double* H = (KIND == KIND_BOT && warps) ? warps + 6 * (size_t)b : nullptr;
   for (int k = tid; k < npool + ((KIND == KIND_BOT) ? nun : 0); k += WG) {
@@ -372,6 +478,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   W.gcol = P.gcol + (size_t)s * T * D; W.gcost = P.gcost + (size_t)s * T * D;
   W.elds = P.elds; W.col4row = s_c4r; W.row4col = s_r4c; W.u = s_u; W.v = s_v;
   W.spc = s_spc; W.path = s_path; W.colflag = s_colf; W.touched = s_touch; W.srlist = s_srl;
+  W.coldeg = (int*)(smem + Lo.o_cdeg);
   uint16_t* e_gcol = P.gcol + (size_t)s * T * D;
   double* e_gcost = P.gcost + (size_t)s * T * D;
   auto put_edge = [&](int e, int col, double cost) {
@@ -387,9 +494,10 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   // then solve.  mode: 0 = IoU distance, 1 = fused (fuse_score), 2 = BoT-SORT first
   // association, 3 = BoT-SORT unconfirmed association.
   auto associate = [&](const uint16_t* rows, int R, const uint16_t* cols, int C, double L,
-                       int mode) {
-    const bool prefilter = L <= 1.0;  // non-overlapping pairs cost >= 1 and are never admissible
+                       int mode, int stamp) {
     const bool reid = REID && (mode == 2 || mode == 3);
+    // non-overlapping pairs have IoU 0: cost >= 1, never admissible, never gated (prox < 1)
+    const bool prefilter = L <= 1.0 && (!reid || P.prox < 1.0);
     auto pair_cost = [&](const double* tb, int dk, bool& gated, bool& cand) -> double {
       double c = 1 - iou_pair(tb, s_dbox + 4 * dk);
       gated = false;
@@ -402,52 +510,93 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
       cand = c < L || gated;
       return c;
     };
-    // pass 1: count candidates per row (thread per row)
+    // Candidates: one wave per row, lanes over columns, a conservative fp32 intersection test on
+    // outward-rounded boxes (never misses an fp64-intersecting pair); a row's candidates keep
+    // column order (ballot prefix).  Exact fp64 costs are then computed once per candidate with
+    // every lane busy; candidates that turn out inadmissible stay in the CSR with cost INF,
+    // which the solver treats as absent.  Row boxes are gathered into LDS first.
+    double* s_tbox = (double*)(smem + Lo.o_tbox);
     for (int i = tid; i < R; i += WG) {
-      double tb[4];
-      track_box(rows[i], tb);
+      track_box(rows[i], s_tbox + 4 * i);
+      s_srl[i] = 0;  // "row has a gated edge" flag; the LAP reuses s_srl afterwards
+    }
+    __syncthreads();
+    const int lane = lane_id();
+    auto cand_test = [&](const float4& tb, int j) -> bool {
+      if (j >= C) return false;
+      if (!prefilter) return true;
+      const float4 db = s_dboxf[cols[j]];
+      return fminf(tb.z, db.z) > fmaxf(tb.x, db.x) && fminf(tb.w, db.w) > fmaxf(tb.y, db.y);
+    };
+    auto row_boxf = [&](int i) {
+      const double* t = s_tbox + 4 * i;
+      return make_float4(__double2float_rd(t[0]), __double2float_rd(t[1]),
+                         __double2float_ru(t[2]), __double2float_ru(t[3]));
+    };
+    // pass 1: count candidates per row
+    for (int i = wave_id(); i < R; i += WG / WAVE) {
+      const float4 tb = row_boxf(i);
       int cnt = 0;
-      for (int j = 0; j < C; j++) {
-        const int dk = cols[j];
-        if (prefilter && !boxes_intersect(tb, s_dbox + 4 * dk)) continue;
-        bool g, cand;
-        pair_cost(tb, dk, g, cand);
-        cnt += cand;
-      }
-      s_rowptr[i] = cnt;
+      for (int j0 = 0; j0 < C; j0 += WAVE) cnt += __popcll(__ballot(cand_test(tb, j0 + lane)));
+      if (lane == 0) s_rowptr[i] = cnt;
     }
     __syncthreads();
     wave0_exclusive_scan(s_rowptr, R);
     __syncthreads();
-    // pass 2: write edges; gated edges get the appearance term
-    bool any_gated = false;
-    for (int i = tid; i < R; i += WG) {
-      double tb[4];
-      const int slot = rows[i];
-      track_box(slot, tb);
+    // pass 2: write candidate columns; the row index is parked in the cost slot
+    for (int i = wave_id(); i < R; i += WG / WAVE) {
+      const float4 tb = row_boxf(i);
       int e = s_rowptr[i];
-      bool row_gated = false;
-      for (int j = 0; j < C; j++) {
-        const int dk = cols[j];
-        if (prefilter && !boxes_intersect(tb, s_dbox + 4 * dk)) continue;
-        bool g, cand;
-        double c = pair_cost(tb, dk, g, cand);
-        if (!cand) continue;
-        // gated edges are marked by a NaN-free negative-zero trick: column | 0x8000
-        put_edge(e++, g ? (j | 0x8000) : j, c);
-        row_gated |= g;
+      for (int j0 = 0; j0 < C; j0 += WAVE) {
+        const int j = j0 + lane;
+        const bool cand = cand_test(tb, j);
+        const unsigned long long m = __ballot(cand);
+        if (cand) put_edge(e + __popcll(m & ((1ull << lane) - 1ull)), j, (double)i);
+        e += __popcll(m);
       }
-      if (reid && row_gated) {
-        const FT* tf = g_feat + (size_t)slot * F;
-        float dn = np_norm_of(tf, F) + 1e-8f;
-        NormF32View<FT> A{tf, dn};
-        s_tdn[slot] = dn;
-        s_tna[slot] = sqrt(dot2(A, A, F));
-      }
-      any_gated |= row_gated;
+    }
+    __syncthreads();
+    // pass 3: exact fp64 cost per candidate (gated ones flagged in the column's top bit)
+    for (int e = tid; e < s_rowptr[R]; e += WG) {
+      int j;
+      double ri;
+      get_edge(e, j, ri);
+      const int i = (int)ri;
+      bool g, cand;
+      const double c = pair_cost(s_tbox + 4 * i, cols[j], g, cand);
+      put_edge(e, (g && cand) ? (j | 0x8000) : j, cand ? c : INF);
+      if (g && cand) s_srl[i] = 1;
     }
     __syncthreads();
     if (reid) {
+      // track rows as embedding_distance sees them: float32 smooth_feat / (np norm + 1e-8)
+      for (int i = wave_id(); i < R; i += WG / WAVE) {
+        if (!s_srl[i]) continue;  // wave-uniform
+        const int slot = rows[i], lane = lane_id();
+        const FT* tf = g_feat + (size_t)slot * F;
+        float* A = P.tA + ((size_t)s * T + slot) * F;
+        if (F <= REG_F) {
+          RegRow<FT> x;
+          x.load(tf, F);
+          const float dn = x.np_dn(s_wbuf, F);
+#pragma unroll
+          for (int r = 0; r < REG_EPL; r++) {
+            const int q = lane + 64 * r;
+            if (q < F) A[q] = (float)x.v[r] / dn;
+          }
+          continue;
+        }
+        const float dn = sqrtf(np_sumsq_wave(tf, F)) + 1e-8f;
+        for (int q = lane; q < F; q += WAVE) A[q] = (float)tf[q] / dn;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      __syncthreads();
+      for (int i = tid; i < R; i += WG) {
+        if (!s_srl[i]) continue;
+        F32Row A{P.tA + ((size_t)s * T + rows[i]) * F};
+        s_tna[rows[i]] = sqrt(dot2(A, A, F));
+      }
+      __syncthreads();
       // emb_dists = cdist/2; > appearance_thresh → 1; (not gated → 1); dists = min(iou, emb)
       const int E = s_rowptr[R];
       // thread per edge: find its row by binary search over row_ptr
@@ -462,24 +611,99 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
           if (s_rowptr[mid] <= e) lo = mid; else hi = mid;
         }
         const int slot = rows[lo], j = col & 0x7fff, dk = cols[j];
-        double ed = emb_cost_pair<FT>(g_feat + (size_t)slot * F, s_tdn[slot], s_tna[slot],
-                                      g_df2 + (size_t)dk * F, s_ddn[dk], s_dnb[dk], F) / 2.0;
+        double ed = cosine_rows(P.tA + ((size_t)s * T + slot) * F, s_tna[slot],
+                                P.dB + ((size_t)s * D + dk) * F, s_dnb[dk], F) / 2.0;
         if (ed > P.app) ed = 1.0;
         double cm = c < ed ? c : ed;  // np.minimum(ious_dists, emb_dists)
         put_edge(e, j, cm < L ? cm : INF);
       }
       __syncthreads();
     }
-    (void)any_gated;
+    BX_STAMP(stamp);
     if (wave_id() == 0) lap_solve_wave(R, C, L, W);
     __syncthreads();
   };
 
   // ---------------- P4/P5: first association: pool x high dets
-  associate(s_pool, npool, s_hd, Dh, P.match_thresh, KIND == KIND_BYTE ? 1 : 2);
+  BX_STAMP(3);
+  associate(s_pool, npool, s_hd, Dh, P.match_thresh, KIND == KIND_BYTE ? 1 : 2, 4);
+  BX_STAMP(5);
 
   // per-track matched update (STrack.update / re_activate)
+  // botsort_track.py:40-49 update_features(det.curr_feat) on one track — one wave, lane-strided:
+  // feat /= |feat|; smooth = 0.9 smooth + 0.1 feat; smooth /= |smooth|
+  auto feature_update_wave = [&](int slot, int dk) {
+    const int lane = lane_id();
+    FT* sm = g_feat + (size_t)slot * F;
+    const FT* f2 = g_df2 + (size_t)dk * F;
+    const FT a = (FT)0.9, bb = (FT)(1.0 - 0.9);
+    if (F <= REG_F) {
+      RegRow<FT> g, m;
+      g.load(f2, F);
+      m.load(sm, F);
+      const FT n3 = g.norm(F);
+#pragma unroll
+      for (int r = 0; r < REG_EPL; r++) {
+        FT g3 = g.v[r] / n3;
+        m.v[r] = a * m.v[r] + bb * g3;
+      }
+      m.div(m.norm(F));
+      m.store(sm, F);
+      return;
+    }
+    const FT n3 = wave_norm(f2, F);
+    for (int q = lane; q < F; q += WAVE) {
+      FT g3 = f2[q] / n3;
+      sm[q] = a * sm[q] + bb * g3;
+    }
+    const FT ns = wave_norm((const FT*)sm, F);  // same lane mapping: reads own writes
+    for (int q = lane; q < F; q += WAVE) sm[q] = sm[q] / ns;
+  };
+  // feature updates for the rows of the last solve that matched (rows[i] ↔ cols[c4r[i]]):
+  // the matched pairs are compacted into the (now idle) LAP scratch, then one wave per pair
+  // with the next pair's two rows prefetched into registers while this one computes.
+  auto feature_updates = [&](const uint16_t* rows, int R, const uint16_t* cols) {
+    uint16_t* ms = s_touch;
+    int16_t* md = s_path;
+    const int nm = block_compact(R, [&](int i) { return s_c4r[i] >= 0; },
+                                 [&](int i, int p) {
+                                   ms[p] = rows[i];
+                                   md[p] = (int16_t)cols[s_c4r[i]];
+                                 },
+                                 scan_tmp);
+    if (F > REG_F) {
+      for (int p = wave_id(); p < nm; p += WG / WAVE) feature_update_wave(ms[p], md[p]);
+      return;
+    }
+    const FT a = (FT)0.9, bb = (FT)(1.0 - 0.9);
+    int p = wave_id();
+    RegRow<FT> g, m;
+    if (p < nm) {
+      g.load(g_df2 + (size_t)md[p] * F, F);
+      m.load(g_feat + (size_t)ms[p] * F, F);
+    }
+    for (; p < nm; p += WG / WAVE) {
+      const int pn = p + WG / WAVE;
+      RegRow<FT> ng, nm_;
+      if (pn < nm) {
+        ng.load(g_df2 + (size_t)md[pn] * F, F);
+        nm_.load(g_feat + (size_t)ms[pn] * F, F);
+      }
+      const FT n3 = g.norm(F);
+#pragma unroll
+      for (int r = 0; r < REG_EPL; r++) {
+        FT g3 = g.v[r] / n3;
+        m.v[r] = a * m.v[r] + bb * g3;
+      }
+      m.div(m.norm(F));
+      m.store(g_feat + (size_t)ms[p] * F, F);
+      g = ng;
+      m = nm_;
+    }
+  };
+
   auto apply_update = [&](int slot, int dk, bool reactivate, bool with_feat) {
+    (void)with_feat;  // features: feature_updates() after the scalar pass
     const float* r = fdets + 6 * dk;
     double xyxy[4] = {(double)r[0], (double)r[1], (double)r[2], (double)r[3]};
     double xywh[4], meas[4];
@@ -492,19 +716,6 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
       for (int q = 0; q < 4; q++) meas[q] = xywh[q];
     }
     kf_update_soa(kf, g_mean + slot, g_cov + slot, T, meas, 0.0);
-    if (KIND == KIND_BOT && with_feat) {
-      // update_features(det.curr_feat): feat /= |feat|; smooth = .9 smooth + .1 feat; renorm
-      FT* sm = g_feat + (size_t)slot * F;
-      const FT* f2 = g_df2 + (size_t)dk * F;
-      FT n3 = blas_norm(f2, F);
-      const FT a = (FT)0.9, bb = (FT)(1.0 - 0.9);
-      for (int q = 0; q < F; q++) {
-        FT g3 = f2[q] / n3;
-        sm[q] = a * sm[q] + bb * g3;
-      }
-      FT ns = blas_norm((const FT*)sm, F);
-      for (int q = 0; q < F; q++) sm[q] = sm[q] / ns;
-    }
     uint32_t fl = s_flags[slot];
     fl = (fl & ~F_STATE) | ST_TRACKED | F_ACT;
     s_flags[slot] = fl;
@@ -541,6 +752,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
     apply_update(slot, s_hd[j], !tracked, REID);
     if (!tracked) s_mark[slot] |= M_TMP;  // refind
   }
+  if (REID) feature_updates(s_pool, npool, s_hd);
   __syncthreads();
   const int nref = block_compact(npool, [&](int k) { return (s_mark[s_pool[k]] & M_TMP) != 0; },
                                  [&](int k, int p) { s_refind[p] = s_pool[k]; }, scan_tmp);
@@ -553,8 +765,9 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
       npool, [&](int k) { return s_c4r[k] < 0 && st_of(s_flags[s_pool[k]]) == ST_TRACKED; },
       [&](int k, int p) { s_rtr[p] = s_pool[k]; }, scan_tmp);
 
+  BX_STAMP(6);
   // ---------------- P7: second association: r_tracked x low-confidence dets (IoU, 0.5)
-  associate(s_rtr, nrtr, s_sd, Ds, 0.5, 0);
+  associate(s_rtr, nrtr, s_sd, Ds, 0.5, 0, 7);
   for (int i = tid; i < nrtr; i += WG) {
     const int j = s_c4r[i];
     if (j < 0) continue;
@@ -571,7 +784,9 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
       scan_tmp);
 
   // ---------------- P8: unconfirmed x remaining high dets (fused, 0.7)
-  associate(s_unconf, nun, s_rem, nrem, 0.7, KIND == KIND_BYTE ? 1 : 3);
+  BX_STAMP(8);
+  associate(s_unconf, nun, s_rem, nrem, 0.7, KIND == KIND_BYTE ? 1 : 3, 9);
+  BX_STAMP(10);
   for (int i = tid; i < nun; i += WG) {
     const int j = s_c4r[i];
     const int slot = s_unconf[i];
@@ -582,6 +797,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
       s_mark[slot] |= M_REMNOW;
     }
   }
+  if (REID) feature_updates(s_unconf, nun, s_rem);
   __syncthreads();
 
   // ---------------- P9: new tracks from the detections left over (conf >= det/new thresh)
@@ -638,17 +854,21 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
       h[0] = (double)r[5];
       h[1] = (double)r[4];
       g_ncls[slot] = 1;
-      if (REID) {
-        FT* sm = g_feat + (size_t)slot * F;
-        const FT* f2 = g_df2 + (size_t)dk * F;
-        for (int q = 0; q < F; q++) sm[q] = f2[q];
-      }
     }
     s_newt[p] = (uint16_t)slot;
   }
   if (tid == 0) I[I_IDC] = idc0 + nnew_ok;
   __syncthreads();
+  if (REID) {  // smooth_feat of a new track = the detection's (already twice-normalised) feature
+    for (int p = wave_id(); p < nnew_ok; p += WG / WAVE) {
+      const int slot = s_newt[p], dk = g_detind[slot];
+      FT* sm = g_feat + (size_t)slot * F;
+      const FT* f2 = g_df2 + (size_t)dk * F;
+      for (int q = lane_id(); q < F; q += WAVE) sm[q] = f2[q];
+    }
+  }
 
+  BX_STAMP(11);
   // ---------------- P10: lost tracks past the buffer → removed
   for (int k = tid; k < nl; k += WG) {
     const int slot = s_lost[k];
@@ -688,21 +908,37 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
     if (s_mark[k] & M_REMNOW) s_flags[k] |= F_INREM;
   __syncthreads();
   // remove_duplicate_stracks(act2, lost2): iou distance < 0.15 → drop the younger track
-  for (int p = tid; p < nact2; p += WG) {
-    const int sa = s_fa[p];
-    double ba[4];
-    track_box(sa, ba);
-    const int ta = s_fid[sa] - g_start[sa];
-    for (int q = 0; q < nlost2; q++) {
-      const int sb = s_tracked[q];
-      double bb[4];
-      track_box(sb, bb);
-      if (!boxes_intersect(ba, bb)) continue;
-      if (1 - iou_pair(ba, bb) < 0.15) {
-        const int tb = s_fid[sb] - g_start[sb];
-        if (ta > tb) atomicOr((unsigned*)&s_flags[sb], 0x80000000u);  // dupb (transient bit)
-        else s_mark[sa] |= M_DUP;                                   // dupa
+  {
+    double* lbox = s_ecost;  // the LAP edge store is dead by now: lost boxes + ages live there
+    const bool in_lds = nlost2 * 5 <= P.elds;
+    double* abox = (double*)(smem + Lo.o_tbox);
+    if (in_lds)
+      for (int q = tid; q < nlost2; q += WG) {
+        const int sb = s_tracked[q];
+        track_box(sb, lbox + 4 * q);
+        lbox[4 * nlost2 + q] = (double)(s_fid[sb] - g_start[sb]);
       }
+    for (int p = tid; p < nact2; p += WG) track_box(s_fa[p], abox + 4 * p);
+    __syncthreads();
+    const int lane = lane_id();
+    for (int p = wave_id(); p < nact2; p += WG / WAVE) {  // wave per active track
+      const int sa = s_fa[p];
+      const double* ba = abox + 4 * p;
+      const int ta = s_fid[sa] - g_start[sa];
+      bool dupa = false;
+      for (int q = lane; q < nlost2; q += WAVE) {
+        const int sb = s_tracked[q];
+        double bb[4];
+        if (in_lds) for (int k = 0; k < 4; k++) bb[k] = lbox[4 * q + k];
+        else track_box(sb, bb);
+        if (!boxes_intersect(ba, bb)) continue;
+        if (1 - iou_pair(ba, bb) < 0.15) {
+          const int tb = in_lds ? (int)lbox[4 * nlost2 + q] : s_fid[sb] - g_start[sb];
+          if (ta > tb) atomicOr((unsigned*)&s_flags[sb], 0x80000000u);  // dupb (transient bit)
+          else dupa = true;                                             // dupa
+        }
+      }
+      if (__ballot(dupa) != 0ull && lane == 0) s_mark[sa] |= M_DUP;
     }
   }
   __syncthreads();
@@ -714,6 +950,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   for (int k = tid; k < nlost2; k += WG) s_flags[s_tracked[k]] &= ~0x80000000u;
   __syncthreads();
 
+  BX_STAMP(12);
   // ---------------- P12: outputs [x1,y1,x2,y2,id,conf,cls,det_ind] for activated tracks
   const int nout = block_compact(
       nfa, [&](int k) { return (s_flags[s_unconf[k]] & F_ACT) != 0; },
@@ -752,6 +989,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
     if (I[I_ERR]) seq[SQ_STATUS] |= 1 << BX_ERR_TRACK_OVERFLOW;
     out_count[b] = nout;
   }
+  BX_STAMP(13);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -864,6 +1102,7 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
   acc(4 * ST); acc(4 * ST); acc(4 * ST); acc(4 * ST); acc(8 * ST); acc(8 * ST);
   acc(8 * ST * 8); acc(8 * ST * 64); acc(fs * ST * (F ? F : 1)); acc(8 * ST * CLS_HIST * 2);
   acc(4 * ST); acc(2 * ST * D); acc(8 * ST * D); acc(fs * (size_t)S * D * (F ? F : 1)); acc(64);
+  acc(4 * (size_t)S * D * (F ? F : 1)); acc(4 * ST * (F ? F : 1));
   e->arena_bytes = bytes;
   if (hipMalloc(&e->arena, bytes) != hipSuccess) {
     delete e;
@@ -890,8 +1129,15 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
   d.gcost = carve<double>(p, ST * D);
   d.df2 = carve<char>(p, fs * (size_t)S * D * (F ? F : 1));
   d.status = carve<int>(p, 16);
+  d.dB = carve<float>(p, (size_t)S * D * (F ? F : 1));
+  d.tA = carve<float>(p, ST * (F ? F : 1));
+  d.dbg = nullptr;
+#ifdef BX_PHASE_TIMING
+  HIPCHK(hipMalloc(&d.dbg, sizeof(unsigned long long) * 32 * S));
+  HIPCHK(hipMemset(d.dbg, 0, sizeof(unsigned long long) * 32 * S));
+#endif
   HIPCHK(hipMemset(e->arena, 0, bytes));
-  e->lds_bytes = Lds(T, D, d.elds).total;
+  e->lds_bytes = Lds(T, D, d.elds, F).total;
   if (e->lds_bytes > 160 * 1024) {
     (void)hipFree(e->arena);
     delete e;
@@ -978,6 +1224,16 @@ int bx_engine_update_host(bx_engine* e, int seq, const float* dets, int n, const
     return set_err(BX_ERR_TRACK_OVERFLOW, "a sequence ran out of track slots (raise track_cap)");
   return BX_OK;
 }
+
+#ifdef BX_PHASE_TIMING
+// diagnostic only: copy the [S][32] phase stamps of the last launch to the host
+int bx_debug_stamps_host(bx_engine* e, unsigned long long* out) {
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, e->dev.dbg, sizeof(unsigned long long) * 32 * e->dev.S,
+                   hipMemcpyDeviceToHost));
+  return BX_OK;
+}
+#endif
 
 int bx_engine_status(bx_engine* e, int* status) {
   if (!e || !status) return set_err(BX_ERR_INVALID, "null argument");

@@ -37,7 +37,7 @@ class EngineParams:
 
 
 class Engine:
-    def __init__(self, kind: str, n_seq: int = 1, track_cap: int = 1024, det_cap: int = 512,
+    def __init__(self, kind: str, n_seq: int = 1, track_cap: int = 1024, det_cap: int = 384,
                  emb_dim: int = 0, emb_f64: bool = False, params: EngineParams | None = None):
         if kind not in KINDS:
             raise KeyError(kind)

@@ -33,7 +33,7 @@ class BotSort(BaseTracker):
                  track_buffer: int = 30, match_thresh: float = 0.8,
                  proximity_thresh: float = 0.5, appearance_thresh: float = 0.25,
                  cmc_method: str = "ecc", frame_rate=30, fuse_first_associate: bool = False,
-                 with_reid: bool = True, track_cap: int = 1024, det_cap: int = 512):
+                 with_reid: bool = True, track_cap: int = 1024, det_cap: int = 384):
         super().__init__(per_class=bool(per_class))
         self.track_high_thresh = track_high_thresh
         self.track_low_thresh = track_low_thresh

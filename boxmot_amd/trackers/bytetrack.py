@@ -24,7 +24,7 @@ class ByteTrack(BaseTracker):
 
     def __init__(self, min_conf: float = 0.1, track_thresh: float = 0.45,
                  match_thresh: float = 0.8, track_buffer: int = 25, frame_rate: int = 30,
-                 per_class: bool = False, track_cap: int = 1024, det_cap: int = 512):
+                 per_class: bool = False, track_cap: int = 1024, det_cap: int = 384):
         super().__init__(per_class=bool(per_class))
         self.min_conf = min_conf
         self.track_thresh = track_thresh

@@ -69,11 +69,20 @@ struct bxo_tracker {
 /* ---- feature helpers: values held in double, rounded to float32 after every op in f32 mode - */
 static inline double rnd(const bxo_tracker *T, double x) { return T->f64 ? x : (double)(float)x; }
 
-/* np.linalg.norm(1-D) = sqrt(x.dot(x)) (BLAS dot; summation order not pinned by numpy). */
+/* np.linalg.norm(1-D) = sqrt(x.dot(x)) — a BLAS dot whose summation order numpy does not pin.
+ * The engine fixes it as the "wave order": 64 lane-strided sequential fp64 partial sums
+ * (lane l: x[l], x[l+64], ...) combined by an xor butterfly (d = 32..1); restated here. */
 static double vnorm(const bxo_tracker *T, const double *x) {
-    double s = 0.0;
-    for (int k = 0; k < T->emb_dim; k++) s += x[k] * x[k];
-    return T->f64 ? sqrt(s) : (double)sqrtf((float)s);
+    double s[64], t[64];
+    for (int l = 0; l < 64; l++) {
+        s[l] = 0.0;
+        for (int k = l; k < T->emb_dim; k += 64) s[l] += x[k] * x[k];
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        for (int l = 0; l < 64; l++) t[l] = s[l] + s[l ^ d];
+        memcpy(s, t, sizeof s);
+    }
+    return T->f64 ? sqrt(s[0]) : (double)sqrtf((float)s[0]);
 }
 
 static void vdiv_inplace(const bxo_tracker *T, double *x, double n) {

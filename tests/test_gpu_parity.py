@@ -192,7 +192,7 @@ def run_batched(torch, kind, scenes, n_frames, args, emb_dim=0, seq_frames=None)
     from boxmot_amd.engine import Engine, EngineParams
 
     S = len(scenes)
-    eng = Engine(kind, n_seq=S, track_cap=1024, det_cap=512, emb_dim=emb_dim,
+    eng = Engine(kind, n_seq=S, track_cap=1024, det_cap=384, emb_dim=emb_dim,
                  params=EngineParams(**args))
     outs = [[] for _ in range(S)]
     for t in range(1, n_frames + 1):

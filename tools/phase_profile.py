@@ -1,0 +1,75 @@
+#!/usr/bin/env python
+"""Diagnostic: per-phase cycle shares of the frame kernel from in-kernel s_memtime stamps.
+
+Builds boxmot_amd/lib/libbxassoc_timing.so with -DBX_PHASE_TIMING (a separate diagnostic build;
+the stamps' barriers forbid overlaps the real kernel has, so read SHARES, not totals), runs the
+bench workload and prints the mean / max cycles per phase over all sequences of the last frame.
+"""
+import argparse
+import ctypes as C
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+LIB = ROOT / "boxmot_amd" / "lib" / "libbxassoc_timing.so"
+PHASES = ["dets+features", "lists", "predict+gmc", "assoc1 CSR", "assoc1 LAP", "assoc1 apply",
+          "assoc2 CSR", "assoc2 LAP+apply", "assoc3 CSR", "assoc3 LAP", "new tracks",
+          "lists+dedup", "outputs+writeback"]
+
+
+def build():
+    from boxmot_amd import _native as N
+
+    cmd = ["/opt/rocm/bin/hipcc", *N.HIPCC_FLAGS, "-DBX_PHASE_TIMING", "-o", str(LIB),
+           *[str(N.CSRC / s) for s in N.SOURCES]]
+    subprocess.run(cmd, check=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="botsort")
+    ap.add_argument("--seqs", type=int, default=256)
+    ap.add_argument("--frames", type=int, default=30)
+    ap.add_argument("--no-build", action="store_true")
+    a = ap.parse_args()
+    if not a.no_build:
+        build()
+    os.environ["BX_LIB_PATH"] = str(LIB)
+    import torch
+
+    from bench import CONFIGS
+    from boxmot_amd import _native as N
+    from boxmot_amd.engine import Engine, EngineParams
+    from boxmot_amd.synth import TorchSceneBatch
+
+    kind, n_obj, F, params = CONFIGS[a.config]
+    eng = Engine(kind, n_seq=a.seqs, track_cap=512, det_cap=256, emb_dim=F,
+                 params=EngineParams(**params))
+    gen = TorchSceneBatch(a.seqs, n_obj, emb_dim=F, seed=7, device="cuda")
+    L = N.load()
+    L.bx_debug_stamps_host.argtypes = [C.c_void_p, C.c_void_p]
+    out = torch.empty((a.seqs * n_obj, 8), dtype=torch.float64, device="cuda")
+    cnt = torch.empty(a.seqs, dtype=torch.int32, device="cuda")
+    for t in range(1, a.frames + 1):
+        d, off, e = gen.frame(t)
+        eng.step(d, off, e, None, out, cnt)
+    torch.cuda.synchronize()
+    st = np.zeros((a.seqs, 32), np.uint64)
+    L.bx_debug_stamps_host(eng._h, st.ctypes.data)
+    st = st.astype(np.int64)
+    d = np.diff(st[:, :14], axis=1)
+    tot = st[:, 13] - st[:, 0]
+    print(f"{a.config}: {a.seqs} seqs, frame {a.frames}: total cycles mean {tot.mean():.0f} "
+          f"max {tot.max():.0f}")
+    for k, name in enumerate(PHASES):
+        print(f"  {name:18s} mean {d[:, k].mean():10.0f}  max {d[:, k].max():10.0f}  "
+              f"share {d[:, k].mean() / tot.mean() * 100:5.1f}%")
+
+
+if __name__ == "__main__":
+    main()
