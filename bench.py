@@ -104,16 +104,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    backend = os.environ.get("BX_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI on ROCm
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # one process per GPU; modulo only so a 1-GPU rehearsal (gloo) can run 2 ranks
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from boxmot_amd.engine import Engine, EngineParams
+    from boxmot_amd.shard import gather_records, output_checksum, shard_sequences
     from boxmot_amd.synth import TorchSceneBatch
 
     kind, n_obj, F, params = CONFIGS[args.config]
@@ -121,6 +124,7 @@ def main():
     D_cap = 256
     eng = Engine(kind, n_seq=S, track_cap=512, det_cap=D_cap, emb_dim=F,
                  params=EngineParams(**params))
+    # this rank's shard: global sequences [rank*S, (rank+1)*S) — weak scaling, no exchange
     gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev)
     total = args.warmup + args.steps
     frames = [gen.frame(t) for t in range(1, total + 1)]  # resident in HBM before timing
@@ -155,21 +159,23 @@ def main():
     if eng.status() != 0:
         raise RuntimeError(f"engine status {eng.status()} (capacity overflow)")
 
-    dets_timed = sum(int(frames[k][1][-1].item()) for k in range(args.warmup, total))
-    stats = torch.tensor([wall, float(S * args.steps), float(dets_timed), kern_ms],
-                         dtype=torch.float64, device=dev)
-    if dist:
-        # RCCL over xGMI only to gather per-rank results (KB-scale), never per frame
-        gathered = [torch.zeros_like(stats) for _ in range(world)]
-        dist.all_gather(gathered, stats)
-        allst = torch.stack(gathered).cpu().numpy()
-    else:
-        allst = stats[None].cpu().numpy()
-    t_max = float(allst[:, 0].max())
-    total_frames = float(allst[:, 1].sum())
+    # per-sequence records of this rank's shard: [global seq id, frames timed, dets timed,
+    # rows of the last frame, checksum of the last frame, rank wall s, rank kernel ms]
+    off_h = [frames[k][1].cpu().numpy() for k in range(args.warmup, total)]
+    dets_seq = np.sum([np.diff(o) for o in off_h], 0)
+    last_off, cnt_h, out_h = off_h[-1], cnt.cpu().numpy(), out.cpu().numpy()
+    recs = np.zeros((S, 7))
+    for i, g in enumerate(shard_sequences(S * world, world, rank)):
+        rows_i = out_h[last_off[i]: last_off[i] + cnt_h[i]]
+        recs[i] = [g, args.steps, dets_seq[i], cnt_h[i], output_checksum(rows_i), wall, kern_ms]
+    # RCCL over xGMI only to gather these KB-scale records once, never per frame
+    allrec = gather_records(recs, dist, dev if backend == "nccl" else "cpu")
+    t_max = float(allrec[:, 5].max())
+    total_frames = float(allrec[:, 1].sum())
     value = total_frames / t_max
     if rank == 0:
-        mean_d = float(allst[:, 2].sum() / allst[:, 1].sum())
+        assert np.array_equal(np.sort(allrec[:, 0]), np.arange(S * world)), "shard gather"
+        mean_d = float(allrec[:, 2].sum() / allrec[:, 1].sum())
         T_pool = n_obj
         per_frame = algorithmic_bytes_per_frame(T_pool, mean_d, F, mean_d)
         per_launch = per_frame * S
