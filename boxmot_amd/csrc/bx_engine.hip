@@ -140,7 +140,7 @@ struct Lds {
   size_t o_act, o_lost, o_tracked, o_unconf, o_pool, o_rtr, o_lostl, o_refind, o_fa, o_fl,
       o_newt, o_flags, o_fid, o_mark, o_rowptr, o_c4r, o_u, o_srl, o_r4c, o_v, o_spc, o_path,
       o_colf, o_touch, o_dbox, o_dconf, o_dkind, o_hd, o_sd, o_rem, o_ecol, o_ecost, o_tdn,
-      o_tna, o_ddn, o_dnb, o_ints, o_cdeg, o_wbuf, o_tbox, o_dboxf, total;
+      o_tna, o_ddn, o_dnb, o_ints, o_cdeg, o_wbuf, o_tbox, o_dboxf, o_tboxf, total;
   __host__ __device__ Lds(int T, int D, int elds, int F) {
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -153,6 +153,7 @@ struct Lds {
     o_tbox = take(sizeof(double) * 4 * T);  // row boxes of the current association / dedup
     o_dconf = take(sizeof(double) * D);
     o_dboxf = take(sizeof(float) * 4 * D);  // outward-rounded fp32 copy for candidate tests
+    o_tboxf = take(sizeof(float) * 4 * T);  // same for the rows of the current association
     o_u = take(sizeof(double) * T);
     o_v = take(sizeof(double) * D);
     o_spc = take(sizeof(double) * D);
@@ -515,44 +516,68 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
     // column order (ballot prefix).  Exact fp64 costs are then computed once per candidate with
     // every lane busy; candidates that turn out inadmissible stay in the CSR with cost INF,
     // which the solver treats as absent.  Row boxes are gathered into LDS first.
+    // Lanes own columns: a lane keeps the boxes of its columns j = lane + 64k (k < 4, i.e.
+    // C <= 256) in registers for the whole row sweep, so a row costs one broadcast LDS read.
     double* s_tbox = (double*)(smem + Lo.o_tbox);
+    float4* s_tboxf = (float4*)(smem + Lo.o_tboxf);
     for (int i = tid; i < R; i += WG) {
-      track_box(rows[i], s_tbox + 4 * i);
+      double* t = s_tbox + 4 * i;
+      track_box(rows[i], t);
+      s_tboxf[i] = make_float4(__double2float_rd(t[0]), __double2float_rd(t[1]),
+                               __double2float_ru(t[2]), __double2float_ru(t[3]));
       s_srl[i] = 0;  // "row has a gated edge" flag; the LAP reuses s_srl afterwards
     }
     __syncthreads();
     const int lane = lane_id();
-    auto cand_test = [&](const float4& tb, int j) -> bool {
-      if (j >= C) return false;
-      if (!prefilter) return true;
-      const float4 db = s_dboxf[cols[j]];
-      return fminf(tb.z, db.z) > fmaxf(tb.x, db.x) && fminf(tb.w, db.w) > fmaxf(tb.y, db.y);
+    constexpr int MAXCH = 4;
+    const int nch = (C + WAVE - 1) / WAVE;
+    const bool regcols = nch <= MAXCH;
+    const float4 empty = make_float4(INFINITY, INFINITY, -INFINITY, -INFINITY);
+    float4 cb[MAXCH];
+#pragma unroll
+    for (int k = 0; k < MAXCH; k++) {
+      const int j = lane + WAVE * k;
+      cb[k] = (regcols && j < C) ? s_dboxf[cols[j]] : empty;
+    }
+    auto hit = [&](const float4& tb, const float4& db, int j) -> bool {
+      if (!prefilter) return j < C;
+      return (fminf(tb.z, db.z) > fmaxf(tb.x, db.x)) & (fminf(tb.w, db.w) > fmaxf(tb.y, db.y));
     };
-    auto row_boxf = [&](int i) {
-      const double* t = s_tbox + 4 * i;
-      return make_float4(__double2float_rd(t[0]), __double2float_rd(t[1]),
-                         __double2float_ru(t[2]), __double2float_ru(t[3]));
+    auto chunk_mask = [&](const float4& tb, int k) -> unsigned long long {  // runtime k
+      const int j = lane + WAVE * k;
+      return __ballot(j < C && hit(tb, j < C ? s_dboxf[cols[j]] : empty, j));
     };
     // pass 1: count candidates per row
     for (int i = wave_id(); i < R; i += WG / WAVE) {
-      const float4 tb = row_boxf(i);
+      const float4 tb = s_tboxf[i];
       int cnt = 0;
-      for (int j0 = 0; j0 < C; j0 += WAVE) cnt += __popcll(__ballot(cand_test(tb, j0 + lane)));
+      if (regcols) {
+#pragma unroll
+        for (int k = 0; k < MAXCH; k++)
+          if (k < nch) cnt += __popcll(__ballot(hit(tb, cb[k], lane + WAVE * k)));
+      } else {
+        for (int k = 0; k < nch; k++) cnt += __popcll(chunk_mask(tb, k));
+      }
       if (lane == 0) s_rowptr[i] = cnt;
     }
     __syncthreads();
     wave0_exclusive_scan(s_rowptr, R);
     __syncthreads();
-    // pass 2: write candidate columns; the row index is parked in the cost slot
+    // pass 2: write candidate columns in column order; the row index is parked in the cost slot
     for (int i = wave_id(); i < R; i += WG / WAVE) {
-      const float4 tb = row_boxf(i);
+      const float4 tb = s_tboxf[i];
       int e = s_rowptr[i];
-      for (int j0 = 0; j0 < C; j0 += WAVE) {
-        const int j = j0 + lane;
-        const bool cand = cand_test(tb, j);
-        const unsigned long long m = __ballot(cand);
-        if (cand) put_edge(e + __popcll(m & ((1ull << lane) - 1ull)), j, (double)i);
+      auto emit = [&](unsigned long long m, int k) {
+        if ((m >> lane) & 1ull)
+          put_edge(e + __popcll(m & ((1ull << lane) - 1ull)), lane + WAVE * k, (double)i);
         e += __popcll(m);
+      };
+      if (regcols) {
+#pragma unroll
+        for (int k = 0; k < MAXCH; k++)
+          if (k < nch) emit(__ballot(hit(tb, cb[k], lane + WAVE * k)), k);
+      } else {
+        for (int k = 0; k < nch; k++) emit(chunk_mask(tb, k), k);
       }
     }
     __syncthreads();
