@@ -17,8 +17,12 @@ constexpr double INF = __builtin_huge_val();
 
 enum : int { KIND_BYTE = 0, KIND_BOT = 1 };
 enum : uint32_t { ST_NEW = 0, ST_TRACKED = 1, ST_LOST = 2, ST_REMOVED = 3 };
-// per-slot persistent flag word
-enum : uint32_t { F_STATE = 0x7u, F_ACT = 0x8u, F_INREM = 0x10u, F_INUSE = 0x20u };
+// per-slot persistent flag word; F_INACT / F_INLOST: the slot is on the active / lost list
+// (lets the slot-parallel kernels select joint(tracked, lost) without walking the lists)
+enum : uint32_t {
+  F_STATE = 0x7u, F_ACT = 0x8u, F_INREM = 0x10u, F_INUSE = 0x20u, F_INACT = 0x40u,
+  F_INLOST = 0x80u
+};
 
 __device__ __forceinline__ uint32_t st_of(uint32_t f) { return f & F_STATE; }
 
@@ -306,33 +310,45 @@ __device__ inline FT wave_norm(const FT* x, int n) {
 // recursion when n = 128 * 2^m (every split lands on a 128-element leaf): accumulator a (leaf
 // a/8, slot a%8) sums x[128*(a/8) + 8i + a%8]^2 over i in order; slots and leaves then combine
 // as balanced binary trees = xor butterflies.  Other n fall back to one lane's sequential walk.
+__host__ __device__ inline bool np_wave_exact(int n) {
+  const int nleaf = n >> 7;
+  return (n & 127) == 0 && nleaf > 0 && (nleaf & (nleaf - 1)) == 0 && nleaf <= 32;
+}
+template <typename XT>
+__device__ inline float np_sumsq_wave_fast(const XT* x, int n) {  // requires np_wave_exact(n)
+  const int lane = threadIdx.x & 63;
+  const int nacc = (n >> 7) * 8;  // 8 .. 256 accumulators
+  const int regs = nacc > 64 ? nacc / 64 : 1;
+  float part[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    part[r] = 0.0f;
+    const int a = lane + 64 * r;
+    if (r < regs && a < nacc) {
+      const XT* p = x + 128 * (a >> 3) + (a & 7);
+      float acc = (float)p[0] * (float)p[0];
+      for (int i = 1; i < 16; i++) { float v = (float)p[8 * i]; acc += v * v; }
+      part[r] = acc;
+    }
+    const int width = nacc < 64 ? nacc : 64;
+    for (int d = 1; d < width; d <<= 1) part[r] += __shfl_xor(part[r], d);
+  }
+  // registers hold consecutive blocks of 8 leaves; combine them as a balanced tree
+  float res = regs == 1 ? part[0]
+              : regs == 2 ? part[0] + part[1]
+                          : (part[0] + part[1]) + (part[2] + part[3]);
+  return __shfl(res, 0);
+}
+// NPF: the caller knows np_wave_exact(n) (compile-time split keeps the sequential fallback and
+// its register footprint out of the fast kernels)
+template <bool NPF, typename XT>
+__device__ inline float np_sumsq_sel(const XT* x, int n) {
+  if constexpr (NPF) return np_sumsq_wave_fast(x, n);
+  else return __shfl(np_pairwise_sumsq_f32(x, n), 0);
+}
 template <typename XT>
 __device__ inline float np_sumsq_wave(const XT* x, int n) {
-  const int lane = threadIdx.x & 63;
-  const int nleaf = n >> 7;
-  if ((n & 127) == 0 && nleaf > 0 && (nleaf & (nleaf - 1)) == 0 && nleaf <= 32) {
-    const int nacc = nleaf * 8;            // 8 .. 256 accumulators
-    const int regs = nacc > 64 ? nacc / 64 : 1;
-    float part[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      part[r] = 0.0f;
-      const int a = lane + 64 * r;
-      if (r < regs && a < nacc) {
-        const XT* p = x + 128 * (a >> 3) + (a & 7);
-        float acc = (float)p[0] * (float)p[0];
-        for (int i = 1; i < 16; i++) { float v = (float)p[8 * i]; acc += v * v; }
-        part[r] = acc;
-      }
-      const int width = nacc < 64 ? nacc : 64;
-      for (int d = 1; d < width; d <<= 1) part[r] += __shfl_xor(part[r], d);
-    }
-    // registers hold consecutive blocks of 8 leaves; combine them as a balanced tree
-    float res = regs == 1 ? part[0]
-                : regs == 2 ? part[0] + part[1]
-                            : (part[0] + part[1]) + (part[2] + part[3]);
-    return __shfl(res, 0);
-  }
+  if (np_wave_exact(n)) return np_sumsq_wave_fast(x, n);
   float s = np_pairwise_sumsq_f32(x, n);
   return __shfl(s, 0);
 }
@@ -417,6 +433,7 @@ struct LapWS {
   uint16_t* touched;      // [C] touched column list
   uint16_t* srlist;       // [R] rows visited (SR) except the root
   int* coldeg;            // [C] finite-edge degree per column (single-edge-component fast path)
+  uint16_t* roots;        // [R] rows left for the Dijkstra phase, ascending
 };
 
 __device__ __forceinline__ void lap_edge(const LapWS& w, int e, int& col, double& cost) {
@@ -473,10 +490,20 @@ __device__ inline void lap_solve_wave(int R, int C, double L, const LapWS& w) {
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  for (int root = 0; root < R; root++) {
-    const int rb = w.row_ptr[root], re = w.row_ptr[root + 1];
-    if (rb == re) continue;  // no admissible edge: stays unmatched (its dummy)
-    if (w.col4row[root] >= 0) continue;  // matched by the single-edge fast path
+  // rows that still need a shortest-path search (have an edge, not fast-matched), ascending:
+  // the serial loop below then touches only those
+  int nroots = 0;
+  for (int c = 0; c < R; c += WAVE) {
+    const int r = c + lane;
+    const bool need = r < R && w.row_ptr[r + 1] > w.row_ptr[r] && w.col4row[r] < 0;
+    const unsigned long long m = __ballot(need);
+    if (need) w.roots[nroots + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)r;
+    nroots += __popcll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  for (int t = 0; t < nroots; t++) {
+    const int root = w.roots[t];
     double minVal = 0.0;
     int i = root;
     int ntouched = 0, nsr = 0;

@@ -1,13 +1,22 @@
-// bx_engine.hip — the per-frame association engine: ONE kernel launch advances one frame of
-// many independent sequences, one 256-thread workgroup per sequence.
+// bx_engine.hip — the per-frame association engine.  One frame of many independent sequences is
+// advanced by a short pipeline of kernels on one stream (bx_engine_step):
 //
-// Everything the reference's ByteTrack.update (trackers/bytetrack/bytetrack.py:158-302) and
-// BotSort.update (trackers/botsort/botsort.py:94-411) do for a frame runs inside that
-// workgroup: detection split, list bookkeeping (joint/sub/remove_duplicate_stracks), batched
-// Kalman predict (+ CMC warp), IoU / score-fusion / re-ID cosine costs, three lapx-semantics
-// assignments, Kalman updates, feature EMA, new-track initiation and output rows.  Track state
-// stays resident in HBM between frames (SoA per sequence); lists, dets and the assignment
-// workspace live in LDS for the frame.
+//   K1 det_feature_kernel   grid, wave per high-conf detection   (BoT-SORT + ReID only)
+//   K2 predict_kernel       grid, thread per track slot           multi_predict (+ multi_gmc)
+//   K3 assoc_kernel         workgroup per sequence                costs, 3 assignments, lists
+//   K4 update_kernel        grid, thread per update record        KF update / initiate, scalars
+//   K5 feature_kernel       grid, wave per record with a feature  feature EMA  (BoT-SORT + ReID)
+//   K6 finish_kernel        workgroup per sequence                remove_duplicate, outputs
+//
+// Together they do what the reference's ByteTrack.update (trackers/bytetrack/bytetrack.py:
+// 158-302) and BotSort.update (trackers/botsort/botsort.py:94-411) do for one frame.  The heavy,
+// regular math (feature normalisation and EMA, Kalman predict/update) runs as full-width grid
+// kernels; only the inherently sequential part of a frame (list bookkeeping, candidate CSR,
+// shortest-augmenting-path assignment) runs one workgroup per sequence, on lean LDS.  Track
+// state stays resident in HBM between frames (SoA per sequence).  Grids put the sequence index
+// in blockIdx.x so that every kernel's workgroups for sequence s land on the same XCD (the
+// dispatcher deals linear workgroup ids round-robin over the 8 XCDs): per-sequence state written
+// by one kernel is re-read by the next from the same L2.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,6 +38,7 @@ constexpr int CLS_HIST = 8;  // BoT-SORT per-track class-history entries (update
 constexpr int ELDS_DEFAULT = 1024;  // LAP edges kept in LDS; the rest spill to global scratch
 constexpr int REG_F = 512;   // feature rows up to this width live in registers: 8 per lane
 constexpr int REG_EPL = REG_F / 64;
+constexpr int NWAVE = WG / WAVE;
 
 // A feature row held by one wave, element q = lane + 64 r in v[r] (F <= REG_F).
 template <typename FT>
@@ -69,15 +79,50 @@ struct RegRow {
   }
   // numpy float32 norm of the float32-cast row (+1e-8 as embedding_distance adds it), staged
   // through this wave's LDS row so lanes can read numpy's accumulator layout
+  template <bool NPF>
   __device__ float np_dn(float* wbuf, int F) const {
     store(wbuf, F);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    float dn = sqrtf(np_sumsq_wave((const float*)wbuf, F)) + 1e-8f;
+    float dn = sqrtf(np_sumsq_sel<NPF>((const float*)wbuf, F)) + 1e-8f;
     __builtin_amdgcn_wave_barrier();
     return dn;
   }
 };
+
+// scipy cdist's two-accumulator inner product (see dot2) of two float32 rows, 16-byte loads
+__device__ inline double dot2_f32(const float* a, const float* b, int n) {
+  double a0 = 0.0, a1 = 0.0;
+  int i = 0;
+  if ((n & 3) == 0) {
+    const float4* a4 = (const float4*)a;
+    const float4* b4 = (const float4*)b;
+    for (; i < n; i += 4) {
+      const float4 x = a4[i >> 2], y = b4[i >> 2];
+      a0 += (double)x.x * (double)y.x;
+      a1 += (double)x.y * (double)y.y;
+      a0 += (double)x.z * (double)y.z;
+      a1 += (double)x.w * (double)y.w;
+    }
+    return a0 + a1;
+  }
+  for (; i + 2 <= n; i += 2) {
+    a0 += (double)a[i] * (double)b[i];
+    a1 += (double)a[i + 1] * (double)b[i + 1];
+  }
+  double s = a0 + a1;
+  if (i < n) s += (double)a[i] * (double)b[i];
+  return s;
+}
+
+// scipy cdist-cosine of two already-normalised float32 rows (matching.py:283-287), max(0, .)
+__device__ inline double cosine_rows(const float* a, double na, const float* b, double nb,
+                                     int F) {
+  double c = dot2_f32(a, b, F) / (na * nb);
+  if (fabs(c) > 1.0) c = copysign(1.0, c);
+  double d = 1.0 - c;
+  return d < 0.0 ? 0.0 : d;
+}
 
 thread_local std::string g_err;
 int set_err(int code, const std::string& msg) {
@@ -91,14 +136,16 @@ int set_err(int code, const std::string& msg) {
       return set_err(BX_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(_e));          \
   } while (0)
 
-// Device-side view of an engine (passed by value to the frame kernel).
+// Device-side view of an engine (passed by value to every kernel).
 struct Dev {
   int S, T, D, F, kind, emb_f64, with_reid, fuse_first, max_time_lost, elds;
   double low, high, new_thresh, match_thresh, prox, app;
-  int* seq;           // [S][8]: n_active, n_lost, frame_count, id_count, status
-  uint16_t* act;      // [S][T]
-  uint16_t* lost;     // [S][T]
-  uint32_t* flags;    // [S][T]
+  int* seq;           // [S][SQ_STRIDE] per-sequence scalars (SQ_*)
+  uint16_t* act;      // [S][T] active list (slots)
+  uint16_t* lost;     // [S][T] lost list
+  uint16_t* act2;     // [S][T] frame scratch: lists before remove_duplicate (K3 → K6)
+  uint16_t* lost2;    // [S][T]
+  uint32_t* flags;    // [S][T] F_* bits
   int* frame_id;      // [S][T]
   int* start;         // [S][T]
   int* id;            // [S][T]
@@ -108,14 +155,17 @@ struct Dev {
   double* cls;        // [S][T]
   double* mean;       // [S][8][T]
   double* cov;        // [S][64][T]
-  void* feat;         // [S][T][F]
+  void* feat;         // [S][T][F] smooth_feat
   double* clsh;       // [S][T][CLS_HIST][2]
   int* ncls;          // [S][T]
   uint16_t* gcol;     // [S][T*D] LAP edge overflow
   double* gcost;      // [S][T*D]
-  void* df2;          // [S][D][F] frame scratch: detection features after STrack.__init__
+  int2* rec;          // [S][D] frame scratch: update records (K3 → K4/K5)
+  double* dnrm;       // [S][D][2] frame scratch: n1, n2 of STrack.update_features per det
+  double* dnb;        // [S][D] frame scratch: cdist norm of each dB row
   float* dB;          // [S][D][F] frame scratch: det rows as embedding_distance normalises them
   float* tA;          // [S][T][F] frame scratch: track rows as embedding_distance normalises them
+  void* fscr;         // [S][D][F] frame scratch for F > REG_F only: twice-normalised det rows
   int* status;        // [1] latched engine status
   unsigned long long* dbg;  // [S][32] phase stamps (diagnostic builds only, else null)
 };
@@ -133,57 +183,54 @@ struct Dev {
   } while (0)
 #endif
 
-enum { SQ_NA = 0, SQ_NL = 1, SQ_FC = 2, SQ_IDC = 3, SQ_STATUS = 4, SQ_STRIDE = 8 };
+enum {
+  SQ_NA = 0, SQ_NL, SQ_FC, SQ_IDC, SQ_STATUS, SQ_NA2, SQ_NL2, SQ_NREC, SQ_SKIP,
+  SQ_STRIDE = 16
+};
+// update records: x = slot | kind << 16, y = detection index within the sequence's frame
+enum : int { R_UPDATE = 0, R_REACT = 1, R_NEW = 2, R_FEAT = 4 };
 
-// LDS carve-out (host and device agree on it).
-struct Lds {
-  size_t o_act, o_lost, o_tracked, o_unconf, o_pool, o_rtr, o_lostl, o_refind, o_fa, o_fl,
-      o_newt, o_flags, o_fid, o_mark, o_rowptr, o_c4r, o_u, o_srl, o_r4c, o_v, o_spc, o_path,
-      o_colf, o_touch, o_dbox, o_dconf, o_dkind, o_hd, o_sd, o_rem, o_ecol, o_ecost, o_tdn,
-      o_tna, o_ddn, o_dnb, o_ints, o_cdeg, o_wbuf, o_tbox, o_dboxf, o_tboxf, total;
-  __host__ __device__ Lds(int T, int D, int elds, int F) {
+// LDS carve-out of the association kernel (host and device agree on it).
+struct LdsA {
+  size_t o_dbox, o_dboxf, o_dconf, o_tboxf, o_u, o_v, o_spc, o_ecost, o_tna, o_flags, o_fid,
+      o_rowptr, o_ints, o_act, o_lost, o_unconf, o_pool, o_rtr, o_lostl, o_refind, o_newt,
+      o_c4r, o_srl, o_roots, o_r4c, o_path, o_touch, o_cdeg, o_hd, o_sd, o_rem, o_ecol, o_mark,
+      o_colf, o_dkind, total;
+  __host__ __device__ LdsA(int T, int D, int elds) {
     size_t o = 0;
     auto take = [&](size_t bytes) {
       size_t r = o;
       o += (bytes + 15) & ~size_t(15);
       return r;
     };
-    int R = T > D ? T : D;  // assignment rows/cols never exceed these
     o_dbox = take(sizeof(double) * 4 * D);
-    o_tbox = take(sizeof(double) * 4 * T);  // row boxes of the current association / dedup
-    o_dconf = take(sizeof(double) * D);
     o_dboxf = take(sizeof(float) * 4 * D);  // outward-rounded fp32 copy for candidate tests
     o_tboxf = take(sizeof(float) * 4 * T);  // same for the rows of the current association
+    o_dconf = take(sizeof(double) * D);
     o_u = take(sizeof(double) * T);
     o_v = take(sizeof(double) * D);
     o_spc = take(sizeof(double) * D);
     o_ecost = take(sizeof(double) * elds);
     o_tna = take(sizeof(double) * T);
-    o_dnb = take(sizeof(double) * D);
     o_flags = take(sizeof(uint32_t) * T);
     o_fid = take(sizeof(int) * T);
     o_rowptr = take(sizeof(int) * (T + 1));
-    o_tdn = o_ddn = 0;  // (unused: the norms are folded into the dB/tA rows)
+    o_cdeg = take(4 * D);
     o_ints = take(sizeof(int) * 64);
     o_act = take(2 * T);
     o_lost = take(2 * T);
-    o_tracked = take(2 * T);
     o_unconf = take(2 * T);
     o_pool = take(2 * T);
     o_rtr = take(2 * T);
     o_lostl = take(2 * T);
     o_refind = take(2 * T);
-    o_fa = take(2 * T);
-    o_fl = take(2 * T);
-    o_newt = take(2 * D);
     o_c4r = take(2 * T);
     o_srl = take(2 * T);
+    o_roots = take(2 * T);
+    o_newt = take(2 * D);
     o_r4c = take(2 * D);
     o_path = take(2 * D);
     o_touch = take(2 * D);
-    o_cdeg = take(4 * D);
-    // per-wave float32 staging row for numpy's pairwise norm (register fast path, F <= 512)
-    o_wbuf = take(F > 0 && F <= REG_F ? sizeof(float) * 4 * F : 0);
     o_hd = take(2 * D);
     o_sd = take(2 * D);
     o_rem = take(2 * D);
@@ -191,86 +238,200 @@ struct Lds {
     o_mark = take(T);
     o_colf = take(D);
     o_dkind = take(D);
-    (void)R;
+    total = o;
+  }
+};
+
+// LDS carve-out of the finishing kernel.
+struct LdsF {
+  size_t o_lbox, o_lage, o_fa, o_fl, o_dupa, o_dupl, o_keep, o_ints, total;
+  __host__ __device__ LdsF(int T) {
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+      size_t r = o;
+      o += (bytes + 15) & ~size_t(15);
+      return r;
+    };
+    o_lbox = take(sizeof(double) * 4 * T);
+    o_lage = take(sizeof(int) * T);
+    o_fa = take(2 * T);
+    o_fl = take(2 * T);
+    o_dupa = take(T);
+    o_dupl = take(T);
+    o_keep = take(T);
+    o_ints = take(sizeof(int) * 16);
     total = o;
   }
 };
 
 // mark bits (per slot, per frame)
-enum : uint8_t { M_POOL = 1, M_ACT2 = 2, M_REMNOW = 4, M_DUP = 8, M_KEEP = 16, M_TMP = 32 };
+enum : uint8_t { M_POOL = 1, M_ACT2 = 2, M_REMNOW = 4, M_TMP = 32 };
 // ints[] scratch slots
-enum {
-  I_NA = 0, I_NL, I_FC, I_IDC, I_N, I_DH, I_DS, I_NTR, I_NUN, I_NPOOL, I_NRTR, I_NLOSTL,
-  I_NREF, I_NREM, I_NNEW, I_NFA, I_NFL, I_E, I_ERR, I_NACT0, I_NOUT, I_NFREE, I_SCAN = 32
-};
+enum { I_NA = 0, I_NL, I_FC, I_IDC, I_ERR, I_SCAN = 32 };
 
-template <typename FT>
-struct FeatView {
-  const FT* p;
-  __device__ double operator()(int i) const { return (double)p[i]; }
-};
+// STrack.xyxy of a track (mean-based): KF mean (x, y, a|w, h) → xyxy
+template <int KIND>
+__device__ __forceinline__ void track_box(const double* g_mean, int T, int slot, double* box) {
+  double r[4] = {g_mean[slot], g_mean[T + slot], g_mean[2 * T + slot], g_mean[3 * T + slot]};
+  if (KIND == KIND_BYTE) r[2] *= r[3];
+  xywh2xyxy(r, box);
+}
 
-// Normalised-float32 view used by matching.embedding_distance: x / (||x||_np + 1e-8) in f32.
-template <typename FT>
-struct NormF32View {
-  const FT* p;
-  float dn;
-  __device__ double operator()(int i) const { return (double)((float)p[i] / dn); }
-};
-
-struct F32Row {
-  const float* p;
-  __device__ double operator()(int i) const { return (double)p[i]; }
-};
-
-// scipy cdist-cosine of two already-normalised float32 rows (matching.py:283-287), max(0, .)
-__device__ inline double cosine_rows(const float* a, double na, const float* b, double nb,
-                                     int F) {
-  F32Row A{a}, B{b};
-  double c = dot2(A, B, F) / (na * nb);
-  if (fabs(c) > 1.0) c = copysign(1.0, c);
-  double d = 1.0 - c;
-  return d < 0.0 ? 0.0 : d;
+// measurement vector of a detection row (float32 as setup_decorator left it)
+template <int KIND>
+__device__ __forceinline__ void det_measurement(const float* r, double* meas) {
+  double xyxy[4] = {(double)r[0], (double)r[1], (double)r[2], (double)r[3]};
+  double xywh[4];
+  xyxy2xywh(xyxy, xywh);
+  if (KIND == KIND_BYTE) {
+    double tlwh[4];
+    xywh2tlwh(xywh, tlwh);
+    tlwh2xyah(tlwh, meas);
+  } else {
+    for (int q = 0; q < 4; q++) meas[q] = xywh[q];
+  }
 }
 
 // ------------------------------------------------------------------------------------------
-template <int KIND, typename FT>
-__global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float* __restrict__ dets,
-                                                   const int* __restrict__ det_off,
-                                                   const FT* __restrict__ embs,
-                                                   const double* __restrict__ warps,
-                                                   double* __restrict__ out,
-                                                   int* __restrict__ out_count) {
+// K1: BoT-SORT detection features.  STrack(det, feat) → update_features: f1 = f/|f|,
+// f2 = f1/|f1| (botsort_track.py:40-49; curr == smooth for a fresh track), then the float32 row
+// embedding_distance builds from it, B = (float)f2 / (|.|_np + 1e-8) (matching.py:266-287), and
+// scipy cdist's own norm of B.  The two norms n1, n2 are kept so K5 can recompute f2 bitwise
+// from the input row instead of storing it.  Grid (n_seq, ceil(D/4)); one wave per detection.
+template <typename FT, bool NPF>
+__global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
+                                                         const float* __restrict__ dets,
+                                                         const int* __restrict__ det_off,
+                                                         const FT* __restrict__ embs) {
+  __shared__ __align__(16) float s_w[NWAVE * REG_F];
+  const int b = blockIdx.x, s = seq0 + b, w = wave_id(), lane = lane_id();
+  const int F = P.F, D = P.D;
+  const int d0 = det_off[b], N = min(det_off[b + 1] - d0, D);
+  const int k = blockIdx.y * NWAVE + w;
+  if (k >= N) return;  // wave-uniform
+  if (!((double)dets[(size_t)(d0 + k) * 6 + 4] > P.high)) return;
+  const FT* f = embs + (size_t)(d0 + k) * F;
+  float* Bk = P.dB + ((size_t)s * D + k) * F;
+  FT n1, n2;
+  if (F <= REG_F) {
+    float* wb = s_w + w * REG_F;
+    RegRow<FT> x;
+    x.load(f, F);
+    n1 = x.norm(F);
+    x.div(n1);
+    n2 = x.norm(F);
+    x.div(n2);
+    const float dn = x.template np_dn<NPF>(wb, F);
+#pragma unroll
+    for (int r = 0; r < REG_EPL; r++) {
+      const int q = lane + 64 * r;
+      if (q < F) {
+        const float bq = (float)x.v[r] / dn;
+        Bk[q] = bq;
+        wb[q] = bq;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) P.dnb[(size_t)s * D + k] = sqrt(dot2_f32(wb, wb, F));
+  } else {
+    FT* f2 = (FT*)P.fscr + ((size_t)s * D + k) * F;
+    n1 = wave_norm(f, F);
+    for (int q = lane; q < F; q += WAVE) f2[q] = f[q] / n1;
+    n2 = wave_norm((const FT*)f2, F);  // same lane mapping: reads own writes
+    for (int q = lane; q < F; q += WAVE) f2[q] = f2[q] / n2;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // other lanes read f2 next
+    const float dn = sqrtf(np_sumsq_sel<NPF>((const FT*)f2, F)) + 1e-8f;
+    for (int q = lane; q < F; q += WAVE) Bk[q] = (float)f2[q] / dn;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (lane == 0) P.dnb[(size_t)s * D + k] = sqrt(dot2_f32(Bk, Bk, F));
+  }
+  if (lane == 0) {
+    P.dnrm[((size_t)s * D + k) * 2] = (double)n1;
+    P.dnrm[((size_t)s * D + k) * 2 + 1] = (double)n2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K2: STrack.multi_predict over strack_pool = joint(tracked, lost) (bytetrack.py:205-207,
+// botsort.py:188-189) and, for BoT-SORT with a CMC warp, multi_gmc over the pool and the
+// unconfirmed tracks (botsort.py:192-195).  Grid (n_seq, ceil(T/256)); thread per slot.
+template <int KIND, bool GMC>
+__global__ __launch_bounds__(WG) void predict_kernel(Dev P, int seq0,
+                                                     const double* __restrict__ warps) {
+  const int b = blockIdx.x, s = seq0 + b, T = P.T;
+  const int slot = blockIdx.y * WG + threadIdx.x;
+  if (slot >= T) return;
+  const uint32_t f = P.flags[(size_t)s * T + slot];
+  const bool pool = ((f & F_INACT) && (f & F_ACT)) || (f & F_INLOST);
+  const bool unconf = (f & F_INACT) && !(f & F_ACT);
+  const double* H = GMC ? warps + 6 * (size_t)b : nullptr;
+  if (!pool && !(GMC && unconf)) return;
+  double* m = P.mean + (size_t)s * 8 * T + slot;
+  double* c = P.cov + (size_t)s * 64 * T + slot;
+  if (pool) {
+    if (st_of(f) != ST_TRACKED) {
+      if (KIND == KIND_BOT) m[6 * T] = 0.0;
+      m[7 * T] = 0.0;
+    }
+    kf_predict_soa(KIND, m, c, T);
+  }
+  if (GMC) {  // R8 = kron(I4, R): mean = R8·mean + t, cov = R8·cov·R8ᵀ
+    double mm[8];
+    for (int q = 0; q < 8; q++) mm[q] = m[q * T];
+    for (int q = 0; q < 4; q++) {
+      double a0 = H[0] * mm[2 * q] + H[1] * mm[2 * q + 1];
+      double a1 = H[3] * mm[2 * q] + H[4] * mm[2 * q + 1];
+      mm[2 * q] = a0;
+      mm[2 * q + 1] = a1;
+    }
+    mm[0] += H[2];
+    mm[1] += H[5];
+    for (int q = 0; q < 8; q++) m[q * T] = mm[q];
+    double RP[64];
+    for (int bq = 0; bq < 4; bq++)
+      for (int cc = 0; cc < 8; cc++) {
+        double x0 = c[(8 * (2 * bq) + cc) * T], x1 = c[(8 * (2 * bq + 1) + cc) * T];
+        RP[8 * (2 * bq) + cc] = H[0] * x0 + H[1] * x1;
+        RP[8 * (2 * bq + 1) + cc] = H[3] * x0 + H[4] * x1;
+      }
+    for (int r = 0; r < 8; r++)
+      for (int bq = 0; bq < 4; bq++) {
+        double y0 = RP[8 * r + 2 * bq], y1 = RP[8 * r + 2 * bq + 1];
+        c[(8 * r + 2 * bq) * T] = y0 * H[0] + y1 * H[1];
+        c[(8 * r + 2 * bq + 1) * T] = y0 * H[3] + y1 * H[4];
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K3: the sequential heart of a frame, one workgroup per sequence: detection split, track lists,
+// the three assignments (candidate CSR, exact fp64 costs, lapx-semantics LAP), state/list
+// bookkeeping, id allocation.  Kalman/feature work is emitted as update records for K4/K5.
+template <int KIND, typename FT, bool NPF>
+__global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float* __restrict__ dets,
+                                                   const int* __restrict__ det_off) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int T = P.T, D = P.D, F = P.F;
-  const Lds Lo(T, D, P.elds, F);
-  float* s_wbuf = (float*)(smem + Lo.o_wbuf) + (size_t)wave_id() * (F <= REG_F ? F : 0);
+  const LdsA Lo(T, D, P.elds);
   uint16_t* s_act = (uint16_t*)(smem + Lo.o_act);
   uint16_t* s_lost = (uint16_t*)(smem + Lo.o_lost);
-  uint16_t* s_tracked = (uint16_t*)(smem + Lo.o_tracked);
   uint16_t* s_unconf = (uint16_t*)(smem + Lo.o_unconf);
   uint16_t* s_pool = (uint16_t*)(smem + Lo.o_pool);
   uint16_t* s_rtr = (uint16_t*)(smem + Lo.o_rtr);
   uint16_t* s_lostl = (uint16_t*)(smem + Lo.o_lostl);
   uint16_t* s_refind = (uint16_t*)(smem + Lo.o_refind);
-  uint16_t* s_fa = (uint16_t*)(smem + Lo.o_fa);
-  uint16_t* s_fl = (uint16_t*)(smem + Lo.o_fl);
   uint16_t* s_newt = (uint16_t*)(smem + Lo.o_newt);
   uint32_t* s_flags = (uint32_t*)(smem + Lo.o_flags);
   int* s_fid = (int*)(smem + Lo.o_fid);
   uint8_t* s_mark = (uint8_t*)(smem + Lo.o_mark);
   int* s_rowptr = (int*)(smem + Lo.o_rowptr);
   int16_t* s_c4r = (int16_t*)(smem + Lo.o_c4r);
-  double* s_u = (double*)(smem + Lo.o_u);
   uint16_t* s_srl = (uint16_t*)(smem + Lo.o_srl);
   int16_t* s_r4c = (int16_t*)(smem + Lo.o_r4c);
-  double* s_v = (double*)(smem + Lo.o_v);
-  double* s_spc = (double*)(smem + Lo.o_spc);
-  int16_t* s_path = (int16_t*)(smem + Lo.o_path);
-  uint8_t* s_colf = (uint8_t*)(smem + Lo.o_colf);
-  uint16_t* s_touch = (uint16_t*)(smem + Lo.o_touch);
   double* s_dbox = (double*)(smem + Lo.o_dbox);
   float4* s_dboxf = (float4*)(smem + Lo.o_dboxf);
+  float4* s_tboxf = (float4*)(smem + Lo.o_tboxf);
   double* s_dconf = (double*)(smem + Lo.o_dconf);
   uint8_t* s_dkind = (uint8_t*)(smem + Lo.o_dkind);
   uint16_t* s_hd = (uint16_t*)(smem + Lo.o_hd);
@@ -279,7 +440,6 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   uint16_t* s_ecol = (uint16_t*)(smem + Lo.o_ecol);
   double* s_ecost = (double*)(smem + Lo.o_ecost);
   double* s_tna = (double*)(smem + Lo.o_tna);
-  double* s_dnb = (double*)(smem + Lo.o_dnb);
   int* I = (int*)(smem + Lo.o_ints);
   int* scan_tmp = I + I_SCAN;
 
@@ -290,24 +450,13 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   int* seq = P.seq + (size_t)s * SQ_STRIDE;
   uint32_t* g_flags = P.flags + sT;
   int* g_fid = P.frame_id + sT;
-  int* g_start = P.start + sT;
-  int* g_id = P.id + sT;
-  int* g_tlen = P.tlen + sT;
-  int* g_detind = P.detind + sT;
-  double* g_conf = P.conf + sT;
-  double* g_cls = P.cls + sT;
-  double* g_mean = P.mean + (size_t)s * 8 * T;
-  double* g_cov = P.cov + (size_t)s * 64 * T;
-  FT* g_feat = (FT*)P.feat + (size_t)s * T * F;
-  FT* g_df2 = (FT*)P.df2 + (size_t)s * D * F;
-  double* g_clsh = P.clsh + sT * CLS_HIST * 2;
-  int* g_ncls = P.ncls + sT;
-  const int kf = KIND;  // KIND_BYTE → XYAH, KIND_BOT → XYWH
+  const double* g_mean = P.mean + (size_t)s * 8 * T;
+  const FT* g_feat = (const FT*)P.feat + (size_t)s * T * F;
+  int2* g_rec = P.rec + (size_t)s * D;
   const bool REID = (KIND == KIND_BOT) && P.with_reid;
 
   const int d0 = det_off[b], N = det_off[b + 1] - det_off[b];
   const float* fdets = dets + (size_t)d0 * 6;
-  const FT* fembs = REID ? embs + (size_t)d0 * F : nullptr;
 
   BX_STAMP(0);
   // ---------------- P0: sequence state → LDS
@@ -316,13 +465,16 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
     I[I_NL] = seq[SQ_NL];
     I[I_FC] = seq[SQ_FC] + 1;
     I[I_IDC] = seq[SQ_IDC];
-    I[I_N] = N;
     I[I_ERR] = 0;
   }
   __syncthreads();
   const int na = I[I_NA], nl = I[I_NL], fc = I[I_FC];
-  if (N > D) {  // host checks det_cap; never trust it blindly
-    if (tid == 0) { out_count[b] = 0; atomicOr(P.status, 1 << BX_ERR_CAPACITY); }
+  if (N > D || N < 0) {  // host checks det_cap; never trust it blindly
+    if (tid == 0) {
+      seq[SQ_SKIP] = 1;
+      seq[SQ_NREC] = 0;
+      atomicOr(P.status, 1 << BX_ERR_CAPACITY);
+    }
     return;
   }
   for (int k = tid; k < na; k += WG) s_act[k] = P.act[sT + k];
@@ -356,130 +508,31 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   const int Ds = block_compact(N, [&](int k) { return s_dkind[k] == 2; },
                                [&](int k, int p) { s_sd[p] = (uint16_t)k; }, scan_tmp);
 
-  // BoT-SORT: STrack(det, feat) → update_features: f1 = f/|f|, f2 = f1/|f1| (curr == smooth),
-  // plus the float32 norms embedding_distance will need for the det side.
-  if (REID) {
-    // one wave per detection row (lane-strided, coalesced)
-    if (F <= REG_F) {  // whole row in registers: one load, two stores; next row prefetched
-      const int lane = lane_id();
-      int p = wave_id();
-      RegRow<FT> x;
-      if (p < Dh) x.load(fembs + (size_t)s_hd[p] * F, F);
-      for (; p < Dh; p += WG / WAVE) {
-        const int k = s_hd[p], pn = p + WG / WAVE;
-        RegRow<FT> nx;
-        if (pn < Dh) nx.load(fembs + (size_t)s_hd[pn] * F, F);
-        x.div(x.norm(F));
-        x.div(x.norm(F));
-        x.store(g_df2 + (size_t)k * F, F);
-        const float dn = x.np_dn(s_wbuf, F);
-        float* Bk = P.dB + ((size_t)s * D + k) * F;
-#pragma unroll
-        for (int r = 0; r < REG_EPL; r++) {
-          const int q = lane + 64 * r;
-          if (q < F) Bk[q] = (float)x.v[r] / dn;
-        }
-        x = nx;
-      }
-    }
-    for (int p = wave_id(); p < (F <= REG_F ? 0 : Dh); p += WG / WAVE) {
-      const int k = s_hd[p], lane = lane_id();
-      const FT* f = fembs + (size_t)k * F;
-      FT* f2 = g_df2 + (size_t)k * F;
-      const FT n1 = wave_norm(f, F);
-      for (int q = lane; q < F; q += WAVE) f2[q] = f[q] / n1;
-      const FT n2 = wave_norm((const FT*)f2, F);  // same lane mapping: reads own writes
-      for (int q = lane; q < F; q += WAVE) f2[q] = f2[q] / n2;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // other lanes read f2 next
-      const float dn = sqrtf(np_sumsq_wave(f2, F)) + 1e-8f;
-      float* Bk = P.dB + ((size_t)s * D + k) * F;
-      for (int q = lane; q < F; q += WAVE) Bk[q] = (float)f2[q] / dn;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __syncthreads();
-    // scipy cdist's norm of each normalised row: its own two-accumulator sequential order
-    for (int p = tid; p < Dh; p += WG) {
-      const int k = s_hd[p];
-      const float* Bk = P.dB + ((size_t)s * D + k) * F;
-      F32Row B{Bk};
-      s_dnb[k] = sqrt(dot2(B, B, F));
-    }
-  }
-
   BX_STAMP(1);
-  // ---------------- P2: tracked / unconfirmed / strack_pool = joint(tracked, lost)
+  // ---------------- P2: unconfirmed / strack_pool = joint(tracked, lost)
   const int ntr = block_compact(na, [&](int k) { return (s_flags[s_act[k]] & F_ACT) != 0; },
-                                [&](int k, int p) { s_tracked[p] = s_act[k]; }, scan_tmp);
+                                [&](int k, int p) {
+                                  s_pool[p] = s_act[k];
+                                  s_mark[s_act[k]] |= M_POOL;
+                                },
+                                scan_tmp);
   const int nun = block_compact(na, [&](int k) { return (s_flags[s_act[k]] & F_ACT) == 0; },
                                 [&](int k, int p) { s_unconf[p] = s_act[k]; }, scan_tmp);
-  for (int k = tid; k < ntr; k += WG) {
-    s_pool[k] = s_tracked[k];
-    s_mark[s_tracked[k]] |= M_POOL;
-  }
-  __syncthreads();
   const int npl = block_compact(nl, [&](int k) { return !(s_mark[s_lost[k]] & M_POOL); },
                                 [&](int k, int p) { s_pool[ntr + p] = s_lost[k]; }, scan_tmp);
   const int npool = ntr + npl;
   for (int k = tid; k < npool; k += WG) s_mark[s_pool[k]] &= ~M_POOL;
-
   BX_STAMP(2);
-  // ---------------- P3: multi_predict (+ BoT-SORT multi_gmc on pool and unconfirmed)
-  const double* H = (KIND == KIND_BOT && warps) ? warps + 6 * (size_t)b : nullptr;
-  for (int k = tid; k < npool + ((KIND == KIND_BOT) ? nun : 0); k += WG) {
-    const bool is_pool = k < npool;
-    const int slot = is_pool ? s_pool[k] : s_unconf[k - npool];
-    double* m = g_mean + slot;
-    double* c = g_cov + slot;
-    if (is_pool) {
-      if (st_of(s_flags[slot]) != ST_TRACKED) {
-        if (KIND == KIND_BOT) m[6 * T] = 0.0;
-        m[7 * T] = 0.0;
-      }
-      kf_predict_soa(kf, m, c, T);
-    }
-    if (H) {  // R8 = kron(I4, R): mean = R8·mean + t, cov = R8·cov·R8ᵀ
-      double mm[8];
-      for (int q = 0; q < 8; q++) mm[q] = m[q * T];
-      for (int q = 0; q < 4; q++) {
-        double a0 = H[0] * mm[2 * q] + H[1] * mm[2 * q + 1];
-        double a1 = H[3] * mm[2 * q] + H[4] * mm[2 * q + 1];
-        mm[2 * q] = a0;
-        mm[2 * q + 1] = a1;
-      }
-      mm[0] += H[2];
-      mm[1] += H[5];
-      for (int q = 0; q < 8; q++) m[q * T] = mm[q];
-      double RP[64];
-      for (int bq = 0; bq < 4; bq++)
-        for (int cc = 0; cc < 8; cc++) {
-          double x0 = c[(8 * (2 * bq) + cc) * T], x1 = c[(8 * (2 * bq + 1) + cc) * T];
-          RP[8 * (2 * bq) + cc] = H[0] * x0 + H[1] * x1;
-          RP[8 * (2 * bq + 1) + cc] = H[3] * x0 + H[4] * x1;
-        }
-      for (int r = 0; r < 8; r++)
-        for (int bq = 0; bq < 4; bq++) {
-          double y0 = RP[8 * r + 2 * bq], y1 = RP[8 * r + 2 * bq + 1];
-          c[(8 * r + 2 * bq) * T] = y0 * H[0] + y1 * H[1];
-          c[(8 * r + 2 * bq + 1) * T] = y0 * H[3] + y1 * H[4];
-        }
-    }
-  }
-  __syncthreads();
-
-  // track box (STrack.xyxy) from the current mean
-  auto track_box = [&](int slot, double* box) {
-    double r[4] = {g_mean[slot], g_mean[T + slot], g_mean[2 * T + slot], g_mean[3 * T + slot]};
-    if (KIND == KIND_BYTE) r[2] *= r[3];
-    xywh2xyxy(r, box);
-  };
 
   // LAP workspace (rows use s_c4r/s_u/s_srl, columns s_r4c/s_v/s_spc/...)
   LapWS W;
   W.row_ptr = s_rowptr; W.ecol = s_ecol; W.ecost = s_ecost;
   W.gcol = P.gcol + (size_t)s * T * D; W.gcost = P.gcost + (size_t)s * T * D;
-  W.elds = P.elds; W.col4row = s_c4r; W.row4col = s_r4c; W.u = s_u; W.v = s_v;
-  W.spc = s_spc; W.path = s_path; W.colflag = s_colf; W.touched = s_touch; W.srlist = s_srl;
-  W.coldeg = (int*)(smem + Lo.o_cdeg);
+  W.elds = P.elds; W.col4row = s_c4r; W.row4col = s_r4c;
+  W.u = (double*)(smem + Lo.o_u); W.v = (double*)(smem + Lo.o_v);
+  W.spc = (double*)(smem + Lo.o_spc); W.path = (int16_t*)(smem + Lo.o_path);
+  W.colflag = (uint8_t*)(smem + Lo.o_colf); W.touched = (uint16_t*)(smem + Lo.o_touch);
+  W.srlist = s_srl; W.coldeg = (int*)(smem + Lo.o_cdeg); W.roots = (uint16_t*)(smem + Lo.o_roots);
   uint16_t* e_gcol = P.gcol + (size_t)s * T * D;
   double* e_gcost = P.gcost + (size_t)s * T * D;
   auto put_edge = [&](int e, int col, double cost) {
@@ -515,14 +568,11 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
     // outward-rounded boxes (never misses an fp64-intersecting pair); a row's candidates keep
     // column order (ballot prefix).  Exact fp64 costs are then computed once per candidate with
     // every lane busy; candidates that turn out inadmissible stay in the CSR with cost INF,
-    // which the solver treats as absent.  Row boxes are gathered into LDS first.
-    // Lanes own columns: a lane keeps the boxes of its columns j = lane + 64k (k < 4, i.e.
-    // C <= 256) in registers for the whole row sweep, so a row costs one broadcast LDS read.
-    double* s_tbox = (double*)(smem + Lo.o_tbox);
-    float4* s_tboxf = (float4*)(smem + Lo.o_tboxf);
+    // which the solver treats as absent.  Lanes own columns: a lane keeps the boxes of its
+    // columns j = lane + 64k (k < 4, i.e. C <= 256) in registers for the whole row sweep.
     for (int i = tid; i < R; i += WG) {
-      double* t = s_tbox + 4 * i;
-      track_box(rows[i], t);
+      double t[4];
+      track_box<KIND>(g_mean, T, rows[i], t);
       s_tboxf[i] = make_float4(__double2float_rd(t[0]), __double2float_rd(t[1]),
                                __double2float_ru(t[2]), __double2float_ru(t[3]));
       s_srl[i] = 0;  // "row has a gated edge" flag; the LAP reuses s_srl afterwards
@@ -548,7 +598,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
       return __ballot(j < C && hit(tb, j < C ? s_dboxf[cols[j]] : empty, j));
     };
     // pass 1: count candidates per row
-    for (int i = wave_id(); i < R; i += WG / WAVE) {
+    for (int i = wave_id(); i < R; i += NWAVE) {
       const float4 tb = s_tboxf[i];
       int cnt = 0;
       if (regcols) {
@@ -564,7 +614,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
     wave0_exclusive_scan(s_rowptr, R);
     __syncthreads();
     // pass 2: write candidate columns in column order; the row index is parked in the cost slot
-    for (int i = wave_id(); i < R; i += WG / WAVE) {
+    for (int i = wave_id(); i < R; i += NWAVE) {
       const float4 tb = s_tboxf[i];
       int e = s_rowptr[i];
       auto emit = [&](unsigned long long m, int k) {
@@ -582,49 +632,40 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
     }
     __syncthreads();
     // pass 3: exact fp64 cost per candidate (gated ones flagged in the column's top bit)
-    for (int e = tid; e < s_rowptr[R]; e += WG) {
+    const int E = s_rowptr[R];
+    for (int e = tid; e < E; e += WG) {
       int j;
       double ri;
       get_edge(e, j, ri);
       const int i = (int)ri;
+      double tb[4];
+      track_box<KIND>(g_mean, T, rows[i], tb);
       bool g, cand;
-      const double c = pair_cost(s_tbox + 4 * i, cols[j], g, cand);
+      const double c = pair_cost(tb, cols[j], g, cand);
       put_edge(e, (g && cand) ? (j | 0x8000) : j, cand ? c : INF);
       if (g && cand) s_srl[i] = 1;
     }
     __syncthreads();
     if (reid) {
-      // track rows as embedding_distance sees them: float32 smooth_feat / (np norm + 1e-8)
-      for (int i = wave_id(); i < R; i += WG / WAVE) {
+      // track rows as embedding_distance sees them: float32 smooth_feat / (np norm + 1e-8),
+      // one wave per row that has a gated edge
+      for (int i = wave_id(); i < R; i += NWAVE) {
         if (!s_srl[i]) continue;  // wave-uniform
-        const int slot = rows[i], lane = lane_id();
-        const FT* tf = g_feat + (size_t)slot * F;
-        float* A = P.tA + ((size_t)s * T + slot) * F;
-        if (F <= REG_F) {
-          RegRow<FT> x;
-          x.load(tf, F);
-          const float dn = x.np_dn(s_wbuf, F);
-#pragma unroll
-          for (int r = 0; r < REG_EPL; r++) {
-            const int q = lane + 64 * r;
-            if (q < F) A[q] = (float)x.v[r] / dn;
-          }
-          continue;
-        }
-        const float dn = sqrtf(np_sumsq_wave(tf, F)) + 1e-8f;
+        const FT* tf = g_feat + (size_t)rows[i] * F;
+        float* A = P.tA + ((size_t)s * T + rows[i]) * F;
+        const float dn = sqrtf(np_sumsq_sel<NPF>(tf, F)) + 1e-8f;
         for (int q = lane; q < F; q += WAVE) A[q] = (float)tf[q] / dn;
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       __syncthreads();
       for (int i = tid; i < R; i += WG) {
         if (!s_srl[i]) continue;
-        F32Row A{P.tA + ((size_t)s * T + rows[i]) * F};
-        s_tna[rows[i]] = sqrt(dot2(A, A, F));
+        const float* A = P.tA + ((size_t)s * T + rows[i]) * F;
+        s_tna[i] = sqrt(dot2_f32(A, A, F));
       }
       __syncthreads();
       // emb_dists = cdist/2; > appearance_thresh → 1; (not gated → 1); dists = min(iou, emb)
-      const int E = s_rowptr[R];
-      // thread per edge: find its row by binary search over row_ptr
+      // thread per gated edge; its row found by binary search over row_ptr
       for (int e = tid; e < E; e += WG) {
         int col;
         double c;
@@ -635,9 +676,10 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
           int mid = (lo + hi) >> 1;
           if (s_rowptr[mid] <= e) lo = mid; else hi = mid;
         }
-        const int slot = rows[lo], j = col & 0x7fff, dk = cols[j];
-        double ed = cosine_rows(P.tA + ((size_t)s * T + slot) * F, s_tna[slot],
-                                P.dB + ((size_t)s * D + dk) * F, s_dnb[dk], F) / 2.0;
+        const int j = col & 0x7fff, dk = cols[j];
+        double ed = cosine_rows(P.tA + ((size_t)s * T + rows[lo]) * F, s_tna[lo],
+                                P.dB + ((size_t)s * D + dk) * F, P.dnb[(size_t)s * D + dk],
+                                F) / 2.0;
         if (ed > P.app) ed = 1.0;
         double cm = c < ed ? c : ed;  // np.minimum(ious_dists, emb_dists)
         put_edge(e, j, cm < L ? cm : INF);
@@ -649,136 +691,32 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
     __syncthreads();
   };
 
+  // matched rows of the last solve (rows[i] ↔ cols[c4r[i]]): STrack.update / re_activate state
+  // changes here, the Kalman/feature/score work as records for K4/K5 (row order)
+  int nrec = 0;
+  auto record_matches = [&](const uint16_t* rows, int R, const uint16_t* cols, bool feat,
+                            bool refind) {
+    const int base = nrec;
+    nrec += block_compact(
+        R, [&](int i) { return s_c4r[i] >= 0; },
+        [&](int i, int p) {
+          const int slot = rows[i], dk = cols[s_c4r[i]];
+          const uint32_t fl = s_flags[slot];
+          const bool tracked = st_of(fl) == ST_TRACKED;
+          s_flags[slot] = (fl & ~F_STATE) | ST_TRACKED | F_ACT;
+          s_fid[slot] = fc;
+          if (refind && !tracked) s_mark[slot] |= M_TMP;
+          const int kind = (tracked ? R_UPDATE : R_REACT) | (feat ? R_FEAT : 0);
+          g_rec[base + p] = make_int2(slot | (kind << 16), dk);
+        },
+        scan_tmp);
+  };
+
   // ---------------- P4/P5: first association: pool x high dets
   BX_STAMP(3);
   associate(s_pool, npool, s_hd, Dh, P.match_thresh, KIND == KIND_BYTE ? 1 : 2, 4);
   BX_STAMP(5);
-
-  // per-track matched update (STrack.update / re_activate)
-  // botsort_track.py:40-49 update_features(det.curr_feat) on one track — one wave, lane-strided:
-  // feat /= |feat|; smooth = 0.9 smooth + 0.1 feat; smooth /= |smooth|
-  auto feature_update_wave = [&](int slot, int dk) {
-    const int lane = lane_id();
-    FT* sm = g_feat + (size_t)slot * F;
-    const FT* f2 = g_df2 + (size_t)dk * F;
-    const FT a = (FT)0.9, bb = (FT)(1.0 - 0.9);
-    if (F <= REG_F) {
-      RegRow<FT> g, m;
-      g.load(f2, F);
-      m.load(sm, F);
-      const FT n3 = g.norm(F);
-#pragma unroll
-      for (int r = 0; r < REG_EPL; r++) {
-        FT g3 = g.v[r] / n3;
-        m.v[r] = a * m.v[r] + bb * g3;
-      }
-      m.div(m.norm(F));
-      m.store(sm, F);
-      return;
-    }
-    const FT n3 = wave_norm(f2, F);
-    for (int q = lane; q < F; q += WAVE) {
-      FT g3 = f2[q] / n3;
-      sm[q] = a * sm[q] + bb * g3;
-    }
-    const FT ns = wave_norm((const FT*)sm, F);  // same lane mapping: reads own writes
-    for (int q = lane; q < F; q += WAVE) sm[q] = sm[q] / ns;
-  };
-  // feature updates for the rows of the last solve that matched (rows[i] ↔ cols[c4r[i]]):
-  // the matched pairs are compacted into the (now idle) LAP scratch, then one wave per pair
-  // with the next pair's two rows prefetched into registers while this one computes.
-  auto feature_updates = [&](const uint16_t* rows, int R, const uint16_t* cols) {
-    uint16_t* ms = s_touch;
-    int16_t* md = s_path;
-    const int nm = block_compact(R, [&](int i) { return s_c4r[i] >= 0; },
-                                 [&](int i, int p) {
-                                   ms[p] = rows[i];
-                                   md[p] = (int16_t)cols[s_c4r[i]];
-                                 },
-                                 scan_tmp);
-    if (F > REG_F) {
-      for (int p = wave_id(); p < nm; p += WG / WAVE) feature_update_wave(ms[p], md[p]);
-      return;
-    }
-    const FT a = (FT)0.9, bb = (FT)(1.0 - 0.9);
-    int p = wave_id();
-    RegRow<FT> g, m;
-    if (p < nm) {
-      g.load(g_df2 + (size_t)md[p] * F, F);
-      m.load(g_feat + (size_t)ms[p] * F, F);
-    }
-    for (; p < nm; p += WG / WAVE) {
-      const int pn = p + WG / WAVE;
-      RegRow<FT> ng, nm_;
-      if (pn < nm) {
-        ng.load(g_df2 + (size_t)md[pn] * F, F);
-        nm_.load(g_feat + (size_t)ms[pn] * F, F);
-      }
-      const FT n3 = g.norm(F);
-#pragma unroll
-      for (int r = 0; r < REG_EPL; r++) {
-        FT g3 = g.v[r] / n3;
-        m.v[r] = a * m.v[r] + bb * g3;
-      }
-      m.div(m.norm(F));
-      m.store(g_feat + (size_t)ms[p] * F, F);
-      g = ng;
-      m = nm_;
-    }
-  };
-
-  auto apply_update = [&](int slot, int dk, bool reactivate, bool with_feat) {
-    (void)with_feat;  // features: feature_updates() after the scalar pass
-    const float* r = fdets + 6 * dk;
-    double xyxy[4] = {(double)r[0], (double)r[1], (double)r[2], (double)r[3]};
-    double xywh[4], meas[4];
-    xyxy2xywh(xyxy, xywh);
-    if (KIND == KIND_BYTE) {
-      double tlwh[4];
-      xywh2tlwh(xywh, tlwh);
-      tlwh2xyah(tlwh, meas);
-    } else {
-      for (int q = 0; q < 4; q++) meas[q] = xywh[q];
-    }
-    kf_update_soa(kf, g_mean + slot, g_cov + slot, T, meas, 0.0);
-    uint32_t fl = s_flags[slot];
-    fl = (fl & ~F_STATE) | ST_TRACKED | F_ACT;
-    s_flags[slot] = fl;
-    s_fid[slot] = fc;
-    g_tlen[slot] = reactivate ? 0 : g_tlen[slot] + 1;
-    const double conf = (double)r[4], cls = (double)r[5];
-    g_conf[slot] = conf;
-    g_cls[slot] = cls;
-    g_detind[slot] = dk;
-    if (KIND == KIND_BOT) {  // update_cls (botsort_track.py:51-64)
-      double* h = g_clsh + (size_t)slot * CLS_HIST * 2;
-      int nh = g_ncls[slot];
-      double max_freq = 0.0, out_cls = cls;
-      bool found = false;
-      for (int q = 0; q < nh; q++) {
-        if (cls == h[2 * q]) { h[2 * q + 1] += conf; found = true; }
-        if (h[2 * q + 1] > max_freq) { max_freq = h[2 * q + 1]; out_cls = h[2 * q]; }
-      }
-      if (!found) {
-        if (nh < CLS_HIST) { h[2 * nh] = cls; h[2 * nh + 1] = conf; g_ncls[slot] = nh + 1; }
-        else atomicOr(P.status, 1 << BX_ERR_TRACK_OVERFLOW);
-        out_cls = cls;
-      }
-      g_cls[slot] = out_cls;
-    }
-  };
-
-  // ---------------- P6: apply first-association matches (row order)
-  for (int i = tid; i < npool; i += WG) {
-    const int j = s_c4r[i];
-    if (j < 0) continue;
-    const int slot = s_pool[i];
-    const bool tracked = st_of(s_flags[slot]) == ST_TRACKED;
-    apply_update(slot, s_hd[j], !tracked, REID);
-    if (!tracked) s_mark[slot] |= M_TMP;  // refind
-  }
-  if (REID) feature_updates(s_pool, npool, s_hd);
-  __syncthreads();
+  record_matches(s_pool, npool, s_hd, REID, true);
   const int nref = block_compact(npool, [&](int k) { return (s_mark[s_pool[k]] & M_TMP) != 0; },
                                  [&](int k, int p) { s_refind[p] = s_pool[k]; }, scan_tmp);
   // remaining high dets (u_detection, ascending) — saved before the next solve reuses r4c
@@ -793,12 +731,7 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   BX_STAMP(6);
   // ---------------- P7: second association: r_tracked x low-confidence dets (IoU, 0.5)
   associate(s_rtr, nrtr, s_sd, Ds, 0.5, 0, 7);
-  for (int i = tid; i < nrtr; i += WG) {
-    const int j = s_c4r[i];
-    if (j < 0) continue;
-    apply_update(s_rtr[i], s_sd[j], false, false);  // second dets carry no features
-  }
-  __syncthreads();
+  record_matches(s_rtr, nrtr, s_sd, false, false);  // second dets carry no features
   const int nlostl = block_compact(
       nrtr, [&](int k) { return s_c4r[k] < 0; },
       [&](int k, int p) {
@@ -813,25 +746,18 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   associate(s_unconf, nun, s_rem, nrem, 0.7, KIND == KIND_BYTE ? 1 : 3, 9);
   BX_STAMP(10);
   for (int i = tid; i < nun; i += WG) {
-    const int j = s_c4r[i];
+    if (s_c4r[i] >= 0) continue;
     const int slot = s_unconf[i];
-    if (j >= 0) {
-      apply_update(slot, s_rem[j], false, REID);
-    } else {
-      s_flags[slot] = (s_flags[slot] & ~F_STATE) | ST_REMOVED;  // mark_removed
-      s_mark[slot] |= M_REMNOW;
-    }
+    s_flags[slot] = (s_flags[slot] & ~F_STATE) | ST_REMOVED;  // mark_removed
+    s_mark[slot] |= M_REMNOW;
   }
-  if (REID) feature_updates(s_unconf, nun, s_rem);
-  __syncthreads();
+  record_matches(s_unconf, nun, s_rem, REID, false);
 
   // ---------------- P9: new tracks from the detections left over (conf >= det/new thresh)
   const int nnew = block_compact(
       nrem, [&](int k) { return s_r4c[k] < 0 && s_dconf[s_rem[k]] >= P.new_thresh; },
       [&](int k, int p) { s_newt[p] = s_rem[k]; /* det index for now */ }, scan_tmp);
   // allocate the first nnew free slots (ascending)
-  if (tid == 0) I[I_NFREE] = 0;
-  __syncthreads();
   {
     int base = 0;
     for (int c = 0; c < T && base < nnew; c += WG) {
@@ -850,48 +776,17 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   __syncthreads();
   const int nnew_ok = I[I_ERR] ? 0 : nnew;
   const int idc0 = I[I_IDC];
-  for (int p = tid; p < nnew_ok; p += WG) {
+  for (int p = tid; p < nnew_ok; p += WG) {  // STrack.activate (state, ids, frames)
     const int dk = s_newt[p], slot = s_rtr[p];
-    const float* r = fdets + 6 * dk;
-    double xyxy[4] = {(double)r[0], (double)r[1], (double)r[2], (double)r[3]};
-    double xywh[4], meas[4], m8[8], c64[64];
-    xyxy2xywh(xyxy, xywh);
-    if (KIND == KIND_BYTE) {
-      double tlwh[4];
-      xywh2tlwh(xywh, tlwh);
-      tlwh2xyah(tlwh, meas);
-    } else {
-      for (int q = 0; q < 4; q++) meas[q] = xywh[q];
-    }
-    kf_initiate(kf, meas, m8, c64);
-    for (int q = 0; q < 8; q++) g_mean[q * T + slot] = m8[q];
-    for (int q = 0; q < 64; q++) g_cov[q * T + slot] = c64[q];
-    g_id[slot] = idc0 + 1 + p;
-    g_tlen[slot] = 0;
-    g_conf[slot] = (double)r[4];
-    g_cls[slot] = (double)r[5];
-    g_detind[slot] = dk;
+    P.id[sT + slot] = idc0 + 1 + p;
+    P.start[sT + slot] = fc;
     s_flags[slot] = ST_TRACKED | F_INUSE | (fc == 1 ? F_ACT : 0u);
     s_fid[slot] = fc;
-    g_start[slot] = fc;
-    if (KIND == KIND_BOT) {
-      double* h = g_clsh + (size_t)slot * CLS_HIST * 2;
-      h[0] = (double)r[5];
-      h[1] = (double)r[4];
-      g_ncls[slot] = 1;
-    }
+    g_rec[nrec + p] = make_int2(slot | ((R_NEW | (REID ? R_FEAT : 0)) << 16), dk);
     s_newt[p] = (uint16_t)slot;
   }
-  if (tid == 0) I[I_IDC] = idc0 + nnew_ok;
+  nrec += nnew_ok;
   __syncthreads();
-  if (REID) {  // smooth_feat of a new track = the detection's (already twice-normalised) feature
-    for (int p = wave_id(); p < nnew_ok; p += WG / WAVE) {
-      const int slot = s_newt[p], dk = g_detind[slot];
-      FT* sm = g_feat + (size_t)slot * F;
-      const FT* f2 = g_df2 + (size_t)dk * F;
-      for (int q = lane_id(); q < F; q += WAVE) sm[q] = f2[q];
-    }
-  }
 
   BX_STAMP(11);
   // ---------------- P10: lost tracks past the buffer → removed
@@ -904,117 +799,264 @@ __global__ __launch_bounds__(WG) void frame_kernel(Dev P, int seq0, const float*
   }
   __syncthreads();
 
-  // ---------------- P11: list rebuild (bytetrack.py:278-289 / botsort.py:392-403)
+  // ---------------- P11: list rebuild (bytetrack.py:278-289 / botsort.py:392-403), written to
+  // act2/lost2 for K6's remove_duplicate_stracks
   // act2 = [t in active if Tracked] ++ new tracks ++ refind    (joint_stracks x2)
+  uint16_t* g_act2 = P.act2 + sT;
+  uint16_t* g_lost2 = P.lost2 + sT;
   int nact2 = block_compact(na, [&](int k) { return st_of(s_flags[s_act[k]]) == ST_TRACKED; },
-                            [&](int k, int p) { s_fa[p] = s_act[k]; }, scan_tmp);
-  for (int k = tid; k < nact2; k += WG) s_mark[s_fa[k]] |= M_ACT2;
-  __syncthreads();
-  for (int k = tid; k < nnew_ok; k += WG) { s_fa[nact2 + k] = s_newt[k]; s_mark[s_newt[k]] |= M_ACT2; }
+                            [&](int k, int p) {
+                              g_act2[p] = s_act[k];
+                              s_mark[s_act[k]] |= M_ACT2;
+                            },
+                            scan_tmp);
+  for (int k = tid; k < nnew_ok; k += WG) {
+    g_act2[nact2 + k] = s_newt[k];
+    s_mark[s_newt[k]] |= M_ACT2;
+  }
   nact2 += nnew_ok;
   __syncthreads();
-  {
-    const int add = block_compact(nref, [&](int k) { return !(s_mark[s_refind[k]] & M_ACT2); },
-                                  [&](int k, int p) { s_fa[nact2 + p] = s_refind[k]; }, scan_tmp);
-    for (int k = tid; k < add; k += WG) s_mark[s_fa[nact2 + k]] |= M_ACT2;
-    nact2 += add;
-  }
-  __syncthreads();
-  // lost = sub(lost, active) ++ lost_local, then sub(., removed_stracks) (flag from earlier frames)
-  int nlost1 = block_compact(nl, [&](int k) { return !(s_mark[s_lost[k]] & M_ACT2); },
-                             [&](int k, int p) { s_fl[p] = s_lost[k]; }, scan_tmp);
-  for (int k = tid; k < nlostl; k += WG) s_fl[nlost1 + k] = s_lostl[k];
-  nlost1 += nlostl;
-  __syncthreads();
-  const int nlost2 = block_compact(nlost1, [&](int k) { return !(s_flags[s_fl[k]] & F_INREM); },
-                                   [&](int k, int p) { s_tracked[p] = s_fl[k]; }, scan_tmp);
-  // removed_stracks.extend(removed_local)
-  for (int k = tid; k < T; k += WG)
-    if (s_mark[k] & M_REMNOW) s_flags[k] |= F_INREM;
-  __syncthreads();
-  // remove_duplicate_stracks(act2, lost2): iou distance < 0.15 → drop the younger track
-  {
-    double* lbox = s_ecost;  // the LAP edge store is dead by now: lost boxes + ages live there
-    const bool in_lds = nlost2 * 5 <= P.elds;
-    double* abox = (double*)(smem + Lo.o_tbox);
-    if (in_lds)
-      for (int q = tid; q < nlost2; q += WG) {
-        const int sb = s_tracked[q];
-        track_box(sb, lbox + 4 * q);
-        lbox[4 * nlost2 + q] = (double)(s_fid[sb] - g_start[sb]);
-      }
-    for (int p = tid; p < nact2; p += WG) track_box(s_fa[p], abox + 4 * p);
-    __syncthreads();
-    const int lane = lane_id();
-    for (int p = wave_id(); p < nact2; p += WG / WAVE) {  // wave per active track
-      const int sa = s_fa[p];
-      const double* ba = abox + 4 * p;
-      const int ta = s_fid[sa] - g_start[sa];
-      bool dupa = false;
-      for (int q = lane; q < nlost2; q += WAVE) {
-        const int sb = s_tracked[q];
-        double bb[4];
-        if (in_lds) for (int k = 0; k < 4; k++) bb[k] = lbox[4 * q + k];
-        else track_box(sb, bb);
-        if (!boxes_intersect(ba, bb)) continue;
-        if (1 - iou_pair(ba, bb) < 0.15) {
-          const int tb = in_lds ? (int)lbox[4 * nlost2 + q] : s_fid[sb] - g_start[sb];
-          if (ta > tb) atomicOr((unsigned*)&s_flags[sb], 0x80000000u);  // dupb (transient bit)
-          else dupa = true;                                             // dupa
-        }
-      }
-      if (__ballot(dupa) != 0ull && lane == 0) s_mark[sa] |= M_DUP;
-    }
-  }
-  __syncthreads();
-  const int nfa = block_compact(nact2, [&](int k) { return !(s_mark[s_fa[k]] & M_DUP); },
-                                [&](int k, int p) { s_unconf[p] = s_fa[k]; }, scan_tmp);
-  const int nfl = block_compact(
-      nlost2, [&](int k) { return !(s_flags[s_tracked[k]] & 0x80000000u); },
-      [&](int k, int p) { s_pool[p] = s_tracked[k]; }, scan_tmp);
-  for (int k = tid; k < nlost2; k += WG) s_flags[s_tracked[k]] &= ~0x80000000u;
-  __syncthreads();
-
-  BX_STAMP(12);
-  // ---------------- P12: outputs [x1,y1,x2,y2,id,conf,cls,det_ind] for activated tracks
-  const int nout = block_compact(
-      nfa, [&](int k) { return (s_flags[s_unconf[k]] & F_ACT) != 0; },
-      [&](int k, int p) {
-        const int slot = s_unconf[k];
-        double box[4];
-        track_box(slot, box);
-        double* o = out + (size_t)(d0 + p) * 8;
-        o[0] = box[0]; o[1] = box[1]; o[2] = box[2]; o[3] = box[3];
-        o[4] = (double)g_id[slot];
-        o[5] = g_conf[slot];
-        o[6] = g_cls[slot];
-        o[7] = (double)g_detind[slot];
-      },
-      scan_tmp);
-
-  // ---------------- P13: free slots that left both lists; write back
-  for (int k = tid; k < T; k += WG) s_mark[k] = 0;
-  __syncthreads();
-  for (int k = tid; k < nfa; k += WG) s_mark[s_unconf[k]] = M_KEEP;
-  for (int k = tid; k < nfl; k += WG) s_mark[s_pool[k]] = M_KEEP;
-  __syncthreads();
+  nact2 += block_compact(nref, [&](int k) { return !(s_mark[s_refind[k]] & M_ACT2); },
+                         [&](int k, int p) {
+                           g_act2[nact2 + p] = s_refind[k];
+                           s_mark[s_refind[k]] |= M_ACT2;
+                         },
+                         scan_tmp);
+  // lost = sub(lost, active) ++ lost_local, then sub(., removed_stracks) with the removed list
+  // of earlier frames only (F_INREM): the reference extends removed_stracks afterwards
+  int nlost2 = block_compact(
+      nl, [&](int k) { return !(s_mark[s_lost[k]] & M_ACT2) && !(s_flags[s_lost[k]] & F_INREM); },
+      [&](int k, int p) { g_lost2[p] = s_lost[k]; }, scan_tmp);
+  nlost2 += block_compact(nlostl, [&](int k) { return !(s_flags[s_lostl[k]] & F_INREM); },
+                          [&](int k, int p) { g_lost2[nlost2 + p] = s_lostl[k]; }, scan_tmp);
+  // removed_stracks.extend(removed_local); write back slot state
   for (int k = tid; k < T; k += WG) {
     uint32_t f = s_flags[k];
-    if (!(s_mark[k] & M_KEEP)) f = 0;  // slot free (track unreachable from here on)
+    if (s_mark[k] & M_REMNOW) f |= F_INREM;
     g_flags[k] = f;
     g_fid[k] = s_fid[k];
   }
-  for (int k = tid; k < nfa; k += WG) P.act[sT + k] = s_unconf[k];
-  for (int k = tid; k < nfl; k += WG) P.lost[sT + k] = s_pool[k];
+  if (tid == 0) {
+    seq[SQ_FC] = fc;
+    seq[SQ_IDC] = idc0 + nnew_ok;
+    seq[SQ_NA2] = nact2;
+    seq[SQ_NL2] = nlost2;
+    seq[SQ_NREC] = nrec;
+    seq[SQ_SKIP] = 0;
+    if (I[I_ERR]) seq[SQ_STATUS] |= 1 << BX_ERR_TRACK_OVERFLOW;
+  }
+  BX_STAMP(12);
+}
+
+// ------------------------------------------------------------------------------------------
+// K4: per update record, STrack.update / re_activate / activate numerics: Kalman update
+// (kalman_filter.py update) or initiate, tracklet_len, score, cls (+ BoT-SORT update_cls,
+// botsort_track.py:51-64), det_ind.  Grid (n_seq, ceil(D/256)); thread per record.
+template <int KIND>
+__global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float* __restrict__ dets,
+                                                    const int* __restrict__ det_off) {
+  const int b = blockIdx.x, s = seq0 + b, T = P.T;
+  const int r = blockIdx.y * WG + threadIdx.x;
+  const int* seq = P.seq + (size_t)s * SQ_STRIDE;
+  if (r >= seq[SQ_NREC]) return;
+  const int2 rc = P.rec[(size_t)s * P.D + r];
+  const int slot = rc.x & 0xffff, kind = (rc.x >> 16) & 3, dk = rc.y;
+  const size_t sT = (size_t)s * T;
+  const float* row = dets + (size_t)(det_off[b] + dk) * 6;
+  double meas[4];
+  det_measurement<KIND>(row, meas);
+  double* m = P.mean + (size_t)s * 8 * T + slot;
+  double* c = P.cov + (size_t)s * 64 * T + slot;
+  const double conf = (double)row[4], cls = (double)row[5];
+  P.conf[sT + slot] = conf;
+  P.detind[sT + slot] = dk;
+  double* h = P.clsh + (sT + slot) * CLS_HIST * 2;
+  if (kind == R_NEW) {
+    double m8[8], c64[64];
+    kf_initiate(KIND, meas, m8, c64);
+    for (int q = 0; q < 8; q++) m[q * T] = m8[q];
+    for (int q = 0; q < 64; q++) c[q * T] = c64[q];
+    P.tlen[sT + slot] = 0;
+    P.cls[sT + slot] = cls;
+    if (KIND == KIND_BOT) {
+      h[0] = cls;
+      h[1] = conf;
+      P.ncls[sT + slot] = 1;
+    }
+    return;
+  }
+  kf_update_soa(KIND, m, c, T, meas, 0.0);
+  P.tlen[sT + slot] = kind == R_REACT ? 0 : P.tlen[sT + slot] + 1;
+  double out_cls = cls;
+  if (KIND == KIND_BOT) {  // update_cls
+    const int nh = P.ncls[sT + slot];
+    double max_freq = 0.0;
+    bool found = false;
+    for (int q = 0; q < nh; q++) {
+      if (cls == h[2 * q]) { h[2 * q + 1] += conf; found = true; }
+      if (h[2 * q + 1] > max_freq) { max_freq = h[2 * q + 1]; out_cls = h[2 * q]; }
+    }
+    if (!found) {
+      if (nh < CLS_HIST) { h[2 * nh] = cls; h[2 * nh + 1] = conf; P.ncls[sT + slot] = nh + 1; }
+      else atomicOr(P.status, 1 << BX_ERR_TRACK_OVERFLOW);
+      out_cls = cls;
+    }
+  }
+  P.cls[sT + slot] = out_cls;
+}
+
+// ------------------------------------------------------------------------------------------
+// K5: BoT-SORT feature update per record carrying a detection feature (botsort_track.py:40-49):
+// a new track's smooth_feat = f2; otherwise feat = f2/|f2|; smooth = 0.9 smooth + 0.1 feat;
+// smooth /= |smooth|.  f2 is recomputed from the input row with K1's norms (bit-identical).
+// Grid (n_seq, ceil(D/4)); one wave per record.
+template <typename FT>
+__global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
+                                                     const int* __restrict__ det_off,
+                                                     const FT* __restrict__ embs) {
+  const int b = blockIdx.x, s = seq0 + b, F = P.F, D = P.D, lane = lane_id();
+  const int r = blockIdx.y * NWAVE + wave_id();
+  if (r >= P.seq[(size_t)s * SQ_STRIDE + SQ_NREC]) return;  // wave-uniform
+  const int2 rc = P.rec[(size_t)s * D + r];
+  const int slot = rc.x & 0xffff, kind = rc.x >> 16, dk = rc.y;
+  if (!(kind & R_FEAT)) return;
+  FT* sm = (FT*)P.feat + ((size_t)s * P.T + slot) * F;
+  const FT a = (FT)0.9, bb = (FT)(1.0 - 0.9);
+  if (F <= REG_F) {
+    const FT n1 = (FT)P.dnrm[((size_t)s * D + dk) * 2], n2 = (FT)P.dnrm[((size_t)s * D + dk) * 2 + 1];
+    RegRow<FT> g;
+    g.load(embs + (size_t)(det_off[b] + dk) * F, F);
+    g.div(n1);
+    g.div(n2);
+    if ((kind & 3) == R_NEW) {
+      g.store(sm, F);
+      return;
+    }
+    RegRow<FT> m;
+    m.load(sm, F);
+    const FT n3 = g.norm(F);
+#pragma unroll
+    for (int q = 0; q < REG_EPL; q++) {
+      FT g3 = g.v[q] / n3;
+      m.v[q] = a * m.v[q] + bb * g3;
+    }
+    m.div(m.norm(F));
+    m.store(sm, F);
+    return;
+  }
+  const FT* f2 = (const FT*)P.fscr + ((size_t)s * D + dk) * F;
+  if ((kind & 3) == R_NEW) {
+    for (int q = lane; q < F; q += WAVE) sm[q] = f2[q];
+    return;
+  }
+  const FT n3 = wave_norm(f2, F);
+  for (int q = lane; q < F; q += WAVE) {
+    FT g3 = f2[q] / n3;
+    sm[q] = a * sm[q] + bb * g3;
+  }
+  const FT ns = wave_norm((const FT*)sm, F);  // same lane mapping: reads own writes
+  for (int q = lane; q < F; q += WAVE) sm[q] = sm[q] / ns;
+}
+
+// ------------------------------------------------------------------------------------------
+// K6: remove_duplicate_stracks(active, lost) (bytetrack.py:321-335) on the updated means,
+// output rows [x1,y1,x2,y2,id,conf,cls,det_ind] for activated tracks, final lists, slot release.
+// One workgroup per sequence.
+template <int KIND>
+__global__ __launch_bounds__(WG) void finish_kernel(Dev P, int seq0, const int* __restrict__ det_off,
+                                                    double* __restrict__ out,
+                                                    int* __restrict__ out_count) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int T = P.T;
+  const LdsF Lo(T);
+  double* s_lbox = (double*)(smem + Lo.o_lbox);
+  int* s_lage = (int*)(smem + Lo.o_lage);
+  uint16_t* s_fa = (uint16_t*)(smem + Lo.o_fa);
+  uint16_t* s_fl = (uint16_t*)(smem + Lo.o_fl);
+  uint8_t* s_dupa = (uint8_t*)(smem + Lo.o_dupa);
+  uint8_t* s_dupl = (uint8_t*)(smem + Lo.o_dupl);
+  uint8_t* s_keep = (uint8_t*)(smem + Lo.o_keep);
+  int* scan_tmp = (int*)(smem + Lo.o_ints);
+  const int tid = threadIdx.x, b = blockIdx.x, s = seq0 + b;
+  const size_t sT = (size_t)s * T;
+  int* seq = P.seq + (size_t)s * SQ_STRIDE;
+  const double* g_mean = P.mean + (size_t)s * 8 * T;
+  const int* g_fid = P.frame_id + sT;
+  const int* g_start = P.start + sT;
+  uint32_t* g_flags = P.flags + sT;
+  if (seq[SQ_SKIP]) {  // K3 refused the frame (capacity): state untouched, no output
+    if (tid == 0) out_count[b] = 0;
+    return;
+  }
+  const int na2 = seq[SQ_NA2], nl2 = seq[SQ_NL2];
+  for (int k = tid; k < na2; k += WG) { s_fa[k] = P.act2[sT + k]; s_dupa[k] = 0; }
+  for (int q = tid; q < nl2; q += WG) {
+    const int sl = P.lost2[sT + q];
+    s_fl[q] = (uint16_t)sl;
+    s_dupl[q] = 0;
+    track_box<KIND>(g_mean, T, sl, s_lbox + 4 * q);
+    s_lage[q] = g_fid[sl] - g_start[sl];
+  }
+  for (int k = tid; k < T; k += WG) s_keep[k] = 0;
+  __syncthreads();
+  // iou distance < 0.15 → drop the younger track (ties drop the active one)
+  const int lane = lane_id();
+  for (int p = wave_id(); p < na2; p += NWAVE) {  // wave per active track, lanes over lost
+    const int sa = s_fa[p];
+    double ba[4];
+    track_box<KIND>(g_mean, T, sa, ba);
+    const int ta = g_fid[sa] - g_start[sa];
+    bool dupa = false;
+    for (int q = lane; q < nl2; q += WAVE) {
+      const double* bb = s_lbox + 4 * q;
+      if (!boxes_intersect(ba, bb)) continue;
+      if (1 - iou_pair(ba, bb) < 0.15) {
+        if (ta > s_lage[q]) s_dupl[q] = 1;
+        else dupa = true;
+      }
+    }
+    if (__ballot(dupa) != 0ull && lane == 0) s_dupa[p] = 1;
+  }
+  __syncthreads();
+  const int nfa = block_compact(na2, [&](int k) { return !s_dupa[k]; },
+                                [&](int k, int p) {
+                                  P.act[sT + p] = s_fa[k];
+                                  s_keep[s_fa[k]] = 1;
+                                },
+                                scan_tmp);
+  const int nfl = block_compact(nl2, [&](int k) { return !s_dupl[k]; },
+                                [&](int k, int p) {
+                                  P.lost[sT + p] = s_fl[k];
+                                  s_keep[s_fl[k]] = 2;
+                                },
+                                scan_tmp);
+  const int d0 = det_off[b];
+  const int nout = block_compact(
+      na2, [&](int k) { return !s_dupa[k] && (g_flags[s_fa[k]] & F_ACT) != 0; },
+      [&](int k, int p) {
+        const int slot = s_fa[k];
+        double box[4];
+        track_box<KIND>(g_mean, T, slot, box);
+        double* o = out + (size_t)(d0 + p) * 8;
+        o[0] = box[0]; o[1] = box[1]; o[2] = box[2]; o[3] = box[3];
+        o[4] = (double)P.id[sT + slot];
+        o[5] = P.conf[sT + slot];
+        o[6] = P.cls[sT + slot];
+        o[7] = (double)P.detind[sT + slot];
+      },
+      scan_tmp);
+  // slots that left both lists are free from here on; list membership bits for K2/K3
+  for (int k = tid; k < T; k += WG) {
+    const uint32_t f = g_flags[k];
+    const uint8_t kp = s_keep[k];
+    const uint32_t nf = kp ? ((f & ~(F_INACT | F_INLOST)) | (kp == 1 ? F_INACT : F_INLOST)) : 0u;
+    if (nf != f) g_flags[k] = nf;
+  }
   if (tid == 0) {
     seq[SQ_NA] = nfa;
     seq[SQ_NL] = nfl;
-    seq[SQ_FC] = fc;
-    seq[SQ_IDC] = I[I_IDC];
-    if (I[I_ERR]) seq[SQ_STATUS] |= 1 << BX_ERR_TRACK_OVERFLOW;
     out_count[b] = nout;
   }
-  BX_STAMP(13);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1033,7 +1075,7 @@ struct bx_engine {
   bx_config cfg;
   Dev dev;
   int device;
-  size_t lds_bytes;
+  size_t lds_assoc, lds_finish;
   void* arena;
   size_t arena_bytes;
   // host-path staging (device)
@@ -1056,19 +1098,55 @@ T* carve(char*& p, size_t n) {
   return r;
 }
 
-template <int KIND, typename FT>
+// hipFuncSetAttribute once per (kernel, size) for > 64 KiB dynamic LDS
+int lds_attr(const void* kern, size_t bytes) {
+  static std::mutex mu;
+  static std::vector<std::pair<const void*, size_t>> done;
+  if (bytes <= 65536) return BX_OK;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto& d : done)
+    if (d.first == kern && d.second >= bytes) return BX_OK;
+  HIPCHK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  done.emplace_back(kern, bytes);
+  return BX_OK;
+}
+
+// One frame of sequences [seq0, seq0+nseq): the K1..K6 pipeline on stream st.
+template <int KIND, typename FT, bool NPF>
 int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int* det_off,
                  const void* embs, const double* warps, double* out, int* out_count,
                  hipStream_t st) {
-  auto kern = frame_kernel<KIND, FT>;
-  static thread_local size_t attr_set = 0;
-  if (e->lds_bytes > 65536 && attr_set < e->lds_bytes) {
-    HIPCHK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)e->lds_bytes));
-    attr_set = e->lds_bytes;
+  const Dev& d = e->dev;
+  const bool reid = KIND == KIND_BOT && d.with_reid;
+  const int gy_det4 = (d.D + NWAVE - 1) / NWAVE, gy_slot = (d.T + WG - 1) / WG,
+            gy_det = (d.D + WG - 1) / WG;
+  if (reid) {
+    hipLaunchKernelGGL((det_feature_kernel<FT, NPF>), dim3(nseq, gy_det4), dim3(WG), 0, st, d,
+                       seq0, dets, det_off, (const FT*)embs);
+    HIPCHK(hipGetLastError());
   }
-  hipLaunchKernelGGL(kern, dim3(nseq), dim3(WG), e->lds_bytes, st, e->dev, seq0, dets, det_off,
-                     (const FT*)embs, warps, out, out_count);
+  if (KIND == KIND_BOT && warps)
+    hipLaunchKernelGGL((predict_kernel<KIND, true>), dim3(nseq, gy_slot), dim3(WG), 0, st, d,
+                       seq0, warps);
+  else
+    hipLaunchKernelGGL((predict_kernel<KIND, false>), dim3(nseq, gy_slot), dim3(WG), 0, st, d,
+                       seq0, warps);
+  HIPCHK(hipGetLastError());
+  auto assoc = assoc_kernel<KIND, FT, NPF>;
+  if (int rc = lds_attr((const void*)assoc, e->lds_assoc)) return rc;
+  hipLaunchKernelGGL(assoc, dim3(nseq), dim3(WG), e->lds_assoc, st, d, seq0, dets, det_off);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(update_kernel<KIND>, dim3(nseq, gy_det), dim3(WG), 0, st, d, seq0, dets,
+                     det_off);
+  HIPCHK(hipGetLastError());
+  if (reid) {
+    hipLaunchKernelGGL(feature_kernel<FT>, dim3(nseq, gy_det4), dim3(WG), 0, st, d, seq0,
+                       det_off, (const FT*)embs);
+    HIPCHK(hipGetLastError());
+  }
+  if (int rc = lds_attr((const void*)finish_kernel<KIND>, e->lds_finish)) return rc;
+  hipLaunchKernelGGL(finish_kernel<KIND>, dim3(nseq), dim3(WG), e->lds_finish, st, d, seq0,
+                     det_off, out, out_count);
   HIPCHK(hipGetLastError());
   return BX_OK;
 }
@@ -1121,49 +1199,56 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
   d.prox = cfg->proximity_thresh;
   d.app = cfg->appearance_thresh;
   const size_t ST = (size_t)S * T;
-  size_t bytes = 0;
-  auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
-  acc(sizeof(int) * S * SQ_STRIDE); acc(2 * ST); acc(2 * ST); acc(4 * ST); acc(4 * ST);
-  acc(4 * ST); acc(4 * ST); acc(4 * ST); acc(4 * ST); acc(8 * ST); acc(8 * ST);
-  acc(8 * ST * 8); acc(8 * ST * 64); acc(fs * ST * (F ? F : 1)); acc(8 * ST * CLS_HIST * 2);
-  acc(4 * ST); acc(2 * ST * D); acc(8 * ST * D); acc(fs * (size_t)S * D * (F ? F : 1)); acc(64);
-  acc(4 * (size_t)S * D * (F ? F : 1)); acc(4 * ST * (F ? F : 1));
+  const size_t SD = (size_t)S * D, FF = F ? F : 1;
+  const size_t FS = F > REG_F ? F : 1;  // twice-normalised det rows kept only for wide features
+  // carve the arena twice: once from a null base to size it, once for real
+  auto layout = [&](char* p) {
+    char* p0 = p;
+    d.seq = carve<int>(p, (size_t)S * SQ_STRIDE);
+    d.act = carve<uint16_t>(p, ST);
+    d.lost = carve<uint16_t>(p, ST);
+    d.act2 = carve<uint16_t>(p, ST);
+    d.lost2 = carve<uint16_t>(p, ST);
+    d.flags = carve<uint32_t>(p, ST);
+    d.frame_id = carve<int>(p, ST);
+    d.start = carve<int>(p, ST);
+    d.id = carve<int>(p, ST);
+    d.tlen = carve<int>(p, ST);
+    d.detind = carve<int>(p, ST);
+    d.conf = carve<double>(p, ST);
+    d.cls = carve<double>(p, ST);
+    d.mean = carve<double>(p, ST * 8);
+    d.cov = carve<double>(p, ST * 64);
+    d.feat = carve<char>(p, fs * ST * FF);
+    d.clsh = carve<double>(p, ST * CLS_HIST * 2);
+    d.ncls = carve<int>(p, ST);
+    d.gcol = carve<uint16_t>(p, ST * D);
+    d.gcost = carve<double>(p, ST * D);
+    d.rec = carve<int2>(p, SD);
+    d.dnrm = carve<double>(p, SD * 2);
+    d.dnb = carve<double>(p, SD);
+    d.dB = carve<float>(p, SD * FF);
+    d.tA = carve<float>(p, ST * FF);
+    d.fscr = carve<char>(p, fs * SD * FS);
+    d.status = carve<int>(p, 16);
+    return (size_t)(p - p0);
+  };
+  const size_t bytes = layout(nullptr);
   e->arena_bytes = bytes;
   if (hipMalloc(&e->arena, bytes) != hipSuccess) {
     delete e;
     return set_err(BX_ERR_HIP, "hipMalloc of the engine arena failed");
   }
-  char* p = (char*)e->arena;
-  d.seq = carve<int>(p, (size_t)S * SQ_STRIDE);
-  d.act = carve<uint16_t>(p, ST);
-  d.lost = carve<uint16_t>(p, ST);
-  d.flags = carve<uint32_t>(p, ST);
-  d.frame_id = carve<int>(p, ST);
-  d.start = carve<int>(p, ST);
-  d.id = carve<int>(p, ST);
-  d.tlen = carve<int>(p, ST);
-  d.detind = carve<int>(p, ST);
-  d.conf = carve<double>(p, ST);
-  d.cls = carve<double>(p, ST);
-  d.mean = carve<double>(p, ST * 8);
-  d.cov = carve<double>(p, ST * 64);
-  d.feat = carve<char>(p, fs * ST * (F ? F : 1));
-  d.clsh = carve<double>(p, ST * CLS_HIST * 2);
-  d.ncls = carve<int>(p, ST);
-  d.gcol = carve<uint16_t>(p, ST * D);
-  d.gcost = carve<double>(p, ST * D);
-  d.df2 = carve<char>(p, fs * (size_t)S * D * (F ? F : 1));
-  d.status = carve<int>(p, 16);
-  d.dB = carve<float>(p, (size_t)S * D * (F ? F : 1));
-  d.tA = carve<float>(p, ST * (F ? F : 1));
+  layout((char*)e->arena);
   d.dbg = nullptr;
 #ifdef BX_PHASE_TIMING
   HIPCHK(hipMalloc(&d.dbg, sizeof(unsigned long long) * 32 * S));
   HIPCHK(hipMemset(d.dbg, 0, sizeof(unsigned long long) * 32 * S));
 #endif
   HIPCHK(hipMemset(e->arena, 0, bytes));
-  e->lds_bytes = Lds(T, D, d.elds, F).total;
-  if (e->lds_bytes > 160 * 1024) {
+  e->lds_assoc = LdsA(T, D, d.elds).total;
+  e->lds_finish = LdsF(T).total;
+  if (e->lds_assoc > 160 * 1024 || e->lds_finish > 160 * 1024) {
     (void)hipFree(e->arena);
     delete e;
     return set_err(BX_ERR_INVALID, "track_cap/det_cap too large for one workgroup's LDS");
@@ -1209,13 +1294,18 @@ int bx_engine_step(bx_engine* e, int seq0, int nseq, const float* dets, const in
   if (e->dev.with_reid && !embs) return set_err(BX_ERR_SHAPE, "BoT-SORT with_reid needs embs");
   hipStream_t st = (hipStream_t)stream;
   if (e->dev.kind == BX_BYTETRACK)
-    return launch_frame<KIND_BYTE, float>(e, seq0, nseq, dets, det_off, embs, warps, out,
-                                          out_count, st);
+    return launch_frame<KIND_BYTE, float, true>(e, seq0, nseq, dets, det_off, embs, warps, out,
+                                                out_count, st);
+  const bool npf = np_wave_exact(e->dev.F);
   if (e->dev.emb_f64)
-    return launch_frame<KIND_BOT, double>(e, seq0, nseq, dets, det_off, embs, warps, out,
-                                          out_count, st);
-  return launch_frame<KIND_BOT, float>(e, seq0, nseq, dets, det_off, embs, warps, out, out_count,
-                                       st);
+    return npf ? launch_frame<KIND_BOT, double, true>(e, seq0, nseq, dets, det_off, embs, warps,
+                                                      out, out_count, st)
+               : launch_frame<KIND_BOT, double, false>(e, seq0, nseq, dets, det_off, embs, warps,
+                                                       out, out_count, st);
+  return npf ? launch_frame<KIND_BOT, float, true>(e, seq0, nseq, dets, det_off, embs, warps, out,
+                                                   out_count, st)
+             : launch_frame<KIND_BOT, float, false>(e, seq0, nseq, dets, det_off, embs, warps,
+                                                    out, out_count, st);
 }
 
 int bx_engine_update_host(bx_engine* e, int seq, const float* dets, int n, const void* embs,

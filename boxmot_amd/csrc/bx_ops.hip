@@ -125,6 +125,7 @@ __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int n
   uint16_t* ecol = (uint16_t*)take(2 * elds);
   uint8_t* colf = (uint8_t*)take(nc);
   int* cdeg = (int*)take(4 * nc);
+  uint16_t* roots = (uint16_t*)take(2 * nr);
   const int tid = threadIdx.x;
   for (int i = tid; i < nr; i += WG) {
     int cnt = 0;
@@ -149,6 +150,7 @@ __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int n
   W.row_ptr = rowptr; W.ecol = ecol; W.ecost = ecost; W.gcol = gcol; W.gcost = gcost;
   W.elds = elds; W.col4row = c4r; W.row4col = r4c; W.u = u; W.v = v; W.spc = spc;
   W.path = path; W.colflag = colf; W.touched = touch; W.srlist = srl; W.coldeg = cdeg;
+  W.roots = roots;
   if (wave_id() == 0) lap_solve_wave(nr, nc, thr, W);
   __syncthreads();
   for (int i = tid; i < nr; i += WG) x[i] = c4r[i];
@@ -259,6 +261,7 @@ int bx_linear_assignment(const double* cost, int nr, int nc, double thresh, int3
     auto take = [&](size_t b) { o += (b + 15) & ~size_t(15); };
     take(8 * nr); take(8 * nc); take(8 * nc); take(8 * e); take(4 * (nr + 1)); take(2 * nr);
     take(2 * nr); take(2 * nc); take(2 * nc); take(2 * nc); take(2 * e); take(nc); take(4 * nc);
+    take(2 * nr);
     return o;
   };
   while (elds > 0 && lds_for(elds) > 160 * 1024) elds /= 2;
