@@ -39,6 +39,7 @@ constexpr int ELDS_DEFAULT = 1024;  // LAP edges kept in LDS; the rest spill to 
 constexpr int REG_F = 512;   // feature rows up to this width live in registers: 8 per lane
 constexpr int REG_EPL = REG_F / 64;
 constexpr int NWAVE = WG / WAVE;
+constexpr int KF_STRIDE = 72;  // doubles per slot: mean[8] + covariance[64], contiguous
 
 // A feature row held by one wave, element q = lane + 64 r in v[r] (F <= REG_F).
 template <typename FT>
@@ -153,8 +154,7 @@ struct Dev {
   int* detind;        // [S][T]
   double* conf;       // [S][T]
   double* cls;        // [S][T]
-  double* mean;       // [S][8][T]
-  double* cov;        // [S][64][T]
+  double* kf;         // [S][T][KF_STRIDE] Kalman state per slot: mean[8] then cov[64] (576 B)
   void* feat;         // [S][T][F] smooth_feat
   double* clsh;       // [S][T][CLS_HIST][2]
   int* ncls;          // [S][T]
@@ -162,9 +162,11 @@ struct Dev {
   double* gcost;      // [S][T*D]
   int2* rec;          // [S][D] frame scratch: update records (K3 → K4/K5)
   double* dnrm;       // [S][D][2] frame scratch: n1, n2 of STrack.update_features per det
-  double* dnb;        // [S][D] frame scratch: cdist norm of each dB row
   float* dB;          // [S][D][F] frame scratch: det rows as embedding_distance normalises them
-  float* tA;          // [S][T][F] frame scratch: track rows as embedding_distance normalises them
+  float* tdn;         // [S][T] frame scratch: numpy float32 norm (+1e-8) of a gated slot's feature
+  uint32_t* pairs;    // [S][T*D] frame scratch: gated (slot << 16 | det) pairs
+  int* npair;         // [S] gated pair count (zeroed by K6 for the next frame)
+  double* etab;       // [S][T][D] frame scratch: embedding distance of gated pairs
   void* fscr;         // [S][D][F] frame scratch for F > REG_F only: twice-normalised det rows
   int* status;        // [1] latched engine status
   unsigned long long* dbg;  // [S][32] phase stamps (diagnostic builds only, else null)
@@ -192,7 +194,7 @@ enum : int { R_UPDATE = 0, R_REACT = 1, R_NEW = 2, R_FEAT = 4 };
 
 // LDS carve-out of the association kernel (host and device agree on it).
 struct LdsA {
-  size_t o_dbox, o_dboxf, o_dconf, o_tboxf, o_u, o_v, o_spc, o_ecost, o_tna, o_flags, o_fid,
+  size_t o_dbox, o_dboxf, o_dconf, o_tboxf, o_u, o_v, o_spc, o_ecost, o_flags, o_fid,
       o_rowptr, o_ints, o_act, o_lost, o_unconf, o_pool, o_rtr, o_lostl, o_refind, o_newt,
       o_c4r, o_srl, o_roots, o_r4c, o_path, o_touch, o_cdeg, o_hd, o_sd, o_rem, o_ecol, o_mark,
       o_colf, o_dkind, total;
@@ -211,7 +213,6 @@ struct LdsA {
     o_v = take(sizeof(double) * D);
     o_spc = take(sizeof(double) * D);
     o_ecost = take(sizeof(double) * elds);
-    o_tna = take(sizeof(double) * T);
     o_flags = take(sizeof(uint32_t) * T);
     o_fid = take(sizeof(int) * T);
     o_rowptr = take(sizeof(int) * (T + 1));
@@ -271,8 +272,10 @@ enum { I_NA = 0, I_NL, I_FC, I_IDC, I_ERR, I_SCAN = 32 };
 
 // STrack.xyxy of a track (mean-based): KF mean (x, y, a|w, h) → xyxy
 template <int KIND>
-__device__ __forceinline__ void track_box(const double* g_mean, int T, int slot, double* box) {
-  double r[4] = {g_mean[slot], g_mean[T + slot], g_mean[2 * T + slot], g_mean[3 * T + slot]};
+__device__ __forceinline__ void track_box(const double* g_kf, int slot, double* box) {
+  const double2* m = (const double2*)(g_kf + (size_t)slot * KF_STRIDE);
+  const double2 m01 = m[0], m23 = m[1];
+  double r[4] = {m01.x, m01.y, m23.x, m23.y};
   if (KIND == KIND_BYTE) r[2] *= r[3];
   xywh2xyxy(r, box);
 }
@@ -295,9 +298,10 @@ __device__ __forceinline__ void det_measurement(const float* r, double* meas) {
 // ------------------------------------------------------------------------------------------
 // K1: BoT-SORT detection features.  STrack(det, feat) → update_features: f1 = f/|f|,
 // f2 = f1/|f1| (botsort_track.py:40-49; curr == smooth for a fresh track), then the float32 row
-// embedding_distance builds from it, B = (float)f2 / (|.|_np + 1e-8) (matching.py:266-287), and
-// scipy cdist's own norm of B.  The two norms n1, n2 are kept so K5 can recompute f2 bitwise
-// from the input row instead of storing it.  Grid (n_seq, ceil(D/4)); one wave per detection.
+// embedding_distance builds from it, B = (float)f2 / (|.|_np + 1e-8) (matching.py:266-287).  The
+// two norms n1, n2 are kept so K5 can recompute f2 bitwise from the input row instead of storing
+// it.  Grid (n_seq, ceil(D/64)); each wave walks 16 detections of its block's 64, the next
+// row's load in flight while the current one is normalised.
 template <typename FT, bool NPF>
 __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
                                                          const float* __restrict__ dets,
@@ -307,112 +311,315 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
   const int b = blockIdx.x, s = seq0 + b, w = wave_id(), lane = lane_id();
   const int F = P.F, D = P.D;
   const int d0 = det_off[b], N = min(det_off[b + 1] - d0, D);
-  const int k = blockIdx.y * NWAVE + w;
-  if (k >= N) return;  // wave-uniform
-  if (!((double)dets[(size_t)(d0 + k) * 6 + 4] > P.high)) return;
-  const FT* f = embs + (size_t)(d0 + k) * F;
-  float* Bk = P.dB + ((size_t)s * D + k) * F;
-  FT n1, n2;
+  const int k0 = blockIdx.y * 64, k1 = min(k0 + 64, N);
+  auto high = [&](int k) { return (double)dets[(size_t)(d0 + k) * 6 + 4] > P.high; };
+  auto next = [&](int k) {  // next high detection of this wave at or after k
+    for (; k < k1; k += NWAVE)
+      if (high(k)) return k;
+    return k1;
+  };
+  auto put_norms = [&](int k, FT n1, FT n2) {
+    if (lane == 0) {
+      P.dnrm[((size_t)s * D + k) * 2] = (double)n1;
+      P.dnrm[((size_t)s * D + k) * 2 + 1] = (double)n2;
+    }
+  };
   if (F <= REG_F) {
     float* wb = s_w + w * REG_F;
+    int k = next(k0 + w);
     RegRow<FT> x;
-    x.load(f, F);
-    n1 = x.norm(F);
-    x.div(n1);
-    n2 = x.norm(F);
-    x.div(n2);
-    const float dn = x.template np_dn<NPF>(wb, F);
+    if (k < k1) x.load(embs + (size_t)(d0 + k) * F, F);
+    while (k < k1) {
+      const int kn = next(k + NWAVE);
+      RegRow<FT> nx;
+      if (kn < k1) nx.load(embs + (size_t)(d0 + kn) * F, F);
+      const FT n1 = x.norm(F);
+      x.div(n1);
+      const FT n2 = x.norm(F);
+      x.div(n2);
+      const float dn = x.template np_dn<NPF>(wb, F);
+      float* Bk = P.dB + ((size_t)s * D + k) * F;
 #pragma unroll
-    for (int r = 0; r < REG_EPL; r++) {
-      const int q = lane + 64 * r;
-      if (q < F) {
-        const float bq = (float)x.v[r] / dn;
-        Bk[q] = bq;
-        wb[q] = bq;
+      for (int r = 0; r < REG_EPL; r++) {
+        const int q = lane + 64 * r;
+        if (q < F) Bk[q] = (float)x.v[r] / dn;
       }
+      put_norms(k, n1, n2);
+      x = nx;
+      k = kn;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) P.dnb[(size_t)s * D + k] = sqrt(dot2_f32(wb, wb, F));
-  } else {
+    return;
+  }
+  for (int k = next(k0 + w); k < k1; k = next(k + NWAVE)) {
+    const FT* f = embs + (size_t)(d0 + k) * F;
     FT* f2 = (FT*)P.fscr + ((size_t)s * D + k) * F;
-    n1 = wave_norm(f, F);
+    float* Bk = P.dB + ((size_t)s * D + k) * F;
+    const FT n1 = wave_norm(f, F);
     for (int q = lane; q < F; q += WAVE) f2[q] = f[q] / n1;
-    n2 = wave_norm((const FT*)f2, F);  // same lane mapping: reads own writes
+    const FT n2 = wave_norm((const FT*)f2, F);  // same lane mapping: reads own writes
     for (int q = lane; q < F; q += WAVE) f2[q] = f2[q] / n2;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // other lanes read f2 next
     const float dn = sqrtf(np_sumsq_sel<NPF>((const FT*)f2, F)) + 1e-8f;
     for (int q = lane; q < F; q += WAVE) Bk[q] = (float)f2[q] / dn;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    if (lane == 0) P.dnb[(size_t)s * D + k] = sqrt(dot2_f32(Bk, Bk, F));
+    put_norms(k, n1, n2);
   }
-  if (lane == 0) {
-    P.dnrm[((size_t)s * D + k) * 2] = (double)n1;
-    P.dnrm[((size_t)s * D + k) * 2 + 1] = (double)n2;
+}
+
+// ------------------------------------------------------------------------------------------
+// K1b: BoT-SORT gating (botsort.py:200-215): a (track, high det) pair enters the appearance
+// term iff its IoU distance <= proximity_thresh.  Every listed track (active ++ lost = the rows
+// of the first and third association) is tested against every high detection with the exact
+// fp64 cost K3 uses, so K3 finds each gated edge's embedding distance precomputed.  A track with
+// a gated pair gets its numpy float32 feature norm (embedding_distance's track-side row scale).
+// Grid (n_seq, GATE_BLOCKS); detection boxes staged in LDS; one wave per track, lanes over dets.
+constexpr int GATE_BLOCKS = 2;
+template <int KIND, typename FT, bool NPF>
+__global__ __launch_bounds__(WG) void gate_kernel(Dev P, int seq0, const float* __restrict__ dets,
+                                                  const int* __restrict__ det_off) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* s_db = (double*)smem;                      // [D][4] boxes, x1 = NaN if not high
+  const int b = blockIdx.x, s = seq0 + b, lane = lane_id(), T = P.T, D = P.D, F = P.F;
+  const int d0 = det_off[b], N = min(det_off[b + 1] - d0, D);
+  for (int j = threadIdx.x; j < N; j += WG) {
+    const float* r = dets + (size_t)(d0 + j) * 6;
+    double xyxy[4] = {(double)r[0], (double)r[1], (double)r[2], (double)r[3]};
+    double xywh[4], db[4];
+    xyxy2xywh(xyxy, xywh);
+    xywh2xyxy(xywh, db);
+    if (!((double)r[4] > P.high)) db[0] = __builtin_nan("");
+    for (int q = 0; q < 4; q++) s_db[4 * j + q] = db[q];
+  }
+  __syncthreads();
+  const int* seq = P.seq + (size_t)s * SQ_STRIDE;
+  const int na = seq[SQ_NA], nl = seq[SQ_NL];
+  const double* g_kf = P.kf + (size_t)s * T * KF_STRIDE;
+  uint32_t* pairs = P.pairs + (size_t)s * T * D;
+  for (int p = blockIdx.y * NWAVE + wave_id(); p < na + nl; p += GATE_BLOCKS * NWAVE) {
+    const int slot = p < na ? P.act[(size_t)s * T + p] : P.lost[(size_t)s * T + p - na];
+    double tb[4];
+    track_box<KIND>(g_kf, slot, tb);
+    int ng = 0;
+    for (int j0 = 0; j0 < N; j0 += WAVE) {
+      const int j = j0 + lane;
+      bool gated = false;
+      if (j < N && !__builtin_isnan(s_db[4 * j])) gated = !(1 - iou_pair(tb, s_db + 4 * j) > P.prox);
+      const unsigned long long m = __ballot(gated);
+      if (m) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&P.npair[s], __popcll(m));
+        base = __shfl(base, 0);
+        if (gated) pairs[base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(slot << 16 | j);
+        ng += __popcll(m);
+      }
+    }
+    if (ng) {
+      const FT* tf = (const FT*)P.feat + ((size_t)s * T + slot) * F;
+      const float dn = sqrtf(np_sumsq_sel<NPF>(tf, F)) + 1e-8f;
+      if (lane == 0) P.tdn[(size_t)s * T + slot] = dn;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K1c: embedding distance of every gated pair (matching.py:266-287 + botsort.py:209-214):
+// A = (float)smooth_feat / dn_t, B = the det's K1 row; scipy cdist cosine with its own
+// two-accumulator dots for A.B, |A|, |B|; /2; > appearance_thresh → 1.  Stored in the dense
+// per-sequence [T][D] table K3 reads.  The dots are sequential per pair (scipy's order), so a
+// lane owns a pair; a wave's 64 pairs stream through LDS in 16-element chunks loaded coalesced
+// (4 lanes per row, 16 B each), the A-side division done by the loading lane.
+// Grid (n_seq, COS_BLOCKS).
+constexpr int COS_BLOCKS = 2;
+constexpr int COS_CH = 16;
+template <typename FT>
+__device__ inline void cos_finish(Dev& P, int s, int slot, int dk, double ab, double aa,
+                                  double bb) {
+  double c = ab / (sqrt(aa) * sqrt(bb));
+  if (fabs(c) > 1.0) c = copysign(1.0, c);
+  double d = 1.0 - c;
+  d = d < 0.0 ? 0.0 : d;
+  double ed = d / 2.0;
+  if (ed > P.app) ed = 1.0;
+  P.etab[((size_t)s * P.T + slot) * P.D + dk] = ed;
+}
+template <typename FT>
+__global__ __launch_bounds__(WG) void cosine_kernel(Dev P, int seq0) {
+  __shared__ float s_a[NWAVE][WAVE][COS_CH + 1], s_b[NWAVE][WAVE][COS_CH + 1];
+  const int s = seq0 + blockIdx.x, T = P.T, D = P.D, F = P.F, w = wave_id(), lane = lane_id();
+  const int np = P.npair[s];
+  const uint32_t* pairs = P.pairs + (size_t)s * T * D;
+  for (int p0 = (blockIdx.y * NWAVE + w) * WAVE; p0 < np; p0 += COS_BLOCKS * NWAVE * WAVE) {
+    // this lane loads 4-element pieces of rows k*16 + lane/4 (k < 4) of the wave's 64 pairs
+    const FT* arow[4];
+    const float* brow[4];
+    float adn[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int pp = p0 + k * 16 + (lane >> 2);
+      const uint32_t pr = pp < np ? pairs[pp] : pairs[p0];
+      const int slot = pr >> 16, dk = pr & 0xffff;
+      arow[k] = (const FT*)P.feat + ((size_t)s * T + slot) * F + (lane & 3) * 4;
+      brow[k] = P.dB + ((size_t)s * D + dk) * F + (lane & 3) * 4;
+      adn[k] = P.tdn[(size_t)s * T + slot];
+    }
+    double ab0 = 0.0, ab1 = 0.0, aa0 = 0.0, aa1 = 0.0, bb0 = 0.0, bb1 = 0.0;
+    for (int c0 = 0; c0 < F; c0 += COS_CH) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int row = k * 16 + (lane >> 2), col = (lane & 3) * 4;
+        const float4 bv = *(const float4*)(brow[k] + c0);
+        float av[4];
+        if constexpr (sizeof(FT) == 4) {
+          const float4 t = *(const float4*)(arow[k] + c0);
+          av[0] = t.x; av[1] = t.y; av[2] = t.z; av[3] = t.w;
+        } else {
+          const double2 t0 = *(const double2*)(arow[k] + c0),
+                        t1 = *(const double2*)(arow[k] + c0 + 2);
+          av[0] = (float)t0.x; av[1] = (float)t0.y; av[2] = (float)t1.x; av[3] = (float)t1.y;
+        }
+        for (int q = 0; q < 4; q++) s_a[w][row][col + q] = av[q] / adn[k];
+        s_b[w][row][col + 0] = bv.x;
+        s_b[w][row][col + 1] = bv.y;
+        s_b[w][row][col + 2] = bv.z;
+        s_b[w][row][col + 3] = bv.w;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int q = 0; q < COS_CH; q += 2) {
+        const double x0 = (double)s_a[w][lane][q], x1 = (double)s_a[w][lane][q + 1];
+        const double y0 = (double)s_b[w][lane][q], y1 = (double)s_b[w][lane][q + 1];
+        ab0 += x0 * y0; ab1 += x1 * y1;
+        aa0 += x0 * x0; aa1 += x1 * x1;
+        bb0 += y0 * y0; bb1 += y1 * y1;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (p0 + lane < np) {
+      const uint32_t pr = pairs[p0 + lane];
+      cos_finish<FT>(P, s, pr >> 16, pr & 0xffff, ab0 + ab1, aa0 + aa1, bb0 + bb1);
+    }
+  }
+}
+
+// any F: thread per pair, element by element (same arithmetic as above)
+template <typename FT>
+__global__ __launch_bounds__(WG) void cosine_kernel_any(Dev P, int seq0) {
+  const int s = seq0 + blockIdx.x, T = P.T, D = P.D, F = P.F;
+  const int np = P.npair[s];
+  const uint32_t* pairs = P.pairs + (size_t)s * T * D;
+  for (int p = blockIdx.y * WG + threadIdx.x; p < np; p += COS_BLOCKS * WG) {
+    const uint32_t pr = pairs[p];
+    const int slot = pr >> 16, dk = pr & 0xffff;
+    const FT* a = (const FT*)P.feat + ((size_t)s * T + slot) * F;
+    const float* bq = P.dB + ((size_t)s * D + dk) * F;
+    const float dn = P.tdn[(size_t)s * T + slot];
+    double ab0 = 0.0, ab1 = 0.0, aa0 = 0.0, aa1 = 0.0, bb0 = 0.0, bb1 = 0.0;
+    int q = 0;
+    for (; q + 2 <= F; q += 2) {
+      const double x0 = (double)((float)a[q] / dn), x1 = (double)((float)a[q + 1] / dn);
+      const double y0 = (double)bq[q], y1 = (double)bq[q + 1];
+      ab0 += x0 * y0; ab1 += x1 * y1;
+      aa0 += x0 * x0; aa1 += x1 * x1;
+      bb0 += y0 * y0; bb1 += y1 * y1;
+    }
+    double ab = ab0 + ab1, aa = aa0 + aa1, bb = bb0 + bb1;
+    if (q < F) {
+      const double x0 = (double)((float)a[q] / dn), y0 = (double)bq[q];
+      ab += x0 * y0; aa += x0 * x0; bb += y0 * y0;
+    }
+    cos_finish<FT>(P, s, slot, dk, ab, aa, bb);
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // K2: STrack.multi_predict over strack_pool = joint(tracked, lost) (bytetrack.py:205-207,
-// botsort.py:188-189) and, for BoT-SORT with a CMC warp, multi_gmc over the pool and the
-// unconfirmed tracks (botsort.py:192-195).  Grid (n_seq, ceil(T/256)); thread per slot.
-template <int KIND, bool GMC>
-__global__ __launch_bounds__(WG) void predict_kernel(Dev P, int seq0,
-                                                     const double* __restrict__ warps) {
+// botsort.py:188-189).  With dt = 1, F·P·Fᵀ splits into 16 independent 2x2 "quads"
+// {(i,j), (i,j+4), (i+4,j), (i+4,j+4)}, i, j < 4: one thread per quad, 16 threads per slot, so a
+// wave reads/writes 4 slots' contiguous 576-byte states (each output is the same expression
+// kf_predict_soa evaluates).  Grid (n_seq, ceil(T/16)).
+template <int KIND>
+__global__ __launch_bounds__(WG) void predict_kernel(Dev P, int seq0) {
+  const int b = blockIdx.x, s = seq0 + b, T = P.T;
+  const int slot = blockIdx.y * (WG / 16) + (threadIdx.x >> 4), qd = threadIdx.x & 15;
+  if (slot >= T) return;
+  const uint32_t f = P.flags[(size_t)s * T + slot];
+  const bool pool = ((f & F_INACT) && (f & F_ACT)) || (f & F_INLOST);
+  if (!pool) return;
+  double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
+  double* c = m + 8;
+  const int i = qd >> 2, j = qd & 3;
+  double mv[4] = {m[0], m[1], m[2], m[3]}, q[8];
+  kf_process_noise(KIND, mv, q);  // reads mean[2], mean[3] only
+  const double p00 = c[8 * i + j], p10 = c[8 * (i + 4) + j], p01 = c[8 * i + j + 4],
+               p11 = c[8 * (i + 4) + j + 4];
+  double v = (p00 + p10) + (p01 + p11);
+  double v11 = p11;
+  if (i == j) { v = v + q[i]; v11 = v11 + q[i + 4]; }
+  __builtin_amdgcn_wave_barrier();  // every lane of the slot has read mean[0..3] (same wave)
+  c[8 * i + j] = v;
+  c[8 * i + j + 4] = p01 + p11;
+  c[8 * (i + 4) + j] = p10 + p11;
+  c[8 * (i + 4) + j + 4] = v11;
+  if (qd == 0) {
+    double mm[8];
+    for (int k = 0; k < 8; k++) mm[k] = m[k];
+    if (st_of(f) != ST_TRACKED) {
+      if (KIND == KIND_BOT) mm[6] = 0.0;
+      mm[7] = 0.0;
+      m[6] = mm[6];
+      m[7] = mm[7];
+    }
+    for (int k = 0; k < 4; k++) m[k] = mm[k] + mm[k + 4];
+  }
+}
+
+// K2b: BoT-SORT multi_gmc (botsort.py:192-195; cmc warp applied to pool + unconfirmed):
+// R8 = kron(I4, R): mean = R8·mean + t, cov = R8·cov·R8ᵀ.  Thread per slot (only with a warp).
+__global__ __launch_bounds__(WG) void gmc_kernel(Dev P, int seq0, const double* __restrict__ warps) {
   const int b = blockIdx.x, s = seq0 + b, T = P.T;
   const int slot = blockIdx.y * WG + threadIdx.x;
   if (slot >= T) return;
   const uint32_t f = P.flags[(size_t)s * T + slot];
-  const bool pool = ((f & F_INACT) && (f & F_ACT)) || (f & F_INLOST);
-  const bool unconf = (f & F_INACT) && !(f & F_ACT);
-  const double* H = GMC ? warps + 6 * (size_t)b : nullptr;
-  if (!pool && !(GMC && unconf)) return;
-  double* m = P.mean + (size_t)s * 8 * T + slot;
-  double* c = P.cov + (size_t)s * 64 * T + slot;
-  if (pool) {
-    if (st_of(f) != ST_TRACKED) {
-      if (KIND == KIND_BOT) m[6 * T] = 0.0;
-      m[7 * T] = 0.0;
-    }
-    kf_predict_soa(KIND, m, c, T);
+  if (!(f & (F_INACT | F_INLOST))) return;  // pool ∪ unconfirmed = every listed track
+  const double* H = warps + 6 * (size_t)b;
+  double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
+  double* c = m + 8;
+  double mm[8];
+  for (int q = 0; q < 8; q++) mm[q] = m[q];
+  for (int q = 0; q < 4; q++) {
+    double a0 = H[0] * mm[2 * q] + H[1] * mm[2 * q + 1];
+    double a1 = H[3] * mm[2 * q] + H[4] * mm[2 * q + 1];
+    mm[2 * q] = a0;
+    mm[2 * q + 1] = a1;
   }
-  if (GMC) {  // R8 = kron(I4, R): mean = R8·mean + t, cov = R8·cov·R8ᵀ
-    double mm[8];
-    for (int q = 0; q < 8; q++) mm[q] = m[q * T];
-    for (int q = 0; q < 4; q++) {
-      double a0 = H[0] * mm[2 * q] + H[1] * mm[2 * q + 1];
-      double a1 = H[3] * mm[2 * q] + H[4] * mm[2 * q + 1];
-      mm[2 * q] = a0;
-      mm[2 * q + 1] = a1;
+  mm[0] += H[2];
+  mm[1] += H[5];
+  for (int q = 0; q < 8; q++) m[q] = mm[q];
+  double RP[64];
+  for (int bq = 0; bq < 4; bq++)
+    for (int cc = 0; cc < 8; cc++) {
+      double x0 = c[8 * (2 * bq) + cc], x1 = c[8 * (2 * bq + 1) + cc];
+      RP[8 * (2 * bq) + cc] = H[0] * x0 + H[1] * x1;
+      RP[8 * (2 * bq + 1) + cc] = H[3] * x0 + H[4] * x1;
     }
-    mm[0] += H[2];
-    mm[1] += H[5];
-    for (int q = 0; q < 8; q++) m[q * T] = mm[q];
-    double RP[64];
-    for (int bq = 0; bq < 4; bq++)
-      for (int cc = 0; cc < 8; cc++) {
-        double x0 = c[(8 * (2 * bq) + cc) * T], x1 = c[(8 * (2 * bq + 1) + cc) * T];
-        RP[8 * (2 * bq) + cc] = H[0] * x0 + H[1] * x1;
-        RP[8 * (2 * bq + 1) + cc] = H[3] * x0 + H[4] * x1;
-      }
-    for (int r = 0; r < 8; r++)
-      for (int bq = 0; bq < 4; bq++) {
-        double y0 = RP[8 * r + 2 * bq], y1 = RP[8 * r + 2 * bq + 1];
-        c[(8 * r + 2 * bq) * T] = y0 * H[0] + y1 * H[1];
-        c[(8 * r + 2 * bq + 1) * T] = y0 * H[3] + y1 * H[4];
-      }
-  }
+  for (int r = 0; r < 8; r++)
+    for (int bq = 0; bq < 4; bq++) {
+      double y0 = RP[8 * r + 2 * bq], y1 = RP[8 * r + 2 * bq + 1];
+      c[8 * r + 2 * bq] = y0 * H[0] + y1 * H[1];
+      c[8 * r + 2 * bq + 1] = y0 * H[3] + y1 * H[4];
+    }
 }
 
 // ------------------------------------------------------------------------------------------
 // K3: the sequential heart of a frame, one workgroup per sequence: detection split, track lists,
 // the three assignments (candidate CSR, exact fp64 costs, lapx-semantics LAP), state/list
 // bookkeeping, id allocation.  Kalman/feature work is emitted as update records for K4/K5.
-template <int KIND, typename FT, bool NPF>
+template <int KIND>
 __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float* __restrict__ dets,
                                                    const int* __restrict__ det_off) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int T = P.T, D = P.D, F = P.F;
+  const int T = P.T, D = P.D;
   const LdsA Lo(T, D, P.elds);
   uint16_t* s_act = (uint16_t*)(smem + Lo.o_act);
   uint16_t* s_lost = (uint16_t*)(smem + Lo.o_lost);
@@ -439,7 +646,6 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
   uint16_t* s_rem = (uint16_t*)(smem + Lo.o_rem);
   uint16_t* s_ecol = (uint16_t*)(smem + Lo.o_ecol);
   double* s_ecost = (double*)(smem + Lo.o_ecost);
-  double* s_tna = (double*)(smem + Lo.o_tna);
   int* I = (int*)(smem + Lo.o_ints);
   int* scan_tmp = I + I_SCAN;
 
@@ -450,8 +656,7 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
   int* seq = P.seq + (size_t)s * SQ_STRIDE;
   uint32_t* g_flags = P.flags + sT;
   int* g_fid = P.frame_id + sT;
-  const double* g_mean = P.mean + (size_t)s * 8 * T;
-  const FT* g_feat = (const FT*)P.feat + (size_t)s * T * F;
+  const double* g_kf = P.kf + (size_t)s * T * KF_STRIDE;
   int2* g_rec = P.rec + (size_t)s * D;
   const bool REID = (KIND == KIND_BOT) && P.with_reid;
 
@@ -572,10 +777,9 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
     // columns j = lane + 64k (k < 4, i.e. C <= 256) in registers for the whole row sweep.
     for (int i = tid; i < R; i += WG) {
       double t[4];
-      track_box<KIND>(g_mean, T, rows[i], t);
+      track_box<KIND>(g_kf, rows[i], t);
       s_tboxf[i] = make_float4(__double2float_rd(t[0]), __double2float_rd(t[1]),
                                __double2float_ru(t[2]), __double2float_ru(t[3]));
-      s_srl[i] = 0;  // "row has a gated edge" flag; the LAP reuses s_srl afterwards
     }
     __syncthreads();
     const int lane = lane_id();
@@ -631,61 +835,27 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
       }
     }
     __syncthreads();
-    // pass 3: exact fp64 cost per candidate (gated ones flagged in the column's top bit)
+    // pass 3: exact fp64 cost per candidate; a gated pair (botsort.py:209-214) takes
+    // min(iou cost, embedding distance) with the distance K1c precomputed for it
     const int E = s_rowptr[R];
+    const double* etab = P.etab + (size_t)s * T * D;
     for (int e = tid; e < E; e += WG) {
       int j;
       double ri;
       get_edge(e, j, ri);
       const int i = (int)ri;
       double tb[4];
-      track_box<KIND>(g_mean, T, rows[i], tb);
+      track_box<KIND>(g_kf, rows[i], tb);
       bool g, cand;
-      const double c = pair_cost(tb, cols[j], g, cand);
-      put_edge(e, (g && cand) ? (j | 0x8000) : j, cand ? c : INF);
-      if (g && cand) s_srl[i] = 1;
+      double c = pair_cost(tb, cols[j], g, cand);
+      if (g && cand) {
+        const double ed = etab[(size_t)rows[i] * D + cols[j]];
+        c = c < ed ? c : ed;  // np.minimum(ious_dists, emb_dists)
+        cand = c < L;
+      }
+      put_edge(e, j, cand ? c : INF);
     }
     __syncthreads();
-    if (reid) {
-      // track rows as embedding_distance sees them: float32 smooth_feat / (np norm + 1e-8),
-      // one wave per row that has a gated edge
-      for (int i = wave_id(); i < R; i += NWAVE) {
-        if (!s_srl[i]) continue;  // wave-uniform
-        const FT* tf = g_feat + (size_t)rows[i] * F;
-        float* A = P.tA + ((size_t)s * T + rows[i]) * F;
-        const float dn = sqrtf(np_sumsq_sel<NPF>(tf, F)) + 1e-8f;
-        for (int q = lane; q < F; q += WAVE) A[q] = (float)tf[q] / dn;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-      __syncthreads();
-      for (int i = tid; i < R; i += WG) {
-        if (!s_srl[i]) continue;
-        const float* A = P.tA + ((size_t)s * T + rows[i]) * F;
-        s_tna[i] = sqrt(dot2_f32(A, A, F));
-      }
-      __syncthreads();
-      // emb_dists = cdist/2; > appearance_thresh → 1; (not gated → 1); dists = min(iou, emb)
-      // thread per gated edge; its row found by binary search over row_ptr
-      for (int e = tid; e < E; e += WG) {
-        int col;
-        double c;
-        get_edge(e, col, c);
-        if (!(col & 0x8000)) continue;
-        int lo = 0, hi = R;  // row_ptr[lo] <= e < row_ptr[lo+1]
-        while (hi - lo > 1) {
-          int mid = (lo + hi) >> 1;
-          if (s_rowptr[mid] <= e) lo = mid; else hi = mid;
-        }
-        const int j = col & 0x7fff, dk = cols[j];
-        double ed = cosine_rows(P.tA + ((size_t)s * T + rows[lo]) * F, s_tna[lo],
-                                P.dB + ((size_t)s * D + dk) * F, P.dnb[(size_t)s * D + dk],
-                                F) / 2.0;
-        if (ed > P.app) ed = 1.0;
-        double cm = c < ed ? c : ed;  // np.minimum(ious_dists, emb_dists)
-        put_edge(e, j, cm < L ? cm : INF);
-      }
-      __syncthreads();
-    }
     BX_STAMP(stamp);
     if (wave_id() == 0) lap_solve_wave(R, C, L, W);
     __syncthreads();
@@ -865,8 +1035,8 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
   const float* row = dets + (size_t)(det_off[b] + dk) * 6;
   double meas[4];
   det_measurement<KIND>(row, meas);
-  double* m = P.mean + (size_t)s * 8 * T + slot;
-  double* c = P.cov + (size_t)s * 64 * T + slot;
+  double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
+  double* c = m + 8;
   const double conf = (double)row[4], cls = (double)row[5];
   P.conf[sT + slot] = conf;
   P.detind[sT + slot] = dk;
@@ -874,8 +1044,8 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
   if (kind == R_NEW) {
     double m8[8], c64[64];
     kf_initiate(KIND, meas, m8, c64);
-    for (int q = 0; q < 8; q++) m[q * T] = m8[q];
-    for (int q = 0; q < 64; q++) c[q * T] = c64[q];
+    for (int q = 0; q < 8; q++) m[q] = m8[q];
+    for (int q = 0; q < 64; q++) c[q] = c64[q];
     P.tlen[sT + slot] = 0;
     P.cls[sT + slot] = cls;
     if (KIND == KIND_BOT) {
@@ -885,7 +1055,7 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
     }
     return;
   }
-  kf_update_soa(KIND, m, c, T, meas, 0.0);
+  kf_update_soa(KIND, m, c, 1, meas, 0.0);
   P.tlen[sT + slot] = kind == R_REACT ? 0 : P.tlen[sT + slot] + 1;
   double out_cls = cls;
   if (KIND == KIND_BOT) {  // update_cls
@@ -909,53 +1079,56 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
 // K5: BoT-SORT feature update per record carrying a detection feature (botsort_track.py:40-49):
 // a new track's smooth_feat = f2; otherwise feat = f2/|f2|; smooth = 0.9 smooth + 0.1 feat;
 // smooth /= |smooth|.  f2 is recomputed from the input row with K1's norms (bit-identical).
-// Grid (n_seq, ceil(D/4)); one wave per record.
+// Grid (n_seq, FEAT_BLOCKS); one wave per record.
+constexpr int FEAT_BLOCKS = 8;
 template <typename FT>
 __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
                                                      const int* __restrict__ det_off,
                                                      const FT* __restrict__ embs) {
   const int b = blockIdx.x, s = seq0 + b, F = P.F, D = P.D, lane = lane_id();
-  const int r = blockIdx.y * NWAVE + wave_id();
-  if (r >= P.seq[(size_t)s * SQ_STRIDE + SQ_NREC]) return;  // wave-uniform
-  const int2 rc = P.rec[(size_t)s * D + r];
-  const int slot = rc.x & 0xffff, kind = rc.x >> 16, dk = rc.y;
-  if (!(kind & R_FEAT)) return;
-  FT* sm = (FT*)P.feat + ((size_t)s * P.T + slot) * F;
+  const int nrec = P.seq[(size_t)s * SQ_STRIDE + SQ_NREC];
   const FT a = (FT)0.9, bb = (FT)(1.0 - 0.9);
-  if (F <= REG_F) {
-    const FT n1 = (FT)P.dnrm[((size_t)s * D + dk) * 2], n2 = (FT)P.dnrm[((size_t)s * D + dk) * 2 + 1];
-    RegRow<FT> g;
-    g.load(embs + (size_t)(det_off[b] + dk) * F, F);
-    g.div(n1);
-    g.div(n2);
-    if ((kind & 3) == R_NEW) {
-      g.store(sm, F);
-      return;
-    }
-    RegRow<FT> m;
-    m.load(sm, F);
-    const FT n3 = g.norm(F);
+  for (int r = blockIdx.y * NWAVE + wave_id(); r < nrec; r += FEAT_BLOCKS * NWAVE) {
+    const int2 rc = P.rec[(size_t)s * D + r];
+    const int slot = rc.x & 0xffff, kind = rc.x >> 16, dk = rc.y;
+    if (!(kind & R_FEAT)) continue;  // wave-uniform
+    FT* sm = (FT*)P.feat + ((size_t)s * P.T + slot) * F;
+    if (F <= REG_F) {
+      const FT n1 = (FT)P.dnrm[((size_t)s * D + dk) * 2];
+      const FT n2 = (FT)P.dnrm[((size_t)s * D + dk) * 2 + 1];
+      RegRow<FT> g;
+      g.load(embs + (size_t)(det_off[b] + dk) * F, F);
+      g.div(n1);
+      g.div(n2);
+      if ((kind & 3) == R_NEW) {
+        g.store(sm, F);
+        continue;
+      }
+      RegRow<FT> m;
+      m.load(sm, F);
+      const FT n3 = g.norm(F);
 #pragma unroll
-    for (int q = 0; q < REG_EPL; q++) {
-      FT g3 = g.v[q] / n3;
-      m.v[q] = a * m.v[q] + bb * g3;
+      for (int q = 0; q < REG_EPL; q++) {
+        FT g3 = g.v[q] / n3;
+        m.v[q] = a * m.v[q] + bb * g3;
+      }
+      m.div(m.norm(F));
+      m.store(sm, F);
+      continue;
     }
-    m.div(m.norm(F));
-    m.store(sm, F);
-    return;
+    const FT* f2 = (const FT*)P.fscr + ((size_t)s * D + dk) * F;
+    if ((kind & 3) == R_NEW) {
+      for (int q = lane; q < F; q += WAVE) sm[q] = f2[q];
+      continue;
+    }
+    const FT n3 = wave_norm(f2, F);
+    for (int q = lane; q < F; q += WAVE) {
+      FT g3 = f2[q] / n3;
+      sm[q] = a * sm[q] + bb * g3;
+    }
+    const FT ns = wave_norm((const FT*)sm, F);  // same lane mapping: reads own writes
+    for (int q = lane; q < F; q += WAVE) sm[q] = sm[q] / ns;
   }
-  const FT* f2 = (const FT*)P.fscr + ((size_t)s * D + dk) * F;
-  if ((kind & 3) == R_NEW) {
-    for (int q = lane; q < F; q += WAVE) sm[q] = f2[q];
-    return;
-  }
-  const FT n3 = wave_norm(f2, F);
-  for (int q = lane; q < F; q += WAVE) {
-    FT g3 = f2[q] / n3;
-    sm[q] = a * sm[q] + bb * g3;
-  }
-  const FT ns = wave_norm((const FT*)sm, F);  // same lane mapping: reads own writes
-  for (int q = lane; q < F; q += WAVE) sm[q] = sm[q] / ns;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -980,12 +1153,12 @@ __global__ __launch_bounds__(WG) void finish_kernel(Dev P, int seq0, const int* 
   const int tid = threadIdx.x, b = blockIdx.x, s = seq0 + b;
   const size_t sT = (size_t)s * T;
   int* seq = P.seq + (size_t)s * SQ_STRIDE;
-  const double* g_mean = P.mean + (size_t)s * 8 * T;
+  const double* g_kf = P.kf + (size_t)s * T * KF_STRIDE;
   const int* g_fid = P.frame_id + sT;
   const int* g_start = P.start + sT;
   uint32_t* g_flags = P.flags + sT;
   if (seq[SQ_SKIP]) {  // K3 refused the frame (capacity): state untouched, no output
-    if (tid == 0) out_count[b] = 0;
+    if (tid == 0) { out_count[b] = 0; P.npair[s] = 0; }
     return;
   }
   const int na2 = seq[SQ_NA2], nl2 = seq[SQ_NL2];
@@ -994,7 +1167,7 @@ __global__ __launch_bounds__(WG) void finish_kernel(Dev P, int seq0, const int* 
     const int sl = P.lost2[sT + q];
     s_fl[q] = (uint16_t)sl;
     s_dupl[q] = 0;
-    track_box<KIND>(g_mean, T, sl, s_lbox + 4 * q);
+    track_box<KIND>(g_kf, sl, s_lbox + 4 * q);
     s_lage[q] = g_fid[sl] - g_start[sl];
   }
   for (int k = tid; k < T; k += WG) s_keep[k] = 0;
@@ -1004,7 +1177,7 @@ __global__ __launch_bounds__(WG) void finish_kernel(Dev P, int seq0, const int* 
   for (int p = wave_id(); p < na2; p += NWAVE) {  // wave per active track, lanes over lost
     const int sa = s_fa[p];
     double ba[4];
-    track_box<KIND>(g_mean, T, sa, ba);
+    track_box<KIND>(g_kf, sa, ba);
     const int ta = g_fid[sa] - g_start[sa];
     bool dupa = false;
     for (int q = lane; q < nl2; q += WAVE) {
@@ -1036,7 +1209,7 @@ __global__ __launch_bounds__(WG) void finish_kernel(Dev P, int seq0, const int* 
       [&](int k, int p) {
         const int slot = s_fa[k];
         double box[4];
-        track_box<KIND>(g_mean, T, slot, box);
+        track_box<KIND>(g_kf, slot, box);
         double* o = out + (size_t)(d0 + p) * 8;
         o[0] = box[0]; o[1] = box[1]; o[2] = box[2]; o[3] = box[3];
         o[4] = (double)P.id[sT + slot];
@@ -1056,6 +1229,7 @@ __global__ __launch_bounds__(WG) void finish_kernel(Dev P, int seq0, const int* 
     seq[SQ_NA] = nfa;
     seq[SQ_NL] = nfl;
     out_count[b] = nout;
+    P.npair[s] = 0;
   }
 }
 
@@ -1118,21 +1292,29 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
                  hipStream_t st) {
   const Dev& d = e->dev;
   const bool reid = KIND == KIND_BOT && d.with_reid;
-  const int gy_det4 = (d.D + NWAVE - 1) / NWAVE, gy_slot = (d.T + WG - 1) / WG,
+  const int gy_det64 = (d.D + 63) / 64, gy_det4 = (d.D + NWAVE - 1) / NWAVE, gy_slot = (d.T + WG - 1) / WG,
             gy_det = (d.D + WG - 1) / WG;
   if (reid) {
-    hipLaunchKernelGGL((det_feature_kernel<FT, NPF>), dim3(nseq, gy_det4), dim3(WG), 0, st, d,
+    hipLaunchKernelGGL((det_feature_kernel<FT, NPF>), dim3(nseq, gy_det64), dim3(WG), 0, st, d,
                        seq0, dets, det_off, (const FT*)embs);
     HIPCHK(hipGetLastError());
   }
-  if (KIND == KIND_BOT && warps)
-    hipLaunchKernelGGL((predict_kernel<KIND, true>), dim3(nseq, gy_slot), dim3(WG), 0, st, d,
-                       seq0, warps);
-  else
-    hipLaunchKernelGGL((predict_kernel<KIND, false>), dim3(nseq, gy_slot), dim3(WG), 0, st, d,
-                       seq0, warps);
+  hipLaunchKernelGGL(predict_kernel<KIND>, dim3(nseq, (d.T + 15) / 16), dim3(WG), 0, st, d, seq0);
   HIPCHK(hipGetLastError());
-  auto assoc = assoc_kernel<KIND, FT, NPF>;
+  if (KIND == KIND_BOT && warps)
+    hipLaunchKernelGGL(gmc_kernel, dim3(nseq, gy_slot), dim3(WG), 0, st, d, seq0, warps);
+  HIPCHK(hipGetLastError());
+  if (reid) {
+    hipLaunchKernelGGL((gate_kernel<KIND, FT, NPF>), dim3(nseq, GATE_BLOCKS), dim3(WG),
+                       sizeof(double) * 4 * d.D, st, d, seq0, dets, det_off);
+    HIPCHK(hipGetLastError());
+    if (d.F % COS_CH == 0)
+      hipLaunchKernelGGL(cosine_kernel<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st, d, seq0);
+    else
+      hipLaunchKernelGGL(cosine_kernel_any<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st, d, seq0);
+    HIPCHK(hipGetLastError());
+  }
+  auto assoc = assoc_kernel<KIND>;
   if (int rc = lds_attr((const void*)assoc, e->lds_assoc)) return rc;
   hipLaunchKernelGGL(assoc, dim3(nseq), dim3(WG), e->lds_assoc, st, d, seq0, dets, det_off);
   HIPCHK(hipGetLastError());
@@ -1140,7 +1322,7 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
                      det_off);
   HIPCHK(hipGetLastError());
   if (reid) {
-    hipLaunchKernelGGL(feature_kernel<FT>, dim3(nseq, gy_det4), dim3(WG), 0, st, d, seq0,
+    hipLaunchKernelGGL(feature_kernel<FT>, dim3(nseq, FEAT_BLOCKS), dim3(WG), 0, st, d, seq0,
                        det_off, (const FT*)embs);
     HIPCHK(hipGetLastError());
   }
@@ -1217,8 +1399,7 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
     d.detind = carve<int>(p, ST);
     d.conf = carve<double>(p, ST);
     d.cls = carve<double>(p, ST);
-    d.mean = carve<double>(p, ST * 8);
-    d.cov = carve<double>(p, ST * 64);
+    d.kf = carve<double>(p, ST * KF_STRIDE);
     d.feat = carve<char>(p, fs * ST * FF);
     d.clsh = carve<double>(p, ST * CLS_HIST * 2);
     d.ncls = carve<int>(p, ST);
@@ -1226,9 +1407,11 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
     d.gcost = carve<double>(p, ST * D);
     d.rec = carve<int2>(p, SD);
     d.dnrm = carve<double>(p, SD * 2);
-    d.dnb = carve<double>(p, SD);
     d.dB = carve<float>(p, SD * FF);
-    d.tA = carve<float>(p, ST * FF);
+    d.tdn = carve<float>(p, reid ? ST : 1);
+    d.pairs = carve<uint32_t>(p, reid ? ST * D : 1);
+    d.npair = carve<int>(p, S);
+    d.etab = carve<double>(p, reid ? ST * D : 1);
     d.fscr = carve<char>(p, fs * SD * FS);
     d.status = carve<int>(p, 16);
     return (size_t)(p - p0);
@@ -1395,7 +1578,7 @@ int bx_engine_tracks_host(bx_engine* e, int seq, int cap, int32_t* ids, int32_t*
   std::vector<uint16_t> act(T), lost(T);
   std::vector<uint32_t> fl(T);
   std::vector<int> id(T), fid(T), st(T);
-  std::vector<double> m((size_t)8 * T), c((size_t)64 * T);
+  std::vector<double> kf((size_t)KF_STRIDE * T);
   const size_t sT = (size_t)seq * T;
   HIPCHK(hipMemcpy(act.data(), e->dev.act + sT, 2 * T, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(lost.data(), e->dev.lost + sT, 2 * T, hipMemcpyDeviceToHost));
@@ -1403,8 +1586,8 @@ int bx_engine_tracks_host(bx_engine* e, int seq, int cap, int32_t* ids, int32_t*
   HIPCHK(hipMemcpy(id.data(), e->dev.id + sT, 4 * T, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(fid.data(), e->dev.frame_id + sT, 4 * T, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(st.data(), e->dev.start + sT, 4 * T, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(m.data(), e->dev.mean + sT * 8, 8 * 8 * (size_t)T, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(c.data(), e->dev.cov + sT * 64, 8 * 64 * (size_t)T, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(kf.data(), e->dev.kf + sT * KF_STRIDE, 8 * KF_STRIDE * (size_t)T,
+                   hipMemcpyDeviceToHost));
   for (int k = 0; k < na + nl; k++) {
     const int slot = k < na ? act[k] : lost[k - na];
     if (ids) ids[k] = id[slot];
@@ -1412,8 +1595,8 @@ int bx_engine_tracks_host(bx_engine* e, int seq, int cap, int32_t* ids, int32_t*
     if (is_activated) is_activated[k] = (fl[slot] & F_ACT) ? 1 : 0;
     if (frame_id) frame_id[k] = fid[slot];
     if (start_frame) start_frame[k] = st[slot];
-    for (int q = 0; q < 8 && mean; q++) mean[8 * k + q] = m[(size_t)q * T + slot];
-    for (int q = 0; q < 64 && cov; q++) cov[64 * k + q] = c[(size_t)q * T + slot];
+    for (int q = 0; q < 8 && mean; q++) mean[8 * k + q] = kf[(size_t)slot * KF_STRIDE + q];
+    for (int q = 0; q < 64 && cov; q++) cov[64 * k + q] = kf[(size_t)slot * KF_STRIDE + 8 + q];
   }
   return BX_OK;
 }
