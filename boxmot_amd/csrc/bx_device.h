@@ -19,9 +19,11 @@ enum : int { KIND_BYTE = 0, KIND_BOT = 1 };
 enum : uint32_t { ST_NEW = 0, ST_TRACKED = 1, ST_LOST = 2, ST_REMOVED = 3 };
 // per-slot persistent flag word; F_INACT / F_INLOST: the slot is on the active / lost list
 // (lets the slot-parallel kernels select joint(tracked, lost) without walking the lists)
+// F_PRED / F_GMC / F_REC are frame-transient: mean predicted (covariance predict pending), CMC
+// warp applied to the mean (covariance warp pending), slot has an update record this frame.
 enum : uint32_t {
   F_STATE = 0x7u, F_ACT = 0x8u, F_INREM = 0x10u, F_INUSE = 0x20u, F_INACT = 0x40u,
-  F_INLOST = 0x80u
+  F_INLOST = 0x80u, F_PRED = 0x100u, F_GMC = 0x200u, F_REC = 0x400u, F_TRANSIENT = 0x700u
 };
 
 __device__ __forceinline__ uint32_t st_of(uint32_t f) { return f & F_STATE; }
@@ -434,6 +436,7 @@ struct LapWS {
   uint16_t* srlist;       // [R] rows visited (SR) except the root
   int* coldeg;            // [C] finite-edge degree per column (single-edge-component fast path)
   uint16_t* roots;        // [R] rows left for the Dijkstra phase, ascending
+  unsigned long long* dbg = nullptr;  // diagnostic counters (phase-timing builds only)
 };
 
 __device__ __forceinline__ void lap_edge(const LapWS& w, int e, int& col, double& cost) {
@@ -486,6 +489,8 @@ __device__ inline void lap_solve_wave(int R, int C, double L, const LapWS& w) {
       w.col4row[r] = (int16_t)jj;
       w.row4col[jj] = (int16_t)r;
       w.u[r] = cc - L;
+    } else if (nf == 0) {
+      w.col4row[r] = -2;  // only inadmissible candidates: its search would end at its dummy
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -495,13 +500,15 @@ __device__ inline void lap_solve_wave(int R, int C, double L, const LapWS& w) {
   int nroots = 0;
   for (int c = 0; c < R; c += WAVE) {
     const int r = c + lane;
-    const bool need = r < R && w.row_ptr[r + 1] > w.row_ptr[r] && w.col4row[r] < 0;
+    const bool need = r < R && w.row_ptr[r + 1] > w.row_ptr[r] && w.col4row[r] == -1;
     const unsigned long long m = __ballot(need);
     if (need) w.roots[nroots + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)r;
     nroots += __popcll(m);
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  int nsteps = 0;
+  if (w.dbg && lane == 0) w.dbg[3] = __builtin_amdgcn_s_memtime();
   for (int t = 0; t < nroots; t++) {
     const int root = w.roots[t];
     double minVal = 0.0;
@@ -557,6 +564,7 @@ __device__ inline void lap_solve_wave(int R, int C, double L, const LapWS& w) {
         break;
       }
       const int j = w.touched[bk];
+      nsteps++;
       minVal = bv;
       if (lane == 0) w.colflag[j] |= 1;
       const int r4c = w.row4col[j];
@@ -608,6 +616,15 @@ __device__ inline void lap_solve_wave(int R, int C, double L, const LapWS& w) {
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  for (int r = lane; r < R; r += WAVE)
+    if (w.col4row[r] == -2) w.col4row[r] = -1;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  if (w.dbg && lane == 0) {
+    w.dbg[0] = nroots;
+    w.dbg[1] = nsteps;
+    w.dbg[2] = R;
   }
 }
 

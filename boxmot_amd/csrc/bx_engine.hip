@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -39,7 +40,10 @@ constexpr int ELDS_DEFAULT = 1024;  // LAP edges kept in LDS; the rest spill to 
 constexpr int REG_F = 512;   // feature rows up to this width live in registers: 8 per lane
 constexpr int REG_EPL = REG_F / 64;
 constexpr int NWAVE = WG / WAVE;
-constexpr int KF_STRIDE = 72;  // doubles per slot: mean[8] + covariance[64], contiguous
+// doubles per slot: mean[8], covariance[64], then the pre-predict mean[2], mean[3] the pending
+// covariance predict's process noise is computed from (see K2)
+constexpr int KF_STRIDE = 74;
+constexpr int KF_QM = 72;
 
 // A feature row held by one wave, element q = lane + 64 r in v[r] (F <= REG_F).
 template <typename FT>
@@ -161,9 +165,8 @@ struct Dev {
   uint16_t* gcol;     // [S][T*D] LAP edge overflow
   double* gcost;      // [S][T*D]
   int2* rec;          // [S][D] frame scratch: update records (K3 → K4/K5)
-  double* dnrm;       // [S][D][2] frame scratch: n1, n2 of STrack.update_features per det
-  float* dB;          // [S][D][F] frame scratch: det rows as embedding_distance normalises them
-  float* tdn;         // [S][T] frame scratch: numpy float32 norm (+1e-8) of a gated slot's feature
+  double* dnrm;       // [S][D][4] frame scratch: n1, n2 (update_features), dn (embedding_distance)
+  float* tdn;         // [S][T] numpy float32 norm (+1e-8) of each track's smooth_feat (K5 keeps it)
   uint32_t* pairs;    // [S][T*D] frame scratch: gated (slot << 16 | det) pairs
   int* npair;         // [S] gated pair count (zeroed by K6 for the next frame)
   double* etab;       // [S][T][D] frame scratch: embedding distance of gated pairs
@@ -192,9 +195,10 @@ enum {
 // update records: x = slot | kind << 16, y = detection index within the sequence's frame
 enum : int { R_UPDATE = 0, R_REACT = 1, R_NEW = 2, R_FEAT = 4 };
 
+constexpr int NBIN = 64;  // x-bins of the candidate sweep (one wave scans them)
 // LDS carve-out of the association kernel (host and device agree on it).
 struct LdsA {
-  size_t o_dbox, o_dboxf, o_dconf, o_tboxf, o_u, o_v, o_spc, o_ecost, o_flags, o_fid,
+  size_t o_dbox, o_dboxf, o_dconf, o_tboxf, o_cbox, o_bin, o_bcol, o_u, o_v, o_spc, o_ecost, o_flags, o_fid,
       o_rowptr, o_ints, o_act, o_lost, o_unconf, o_pool, o_rtr, o_lostl, o_refind, o_newt,
       o_c4r, o_srl, o_roots, o_r4c, o_path, o_touch, o_cdeg, o_hd, o_sd, o_rem, o_ecol, o_mark,
       o_colf, o_dkind, total;
@@ -208,6 +212,9 @@ struct LdsA {
     o_dbox = take(sizeof(double) * 4 * D);
     o_dboxf = take(sizeof(float) * 4 * D);  // outward-rounded fp32 copy for candidate tests
     o_tboxf = take(sizeof(float) * 4 * T);  // same for the rows of the current association
+    o_cbox = take(sizeof(float) * 4 * D);   // the current association's column boxes, in order
+    o_bin = take(sizeof(int) * (2 * NBIN + 2));  // x-bin starts and cursors
+    o_bcol = take(2 * D);                        // columns grouped by x-bin
     o_dconf = take(sizeof(double) * D);
     o_u = take(sizeof(double) * T);
     o_v = take(sizeof(double) * D);
@@ -268,7 +275,7 @@ struct LdsF {
 // mark bits (per slot, per frame)
 enum : uint8_t { M_POOL = 1, M_ACT2 = 2, M_REMNOW = 4, M_TMP = 32 };
 // ints[] scratch slots
-enum { I_NA = 0, I_NL, I_FC, I_IDC, I_ERR, I_SCAN = 32 };
+enum { I_NA = 0, I_NL, I_FC, I_IDC, I_ERR, I_XMIN, I_XMAX, I_W, I_SCAN = 32 };
 
 // STrack.xyxy of a track (mean-based): KF mean (x, y, a|w, h) → xyxy
 template <int KIND>
@@ -297,11 +304,12 @@ __device__ __forceinline__ void det_measurement(const float* r, double* meas) {
 
 // ------------------------------------------------------------------------------------------
 // K1: BoT-SORT detection features.  STrack(det, feat) → update_features: f1 = f/|f|,
-// f2 = f1/|f1| (botsort_track.py:40-49; curr == smooth for a fresh track), then the float32 row
-// embedding_distance builds from it, B = (float)f2 / (|.|_np + 1e-8) (matching.py:266-287).  The
-// two norms n1, n2 are kept so K5 can recompute f2 bitwise from the input row instead of storing
-// it.  Grid (n_seq, ceil(D/64)); each wave walks 16 detections of its block's 64, the next
-// row's load in flight while the current one is normalised.
+// f2 = f1/|f1| (botsort_track.py:40-49; curr == smooth for a fresh track), and the numpy
+// float32 norm dn of (float)f2 that embedding_distance scales the det row by (matching.py:
+// 266-287).  Only the three norms are stored: every later use (K1c's cosine rows, K5's EMA)
+// recomputes f2 = (f / n1) / n2 elementwise from the input row, bit-identically.
+// Grid (n_seq, ceil(D/64)); each wave walks 16 detections of its block's 64, the next row's
+// load in flight while the current one is normalised.
 template <typename FT, bool NPF>
 __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
                                                          const float* __restrict__ dets,
@@ -318,10 +326,12 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
       if (high(k)) return k;
     return k1;
   };
-  auto put_norms = [&](int k, FT n1, FT n2) {
+  auto put_norms = [&](int k, FT n1, FT n2, float dn) {
     if (lane == 0) {
-      P.dnrm[((size_t)s * D + k) * 2] = (double)n1;
-      P.dnrm[((size_t)s * D + k) * 2 + 1] = (double)n2;
+      double* o = P.dnrm + ((size_t)s * D + k) * 4;
+      o[0] = (double)n1;
+      o[1] = (double)n2;
+      o[2] = (double)dn;
     }
   };
   if (F <= REG_F) {
@@ -337,14 +347,7 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
       x.div(n1);
       const FT n2 = x.norm(F);
       x.div(n2);
-      const float dn = x.template np_dn<NPF>(wb, F);
-      float* Bk = P.dB + ((size_t)s * D + k) * F;
-#pragma unroll
-      for (int r = 0; r < REG_EPL; r++) {
-        const int q = lane + 64 * r;
-        if (q < F) Bk[q] = (float)x.v[r] / dn;
-      }
-      put_norms(k, n1, n2);
+      put_norms(k, n1, n2, x.template np_dn<NPF>(wb, F));
       x = nx;
       k = kn;
     }
@@ -353,15 +356,12 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
   for (int k = next(k0 + w); k < k1; k = next(k + NWAVE)) {
     const FT* f = embs + (size_t)(d0 + k) * F;
     FT* f2 = (FT*)P.fscr + ((size_t)s * D + k) * F;
-    float* Bk = P.dB + ((size_t)s * D + k) * F;
     const FT n1 = wave_norm(f, F);
     for (int q = lane; q < F; q += WAVE) f2[q] = f[q] / n1;
     const FT n2 = wave_norm((const FT*)f2, F);  // same lane mapping: reads own writes
     for (int q = lane; q < F; q += WAVE) f2[q] = f2[q] / n2;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // other lanes read f2 next
-    const float dn = sqrtf(np_sumsq_sel<NPF>((const FT*)f2, F)) + 1e-8f;
-    for (int q = lane; q < F; q += WAVE) Bk[q] = (float)f2[q] / dn;
-    put_norms(k, n1, n2);
+    put_norms(k, n1, n2, sqrtf(np_sumsq_sel<NPF>((const FT*)f2, F)) + 1e-8f);
   }
 }
 
@@ -369,16 +369,17 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
 // K1b: BoT-SORT gating (botsort.py:200-215): a (track, high det) pair enters the appearance
 // term iff its IoU distance <= proximity_thresh.  Every listed track (active ++ lost = the rows
 // of the first and third association) is tested against every high detection with the exact
-// fp64 cost K3 uses, so K3 finds each gated edge's embedding distance precomputed.  A track with
-// a gated pair gets its numpy float32 feature norm (embedding_distance's track-side row scale).
-// Grid (n_seq, GATE_BLOCKS); detection boxes staged in LDS; one wave per track, lanes over dets.
+// fp64 cost K3 uses, so K3 finds each gated edge's embedding distance precomputed.
+// Grid (n_seq, GATE_BLOCKS); detection boxes staged in LDS (fp64 + outward-rounded fp32 for a
+// conservative reject); one thread per track, detections walked in order from LDS (broadcast).
 constexpr int GATE_BLOCKS = 2;
-template <int KIND, typename FT, bool NPF>
+template <int KIND>
 __global__ __launch_bounds__(WG) void gate_kernel(Dev P, int seq0, const float* __restrict__ dets,
                                                   const int* __restrict__ det_off) {
   extern __shared__ __align__(16) unsigned char smem[];
-  double* s_db = (double*)smem;                      // [D][4] boxes, x1 = NaN if not high
-  const int b = blockIdx.x, s = seq0 + b, lane = lane_id(), T = P.T, D = P.D, F = P.F;
+  const int b = blockIdx.x, s = seq0 + b, T = P.T, D = P.D;
+  double* s_db = (double*)smem;                             // [D][4]
+  float4* s_fb = (float4*)(smem + sizeof(double) * 4 * D);  // [D], x1 = NaN if not high
   const int d0 = det_off[b], N = min(det_off[b + 1] - d0, D);
   for (int j = threadIdx.x; j < N; j += WG) {
     const float* r = dets + (size_t)(d0 + j) * 6;
@@ -386,51 +387,47 @@ __global__ __launch_bounds__(WG) void gate_kernel(Dev P, int seq0, const float* 
     double xywh[4], db[4];
     xyxy2xywh(xyxy, xywh);
     xywh2xyxy(xywh, db);
-    if (!((double)r[4] > P.high)) db[0] = __builtin_nan("");
     for (int q = 0; q < 4; q++) s_db[4 * j + q] = db[q];
+    s_fb[j] = (double)r[4] > P.high
+                  ? make_float4(__double2float_rd(db[0]), __double2float_rd(db[1]),
+                                __double2float_ru(db[2]), __double2float_ru(db[3]))
+                  : make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
   }
   __syncthreads();
   const int* seq = P.seq + (size_t)s * SQ_STRIDE;
   const int na = seq[SQ_NA], nl = seq[SQ_NL];
   const double* g_kf = P.kf + (size_t)s * T * KF_STRIDE;
   uint32_t* pairs = P.pairs + (size_t)s * T * D;
-  for (int p = blockIdx.y * NWAVE + wave_id(); p < na + nl; p += GATE_BLOCKS * NWAVE) {
+  const bool prefilter = P.prox < 1.0;  // gating needs IoU > 0, i.e. intersecting boxes
+  for (int p = blockIdx.y * WG + threadIdx.x; p < na + nl; p += GATE_BLOCKS * WG) {
     const int slot = p < na ? P.act[(size_t)s * T + p] : P.lost[(size_t)s * T + p - na];
     double tb[4];
     track_box<KIND>(g_kf, slot, tb);
-    int ng = 0;
-    for (int j0 = 0; j0 < N; j0 += WAVE) {
-      const int j = j0 + lane;
-      bool gated = false;
-      if (j < N && !__builtin_isnan(s_db[4 * j])) gated = !(1 - iou_pair(tb, s_db + 4 * j) > P.prox);
-      const unsigned long long m = __ballot(gated);
-      if (m) {
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&P.npair[s], __popcll(m));
-        base = __shfl(base, 0);
-        if (gated) pairs[base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(slot << 16 | j);
-        ng += __popcll(m);
-      }
-    }
-    if (ng) {
-      const FT* tf = (const FT*)P.feat + ((size_t)s * T + slot) * F;
-      const float dn = sqrtf(np_sumsq_sel<NPF>(tf, F)) + 1e-8f;
-      if (lane == 0) P.tdn[(size_t)s * T + slot] = dn;
+    const float4 tf = make_float4(__double2float_rd(tb[0]), __double2float_rd(tb[1]),
+                                  __double2float_ru(tb[2]), __double2float_ru(tb[3]));
+    for (int j = 0; j < N; j++) {
+      const float4 db = s_fb[j];
+      if (__builtin_isnan(db.x)) continue;  // not a high detection
+      if (prefilter &&
+          !((fminf(tf.z, db.z) > fmaxf(tf.x, db.x)) & (fminf(tf.w, db.w) > fmaxf(tf.y, db.y))))
+        continue;
+      if (!(1 - iou_pair(tb, s_db + 4 * j) > P.prox))
+        pairs[atomicAdd(&P.npair[s], 1)] = (uint32_t)(slot << 16 | j);
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // K1c: embedding distance of every gated pair (matching.py:266-287 + botsort.py:209-214):
-// A = (float)smooth_feat / dn_t, B = the det's K1 row; scipy cdist cosine with its own
+// A = (float)smooth_feat / dn_t (dn_t kept per track by K5), B = (float)f2 / dn_d with f2 =
+// (f / n1) / n2 rebuilt from the input row (K1's norms); scipy cdist cosine with its own
 // two-accumulator dots for A.B, |A|, |B|; /2; > appearance_thresh → 1.  Stored in the dense
 // per-sequence [T][D] table K3 reads.  The dots are sequential per pair (scipy's order), so a
 // lane owns a pair; a wave's 64 pairs stream through LDS in 16-element chunks loaded coalesced
-// (4 lanes per row, 16 B each), the A-side division done by the loading lane.
+// (4 lanes per row, 16 B each), the elementwise divisions done by the loading lane.
 // Grid (n_seq, COS_BLOCKS).
-constexpr int COS_BLOCKS = 2;
+constexpr int COS_BLOCKS = 1;
 constexpr int COS_CH = 16;
-template <typename FT>
 __device__ inline void cos_finish(Dev& P, int s, int slot, int dk, double ab, double aa,
                                   double bb) {
   double c = ab / (sqrt(aa) * sqrt(bb));
@@ -442,45 +439,60 @@ __device__ inline void cos_finish(Dev& P, int s, int slot, int dk, double ab, do
   P.etab[((size_t)s * P.T + slot) * P.D + dk] = ed;
 }
 template <typename FT>
-__global__ __launch_bounds__(WG) void cosine_kernel(Dev P, int seq0) {
+__device__ __forceinline__ void load4(const FT* p, FT* v) {
+  if constexpr (sizeof(FT) == 4) {
+    const float4 t = *(const float4*)p;
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+    const double2 t0 = *(const double2*)p, t1 = *(const double2*)(p + 2);
+    v[0] = t0.x; v[1] = t0.y; v[2] = t1.x; v[3] = t1.y;
+  }
+}
+template <typename FT>
+__global__ __launch_bounds__(WG) void cosine_kernel(Dev P, int seq0, const int* __restrict__ det_off,
+                                                    const FT* __restrict__ embs) {
   __shared__ float s_a[NWAVE][WAVE][COS_CH + 1], s_b[NWAVE][WAVE][COS_CH + 1];
-  const int s = seq0 + blockIdx.x, T = P.T, D = P.D, F = P.F, w = wave_id(), lane = lane_id();
-  const int np = P.npair[s];
+  const int b = blockIdx.x, s = seq0 + b, T = P.T, D = P.D, F = P.F, w = wave_id(),
+            lane = lane_id();
+  const int np = P.npair[s], d0 = det_off[b];
   const uint32_t* pairs = P.pairs + (size_t)s * T * D;
   for (int p0 = (blockIdx.y * NWAVE + w) * WAVE; p0 < np; p0 += COS_BLOCKS * NWAVE * WAVE) {
     // this lane loads 4-element pieces of rows k*16 + lane/4 (k < 4) of the wave's 64 pairs
     const FT* arow[4];
-    const float* brow[4];
-    float adn[4];
+    const FT* brow[4];
+    float adn[4], bdn[4];
+    FT bn1[4], bn2[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const int pp = p0 + k * 16 + (lane >> 2);
       const uint32_t pr = pp < np ? pairs[pp] : pairs[p0];
       const int slot = pr >> 16, dk = pr & 0xffff;
       arow[k] = (const FT*)P.feat + ((size_t)s * T + slot) * F + (lane & 3) * 4;
-      brow[k] = P.dB + ((size_t)s * D + dk) * F + (lane & 3) * 4;
+      brow[k] = embs + (size_t)(d0 + dk) * F + (lane & 3) * 4;
       adn[k] = P.tdn[(size_t)s * T + slot];
+      const double* nr = P.dnrm + ((size_t)s * D + dk) * 4;
+      bn1[k] = (FT)nr[0];
+      bn2[k] = (FT)nr[1];
+      bdn[k] = (float)nr[2];
     }
     double ab0 = 0.0, ab1 = 0.0, aa0 = 0.0, aa1 = 0.0, bb0 = 0.0, bb1 = 0.0;
+    FT av[4][4], bv[4][4];  // raw elements of the current chunk; the next chunk's are in flight
+#pragma unroll
+    for (int k = 0; k < 4; k++) { load4(arow[k], av[k]); load4(brow[k], bv[k]); }
     for (int c0 = 0; c0 < F; c0 += COS_CH) {
+      FT nav[4][4], nbv[4][4];
+      const int cn = c0 + COS_CH < F ? c0 + COS_CH : c0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) { load4(arow[k] + cn, nav[k]); load4(brow[k] + cn, nbv[k]); }
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const int row = k * 16 + (lane >> 2), col = (lane & 3) * 4;
-        const float4 bv = *(const float4*)(brow[k] + c0);
-        float av[4];
-        if constexpr (sizeof(FT) == 4) {
-          const float4 t = *(const float4*)(arow[k] + c0);
-          av[0] = t.x; av[1] = t.y; av[2] = t.z; av[3] = t.w;
-        } else {
-          const double2 t0 = *(const double2*)(arow[k] + c0),
-                        t1 = *(const double2*)(arow[k] + c0 + 2);
-          av[0] = (float)t0.x; av[1] = (float)t0.y; av[2] = (float)t1.x; av[3] = (float)t1.y;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          s_a[w][row][col + q] = (float)av[k][q] / adn[k];
+          const FT f2 = (bv[k][q] / bn1[k]) / bn2[k];
+          s_b[w][row][col + q] = (float)f2 / bdn[k];
         }
-        for (int q = 0; q < 4; q++) s_a[w][row][col + q] = av[q] / adn[k];
-        s_b[w][row][col + 0] = bv.x;
-        s_b[w][row][col + 1] = bv.y;
-        s_b[w][row][col + 2] = bv.z;
-        s_b[w][row][col + 3] = bv.w;
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -494,108 +506,80 @@ __global__ __launch_bounds__(WG) void cosine_kernel(Dev P, int seq0) {
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) { av[k][q] = nav[k][q]; bv[k][q] = nbv[k][q]; }
     }
     if (p0 + lane < np) {
       const uint32_t pr = pairs[p0 + lane];
-      cos_finish<FT>(P, s, pr >> 16, pr & 0xffff, ab0 + ab1, aa0 + aa1, bb0 + bb1);
+      cos_finish(P, s, pr >> 16, pr & 0xffff, ab0 + ab1, aa0 + aa1, bb0 + bb1);
     }
   }
 }
 
 // any F: thread per pair, element by element (same arithmetic as above)
 template <typename FT>
-__global__ __launch_bounds__(WG) void cosine_kernel_any(Dev P, int seq0) {
-  const int s = seq0 + blockIdx.x, T = P.T, D = P.D, F = P.F;
+__global__ __launch_bounds__(WG) void cosine_kernel_any(Dev P, int seq0,
+                                                        const int* __restrict__ det_off,
+                                                        const FT* __restrict__ embs) {
+  const int b = blockIdx.x, s = seq0 + b, T = P.T, D = P.D, F = P.F;
   const int np = P.npair[s];
   const uint32_t* pairs = P.pairs + (size_t)s * T * D;
   for (int p = blockIdx.y * WG + threadIdx.x; p < np; p += COS_BLOCKS * WG) {
     const uint32_t pr = pairs[p];
     const int slot = pr >> 16, dk = pr & 0xffff;
     const FT* a = (const FT*)P.feat + ((size_t)s * T + slot) * F;
-    const float* bq = P.dB + ((size_t)s * D + dk) * F;
+    const FT* f = embs + (size_t)(det_off[b] + dk) * F;
     const float dn = P.tdn[(size_t)s * T + slot];
+    const double* nr = P.dnrm + ((size_t)s * D + dk) * 4;
+    const FT n1 = (FT)nr[0], n2 = (FT)nr[1];
+    const float bdn = (float)nr[2];
+    auto A = [&](int q) { return (double)((float)a[q] / dn); };
+    auto B = [&](int q) { return (double)((float)((f[q] / n1) / n2) / bdn); };
     double ab0 = 0.0, ab1 = 0.0, aa0 = 0.0, aa1 = 0.0, bb0 = 0.0, bb1 = 0.0;
     int q = 0;
     for (; q + 2 <= F; q += 2) {
-      const double x0 = (double)((float)a[q] / dn), x1 = (double)((float)a[q + 1] / dn);
-      const double y0 = (double)bq[q], y1 = (double)bq[q + 1];
+      const double x0 = A(q), x1 = A(q + 1), y0 = B(q), y1 = B(q + 1);
       ab0 += x0 * y0; ab1 += x1 * y1;
       aa0 += x0 * x0; aa1 += x1 * x1;
       bb0 += y0 * y0; bb1 += y1 * y1;
     }
     double ab = ab0 + ab1, aa = aa0 + aa1, bb = bb0 + bb1;
     if (q < F) {
-      const double x0 = (double)((float)a[q] / dn), y0 = (double)bq[q];
+      const double x0 = A(q), y0 = B(q);
       ab += x0 * y0; aa += x0 * x0; bb += y0 * y0;
     }
-    cos_finish<FT>(P, s, slot, dk, ab, aa, bb);
+    cos_finish(P, s, slot, dk, ab, aa, bb);
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// K2: STrack.multi_predict over strack_pool = joint(tracked, lost) (bytetrack.py:205-207,
-// botsort.py:188-189).  With dt = 1, F·P·Fᵀ splits into 16 independent 2x2 "quads"
-// {(i,j), (i,j+4), (i+4,j), (i+4,j+4)}, i, j < 4: one thread per quad, 16 threads per slot, so a
-// wave reads/writes 4 slots' contiguous 576-byte states (each output is the same expression
-// kf_predict_soa evaluates).  Grid (n_seq, ceil(T/16)).
-template <int KIND>
-__global__ __launch_bounds__(WG) void predict_kernel(Dev P, int seq0) {
-  const int b = blockIdx.x, s = seq0 + b, T = P.T;
-  const int slot = blockIdx.y * (WG / 16) + (threadIdx.x >> 4), qd = threadIdx.x & 15;
-  if (slot >= T) return;
-  const uint32_t f = P.flags[(size_t)s * T + slot];
-  const bool pool = ((f & F_INACT) && (f & F_ACT)) || (f & F_INLOST);
-  if (!pool) return;
-  double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
-  double* c = m + 8;
-  const int i = qd >> 2, j = qd & 3;
-  double mv[4] = {m[0], m[1], m[2], m[3]}, q[8];
-  kf_process_noise(KIND, mv, q);  // reads mean[2], mean[3] only
+// Kalman predict split in two (kf_predict_soa restated): the association only needs predicted
+// MEANS (boxes), so K2 predicts the mean now and the covariance predict is deferred to the pass
+// that updates the track anyway (K4) — one read/write of the 512-byte covariance per frame.
+// F·P·Fᵀ with dt = 1 splits into 16 independent 2x2 "quads" {(i,j),(i,j+4),(i+4,j),(i+4,j+4)};
+// quad (i, j) is exactly the expressions kf_predict_soa evaluates for those four entries.
+__device__ __forceinline__ void kf_predict_quad(int kind, const double* qm, double* c, int i,
+                                                int j) {
+  double mv[4] = {0.0, 0.0, qm[0], qm[1]}, q[8];
+  kf_process_noise(kind, mv, q);  // reads mean[2], mean[3] only (pre-predict values)
   const double p00 = c[8 * i + j], p10 = c[8 * (i + 4) + j], p01 = c[8 * i + j + 4],
                p11 = c[8 * (i + 4) + j + 4];
   double v = (p00 + p10) + (p01 + p11);
   double v11 = p11;
   if (i == j) { v = v + q[i]; v11 = v11 + q[i + 4]; }
-  __builtin_amdgcn_wave_barrier();  // every lane of the slot has read mean[0..3] (same wave)
   c[8 * i + j] = v;
   c[8 * i + j + 4] = p01 + p11;
   c[8 * (i + 4) + j] = p10 + p11;
   c[8 * (i + 4) + j + 4] = v11;
-  if (qd == 0) {
-    double mm[8];
-    for (int k = 0; k < 8; k++) mm[k] = m[k];
-    if (st_of(f) != ST_TRACKED) {
-      if (KIND == KIND_BOT) mm[6] = 0.0;
-      mm[7] = 0.0;
-      m[6] = mm[6];
-      m[7] = mm[7];
-    }
-    for (int k = 0; k < 4; k++) m[k] = mm[k] + mm[k + 4];
-  }
 }
-
-// K2b: BoT-SORT multi_gmc (botsort.py:192-195; cmc warp applied to pool + unconfirmed):
-// R8 = kron(I4, R): mean = R8·mean + t, cov = R8·cov·R8ᵀ.  Thread per slot (only with a warp).
-__global__ __launch_bounds__(WG) void gmc_kernel(Dev P, int seq0, const double* __restrict__ warps) {
-  const int b = blockIdx.x, s = seq0 + b, T = P.T;
-  const int slot = blockIdx.y * WG + threadIdx.x;
-  if (slot >= T) return;
-  const uint32_t f = P.flags[(size_t)s * T + slot];
-  if (!(f & (F_INACT | F_INLOST))) return;  // pool ∪ unconfirmed = every listed track
-  const double* H = warps + 6 * (size_t)b;
-  double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
-  double* c = m + 8;
-  double mm[8];
-  for (int q = 0; q < 8; q++) mm[q] = m[q];
-  for (int q = 0; q < 4; q++) {
-    double a0 = H[0] * mm[2 * q] + H[1] * mm[2 * q + 1];
-    double a1 = H[3] * mm[2 * q] + H[4] * mm[2 * q + 1];
-    mm[2 * q] = a0;
-    mm[2 * q + 1] = a1;
-  }
-  mm[0] += H[2];
-  mm[1] += H[5];
-  for (int q = 0; q < 8; q++) m[q] = mm[q];
+__device__ __forceinline__ void kf_predict_cov(int kind, const double* qm, double* c) {
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) kf_predict_quad(kind, qm, c, i, j);
+}
+// multi_gmc covariance part: cov = R8·cov·R8ᵀ, R8 = kron(I4, R) (botsort.py:192-195)
+__device__ inline void gmc_cov(const double* H, double* c) {
   double RP[64];
   for (int bq = 0; bq < 4; bq++)
     for (int cc = 0; cc < 8; cc++) {
@@ -609,6 +593,78 @@ __global__ __launch_bounds__(WG) void gmc_kernel(Dev P, int seq0, const double* 
       c[8 * r + 2 * bq] = y0 * H[0] + y1 * H[1];
       c[8 * r + 2 * bq + 1] = y0 * H[3] + y1 * H[4];
     }
+}
+
+// K2: STrack.multi_predict MEAN part over strack_pool = joint(tracked, lost) (bytetrack.py:
+// 205-207, botsort.py:188-189) and, for BoT-SORT with a CMC warp, multi_gmc's mean part over the
+// pool and the unconfirmed tracks (botsort.py:192-195).  Sets F_PRED / F_GMC for K4.
+// Grid (n_seq, ceil(T/256)); thread per slot.
+template <int KIND, bool GMC>
+__global__ __launch_bounds__(WG) void predict_kernel(Dev P, int seq0,
+                                                     const double* __restrict__ warps) {
+  const int b = blockIdx.x, s = seq0 + b, T = P.T;
+  const int slot = blockIdx.y * WG + threadIdx.x;
+  if (slot >= T) return;
+  uint32_t* fp = P.flags + (size_t)s * T + slot;
+  const uint32_t f = *fp;
+  const bool pool = ((f & F_INACT) && (f & F_ACT)) || (f & F_INLOST);
+  const bool unconf = (f & F_INACT) && !(f & F_ACT);
+  if (!pool && !(GMC && unconf)) return;
+  double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
+  double2* m2 = (double2*)m;
+  double mm[8];
+  for (int q = 0; q < 4; q++) { const double2 t = m2[q]; mm[2 * q] = t.x; mm[2 * q + 1] = t.y; }
+  uint32_t nf = f;
+  if (pool) {
+    if (st_of(f) != ST_TRACKED) {
+      if (KIND == KIND_BOT) mm[6] = 0.0;
+      mm[7] = 0.0;
+    }
+    m2[KF_QM / 2] = make_double2(mm[2], mm[3]);
+    for (int k = 0; k < 4; k++) mm[k] = mm[k] + mm[k + 4];
+    nf |= F_PRED;
+  }
+  if (GMC) {  // mean = R8·mean + t
+    const double* H = warps + 6 * (size_t)b;
+    for (int q = 0; q < 4; q++) {
+      double a0 = H[0] * mm[2 * q] + H[1] * mm[2 * q + 1];
+      double a1 = H[3] * mm[2 * q] + H[4] * mm[2 * q + 1];
+      mm[2 * q] = a0;
+      mm[2 * q + 1] = a1;
+    }
+    mm[0] += H[2];
+    mm[1] += H[5];
+    nf |= F_GMC;
+  }
+  for (int q = 0; q < 4; q++) m2[q] = make_double2(mm[2 * q], mm[2 * q + 1]);
+  *fp = nf;
+}
+
+// K4b: the deferred covariance predict (+ CMC warp) of pool tracks that got no update record
+// (matched tracks have theirs done inside K4).  Without a warp: one thread per quad, 16 threads
+// per slot, so a wave touches 4 slots' contiguous state.  Grid (n_seq, ceil(T/16)).
+template <int KIND>
+__global__ __launch_bounds__(WG) void cov_predict_kernel(Dev P, int seq0) {
+  const int s = seq0 + blockIdx.x, T = P.T;
+  const int slot = blockIdx.y * (WG / 16) + (threadIdx.x >> 4), qd = threadIdx.x & 15;
+  if (slot >= T) return;
+  const uint32_t f = P.flags[(size_t)s * T + slot];
+  if ((f & (F_PRED | F_REC)) != F_PRED) return;
+  double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
+  kf_predict_quad(KIND, m + KF_QM, m + 8, qd >> 2, qd & 3);
+}
+// with a CMC warp: thread per slot, predict then warp (and warp-only for unconfirmed tracks)
+template <int KIND>
+__global__ __launch_bounds__(WG) void cov_predict_gmc_kernel(Dev P, int seq0,
+                                                             const double* __restrict__ warps) {
+  const int b = blockIdx.x, s = seq0 + b, T = P.T;
+  const int slot = blockIdx.y * WG + threadIdx.x;
+  if (slot >= T) return;
+  const uint32_t f = P.flags[(size_t)s * T + slot];
+  if ((f & F_REC) || !(f & (F_PRED | F_GMC))) return;
+  double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
+  if (f & F_PRED) kf_predict_cov(KIND, m + KF_QM, m + 8);
+  if (f & F_GMC) gmc_cov(warps + 6 * (size_t)b, m + 8);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -769,12 +825,17 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
       cand = c < L || gated;
       return c;
     };
-    // Candidates: one wave per row, lanes over columns, a conservative fp32 intersection test on
-    // outward-rounded boxes (never misses an fp64-intersecting pair); a row's candidates keep
-    // column order (ballot prefix).  Exact fp64 costs are then computed once per candidate with
+    // Candidates: a conservative fp32 intersection test on outward-rounded boxes (never misses
+    // an fp64-intersecting pair); exact fp64 costs are then computed once per candidate with
     // every lane busy; candidates that turn out inadmissible stay in the CSR with cost INF,
-    // which the solver treats as absent.  Lanes own columns: a lane keeps the boxes of its
-    // columns j = lane + 64k (k < 4, i.e. C <= 256) in registers for the whole row sweep.
+    // which the solver treats as absent.  One thread per row walks the columns in order
+    // (column boxes broadcast from LDS), so a row's candidates come out in column order.
+    float4* s_cbox = (float4*)(smem + Lo.o_cbox);
+    int* s_bin = (int*)(smem + Lo.o_bin);  // [NBIN + 1] starts, then [NBIN] cursors
+    uint16_t* s_bcol = (uint16_t*)(smem + Lo.o_bcol);
+    if (tid == 0) { I[I_XMIN] = INT_MAX; I[I_XMAX] = INT_MIN; I[I_W] = INT_MIN; }
+    if (tid < NBIN) s_bin[tid] = 0;
+    for (int j = tid; j < C; j += WG) s_cbox[j] = s_dboxf[cols[j]];
     for (int i = tid; i < R; i += WG) {
       double t[4];
       track_box<KIND>(g_kf, rows[i], t);
@@ -782,59 +843,117 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
                                __double2float_ru(t[2]), __double2float_ru(t[3]));
     }
     __syncthreads();
-    const int lane = lane_id();
-    constexpr int MAXCH = 4;
-    const int nch = (C + WAVE - 1) / WAVE;
-    const bool regcols = nch <= MAXCH;
-    const float4 empty = make_float4(INFINITY, INFINITY, -INFINITY, -INFINITY);
-    float4 cb[MAXCH];
-#pragma unroll
-    for (int k = 0; k < MAXCH; k++) {
-      const int j = lane + WAVE * k;
-      cb[k] = (regcols && j < C) ? s_dboxf[cols[j]] : empty;
-    }
-    auto hit = [&](const float4& tb, const float4& db, int j) -> bool {
-      if (!prefilter) return j < C;
+    if (stamp == 4) BX_STAMP(20);
+    auto hit = [&](const float4& tb, const float4& db) -> bool {
+      if (!prefilter) return true;
       return (fminf(tb.z, db.z) > fmaxf(tb.x, db.x)) & (fminf(tb.w, db.w) > fmaxf(tb.y, db.y));
     };
-    auto chunk_mask = [&](const float4& tb, int k) -> unsigned long long {  // runtime k
-      const int j = lane + WAVE * k;
-      return __ballot(j < C && hit(tb, j < C ? s_dboxf[cols[j]] : empty, j));
+    // Column x-binning: a candidate needs db.x1 < tb.x2 and db.x2 > tb.x1, so with wmax >= every
+    // column's width its x1 lies in (tb.x1 - wmax, tb.x2): a row scans only the bins covering that
+    // range (the bin map is monotone in x; bounds rounded outward).  Non-finite boxes or no
+    // prefilter: every row scans every column.
+    auto okey = [](float f) {  // order-preserving float → int
+      const int i = __builtin_bit_cast(int, f);
+      return i >= 0 ? i : i ^ 0x7fffffff;
     };
-    // pass 1: count candidates per row
-    for (int i = wave_id(); i < R; i += NWAVE) {
-      const float4 tb = s_tboxf[i];
-      int cnt = 0;
-      if (regcols) {
-#pragma unroll
-        for (int k = 0; k < MAXCH; k++)
-          if (k < nch) cnt += __popcll(__ballot(hit(tb, cb[k], lane + WAVE * k)));
-      } else {
-        for (int k = 0; k < nch; k++) cnt += __popcll(chunk_mask(tb, k));
+    auto ofloat = [](int k) { return __builtin_bit_cast(float, k >= 0 ? k : k ^ 0x7fffffff); };
+    if (prefilter) {
+      int kmin = INT_MAX, kmax = INT_MIN, kw = INT_MIN;
+      for (int j = tid; j < C; j += WG) {
+        const float4 cb = s_cbox[j];
+        kmin = min(kmin, okey(cb.x));
+        kmax = max(kmax, okey(cb.x));
+        kw = max(kw, okey(nextafterf(__double2float_ru((double)cb.z - (double)cb.x), INFINITY)));
       }
-      if (lane == 0) s_rowptr[i] = cnt;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        kmin = min(kmin, __shfl_xor(kmin, d));
+        kmax = max(kmax, __shfl_xor(kmax, d));
+        kw = max(kw, __shfl_xor(kw, d));
+      }
+      if (lane_id() == 0) {
+        atomicMin(&I[I_XMIN], kmin);
+        atomicMax(&I[I_XMAX], kmax);
+        atomicMax(&I[I_W], kw);
+      }
+      __syncthreads();
+    }
+    const float xmin = ofloat(I[I_XMIN]), xmax = ofloat(I[I_XMAX]), wmax = ofloat(I[I_W]);
+    const bool binned = prefilter && C > 0 && isfinite(xmin) && isfinite(xmax) && isfinite(wmax) &&
+                        wmax >= 0.f;
+    const float inv = xmax > xmin ? (float)NBIN / (xmax - xmin) : 0.f;
+    auto bin = [&](float x) {
+      const float t = (x - xmin) * inv;
+      return !(t > 0.f) ? 0 : (t >= (float)NBIN ? NBIN - 1 : (int)t);
+    };
+    int* s_bcur = s_bin + NBIN + 1;
+    if (binned) {
+      for (int j = tid; j < C; j += WG) atomicAdd(&s_bin[bin(s_cbox[j].x)], 1);
+      __syncthreads();
+      if (wave_id() == 0) {  // NBIN == WAVE: one exclusive scan step
+        const int lane = lane_id(), v = s_bin[lane];
+        int x = v;
+#pragma unroll
+        for (int d = 1; d < WAVE; d <<= 1) {
+          const int y = __shfl_up(x, d);
+          if (lane >= d) x += y;
+        }
+        s_bin[lane] = x - v;
+        s_bcur[lane] = x - v;
+        if (lane == WAVE - 1) s_bin[NBIN] = x;
+      }
+      __syncthreads();
+      for (int j = tid; j < C; j += WG) s_bcol[atomicAdd(&s_bcur[bin(s_cbox[j].x)], 1)] = j;
+      __syncthreads();
+    }
+    // visit the candidate columns of row box tb (binned: bin order, else column order)
+    auto scan_row = [&](const float4& tb, auto&& on_hit) {
+      if (binned) {
+        const float lo =
+            nextafterf(__double2float_rd((double)tb.x - (double)wmax), -INFINITY);
+        const int b0 = bin(lo), b1 = bin(tb.z);
+        for (int k = s_bin[b0]; k < s_bin[b1 + 1]; k++) {
+          const int j = s_bcol[k];
+          if (hit(tb, s_cbox[j])) on_hit(j);
+        }
+      } else {
+        for (int j = 0; j < C; j++)
+          if (hit(tb, s_cbox[j])) on_hit(j);
+      }
+    };
+    // pass 1: count candidates per row (one thread per row)
+    for (int i = tid; i < R; i += WG) {
+      int cnt = 0;
+      scan_row(s_tboxf[i], [&](int) { cnt++; });
+      s_rowptr[i] = cnt;
     }
     __syncthreads();
+    if (stamp == 4) BX_STAMP(21);
     wave0_exclusive_scan(s_rowptr, R);
     __syncthreads();
-    // pass 2: write candidate columns in column order; the row index is parked in the cost slot
-    for (int i = wave_id(); i < R; i += NWAVE) {
-      const float4 tb = s_tboxf[i];
-      int e = s_rowptr[i];
-      auto emit = [&](unsigned long long m, int k) {
-        if ((m >> lane) & 1ull)
-          put_edge(e + __popcll(m & ((1ull << lane) - 1ull)), lane + WAVE * k, (double)i);
-        e += __popcll(m);
-      };
-      if (regcols) {
-#pragma unroll
-        for (int k = 0; k < MAXCH; k++)
-          if (k < nch) emit(__ballot(hit(tb, cb[k], lane + WAVE * k)), k);
-      } else {
-        for (int k = 0; k < nch; k++) emit(chunk_mask(tb, k), k);
-      }
+    if (stamp == 4) BX_STAMP(22);
+    // pass 2: write each row's candidate columns, sorted ascending (the solver's tie-breaking
+    // follows edge order); the row index is parked in the cost slot
+    for (int i = tid; i < R; i += WG) {
+      const int e0 = s_rowptr[i];
+      int e = e0;
+      scan_row(s_tboxf[i], [&](int j) { put_edge(e++, j, (double)i); });
+      if (binned)
+        for (int a = e0 + 1; a < e; a++) {  // insertion sort (a row has few candidates)
+          int ca, cb;
+          double d;
+          get_edge(a, ca, d);
+          int q = a - 1;
+          for (; q >= e0; q--) {
+            get_edge(q, cb, d);
+            if (cb < ca) break;
+            put_edge(q + 1, cb, d);
+          }
+          put_edge(q + 1, ca, d);
+        }
     }
     __syncthreads();
+    if (stamp == 4) BX_STAMP(23);
     // pass 3: exact fp64 cost per candidate; a gated pair (botsort.py:209-214) takes
     // min(iou cost, embedding distance) with the distance K1c precomputed for it
     const int E = s_rowptr[R];
@@ -857,6 +976,9 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
     }
     __syncthreads();
     BX_STAMP(stamp);
+#ifdef BX_PHASE_TIMING
+    W.dbg = (stamp == 4 && P.dbg) ? P.dbg + (size_t)s * 32 + 26 : nullptr;
+#endif
     if (wave_id() == 0) lap_solve_wave(R, C, L, W);
     __syncthreads();
   };
@@ -873,7 +995,7 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
           const int slot = rows[i], dk = cols[s_c4r[i]];
           const uint32_t fl = s_flags[slot];
           const bool tracked = st_of(fl) == ST_TRACKED;
-          s_flags[slot] = (fl & ~F_STATE) | ST_TRACKED | F_ACT;
+          s_flags[slot] = (fl & ~F_STATE) | ST_TRACKED | F_ACT | F_REC;
           s_fid[slot] = fc;
           if (refind && !tracked) s_mark[slot] |= M_TMP;
           const int kind = (tracked ? R_UPDATE : R_REACT) | (feat ? R_FEAT : 0);
@@ -1020,42 +1142,131 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
 
 // ------------------------------------------------------------------------------------------
 // K4: per update record, STrack.update / re_activate / activate numerics: Kalman update
-// (kalman_filter.py update) or initiate, tracklet_len, score, cls (+ BoT-SORT update_cls,
-// botsort_track.py:51-64), det_ind.  Grid (n_seq, ceil(D/256)); thread per record.
+// (base_kalman_filter.py:129-155, after K2's deferred covariance predict + CMC warp) or
+// initiate, tracklet_len, score, cls (+ BoT-SORT update_cls, botsort_track.py:51-64), det_ind.
+// Eight lanes per record: lane r owns covariance row r (and mean[r]); the 4x4 innovation
+// covariance and the Kalman gain rows are exchanged with in-group shuffles, every entry being
+// the same expression kf_predict_soa / kf_update_soa evaluate.  Grid (n_seq, ceil(D/32)).
+constexpr int UPD_PER_BLOCK = WG / 8;
 template <int KIND>
 __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float* __restrict__ dets,
-                                                    const int* __restrict__ det_off) {
+                                                    const int* __restrict__ det_off,
+                                                    const double* __restrict__ warps) {
   const int b = blockIdx.x, s = seq0 + b, T = P.T;
-  const int r = blockIdx.y * WG + threadIdx.x;
+  const int ri = blockIdx.y * UPD_PER_BLOCK + (threadIdx.x >> 3), r = threadIdx.x & 7;
   const int* seq = P.seq + (size_t)s * SQ_STRIDE;
-  if (r >= seq[SQ_NREC]) return;
-  const int2 rc = P.rec[(size_t)s * P.D + r];
+  if (ri >= seq[SQ_NREC]) return;  // whole 8-lane groups leave together
+  const int2 rc = P.rec[(size_t)s * P.D + ri];
   const int slot = rc.x & 0xffff, kind = (rc.x >> 16) & 3, dk = rc.y;
   const size_t sT = (size_t)s * T;
   const float* row = dets + (size_t)(det_off[b] + dk) * 6;
   double meas[4];
   det_measurement<KIND>(row, meas);
   double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
-  double* c = m + 8;
+  double2* crow = (double2*)(m + 8 + 8 * r);  // this lane's covariance row
   const double conf = (double)row[4], cls = (double)row[5];
-  P.conf[sT + slot] = conf;
-  P.detind[sT + slot] = dk;
   double* h = P.clsh + (sT + slot) * CLS_HIST * 2;
-  if (kind == R_NEW) {
+  auto shfl = [&](double v, int src) { return __shfl(v, src, 8); };
+  if (kind == R_NEW) {  // kf_initiate: mean = [z, 0], cov = diag(std^2)
     double m8[8], c64[64];
     kf_initiate(KIND, meas, m8, c64);
-    for (int q = 0; q < 8; q++) m[q] = m8[q];
-    for (int q = 0; q < 64; q++) c[q] = c64[q];
-    P.tlen[sT + slot] = 0;
-    P.cls[sT + slot] = cls;
-    if (KIND == KIND_BOT) {
-      h[0] = cls;
-      h[1] = conf;
-      P.ncls[sT + slot] = 1;
+    m[r] = m8[r];
+    for (int q = 0; q < 4; q++) crow[q] = make_double2(c64[8 * r + 2 * q], c64[8 * r + 2 * q + 1]);
+    if (r == 0) {
+      P.conf[sT + slot] = conf;
+      P.detind[sT + slot] = dk;
+      P.tlen[sT + slot] = 0;
+      P.cls[sT + slot] = cls;
+      if (KIND == KIND_BOT) {
+        h[0] = cls;
+        h[1] = conf;
+        P.ncls[sT + slot] = 1;
+      }
     }
     return;
   }
-  kf_update_soa(KIND, m, c, 1, meas, 0.0);
+  const uint32_t fl = P.flags[sT + slot];
+  double cr[8];
+  for (int q = 0; q < 4; q++) { const double2 t = crow[q]; cr[2 * q] = t.x; cr[2 * q + 1] = t.y; }
+  if (fl & F_PRED) {  // K2's deferred half: rows i < 4 need row i + 4
+    double o[8];
+    for (int j = 0; j < 8; j++) o[j] = shfl(cr[j], (r + 4) & 7);
+    double mv[4] = {0.0, 0.0, m[KF_QM], m[KF_QM + 1]}, q[8];
+    kf_process_noise(KIND, mv, q);
+    double nr[8];
+    if (r < 4) {
+      for (int j = 0; j < 4; j++) {
+        double v = (cr[j] + o[j]) + (cr[j + 4] + o[j + 4]);
+        nr[j] = (j == r) ? v + q[r] : v;
+        nr[j + 4] = cr[j + 4] + o[j + 4];
+      }
+    } else {
+      for (int j = 0; j < 4; j++) {
+        nr[j] = cr[j] + cr[j + 4];
+        nr[j + 4] = (j + 4 == r) ? cr[j + 4] + q[r] : cr[j + 4];
+      }
+    }
+    for (int j = 0; j < 8; j++) cr[j] = nr[j];
+  }
+  if (fl & F_GMC) {  // cov = R8·cov·R8ᵀ: row pairs (2b, 2b+1) mix, then column pairs
+    const double* H = warps + 6 * (size_t)b;
+    double o[8], rp[8];
+    for (int j = 0; j < 8; j++) o[j] = shfl(cr[j], r ^ 1);
+    for (int j = 0; j < 8; j++)
+      rp[j] = (r & 1) ? H[3] * o[j] + H[4] * cr[j] : H[0] * cr[j] + H[1] * o[j];
+    for (int bq = 0; bq < 4; bq++) {
+      const double y0 = rp[2 * bq], y1 = rp[2 * bq + 1];
+      cr[2 * bq] = y0 * H[0] + y1 * H[1];
+      cr[2 * bq + 1] = y0 * H[3] + y1 * H[4];
+    }
+  }
+  // kf_update_soa, distributed
+  double mm[8];
+  for (int q = 0; q < 8; q++) mm[q] = m[q];
+  double rr[4], S[16], L[16];
+  kf_meas_noise(KIND, mm, 0.0, rr);
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) {
+      const double v = shfl(cr[j], i);
+      S[4 * i + j] = v + (i == j ? rr[i] : 0.0);
+    }
+  const bool ok = chol4(S, L);
+  if (ok) {
+    double Kr[4], y[4];  // gain row r: solves on covariance row r's first four entries
+    for (int i = 0; i < 4; i++) {
+      double sv = cr[i];
+      for (int k = 0; k < i; k++) sv -= L[4 * i + k] * y[k];
+      y[i] = sv / L[4 * i + i];
+    }
+    for (int i = 3; i >= 0; i--) {
+      double sv = y[i];
+      for (int k = i + 1; k < 4; k++) sv -= L[4 * k + i] * Kr[k];
+      Kr[i] = sv / L[4 * i + i];
+    }
+    double innov[4];
+    for (int k = 0; k < 4; k++) innov[k] = meas[k] - mm[k];
+    double sm = 0.0;
+    for (int k = 0; k < 4; k++) sm += innov[k] * Kr[k];
+    const double mnew = mm[r] + sm;
+    double ks[4];
+    for (int j = 0; j < 4; j++) {
+      double sv = 0.0;
+      for (int k = 0; k < 4; k++) sv += Kr[k] * S[4 * k + j];
+      ks[j] = sv;
+    }
+    for (int j = 0; j < 8; j++) {
+      double Kj[4];
+      for (int k = 0; k < 4; k++) Kj[k] = shfl(Kr[k], j);
+      double sv = 0.0;
+      for (int k = 0; k < 4; k++) sv += ks[k] * Kj[k];
+      cr[j] = cr[j] - sv;
+    }
+    m[r] = mnew;  // every lane has read mean[] above (same wave, in order)
+  }
+  for (int q = 0; q < 4; q++) crow[q] = make_double2(cr[2 * q], cr[2 * q + 1]);
+  if (r != 0) return;
+  P.conf[sT + slot] = conf;
+  P.detind[sT + slot] = dk;
   P.tlen[sT + slot] = kind == R_REACT ? 0 : P.tlen[sT + slot] + 1;
   double out_cls = cls;
   if (KIND == KIND_BOT) {  // update_cls
@@ -1078,56 +1289,98 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
 // ------------------------------------------------------------------------------------------
 // K5: BoT-SORT feature update per record carrying a detection feature (botsort_track.py:40-49):
 // a new track's smooth_feat = f2; otherwise feat = f2/|f2|; smooth = 0.9 smooth + 0.1 feat;
-// smooth /= |smooth|.  f2 is recomputed from the input row with K1's norms (bit-identical).
-// Grid (n_seq, FEAT_BLOCKS); one wave per record.
+// smooth /= |smooth|.  f2 is recomputed from the input row with K1's norms (bit-identical).  The
+// new smooth_feat's numpy float32 norm (embedding_distance's track-side scale) is refreshed here,
+// while the row is in registers, for the next frame's K1c.  Grid (n_seq, FEAT_BLOCKS); one wave
+// per record.
 constexpr int FEAT_BLOCKS = 8;
-template <typename FT>
+template <typename FT, bool NPF>
 __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
                                                      const int* __restrict__ det_off,
                                                      const FT* __restrict__ embs) {
-  const int b = blockIdx.x, s = seq0 + b, F = P.F, D = P.D, lane = lane_id();
+  __shared__ __align__(16) float s_w[NWAVE * REG_F];
+  const int b = blockIdx.x, s = seq0 + b, F = P.F, D = P.D, T = P.T, lane = lane_id();
   const int nrec = P.seq[(size_t)s * SQ_STRIDE + SQ_NREC];
   const FT a = (FT)0.9, bb = (FT)(1.0 - 0.9);
-  for (int r = blockIdx.y * NWAVE + wave_id(); r < nrec; r += FEAT_BLOCKS * NWAVE) {
-    const int2 rc = P.rec[(size_t)s * D + r];
-    const int slot = rc.x & 0xffff, kind = rc.x >> 16, dk = rc.y;
-    if (!(kind & R_FEAT)) continue;  // wave-uniform
-    FT* sm = (FT*)P.feat + ((size_t)s * P.T + slot) * F;
-    if (F <= REG_F) {
-      const FT n1 = (FT)P.dnrm[((size_t)s * D + dk) * 2];
-      const FT n2 = (FT)P.dnrm[((size_t)s * D + dk) * 2 + 1];
-      RegRow<FT> g;
-      g.load(embs + (size_t)(det_off[b] + dk) * F, F);
+  float* wb = s_w + wave_id() * REG_F;
+  const FT* fembs = embs + (size_t)det_off[b] * F;
+  FT* feat = (FT*)P.feat + (size_t)s * T * F;
+  constexpr int STEP = FEAT_BLOCKS * NWAVE;
+  auto next = [&](int r) {  // next record with a feature at or after r
+    for (; r < nrec; r += STEP)
+      if ((P.rec[(size_t)s * D + r].x >> 16) & R_FEAT) return r;
+    return nrec;
+  };
+  if (F <= REG_F) {
+    int r = next(blockIdx.y * NWAVE + wave_id());
+    RegRow<FT> g, m;
+    int2 rc = make_int2(0, 0);
+    if (r < nrec) {
+      rc = P.rec[(size_t)s * D + r];
+      g.load(fembs + (size_t)rc.y * F, F);
+      m.load(feat + (size_t)(rc.x & 0xffff) * F, F);
+    }
+    while (r < nrec) {  // rows of the next record load while this one is computed
+      const int rn = next(r + STEP);
+      RegRow<FT> ng, nm;
+      int2 nrc = make_int2(0, 0);
+      if (rn < nrec) {
+        nrc = P.rec[(size_t)s * D + rn];
+        ng.load(fembs + (size_t)nrc.y * F, F);
+        nm.load(feat + (size_t)(nrc.x & 0xffff) * F, F);
+      }
+      const int slot = rc.x & 0xffff, kind = rc.x >> 16, dk = rc.y;
+      const FT n1 = (FT)P.dnrm[((size_t)s * D + dk) * 4];
+      const FT n2 = (FT)P.dnrm[((size_t)s * D + dk) * 4 + 1];
+      FT* sm = feat + (size_t)slot * F;
       g.div(n1);
       g.div(n2);
+      float dn;  // the new smooth_feat's numpy float32 norm, for the next frame's K1c
       if ((kind & 3) == R_NEW) {
         g.store(sm, F);
-        continue;
-      }
-      RegRow<FT> m;
-      m.load(sm, F);
-      const FT n3 = g.norm(F);
+        dn = g.template np_dn<NPF>(wb, F);
+      } else {
+        const FT n3 = g.norm(F);
 #pragma unroll
-      for (int q = 0; q < REG_EPL; q++) {
-        FT g3 = g.v[q] / n3;
-        m.v[q] = a * m.v[q] + bb * g3;
+        for (int q = 0; q < REG_EPL; q++) {
+          FT g3 = g.v[q] / n3;
+          m.v[q] = a * m.v[q] + bb * g3;
+        }
+        m.div(m.norm(F));
+        m.store(sm, F);
+        dn = m.template np_dn<NPF>(wb, F);
       }
-      m.div(m.norm(F));
-      m.store(sm, F);
-      continue;
+      if (lane == 0) P.tdn[(size_t)s * T + slot] = dn;
+      r = rn;
+      rc = nrc;
+      g = ng;
+      m = nm;
     }
-    const FT* f2 = (const FT*)P.fscr + ((size_t)s * D + dk) * F;
+    return;
+  }
+  for (int r = next(blockIdx.y * NWAVE + wave_id()); r < nrec; r = next(r + STEP)) {
+    const int2 rc = P.rec[(size_t)s * D + r];
+    const int slot = rc.x & 0xffff, kind = rc.x >> 16, dk = rc.y;
+    FT* sm = feat + (size_t)slot * F;
+    const FT* f = fembs + (size_t)dk * F;
+    const FT n1 = (FT)P.dnrm[((size_t)s * D + dk) * 4];
+    const FT n2 = (FT)P.dnrm[((size_t)s * D + dk) * 4 + 1];
+    FT* f2 = (FT*)P.fscr + ((size_t)s * D + dk) * F;  // this wave's scratch row
+    for (int q = lane; q < F; q += WAVE) f2[q] = (f[q] / n1) / n2;
     if ((kind & 3) == R_NEW) {
       for (int q = lane; q < F; q += WAVE) sm[q] = f2[q];
-      continue;
+    } else {
+      const FT n3 = wave_norm((const FT*)f2, F);  // same lane mapping: reads own writes
+      for (int q = lane; q < F; q += WAVE) {
+        FT g3 = f2[q] / n3;
+        sm[q] = a * sm[q] + bb * g3;
+      }
+      const FT ns = wave_norm((const FT*)sm, F);
+      for (int q = lane; q < F; q += WAVE) sm[q] = sm[q] / ns;
     }
-    const FT n3 = wave_norm(f2, F);
-    for (int q = lane; q < F; q += WAVE) {
-      FT g3 = f2[q] / n3;
-      sm[q] = a * sm[q] + bb * g3;
-    }
-    const FT ns = wave_norm((const FT*)sm, F);  // same lane mapping: reads own writes
-    for (int q = lane; q < F; q += WAVE) sm[q] = sm[q] / ns;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // other lanes read sm next
+    const float dn = sqrtf(np_sumsq_sel<NPF>((const FT*)sm, F)) + 1e-8f;
+    if (lane == 0) P.tdn[(size_t)s * T + slot] = dn;
   }
 }
 
@@ -1222,7 +1475,8 @@ __global__ __launch_bounds__(WG) void finish_kernel(Dev P, int seq0, const int* 
   for (int k = tid; k < T; k += WG) {
     const uint32_t f = g_flags[k];
     const uint8_t kp = s_keep[k];
-    const uint32_t nf = kp ? ((f & ~(F_INACT | F_INLOST)) | (kp == 1 ? F_INACT : F_INLOST)) : 0u;
+    const uint32_t nf =
+        kp ? ((f & ~(F_INACT | F_INLOST | F_TRANSIENT)) | (kp == 1 ? F_INACT : F_INLOST)) : 0u;
     if (nf != f) g_flags[k] = nf;
   }
   if (tid == 0) {
@@ -1292,38 +1546,49 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
                  hipStream_t st) {
   const Dev& d = e->dev;
   const bool reid = KIND == KIND_BOT && d.with_reid;
-  const int gy_det64 = (d.D + 63) / 64, gy_det4 = (d.D + NWAVE - 1) / NWAVE, gy_slot = (d.T + WG - 1) / WG,
-            gy_det = (d.D + WG - 1) / WG;
+  const int gy_det64 = (d.D + 63) / 64, gy_slot = (d.T + WG - 1) / WG;
   if (reid) {
     hipLaunchKernelGGL((det_feature_kernel<FT, NPF>), dim3(nseq, gy_det64), dim3(WG), 0, st, d,
                        seq0, dets, det_off, (const FT*)embs);
     HIPCHK(hipGetLastError());
   }
-  hipLaunchKernelGGL(predict_kernel<KIND>, dim3(nseq, (d.T + 15) / 16), dim3(WG), 0, st, d, seq0);
-  HIPCHK(hipGetLastError());
-  if (KIND == KIND_BOT && warps)
-    hipLaunchKernelGGL(gmc_kernel, dim3(nseq, gy_slot), dim3(WG), 0, st, d, seq0, warps);
+  const bool gmc = KIND == KIND_BOT && warps;
+  if (gmc)
+    hipLaunchKernelGGL((predict_kernel<KIND, true>), dim3(nseq, gy_slot), dim3(WG), 0, st, d,
+                       seq0, warps);
+  else
+    hipLaunchKernelGGL((predict_kernel<KIND, false>), dim3(nseq, gy_slot), dim3(WG), 0, st, d,
+                       seq0, warps);
   HIPCHK(hipGetLastError());
   if (reid) {
-    hipLaunchKernelGGL((gate_kernel<KIND, FT, NPF>), dim3(nseq, GATE_BLOCKS), dim3(WG),
-                       sizeof(double) * 4 * d.D, st, d, seq0, dets, det_off);
+    hipLaunchKernelGGL(gate_kernel<KIND>, dim3(nseq, GATE_BLOCKS), dim3(WG),
+                       (sizeof(double) * 4 + sizeof(float4)) * d.D, st, d, seq0, dets, det_off);
     HIPCHK(hipGetLastError());
     if (d.F % COS_CH == 0)
-      hipLaunchKernelGGL(cosine_kernel<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st, d, seq0);
+      hipLaunchKernelGGL(cosine_kernel<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st, d, seq0,
+                         det_off, (const FT*)embs);
     else
-      hipLaunchKernelGGL(cosine_kernel_any<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st, d, seq0);
+      hipLaunchKernelGGL(cosine_kernel_any<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st, d, seq0,
+                         det_off, (const FT*)embs);
     HIPCHK(hipGetLastError());
   }
   auto assoc = assoc_kernel<KIND>;
   if (int rc = lds_attr((const void*)assoc, e->lds_assoc)) return rc;
   hipLaunchKernelGGL(assoc, dim3(nseq), dim3(WG), e->lds_assoc, st, d, seq0, dets, det_off);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(update_kernel<KIND>, dim3(nseq, gy_det), dim3(WG), 0, st, d, seq0, dets,
-                     det_off);
+  hipLaunchKernelGGL(update_kernel<KIND>, dim3(nseq, (d.D + UPD_PER_BLOCK - 1) / UPD_PER_BLOCK),
+                     dim3(WG), 0, st, d, seq0, dets, det_off, warps);
+  HIPCHK(hipGetLastError());
+  if (gmc)
+    hipLaunchKernelGGL(cov_predict_gmc_kernel<KIND>, dim3(nseq, gy_slot), dim3(WG), 0, st, d,
+                       seq0, warps);
+  else
+    hipLaunchKernelGGL(cov_predict_kernel<KIND>, dim3(nseq, (d.T + 15) / 16), dim3(WG), 0, st, d,
+                       seq0);
   HIPCHK(hipGetLastError());
   if (reid) {
-    hipLaunchKernelGGL(feature_kernel<FT>, dim3(nseq, FEAT_BLOCKS), dim3(WG), 0, st, d, seq0,
-                       det_off, (const FT*)embs);
+    hipLaunchKernelGGL((feature_kernel<FT, NPF>), dim3(nseq, FEAT_BLOCKS), dim3(WG), 0, st, d,
+                       seq0, det_off, (const FT*)embs);
     HIPCHK(hipGetLastError());
   }
   if (int rc = lds_attr((const void*)finish_kernel<KIND>, e->lds_finish)) return rc;
@@ -1406,8 +1671,7 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
     d.gcol = carve<uint16_t>(p, ST * D);
     d.gcost = carve<double>(p, ST * D);
     d.rec = carve<int2>(p, SD);
-    d.dnrm = carve<double>(p, SD * 2);
-    d.dB = carve<float>(p, SD * FF);
+    d.dnrm = carve<double>(p, SD * 4);
     d.tdn = carve<float>(p, reid ? ST : 1);
     d.pairs = carve<uint32_t>(p, reid ? ST * D : 1);
     d.npair = carve<int>(p, S);

@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Diagnostic: per-phase cycle shares of the frame kernel from in-kernel s_memtime stamps.
+"""Diagnostic: per-phase cycle shares of the association kernel (K3) from s_memtime stamps.
 
 Builds boxmot_amd/lib/libbxassoc_timing.so with -DBX_PHASE_TIMING (a separate diagnostic build;
 the stamps' barriers forbid overlaps the real kernel has, so read SHARES, not totals), runs the
@@ -17,9 +17,9 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 LIB = ROOT / "boxmot_amd" / "lib" / "libbxassoc_timing.so"
-PHASES = ["dets+features", "lists", "predict+gmc", "assoc1 CSR", "assoc1 LAP", "assoc1 apply",
-          "assoc2 CSR", "assoc2 LAP+apply", "assoc3 CSR", "assoc3 LAP", "new tracks",
-          "lists+dedup", "outputs+writeback"]
+PHASES = ["dets split", "lists", "-", "assoc1 CSR+costs", "assoc1 LAP", "assoc1 records",
+          "assoc2 CSR", "assoc2 LAP+records", "assoc3 CSR", "assoc3 LAP", "assoc3 rec+new",
+          "expiry+lists+writeback"]
 
 
 def build():
@@ -62,10 +62,25 @@ def main():
     st = np.zeros((a.seqs, 32), np.uint64)
     L.bx_debug_stamps_host(eng._h, st.ctypes.data)
     st = st.astype(np.int64)
-    d = np.diff(st[:, :14], axis=1)
-    tot = st[:, 13] - st[:, 0]
+    d = np.diff(st[:, :13], axis=1)
+    tot = st[:, 12] - st[:, 0]
     print(f"{a.config}: {a.seqs} seqs, frame {a.frames}: total cycles mean {tot.mean():.0f} "
           f"max {tot.max():.0f}")
+    sub = [("row boxes", 3, 20), ("pass1 count", 20, 21), ("scan", 21, 22), ("pass2 emit", 22, 23),
+           ("pass3 costs", 23, 4)]
+    for name, a0, a1 in sub:
+        dd = st[:, a1] - st[:, a0]
+        if (st[:, a1] > 0).all():
+            print(f"    assoc1 {name:12s} mean {dd.mean():10.0f}  max {dd.max():10.0f}")
+    ne = st[:, 24]
+    if ne.any():
+        print(f"    assoc1 edges mean {ne.mean():.1f} max {ne.max()}  rows {st[:, 25].mean():.1f}")
+    if st[:, 28].any():
+        print(f"    assoc1 LAP: dijkstra roots mean {st[:, 26].mean():.1f} max {st[:, 26].max()}, "
+              f"steps mean {st[:, 27].mean():.1f} max {st[:, 27].max()}, rows {st[:, 28].mean():.1f}")
+        pre = st[:, 29] - st[:, 4]
+        print(f"    assoc1 LAP init+fast path mean {pre.mean():.0f}, dijkstra mean "
+              f"{(st[:, 5] - st[:, 29]).mean():.0f}")
     for k, name in enumerate(PHASES):
         print(f"  {name:18s} mean {d[:, k].mean():10.0f}  max {d[:, k].max():10.0f}  "
               f"share {d[:, k].mean() / tot.mean() * 100:5.1f}%")
