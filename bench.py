@@ -1,16 +1,22 @@
 #!/usr/bin/env python
 """Association-FPS benchmark (BASELINE.json metric) for the MI355X engine.
 
-A step = one frame of every sequence this rank holds, advanced by ONE launch of the fused frame
-kernel.  Workload (BASELINE.json configs[2], the north_star's 256-track x 128-det x 512-d
-target): BoT-SORT on synthetic grid scenes of 256 objects detected w.p. 0.5 (≈128 dets/frame,
-all above track_high_thresh) with 512-d float32 embeddings; `--config bytetrack` runs configs[1]
-(ByteTrack, IoU only).  Each rank holds `--seqs` independent sequences (weak scaling: the
-sequence count per GPU is fixed as N grows; no per-frame collective).  Inputs for every timed
-frame are generated on the GPU and resident in HBM before the timed region.
+A step = one frame of every sequence this rank holds, advanced by one `Engine.step` (the frame
+pipeline of kernels).  Workload (BASELINE.json configs[2], the north_star's
+256-track x 128-det x 512-d target): BoT-SORT on synthetic grid scenes of 256 objects detected
+w.p. 0.5 (~128 dets/frame, all above track_high_thresh) with 512-d float32 embeddings;
+`--config bytetrack` runs configs[1] (ByteTrack, IoU only).  Each rank holds `--seqs` independent
+sequences (weak scaling: the sequence count per GPU is fixed as N grows; no per-frame
+collective).  Inputs for every timed frame are generated on the GPU and resident in HBM before
+the timed region.
+
+Roofline: the last `len(STAGES)` warm-up steps time each pipeline stage once (HIP events around
+that stage's launch, `Engine.probe`); the slowest stage is the dominant kernel and is probed on
+every timed step.  Its algorithmic bytes per launch (DESIGN.md §4 per-stage model, priced with
+the engine's own per-frame unit counts) over its measured average launch time is `achieved`.
 
 Single process: `python bench.py`.  Multi-GPU: `torch.distributed.run --nproc-per-node N
-bench.py --gpus N` (RCCL is used only to gather per-rank frame counts/time: max over ranks).
+bench.py --gpus N` (RCCL only gathers the per-sequence records once, at the end).
 """
 from __future__ import annotations
 
@@ -39,14 +45,33 @@ CONFIGS = {
                                             track_buffer=30)),
 }
 
+KF_STATE = 576  # fp64 mean[8] + covariance[64] per track
 
-def algorithmic_bytes_per_frame(T, D, F, K):
-    """B = 2·T·576 + D·48 + (T_f + D)·F·4 + K·F·4 (fp64 track state read +
-    write, det rows, track + det features, updated features); T_f = T when F > 0."""
-    b = 2 * T * 576 + D * 48
-    if F:
-        b += (T + D) * F * 4 + K * F * 4
-    return b
+
+def stage_bytes(stage, u, F, es=4):
+    """Algorithmic HBM bytes of one launch of `stage`, from the unit counts `u`
+    of a frame summed over sequences: dets, high, active, lost, records, pairs."""
+    listed = u["active"] + u["lost"]
+    return {
+        # the embedding row of every high detection + 3 norms out
+        "det_features": u["high"] * (F * es + 24),
+        # mean read + predicted mean and pre-predict (h, a|w) written, per pooled track
+        "predict": listed * (64 + 64 + 16),
+        # track box per listed track, det row per det, one pair word per gated pair
+        "gate": listed * 32 + u["dets"] * 24 + u["pairs"] * 4,
+        # smooth_feat row + embedding row per gated pair, distance out
+        "cosine": u["pairs"] * (2 * F * es + 8),
+        # det rows, track boxes/flags/lists, records out
+        "assoc": u["dets"] * 24 + listed * (32 + 16) + u["records"] * 8,
+        # state read + written per update record, det row in
+        "update": u["records"] * (2 * KF_STATE + 24),
+        # covariance read + written for pooled tracks without an update
+        "cov_predict": max(listed - u["records"], 0) * 2 * 512,
+        # embedding row + smooth_feat read, smooth_feat written, per record with a feature
+        "features": u["records"] * 3 * F * es,
+        # box per listed track, output row per activated track
+        "finish": listed * 48 + u["dets"] * 64,
+    }[stage]
 
 
 def cpu_baseline(kind, n_obj, emb_dim, params, seconds=15.0, warm_frames=40):
@@ -76,13 +101,15 @@ def cpu_baseline(kind, n_obj, emb_dim, params, seconds=15.0, warm_frames=40):
                       f"{t} ({frames} timed, {busy:.1f}s single-thread; oracle/ C fp64 port)"}
 
 
-def load_traffic(config):
+def load_traffic(config, stage):
+    """HBM bytes per launch of `stage` from the committed PMC summary (FETCH_SIZE x2 on gfx950
+    + WRITE_SIZE, MI355X_MICROARCH.md §HBM), or None."""
     p = ROOT / "profiles" / f"pmc_{config}.json"
     if not p.exists():
         return None
     try:
         d = json.loads(p.read_text())
-        return d.get("hbm_bytes_per_launch_corrected")
+        return d.get("stages", {}).get(stage, {}).get("hbm_bytes_per_launch_corrected")
     except Exception:
         return None
 
@@ -121,9 +148,10 @@ def main():
 
     kind, n_obj, F, params = CONFIGS[args.config]
     S = args.seqs
-    D_cap = 256
-    eng = Engine(kind, n_seq=S, track_cap=512, det_cap=D_cap, emb_dim=F,
+    eng = Engine(kind, n_seq=S, track_cap=512, det_cap=256, emb_dim=F,
                  params=EngineParams(**params))
+    stages = [s for s in Engine.STAGES
+              if F or s not in ("det_features", "gate", "cosine", "features")]
     # this rank's shard: global sequences [rank*S, (rank+1)*S) — weak scaling, no exchange
     gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev)
     total = args.warmup + args.steps
@@ -138,36 +166,49 @@ def main():
         d, off, e = frames[k]
         eng.step(d, off, e, None, out, cnt, stream=stream.cuda_stream)
 
+    # warm-up; its last len(stages) steps time one stage each to find the dominant kernel
+    stage_ms = {}
+    cyc0 = args.warmup - len(stages)
     for k in range(args.warmup):
+        j = k - cyc0
+        if 0 <= j < len(stages):
+            eng.probe(stages[j])
         step(k)
+        if 0 <= j < len(stages):
+            ms, n = eng.probe_read()
+            stage_ms[stages[j]] = ms / max(n, 1)
+            eng.probe(None)
+    dominant = max(stage_ms, key=stage_ms.get) if stage_ms else (
+        "features" if F else "assoc")
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    eng.probe(dominant)  # two event records per step around that stage's launch
     t0 = time.perf_counter()
-    ev0.record(stream)
     for k in range(args.warmup, total):
         step(k)
-    ev1.record(stream)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one frame-kernel launch per step
+    dom_ms, dom_n = eng.probe_read()
+    eng.probe(None)
+    dom_ms /= max(dom_n, 1)
     if eng.status() != 0:
         raise RuntimeError(f"engine status {eng.status()} (capacity overflow)")
+    units = eng.frame_stats()  # last timed frame, all sequences of this rank
 
     # per-sequence records of this rank's shard: [global seq id, frames timed, dets timed,
-    # rows of the last frame, checksum of the last frame, rank wall s, rank kernel ms]
+    # rows of the last frame, checksum of the last frame, rank wall s, dominant-stage ms]
     off_h = [frames[k][1].cpu().numpy() for k in range(args.warmup, total)]
     dets_seq = np.sum([np.diff(o) for o in off_h], 0)
     last_off, cnt_h, out_h = off_h[-1], cnt.cpu().numpy(), out.cpu().numpy()
     recs = np.zeros((S, 7))
     for i, g in enumerate(shard_sequences(S * world, world, rank)):
         rows_i = out_h[last_off[i]: last_off[i] + cnt_h[i]]
-        recs[i] = [g, args.steps, dets_seq[i], cnt_h[i], output_checksum(rows_i), wall, kern_ms]
+        recs[i] = [g, args.steps, dets_seq[i], cnt_h[i], output_checksum(rows_i), wall, dom_ms]
     # RCCL over xGMI only to gather these KB-scale records once, never per frame
     allrec = gather_records(recs, dist, dev if backend == "nccl" else "cpu")
     t_max = float(allrec[:, 5].max())
@@ -176,11 +217,9 @@ def main():
     if rank == 0:
         assert np.array_equal(np.sort(allrec[:, 0]), np.arange(S * world)), "shard gather"
         mean_d = float(allrec[:, 2].sum() / allrec[:, 1].sum())
-        T_pool = n_obj
-        per_frame = algorithmic_bytes_per_frame(T_pool, mean_d, F, mean_d)
-        per_launch = per_frame * S
-        achieved = per_launch / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(args.config)
+        per_launch = stage_bytes(dominant, units, F)
+        achieved = per_launch / (dom_ms * 1e-3) / 1e9
+        traffic = load_traffic(args.config, dominant)
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -194,9 +233,11 @@ def main():
                        "parallelism": f"seq-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": f"frame_kernel<{kind}>",
-                         "kernel_ms": round(kern_ms, 4),
-                         "algorithmic_bytes_per_launch": int(per_launch)},
+                         "traffic": traffic, "kernel": dominant,
+                         "kernel_ms": round(dom_ms, 4),
+                         "algorithmic_bytes_per_launch": int(per_launch),
+                         "units_last_frame": units,
+                         "stage_ms_warmup": {k: round(v, 4) for k, v in stage_ms.items()}},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace bx {
 
 constexpr int WG = 256;  // threads per workgroup: 4 waves of 64
@@ -223,6 +225,31 @@ __device__ inline void kf_gating_soa(int kind, const double* mean, const double*
     out[q] = s2;
   }
 }
+
+// ------------------------------------------------------------------------------------------
+// x / n correctly rounded to fp32 (what IEEE division gives), from r = RN64(1/n): RN64(x * r)
+// is within 2^-52 (relative) of x/n, while a quotient of two floats lies >= 2^-47 (relative)
+// from every fp32 rounding midpoint — it can never BE one (that would need 25 significant bits
+// in the 24-bit numerator) — so rounding the product to fp32 lands on the same float.  Results
+// outside the fp32 normal range, zeros and NaNs take the plain division.  Three instructions
+// instead of the ~10 of a correctly rounded fp32 divide when one divisor serves a whole row.
+struct Div32 {
+  float n;
+  double r;
+  __device__ explicit Div32(float n_) : n(n_), r(1.0 / (double)n_) {}
+  __device__ __forceinline__ float operator()(float x) const {
+    const double p = (double)x * r;
+    return fabs(p) >= 0x1p-125 ? (float)p : x / n;
+  }
+};
+// same interface for fp64 rows: plain division
+struct Div64 {
+  double n;
+  __device__ explicit Div64(double n_) : n(n_) {}
+  __device__ __forceinline__ double operator()(double x) const { return x / n; }
+};
+template <typename FT>
+using DivBy = typename std::conditional<sizeof(FT) == 4, Div32, Div64>::type;
 
 // ------------------------------------------------------------------------------------------
 // Feature numerics.

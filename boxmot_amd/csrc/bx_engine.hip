@@ -79,8 +79,9 @@ struct RegRow {
     else return sqrt(s);
   }
   __device__ void div(FT n) {
+    const DivBy<FT> d(n);
 #pragma unroll
-    for (int r = 0; r < REG_EPL; r++) v[r] = v[r] / n;
+    for (int r = 0; r < REG_EPL; r++) v[r] = d(v[r]);
   }
   // numpy float32 norm of the float32-cast row (+1e-8 as embedding_distance adds it), staged
   // through this wave's LDS row so lanes can read numpy's accumulator layout
@@ -190,6 +191,7 @@ struct Dev {
 
 enum {
   SQ_NA = 0, SQ_NL, SQ_FC, SQ_IDC, SQ_STATUS, SQ_NA2, SQ_NL2, SQ_NREC, SQ_SKIP,
+  SQ_NHIGH, SQ_NPAIR, SQ_NDET,  // last frame's high dets, gated pairs, dets (statistics)
   SQ_STRIDE = 16
 };
 // update records: x = slot | kind << 16, y = detection index within the sequence's frame
@@ -320,10 +322,18 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
   const int F = P.F, D = P.D;
   const int d0 = det_off[b], N = min(det_off[b + 1] - d0, D);
   const int k0 = blockIdx.y * 64, k1 = min(k0 + 64, N);
-  auto high = [&](int k) { return (double)dets[(size_t)(d0 + k) * 6 + 4] > P.high; };
+  if (k0 >= N) return;  // block-uniform
+  __shared__ unsigned long long s_hi;  // bit k - k0: detection k is high
+  if (w == 0) {
+    const int k = k0 + lane;
+    const unsigned long long m = __ballot(k < k1 && (double)dets[(size_t)(d0 + k) * 6 + 4] > P.high);
+    if (lane == 0) s_hi = m;
+  }
+  __syncthreads();
+  const unsigned long long hi = s_hi;
   auto next = [&](int k) {  // next high detection of this wave at or after k
     for (; k < k1; k += NWAVE)
-      if (high(k)) return k;
+      if ((hi >> (k - k0)) & 1ull) return k;
     return k1;
   };
   auto put_norms = [&](int k, FT n1, FT n2, float dn) {
@@ -475,6 +485,12 @@ __global__ __launch_bounds__(WG) void cosine_kernel(Dev P, int seq0, const int* 
       bn2[k] = (FT)nr[1];
       bdn[k] = (float)nr[2];
     }
+    const Div32 da[4] = {Div32(adn[0]), Div32(adn[1]), Div32(adn[2]), Div32(adn[3])};
+    const Div32 db[4] = {Div32(bdn[0]), Div32(bdn[1]), Div32(bdn[2]), Div32(bdn[3])};
+    const DivBy<FT> d1[4] = {DivBy<FT>(bn1[0]), DivBy<FT>(bn1[1]), DivBy<FT>(bn1[2]),
+                             DivBy<FT>(bn1[3])};
+    const DivBy<FT> d2[4] = {DivBy<FT>(bn2[0]), DivBy<FT>(bn2[1]), DivBy<FT>(bn2[2]),
+                             DivBy<FT>(bn2[3])};
     double ab0 = 0.0, ab1 = 0.0, aa0 = 0.0, aa1 = 0.0, bb0 = 0.0, bb1 = 0.0;
     FT av[4][4], bv[4][4];  // raw elements of the current chunk; the next chunk's are in flight
 #pragma unroll
@@ -489,9 +505,8 @@ __global__ __launch_bounds__(WG) void cosine_kernel(Dev P, int seq0, const int* 
         const int row = k * 16 + (lane >> 2), col = (lane & 3) * 4;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-          s_a[w][row][col + q] = (float)av[k][q] / adn[k];
-          const FT f2 = (bv[k][q] / bn1[k]) / bn2[k];
-          s_b[w][row][col + q] = (float)f2 / bdn[k];
+          s_a[w][row][col + q] = da[k]((float)av[k][q]);
+          s_b[w][row][col + q] = db[k]((float)d2[k](d1[k](bv[k][q])));
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1134,6 +1149,8 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
     seq[SQ_NA2] = nact2;
     seq[SQ_NL2] = nlost2;
     seq[SQ_NREC] = nrec;
+    seq[SQ_NHIGH] = Dh;
+    seq[SQ_NDET] = N;
     seq[SQ_SKIP] = 0;
     if (I[I_ERR]) seq[SQ_STATUS] |= 1 << BX_ERR_TRACK_OVERFLOW;
   }
@@ -1167,11 +1184,17 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
   const double conf = (double)row[4], cls = (double)row[5];
   double* h = P.clsh + (sT + slot) * CLS_HIST * 2;
   auto shfl = [&](double v, int src) { return __shfl(v, src, 8); };
-  if (kind == R_NEW) {  // kf_initiate: mean = [z, 0], cov = diag(std^2)
-    double m8[8], c64[64];
-    kf_initiate(KIND, meas, m8, c64);
-    m[r] = m8[r];
-    for (int q = 0; q < 4; q++) crow[q] = make_double2(c64[8 * r + 2 * q], c64[8 * r + 2 * q + 1]);
+  if (kind == R_NEW) {  // kf_initiate (kf_initiate's expressions): mean = [z, 0], cov = diag(std^2)
+    double dr;
+    if (KIND == KIND_BYTE)
+      dr = r == 2 ? 1e-2 : r == 6 ? 1e-5 : (r < 4 ? 2 * STD_POS : 10 * STD_VEL) * meas[3];
+    else
+      dr = (r < 4 ? 2 * STD_POS : 10 * STD_VEL) * ((r & 1) ? meas[3] : meas[2]);
+    const double mz = r == 0 ? meas[0] : r == 1 ? meas[1] : r == 2 ? meas[2] : r == 3 ? meas[3]
+                                                                                         : 0.0;
+    m[r] = mz;
+    for (int q = 0; q < 4; q++)
+      crow[q] = make_double2(2 * q == r ? dr * dr : 0.0, 2 * q + 1 == r ? dr * dr : 0.0);
     if (r == 0) {
       P.conf[sT + slot] = conf;
       P.detind[sT + slot] = dk;
@@ -1197,13 +1220,13 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
     if (r < 4) {
       for (int j = 0; j < 4; j++) {
         double v = (cr[j] + o[j]) + (cr[j + 4] + o[j + 4]);
-        nr[j] = (j == r) ? v + q[r] : v;
+        nr[j] = (j == r) ? v + q[j] : v;
         nr[j + 4] = cr[j + 4] + o[j + 4];
       }
     } else {
       for (int j = 0; j < 4; j++) {
         nr[j] = cr[j] + cr[j + 4];
-        nr[j + 4] = (j + 4 == r) ? cr[j + 4] + q[r] : cr[j + 4];
+        nr[j + 4] = (j + 4 == r) ? cr[j + 4] + q[j + 4] : cr[j + 4];
       }
     }
     for (int j = 0; j < 8; j++) cr[j] = nr[j];
@@ -1247,7 +1270,7 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
     for (int k = 0; k < 4; k++) innov[k] = meas[k] - mm[k];
     double sm = 0.0;
     for (int k = 0; k < 4; k++) sm += innov[k] * Kr[k];
-    const double mnew = mm[r] + sm;
+    const double mnew = m[r] + sm;
     double ks[4];
     for (int j = 0; j < 4; j++) {
       double sv = 0.0;
@@ -1306,9 +1329,23 @@ __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
   const FT* fembs = embs + (size_t)det_off[b] * F;
   FT* feat = (FT*)P.feat + (size_t)s * T * F;
   constexpr int STEP = FEAT_BLOCKS * NWAVE;
+  // this block's records (r = blockIdx.y*NWAVE + w + k*STEP) staged in LDS up front
+  constexpr int RMAX = 64;
+  __shared__ int2 s_rec[RMAX];
+  const int nmine = nrec > (int)blockIdx.y * NWAVE
+                        ? (nrec - (int)blockIdx.y * NWAVE + STEP - 1) / STEP * NWAVE : 0;
+  for (int t = threadIdx.x; t < min(nmine, RMAX); t += WG) {
+    const int r = blockIdx.y * NWAVE + (t % NWAVE) + (t / NWAVE) * STEP;
+    s_rec[t] = r < nrec ? P.rec[(size_t)s * D + r] : make_int2(0, 0);
+  }
+  __syncthreads();
+  auto rec = [&](int r) {
+    const int t = (r - (int)blockIdx.y * NWAVE) / STEP * NWAVE + (r - (int)blockIdx.y * NWAVE) % STEP;
+    return t < RMAX ? s_rec[t] : P.rec[(size_t)s * D + r];
+  };
   auto next = [&](int r) {  // next record with a feature at or after r
     for (; r < nrec; r += STEP)
-      if ((P.rec[(size_t)s * D + r].x >> 16) & R_FEAT) return r;
+      if ((rec(r).x >> 16) & R_FEAT) return r;
     return nrec;
   };
   if (F <= REG_F) {
@@ -1316,7 +1353,7 @@ __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
     RegRow<FT> g, m;
     int2 rc = make_int2(0, 0);
     if (r < nrec) {
-      rc = P.rec[(size_t)s * D + r];
+      rc = rec(r);
       g.load(fembs + (size_t)rc.y * F, F);
       m.load(feat + (size_t)(rc.x & 0xffff) * F, F);
     }
@@ -1325,7 +1362,7 @@ __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
       RegRow<FT> ng, nm;
       int2 nrc = make_int2(0, 0);
       if (rn < nrec) {
-        nrc = P.rec[(size_t)s * D + rn];
+        nrc = rec(rn);
         ng.load(fembs + (size_t)nrc.y * F, F);
         nm.load(feat + (size_t)(nrc.x & 0xffff) * F, F);
       }
@@ -1340,10 +1377,10 @@ __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
         g.store(sm, F);
         dn = g.template np_dn<NPF>(wb, F);
       } else {
-        const FT n3 = g.norm(F);
+        const DivBy<FT> n3(g.norm(F));
 #pragma unroll
         for (int q = 0; q < REG_EPL; q++) {
-          FT g3 = g.v[q] / n3;
+          FT g3 = n3(g.v[q]);
           m.v[q] = a * m.v[q] + bb * g3;
         }
         m.div(m.norm(F));
@@ -1483,6 +1520,7 @@ __global__ __launch_bounds__(WG) void finish_kernel(Dev P, int seq0, const int* 
     seq[SQ_NA] = nfa;
     seq[SQ_NL] = nfl;
     out_count[b] = nout;
+    seq[SQ_NPAIR] = P.npair[s];
     P.npair[s] = 0;
   }
 }
@@ -1504,6 +1542,10 @@ struct bx_engine {
   Dev dev;
   int device;
   size_t lds_assoc, lds_finish;
+  // stage timing probe (bx_engine_probe)
+  int probe_stage = -1;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> probe_ev;
+  size_t probe_used = 0;
   void* arena;
   size_t arena_bytes;
   // host-path staging (device)
@@ -1546,55 +1588,84 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
                  hipStream_t st) {
   const Dev& d = e->dev;
   const bool reid = KIND == KIND_BOT && d.with_reid;
+  auto probe_begin = [&](int stage) -> int {
+    if (stage != e->probe_stage) return BX_OK;
+    if (e->probe_used == e->probe_ev.size()) {
+      hipEvent_t a, b;
+      // timing-only events: no system-scope fence (cache writeback/invalidate) on record, so
+      // the probe does not perturb the kernels around it
+      HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableSystemFence));
+      HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableSystemFence));
+      e->probe_ev.emplace_back(a, b);
+    }
+    HIPCHK(hipEventRecord(e->probe_ev[e->probe_used].first, st));
+    return BX_OK;
+  };
+  auto probe_end = [&](int stage) -> int {
+    if (stage != e->probe_stage) return BX_OK;
+    HIPCHK(hipEventRecord(e->probe_ev[e->probe_used++].second, st));
+    return BX_OK;
+  };
+#define BX_PROBED(stage, launch)                           \
+  do {                                                     \
+    if (int rc_ = probe_begin(stage)) return rc_;          \
+    launch;                                                \
+    HIPCHK(hipGetLastError());                             \
+    if (int rc_ = probe_end(stage)) return rc_;            \
+  } while (0)
   const int gy_det64 = (d.D + 63) / 64, gy_slot = (d.T + WG - 1) / WG;
-  if (reid) {
-    hipLaunchKernelGGL((det_feature_kernel<FT, NPF>), dim3(nseq, gy_det64), dim3(WG), 0, st, d,
-                       seq0, dets, det_off, (const FT*)embs);
-    HIPCHK(hipGetLastError());
-  }
+  if (reid)
+    BX_PROBED(BX_STAGE_DET_FEATURES,
+              hipLaunchKernelGGL((det_feature_kernel<FT, NPF>), dim3(nseq, gy_det64), dim3(WG), 0,
+                                 st, d, seq0, dets, det_off, (const FT*)embs));
   const bool gmc = KIND == KIND_BOT && warps;
   if (gmc)
-    hipLaunchKernelGGL((predict_kernel<KIND, true>), dim3(nseq, gy_slot), dim3(WG), 0, st, d,
-                       seq0, warps);
+    BX_PROBED(BX_STAGE_PREDICT,
+              hipLaunchKernelGGL((predict_kernel<KIND, true>), dim3(nseq, gy_slot), dim3(WG), 0,
+                                 st, d, seq0, warps));
   else
-    hipLaunchKernelGGL((predict_kernel<KIND, false>), dim3(nseq, gy_slot), dim3(WG), 0, st, d,
-                       seq0, warps);
-  HIPCHK(hipGetLastError());
+    BX_PROBED(BX_STAGE_PREDICT,
+              hipLaunchKernelGGL((predict_kernel<KIND, false>), dim3(nseq, gy_slot), dim3(WG), 0,
+                                 st, d, seq0, warps));
   if (reid) {
-    hipLaunchKernelGGL(gate_kernel<KIND>, dim3(nseq, GATE_BLOCKS), dim3(WG),
-                       (sizeof(double) * 4 + sizeof(float4)) * d.D, st, d, seq0, dets, det_off);
-    HIPCHK(hipGetLastError());
+    BX_PROBED(BX_STAGE_GATE,
+              hipLaunchKernelGGL(gate_kernel<KIND>, dim3(nseq, GATE_BLOCKS), dim3(WG),
+                                 (sizeof(double) * 4 + sizeof(float4)) * d.D, st, d, seq0, dets,
+                                 det_off));
     if (d.F % COS_CH == 0)
-      hipLaunchKernelGGL(cosine_kernel<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st, d, seq0,
-                         det_off, (const FT*)embs);
+      BX_PROBED(BX_STAGE_COSINE,
+                hipLaunchKernelGGL(cosine_kernel<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st, d,
+                                   seq0, det_off, (const FT*)embs));
     else
-      hipLaunchKernelGGL(cosine_kernel_any<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st, d, seq0,
-                         det_off, (const FT*)embs);
-    HIPCHK(hipGetLastError());
+      BX_PROBED(BX_STAGE_COSINE,
+                hipLaunchKernelGGL(cosine_kernel_any<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st,
+                                   d, seq0, det_off, (const FT*)embs));
   }
   auto assoc = assoc_kernel<KIND>;
   if (int rc = lds_attr((const void*)assoc, e->lds_assoc)) return rc;
-  hipLaunchKernelGGL(assoc, dim3(nseq), dim3(WG), e->lds_assoc, st, d, seq0, dets, det_off);
-  HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(update_kernel<KIND>, dim3(nseq, (d.D + UPD_PER_BLOCK - 1) / UPD_PER_BLOCK),
-                     dim3(WG), 0, st, d, seq0, dets, det_off, warps);
-  HIPCHK(hipGetLastError());
+  BX_PROBED(BX_STAGE_ASSOC, hipLaunchKernelGGL(assoc, dim3(nseq), dim3(WG), e->lds_assoc, st, d,
+                                               seq0, dets, det_off));
+  BX_PROBED(BX_STAGE_UPDATE,
+            hipLaunchKernelGGL(update_kernel<KIND>,
+                               dim3(nseq, (d.D + UPD_PER_BLOCK - 1) / UPD_PER_BLOCK), dim3(WG), 0,
+                               st, d, seq0, dets, det_off, warps));
   if (gmc)
-    hipLaunchKernelGGL(cov_predict_gmc_kernel<KIND>, dim3(nseq, gy_slot), dim3(WG), 0, st, d,
-                       seq0, warps);
+    BX_PROBED(BX_STAGE_COV_PREDICT,
+              hipLaunchKernelGGL(cov_predict_gmc_kernel<KIND>, dim3(nseq, gy_slot), dim3(WG), 0,
+                                 st, d, seq0, warps));
   else
-    hipLaunchKernelGGL(cov_predict_kernel<KIND>, dim3(nseq, (d.T + 15) / 16), dim3(WG), 0, st, d,
-                       seq0);
-  HIPCHK(hipGetLastError());
-  if (reid) {
-    hipLaunchKernelGGL((feature_kernel<FT, NPF>), dim3(nseq, FEAT_BLOCKS), dim3(WG), 0, st, d,
-                       seq0, det_off, (const FT*)embs);
-    HIPCHK(hipGetLastError());
-  }
+    BX_PROBED(BX_STAGE_COV_PREDICT,
+              hipLaunchKernelGGL(cov_predict_kernel<KIND>, dim3(nseq, (d.T + 15) / 16), dim3(WG),
+                                 0, st, d, seq0));
+  if (reid)
+    BX_PROBED(BX_STAGE_FEATURES,
+              hipLaunchKernelGGL((feature_kernel<FT, NPF>), dim3(nseq, FEAT_BLOCKS), dim3(WG), 0,
+                                 st, d, seq0, det_off, (const FT*)embs));
   if (int rc = lds_attr((const void*)finish_kernel<KIND>, e->lds_finish)) return rc;
-  hipLaunchKernelGGL(finish_kernel<KIND>, dim3(nseq), dim3(WG), e->lds_finish, st, d, seq0,
-                     det_off, out, out_count);
-  HIPCHK(hipGetLastError());
+  BX_PROBED(BX_STAGE_FINISH,
+            hipLaunchKernelGGL(finish_kernel<KIND>, dim3(nseq), dim3(WG), e->lds_finish, st, d,
+                               seq0, det_off, out, out_count));
+#undef BX_PROBED
   return BX_OK;
 }
 
@@ -1713,6 +1784,10 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
 
 int bx_engine_destroy(bx_engine* e) {
   if (!e) return BX_OK;
+  for (auto& ev : e->probe_ev) {
+    (void)hipEventDestroy(ev.first);
+    (void)hipEventDestroy(ev.second);
+  }
   (void)hipFree(e->arena);
   (void)hipFree(e->h_dets);
   (void)hipFree(e->h_embs);
@@ -1804,6 +1879,43 @@ int bx_engine_status(bx_engine* e, int* status) {
   *status = (s & (1 << BX_ERR_TRACK_OVERFLOW)) ? BX_ERR_TRACK_OVERFLOW
             : (s & (1 << BX_ERR_CAPACITY))     ? BX_ERR_CAPACITY
                                                : BX_OK;
+  return BX_OK;
+}
+
+int bx_engine_frame_stats_host(bx_engine* e, int seq0, int nseq, int64_t* sums) {
+  if (!e || !sums || seq0 < 0 || nseq <= 0 || seq0 + nseq > e->dev.S)
+    return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_frame_stats_host");
+  std::vector<int> v((size_t)nseq * SQ_STRIDE);
+  HIPCHK(hipMemcpy(v.data(), e->dev.seq + (size_t)seq0 * SQ_STRIDE, sizeof(int) * v.size(),
+                   hipMemcpyDeviceToHost));
+  const int idx[7] = {SQ_NDET, SQ_NHIGH, SQ_NA, SQ_NL, SQ_NREC, SQ_NPAIR, SQ_FC};
+  for (int k = 0; k < 7; k++) {
+    int64_t t = 0;
+    for (int q = 0; q < nseq; q++) t += v[(size_t)q * SQ_STRIDE + idx[k]];
+    sums[k] = t;
+  }
+  return BX_OK;
+}
+
+int bx_engine_probe(bx_engine* e, int stage) {
+  if (!e || stage >= BX_STAGE_COUNT) return set_err(BX_ERR_INVALID, "bad probe stage");
+  e->probe_stage = stage < 0 ? -1 : stage;
+  e->probe_used = 0;
+  return BX_OK;
+}
+
+int bx_engine_probe_read(bx_engine* e, double* total_ms, int* count) {
+  if (!e || !total_ms || !count) return set_err(BX_ERR_INVALID, "null argument");
+  double t = 0.0;
+  for (size_t k = 0; k < e->probe_used; k++) {
+    HIPCHK(hipEventSynchronize(e->probe_ev[k].second));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e->probe_ev[k].first, e->probe_ev[k].second));
+    t += ms;
+  }
+  *total_ms = t;
+  *count = (int)e->probe_used;
+  e->probe_used = 0;
   return BX_OK;
 }
 

@@ -122,6 +122,28 @@ class Engine:
         N.check(self._L.bx_engine_status(self._h, C.byref(s)), "bx_engine_status")
         return s.value
 
+    STAGES = ["det_features", "predict", "gate", "cosine", "assoc", "update", "cov_predict",
+              "features", "finish"]  # bx_stage order (include/bxassoc.h)
+
+    def probe(self, stage) -> None:
+        """Time every launch of one pipeline stage with HIP events (None/-1 disables)."""
+        k = -1 if stage is None else (self.STAGES.index(stage) if isinstance(stage, str) else stage)
+        N.check(self._L.bx_engine_probe(self._h, k), "bx_engine_probe")
+
+    def probe_read(self):
+        """(total ms, launches) of the probed stage since the last read."""
+        t, n = C.c_double(), C.c_int()
+        N.check(self._L.bx_engine_probe_read(self._h, C.byref(t), C.byref(n)), "probe_read")
+        return t.value, n.value
+
+    def frame_stats(self, seq0: int = 0, nseq: int = None) -> dict:
+        """Last frame's unit counts summed over sequences (bench byte accounting)."""
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        a = (C.c_int64 * 7)()
+        N.check(self._L.bx_engine_frame_stats_host(self._h, seq0, nseq, a), "frame_stats")
+        keys = ["dets", "high", "active", "lost", "records", "pairs", "frame"]
+        return dict(zip(keys, [int(x) for x in a]))
+
     def counters(self, seq: int = 0) -> dict:
         fc, idc, na, nl = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         N.check(self._L.bx_engine_counters_host(self._h, seq, C.byref(fc), C.byref(idc),

@@ -73,7 +73,9 @@ int bx_engine_destroy(bx_engine *e);
 /* Forget all tracks of sequences [seq0, seq0+nseq) (frame and id counters back to 0). */
 int bx_engine_reset(bx_engine *e, int seq0, int nseq, void *stream);
 
-/* One frame for sequences [seq0, seq0+nseq) in ONE kernel launch.
+/* One frame for sequences [seq0, seq0+nseq): a short pipeline of kernels enqueued on `stream`
+ * (per-detection features, Kalman predict, gating + re-ID distances, the per-sequence
+ * association, Kalman/feature updates, duplicate removal + outputs).
  *   dets    [sum N][6] float32 (x1,y1,x2,y2,conf,cls) — the reference rounds dets to float32
  *           in BaseTracker.setup_decorator (basetracker.py:122-128)
  *   det_off [nseq+1] int32 prefix offsets: sequence k owns rows det_off[k]..det_off[k+1]
@@ -92,6 +94,22 @@ int bx_engine_step(bx_engine *e, int seq0, int nseq, const float *dets, const in
  * NULL; out must hold n rows; *n_out receives the row count. */
 int bx_engine_update_host(bx_engine *e, int seq, const float *dets, int n, const void *embs,
                           const double *warp, double *out, int *n_out, void *stream);
+
+/* Stage timing probe (benchmarks): while enabled, bx_engine_step records a HIP event pair
+ * around every launch of pipeline stage `stage` on its stream; bx_engine_probe_read
+ * synchronises, returns the summed milliseconds and the number of timed launches, and clears
+ * them.  stage < 0 disables the probe.  Costs two event records per step. */
+typedef enum {
+    BX_STAGE_DET_FEATURES = 0, BX_STAGE_PREDICT = 1, BX_STAGE_GATE = 2, BX_STAGE_COSINE = 3,
+    BX_STAGE_ASSOC = 4, BX_STAGE_UPDATE = 5, BX_STAGE_COV_PREDICT = 6, BX_STAGE_FEATURES = 7,
+    BX_STAGE_FINISH = 8, BX_STAGE_COUNT = 9
+} bx_stage;
+int bx_engine_probe(bx_engine *e, int stage);
+/* Last-frame statistics summed over sequences [seq0, seq0+nseq) (host, synchronous):
+ * sums[7] = {detections, high-confidence detections, active tracks, lost tracks, update records,
+ * gated (track, det) pairs, frame counter} — the unit counts bench.py prices bytes with. */
+int bx_engine_frame_stats_host(bx_engine *e, int seq0, int nseq, int64_t *sums);
+int bx_engine_probe_read(bx_engine *e, double *total_ms, int *count);
 
 /* Latched device-side status of the whole engine (BX_OK or BX_ERR_TRACK_OVERFLOW). */
 int bx_engine_status(bx_engine *e, int *status);

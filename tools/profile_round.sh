@@ -1,15 +1,13 @@
 #!/bin/bash
-# rocprofv3 evidence for the bench workload (run on the GPU box from the repo root).
-#   $1 = tag (e.g. r01), $2 = config (botsort|bytetrack), $3 = seqs
-# kernel trace + stats in one pass; HBM counters in their own passes (FETCH_SIZE and WRITE_SIZE
-# cannot share a pass on gfx950, MI355X_MICROARCH.md §rocprofv3 PMC slots).
+# Round evidence for one config (GPU box, repo root): rocprofv3 kernel trace + stats of the bench
+# command, then the PMC passes, summarised ON the box into gpurun_out/summary_<tag>/ (the raw
+# traces stay on the box: gpurun copies back at most 64 MiB).
+#   $1 = tag (e.g. r01), $2 = config (botsort|bytetrack)
 set -euo pipefail
-TAG=${1:-r01}; CFG=${2:-botsort}; SEQS=${3:-1024}
-OUT=gpurun_out/prof_${TAG}_${CFG}
-mkdir -p "$OUT"
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-ARGS="--config $CFG --seqs $SEQS --steps 30 --warmup 10 --no-cpu-baseline"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 bench.py $ARGS > "$OUT/bench_traced.log" 2>&1
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 bench.py $ARGS > "$OUT/bench_fetch.log" 2>&1
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 bench.py $ARGS > "$OUT/bench_write.log" 2>&1
-find "$OUT" -name "*.csv" | head -50
+TAG=${1:-r01}; CFG=${2:-botsort}
+bash tools/trace_only.sh "$TAG" "$CFG"
+bash tools/pmc_passes.sh "$TAG" "$CFG"
+python3 tools/summarize_profile.py "$TAG" "$CFG" "gpurun_out/summary_${TAG}"
+cp "gpurun_out/trace_${TAG}_${CFG}/run_kernel_stats.csv" "gpurun_out/summary_${TAG}/${TAG}_${CFG}_kernel_stats.csv"
+cp "gpurun_out/trace_${TAG}_${CFG}/bench.log" "gpurun_out/summary_${TAG}/${TAG}_${CFG}_bench_traced.log"
+rm -rf "gpurun_out/trace_${TAG}_${CFG}" "gpurun_out/pmc_${TAG}_${CFG}"
