@@ -443,8 +443,16 @@ __device__ inline void wave0_exclusive_scan(int* cnt, int n) {
 // admissible edges (cost < L).  lapx's (n_r+n_c)^2 extension with L/2 fillers is exactly a
 // max-gain partial matching with gains L - c, solved here by successive
 // shortest augmenting paths (Dijkstra with potentials; rectangular LSAP) where every row owns a
-// private zero-cost "dummy" column meaning "unmatched".  Run by ONE wave: relaxations are
-// lane-parallel over a row's edges and the argmin over the touched columns is a wave reduction.
+// private zero-cost "dummy" column meaning "unmatched", rows processed in ascending order.
+//
+// A shortest-path search from a root only ever reaches rows and columns of the root's connected
+// component of the candidate graph, so components are solved independently with the same
+// per-component row order and the same result:
+//   * single-edge components (a row whose only finite edge goes to a column no other row can
+//     reach) are matched directly: exactly the path SSP would find (gain L-c>0, u = c-L, v = 0);
+//   * small components run the sequential SSP on one lane each, all lanes in parallel;
+//   * large components run it wave-parallel (relaxations over a row's edges and the argmin over
+//     touched columns spread over the 64 lanes), one component after another.
 struct LapWS {
   const int* row_ptr;     // [R+1] edge offsets
   const uint16_t* ecol;   // edge columns (first elds in LDS, the rest in gcol)
@@ -459,10 +467,11 @@ struct LapWS {
   double* spc;            // [C] shortest-path costs (INF between solves)
   int16_t* path;          // [C]
   uint8_t* colflag;       // [C] bit0 = in SC, bit1 = touched
-  uint16_t* touched;      // [C] touched column list
-  uint16_t* srlist;       // [R] rows visited (SR) except the root
-  int* coldeg;            // [C] finite-edge degree per column (single-edge-component fast path)
-  uint16_t* roots;        // [R] rows left for the Dijkstra phase, ascending
+  uint16_t* touched;      // [C] touched column list (wave solver) / next-touched links (lane)
+  uint16_t* srlist;       // [R] rows visited (SR) except the root / next-SR links (lane)
+  int* coldeg;            // [C] finite-edge degree per column, then component labels per column
+  uint16_t* roots;        // [R] rows left for the shortest-path phase, ascending
+  int* rlab;              // [R] component label (smallest row index of the component)
   unsigned long long* dbg = nullptr;  // diagnostic counters (phase-timing builds only)
 };
 
@@ -481,19 +490,181 @@ __device__ __forceinline__ void wave_argmin(double& val, int& key) {
   }
 }
 
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+
+// augment along path[] ending at `sink` (>= 0 column, -2 dummy of dummy_row); one lane
+__device__ __forceinline__ void lap_augment(const LapWS& w, int root, int sink, int dummy_row) {
+  int j;
+  if (sink == -2) {
+    j = w.col4row[dummy_row];
+    w.col4row[dummy_row] = -1;
+    if (dummy_row == root) j = -1;
+  } else {
+    j = sink;
+  }
+  while (j >= 0) {
+    int r = w.path[j];
+    w.row4col[j] = (int16_t)r;
+    int old = w.col4row[r];
+    w.col4row[r] = (int16_t)j;
+    if (r == root) break;
+    j = old;
+  }
+}
+
+// One SSP root on ONE lane (the lane's component only touches its own rows/columns).  Touched
+// columns and visited rows are kept as linked lists through touched[] / srlist[].
+__device__ __forceinline__ int lap_root_lane(int root, double L, const LapWS& w) {
+  double minVal = 0.0;
+  int i = root, thead = -1, ttail = -1, shead = -1, stail = -1, steps = 0;
+  double dummy_best = INF;
+  int dummy_row = -1, sink = -1;
+  while (true) {
+    const double ui = w.u[i];
+    for (int e = w.row_ptr[i]; e < w.row_ptr[i + 1]; e++) {
+      int j;
+      double c;
+      lap_edge(w, e, j, c);
+      if (w.colflag[j] & 1) continue;
+      const double r = minVal + (c - L) - ui - w.v[j];
+      if (r < w.spc[j]) {
+        w.spc[j] = r;
+        w.path[j] = (int16_t)i;
+        if (!(w.colflag[j] & 2)) {
+          w.colflag[j] |= 2;
+          if (ttail >= 0) w.touched[ttail] = (uint16_t)j; else thead = j;
+          ttail = j;
+        }
+      }
+    }
+    const double dv = minVal - ui;
+    if (dv < dummy_best) { dummy_best = dv; dummy_row = i; }
+    double bv = INF;
+    int bj = -1;
+    for (int j = thead; j >= 0; j = (j == ttail) ? -1 : (int)w.touched[j])
+      if (!(w.colflag[j] & 1) && w.spc[j] < bv) { bv = w.spc[j]; bj = j; }
+    if (dummy_best <= bv) { minVal = dummy_best; sink = -2; break; }
+    minVal = bv;
+    steps++;
+    w.colflag[bj] |= 1;
+    const int r4c = w.row4col[bj];
+    if (r4c < 0) { sink = bj; break; }
+    i = r4c;
+    if (stail >= 0) w.srlist[stail] = (uint16_t)i; else shead = i;
+    stail = i;
+  }
+  w.u[root] += minVal;
+  for (int r = shead; r >= 0; r = (r == stail) ? -1 : (int)w.srlist[r])
+    w.u[r] += minVal - w.spc[w.col4row[r]];
+  for (int j = thead; j >= 0; j = (j == ttail) ? -1 : (int)w.touched[j])
+    if (w.colflag[j] & 1) w.v[j] -= minVal - w.spc[j];
+  lap_augment(w, root, sink, dummy_row);
+  for (int j = thead; j >= 0;) {
+    const int nx = (j == ttail) ? -1 : (int)w.touched[j];
+    w.spc[j] = INF;
+    w.colflag[j] = 0;
+    j = nx;
+  }
+  return steps;
+}
+
+// One SSP root, wave-parallel (called by all 64 lanes).
+__device__ __forceinline__ int lap_root_wave(int root, double L, const LapWS& w) {
+  const int lane = lane_id();
+  double minVal = 0.0;
+  int i = root, ntouched = 0, nsr = 0, steps = 0;
+  double dummy_best = INF;
+  int dummy_row = -1, sink = -1;  // sink >= 0 real column, -2 dummy of dummy_row
+  while (true) {
+    const double ui = w.u[i];
+    const int b = w.row_ptr[i], e = w.row_ptr[i + 1];
+    for (int base = b; base < e; base += WAVE) {
+      int eidx = base + lane;
+      bool newt = false;
+      int j = 0;
+      if (eidx < e) {
+        double c;
+        lap_edge(w, eidx, j, c);
+        if (!(w.colflag[j] & 1)) {
+          double r = minVal + (c - L) - ui - w.v[j];
+          if (r < w.spc[j]) {
+            w.spc[j] = r;
+            w.path[j] = (int16_t)i;
+            if (!(w.colflag[j] & 2)) { w.colflag[j] |= 2; newt = true; }
+          }
+        }
+      }
+      unsigned long long m = __ballot(newt);
+      if (newt) w.touched[ntouched + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)j;
+      ntouched += __popcll(m);
+    }
+    {  // dummy of row i: reduced cost 0 - u_i - 0 (its potential never moves)
+      double dv = minVal - ui;
+      if (dv < dummy_best) { dummy_best = dv; dummy_row = i; }
+    }
+    wave_sync_lds();
+    // argmin over touched, not-yet-scanned columns (ties: earliest touched)
+    double bv = INF;
+    int bk = 0x7fffffff;
+    for (int k = lane; k < ntouched; k += WAVE) {
+      int j = w.touched[k];
+      if (!(w.colflag[j] & 1)) {
+        double sv = w.spc[j];
+        if (sv < bv) { bv = sv; bk = k; }
+      }
+    }
+    wave_argmin(bv, bk);
+    if (dummy_best <= bv) {  // leave dummy_row unmatched (ties: stop early)
+      minVal = dummy_best;
+      sink = -2;
+      break;
+    }
+    const int j = w.touched[bk];
+    steps++;
+    minVal = bv;
+    if (lane == 0) w.colflag[j] |= 1;
+    const int r4c = w.row4col[j];
+    wave_sync_lds();
+    if (r4c < 0) { sink = j; break; }
+    i = r4c;
+    if (lane == 0) w.srlist[nsr] = (uint16_t)i;
+    nsr++;
+  }
+  // dual updates
+  if (lane == 0) w.u[root] += minVal;
+  for (int k = lane; k < nsr; k += WAVE) {
+    int r = w.srlist[k];
+    w.u[r] += minVal - w.spc[w.col4row[r]];
+  }
+  wave_sync_lds();
+  for (int k = lane; k < ntouched; k += WAVE) {
+    int j = w.touched[k];
+    if (w.colflag[j] & 1) w.v[j] -= minVal - w.spc[j];
+  }
+  wave_sync_lds();
+  if (lane == 0) lap_augment(w, root, sink, dummy_row);
+  for (int k = lane; k < ntouched; k += WAVE) {
+    int j = w.touched[k];
+    w.spc[j] = INF;
+    w.colflag[j] = 0;
+  }
+  wave_sync_lds();
+  return steps;
+}
+
+constexpr int LAP_LANE_ROWS = 16;  // components up to this many rows are solved by one lane
+
 // Called by all 64 lanes of one wave.  R rows, C columns, limit L.
-__device__ inline void lap_solve_wave(int R, int C, double L, const LapWS& w) {
+__device__ __forceinline__ void lap_solve_wave(int R, int C, double L, const LapWS& w) {
   const int lane = lane_id();
   for (int k = lane; k < R; k += WAVE) { w.col4row[k] = -1; w.u[k] = 0.0; }
   for (int k = lane; k < C; k += WAVE) {
-    w.row4col[k] = -1; w.v[k] = 0.0; w.spc[k] = INF; w.colflag[k] = 0;
+    w.row4col[k] = -1; w.v[k] = 0.0; w.spc[k] = INF; w.colflag[k] = 0; w.coldeg[k] = 0;
   }
-  // Single-edge components (a row whose only finite edge goes to a column no other row can
-  // reach) are matched directly: that is exactly the path SSP would find for them (gain L-c>0,
-  // potentials u = c-L, v = 0), and no other row can ever touch that row or column.
-  for (int k = lane; k < C; k += WAVE) w.coldeg[k] = 0;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  wave_sync_lds();
   const int E = w.row_ptr[R];
   for (int e = lane; e < E; e += WAVE) {
     int j;
@@ -501,8 +672,7 @@ __device__ inline void lap_solve_wave(int R, int C, double L, const LapWS& w) {
     lap_edge(w, e, j, c);
     if (c < INF) atomicAdd(&w.coldeg[j], 1);
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  wave_sync_lds();
   for (int r = lane; r < R; r += WAVE) {
     int nf = 0, jj = -1;
     double cc = 0.0;
@@ -520,138 +690,112 @@ __device__ inline void lap_solve_wave(int R, int C, double L, const LapWS& w) {
       w.col4row[r] = -2;  // only inadmissible candidates: its search would end at its dummy
     }
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  // rows that still need a shortest-path search (have an edge, not fast-matched), ascending:
-  // the serial loop below then touches only those
+  wave_sync_lds();
+  // rows that still need a shortest-path search (have a finite edge, not fast-matched)
   int nroots = 0;
   for (int c = 0; c < R; c += WAVE) {
     const int r = c + lane;
-    const bool need = r < R && w.row_ptr[r + 1] > w.row_ptr[r] && w.col4row[r] == -1;
+    const bool need = r < R && w.col4row[r] == -1 && w.row_ptr[r + 1] > w.row_ptr[r];
     const unsigned long long m = __ballot(need);
     if (need) w.roots[nroots + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)r;
     nroots += __popcll(m);
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  int nsteps = 0;
+  wave_sync_lds();
+  int nsteps = 0, ncomp = 0, maxrows = 0, iters = 0;
   if (w.dbg && lane == 0) w.dbg[3] = __builtin_amdgcn_s_memtime();
-  for (int t = 0; t < nroots; t++) {
-    const int root = w.roots[t];
-    double minVal = 0.0;
-    int i = root;
-    int ntouched = 0, nsr = 0;
-    double dummy_best = INF;
-    int dummy_row = -1;
-    int sink = -1;  // >=0 real column, -2 dummy of dummy_row
+  if (nroots > 0) {
+    // component labels by min-label propagation over the roots' finite edges (coldeg reused as
+    // the per-column label)
+    for (int k = lane; k < nroots; k += WAVE) {
+      const int r = w.roots[k];
+      w.rlab[r] = r;
+      for (int e = w.row_ptr[r]; e < w.row_ptr[r + 1]; e++) {
+        int j;
+        double c;
+        lap_edge(w, e, j, c);
+        if (c < INF) w.coldeg[j] = 0x7fffffff;
+      }
+    }
+    wave_sync_lds();
     while (true) {
-      // relax row i
-      const double ui = w.u[i];
-      const int b = w.row_ptr[i], e = w.row_ptr[i + 1];
-      for (int base = b; base < e; base += WAVE) {
-        int eidx = base + lane;
-        bool newt = false;
-        int j = 0;
-        if (eidx < e) {
+      for (int k = lane; k < nroots; k += WAVE) {
+        const int r = w.roots[k], lr = w.rlab[r];
+        for (int e = w.row_ptr[r]; e < w.row_ptr[r + 1]; e++) {
+          int j;
           double c;
-          lap_edge(w, eidx, j, c);
-          if (!(w.colflag[j] & 1)) {
-            double r = minVal + (c - L) - ui - w.v[j];
-            if (r < w.spc[j]) {
-              w.spc[j] = r;
-              w.path[j] = (int16_t)i;
-              if (!(w.colflag[j] & 2)) { w.colflag[j] |= 2; newt = true; }
-            }
-          }
-        }
-        unsigned long long m = __ballot(newt);
-        if (newt) w.touched[ntouched + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)j;
-        ntouched += __popcll(m);
-      }
-      {  // dummy of row i: reduced cost 0 - u_i - 0 (its potential never moves)
-        double dv = minVal - ui;
-        if (dv < dummy_best) { dummy_best = dv; dummy_row = i; }
-      }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      // argmin over touched, not-yet-scanned columns
-      double bv = INF;
-      int bk = 0x7fffffff;
-      for (int k = lane; k < ntouched; k += WAVE) {
-        int j = w.touched[k];
-        if (!(w.colflag[j] & 1)) {
-          double s = w.spc[j];
-          if (s < bv) { bv = s; bk = k; }
+          lap_edge(w, e, j, c);
+          if (c < INF) atomicMin(&w.coldeg[j], lr);
         }
       }
-      wave_argmin(bv, bk);
-      if (dummy_best <= bv) {  // leave dummy_row unmatched (ties: stop early)
-        minVal = dummy_best;
-        sink = -2;
-        break;
+      wave_sync_lds();
+      bool changed = false;
+      for (int k = lane; k < nroots; k += WAVE) {
+        const int r = w.roots[k];
+        int m = w.rlab[r];
+        for (int e = w.row_ptr[r]; e < w.row_ptr[r + 1]; e++) {
+          int j;
+          double c;
+          lap_edge(w, e, j, c);
+          if (c < INF) m = min(m, w.coldeg[j]);
+        }
+        if (m < w.rlab[r]) { w.rlab[r] = m; changed = true; }
       }
-      const int j = w.touched[bk];
-      nsteps++;
-      minVal = bv;
-      if (lane == 0) w.colflag[j] |= 1;
-      const int r4c = w.row4col[j];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      if (r4c < 0) { sink = j; break; }
-      i = r4c;
-      if (lane == 0) w.srlist[nsr] = (uint16_t)i;
-      nsr++;
+      const bool any = __ballot(changed) != 0ull;
+      wave_sync_lds();
+      iters++;
+      if (!any) break;
     }
-    // dual updates
-    if (lane == 0) w.u[root] += minVal;
-    for (int k = lane; k < nsr; k += WAVE) {
-      int r = w.srlist[k];
-      w.u[r] += minVal - w.spc[w.col4row[r]];
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    for (int k = lane; k < ntouched; k += WAVE) {
-      int j = w.touched[k];
-      if (w.colflag[j] & 1) w.v[j] -= minVal - w.spc[j];
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // augment (lane 0; path length <= nsr + 1)
-    if (lane == 0) {
-      int j;
-      if (sink == -2) {
-        j = w.col4row[dummy_row];
-        w.col4row[dummy_row] = -1;
-        if (dummy_row == root) j = -1;
-      } else {
-        j = sink;
-      }
-      while (j >= 0) {
-        int r = w.path[j];
-        w.row4col[j] = (int16_t)r;
-        int old = w.col4row[r];
-        w.col4row[r] = (int16_t)j;
-        if (r == root) break;
-        j = old;
+    if (w.dbg && lane == 0) w.dbg[8] = __builtin_amdgcn_s_memtime();
+    // a component is headed by its smallest row (label == row); its rows are the roots carrying
+    // that label, taken in ascending order.  Small components: one lane each, in parallel.
+    bool big = false;
+    for (int k = lane; k < nroots; k += WAVE) {
+      const int h = w.roots[k];
+      if (w.rlab[h] != h) continue;
+      int nrows = 0;
+      for (int q = k; q < nroots; q++) nrows += w.rlab[w.roots[q]] == h;
+      ncomp++;
+      maxrows = max(maxrows, nrows);
+      if (nrows > LAP_LANE_ROWS) { big = true; continue; }
+      for (int q = k; q < nroots; q++) {
+        const int r = w.roots[q];
+        if (w.rlab[r] == h) nsteps += lap_root_lane(r, L, w);
       }
     }
-    // reset touched columns
-    for (int k = lane; k < ntouched; k += WAVE) {
-      int j = w.touched[k];
-      w.spc[j] = INF;
-      w.colflag[j] = 0;
+    wave_sync_lds();
+    if (w.dbg && lane == 0) w.dbg[9] = __builtin_amdgcn_s_memtime();
+    // large components: wave-parallel, one after another (components are independent)
+    if (__ballot(big) != 0ull) {
+      for (int k = 0; k < nroots; k++) {
+        const int h = w.roots[k];
+        if (w.rlab[h] != h) continue;
+        int nrows = 0;
+        for (int q = k + lane; q < nroots; q += WAVE) nrows += w.rlab[w.roots[q]] == h;
+        for (int d = 32; d >= 1; d >>= 1) nrows += __shfl_xor(nrows, d);
+        if (nrows <= LAP_LANE_ROWS) continue;
+        for (int q = k; q < nroots; q++) {
+          const int r = w.roots[q];
+          if (w.rlab[r] == h) nsteps += lap_root_wave(r, L, w);
+        }
+      }
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   }
   for (int r = lane; r < R; r += WAVE)
     if (w.col4row[r] == -2) w.col4row[r] = -1;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  wave_sync_lds();
+  for (int d = 32; d >= 1; d >>= 1) {
+    nsteps += __shfl_xor(nsteps, d);
+    ncomp += __shfl_xor(ncomp, d);
+    maxrows = max(maxrows, __shfl_xor(maxrows, d));
+  }
   if (w.dbg && lane == 0) {
     w.dbg[0] = nroots;
     w.dbg[1] = nsteps;
     w.dbg[2] = R;
+    w.dbg[4] = ncomp;
+    w.dbg[5] = maxrows;
+    w.dbg[6] = iters;
+    w.dbg[7] = __builtin_amdgcn_s_memtime();  // after labels+solve
   }
 }
 

@@ -177,11 +177,12 @@ struct Dev {
 };
 
 // Diagnostic phase stamps (build with -DBX_PHASE_TIMING; never in the shipped library).
+constexpr int BX_DBG_STRIDE = 64;  // stamps + counters per sequence
 #ifdef BX_PHASE_TIMING
 #define BX_STAMP(k)                                                                   \
   do {                                                                                \
     __syncthreads();                                                                  \
-    if (threadIdx.x == 0 && P.dbg) P.dbg[(size_t)s * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && P.dbg) P.dbg[(size_t)s * BX_DBG_STRIDE + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define BX_STAMP(k) \
@@ -201,7 +202,7 @@ constexpr int NBIN = 64;  // x-bins of the candidate sweep (one wave scans them)
 // LDS carve-out of the association kernel (host and device agree on it).
 struct LdsA {
   size_t o_dbox, o_dboxf, o_dconf, o_tboxf, o_cbox, o_bin, o_bcol, o_u, o_v, o_spc, o_ecost, o_flags, o_fid,
-      o_rowptr, o_ints, o_act, o_lost, o_unconf, o_pool, o_rtr, o_lostl, o_refind, o_newt,
+      o_rowptr, o_rlab, o_ints, o_act, o_lost, o_unconf, o_pool, o_rtr, o_lostl, o_refind, o_newt,
       o_c4r, o_srl, o_roots, o_r4c, o_path, o_touch, o_cdeg, o_hd, o_sd, o_rem, o_ecol, o_mark,
       o_colf, o_dkind, total;
   __host__ __device__ LdsA(int T, int D, int elds) {
@@ -226,6 +227,7 @@ struct LdsA {
     o_fid = take(sizeof(int) * T);
     o_rowptr = take(sizeof(int) * (T + 1));
     o_cdeg = take(4 * D);
+    o_rlab = take(4 * T);
     o_ints = take(sizeof(int) * 64);
     o_act = take(2 * T);
     o_lost = take(2 * T);
@@ -809,6 +811,7 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
   W.spc = (double*)(smem + Lo.o_spc); W.path = (int16_t*)(smem + Lo.o_path);
   W.colflag = (uint8_t*)(smem + Lo.o_colf); W.touched = (uint16_t*)(smem + Lo.o_touch);
   W.srlist = s_srl; W.coldeg = (int*)(smem + Lo.o_cdeg); W.roots = (uint16_t*)(smem + Lo.o_roots);
+  W.rlab = (int*)(smem + Lo.o_rlab);
   uint16_t* e_gcol = P.gcol + (size_t)s * T * D;
   double* e_gcost = P.gcost + (size_t)s * T * D;
   auto put_edge = [&](int e, int col, double cost) {
@@ -992,7 +995,7 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
     __syncthreads();
     BX_STAMP(stamp);
 #ifdef BX_PHASE_TIMING
-    W.dbg = (stamp == 4 && P.dbg) ? P.dbg + (size_t)s * 32 + 26 : nullptr;
+    W.dbg = (stamp == 4 && P.dbg) ? P.dbg + (size_t)s * BX_DBG_STRIDE + 26 : nullptr;
 #endif
     if (wave_id() == 0) lap_solve_wave(R, C, L, W);
     __syncthreads();
@@ -1760,8 +1763,8 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
   layout((char*)e->arena);
   d.dbg = nullptr;
 #ifdef BX_PHASE_TIMING
-  HIPCHK(hipMalloc(&d.dbg, sizeof(unsigned long long) * 32 * S));
-  HIPCHK(hipMemset(d.dbg, 0, sizeof(unsigned long long) * 32 * S));
+  HIPCHK(hipMalloc(&d.dbg, sizeof(unsigned long long) * BX_DBG_STRIDE * S));
+  HIPCHK(hipMemset(d.dbg, 0, sizeof(unsigned long long) * BX_DBG_STRIDE * S));
 #endif
   HIPCHK(hipMemset(e->arena, 0, bytes));
   e->lds_assoc = LdsA(T, D, d.elds).total;
@@ -1866,7 +1869,7 @@ int bx_engine_update_host(bx_engine* e, int seq, const float* dets, int n, const
 // diagnostic only: copy the [S][32] phase stamps of the last launch to the host
 int bx_debug_stamps_host(bx_engine* e, unsigned long long* out) {
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(out, e->dev.dbg, sizeof(unsigned long long) * 32 * e->dev.S,
+  HIPCHK(hipMemcpy(out, e->dev.dbg, sizeof(unsigned long long) * BX_DBG_STRIDE * e->dev.S,
                    hipMemcpyDeviceToHost));
   return BX_OK;
 }

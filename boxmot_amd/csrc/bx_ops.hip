@@ -126,6 +126,7 @@ __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int n
   uint8_t* colf = (uint8_t*)take(nc);
   int* cdeg = (int*)take(4 * nc);
   uint16_t* roots = (uint16_t*)take(2 * nr);
+  int* rlab = (int*)take(4 * nr);
   const int tid = threadIdx.x;
   for (int i = tid; i < nr; i += WG) {
     int cnt = 0;
@@ -151,6 +152,7 @@ __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int n
   W.elds = elds; W.col4row = c4r; W.row4col = r4c; W.u = u; W.v = v; W.spc = spc;
   W.path = path; W.colflag = colf; W.touched = touch; W.srlist = srl; W.coldeg = cdeg;
   W.roots = roots;
+  W.rlab = rlab;
   if (wave_id() == 0) lap_solve_wave(nr, nc, thr, W);
   __syncthreads();
   for (int i = tid; i < nr; i += WG) x[i] = c4r[i];
@@ -262,6 +264,7 @@ int bx_linear_assignment(const double* cost, int nr, int nc, double thresh, int3
     take(8 * nr); take(8 * nc); take(8 * nc); take(8 * e); take(4 * (nr + 1)); take(2 * nr);
     take(2 * nr); take(2 * nc); take(2 * nc); take(2 * nc); take(2 * e); take(nc); take(4 * nc);
     take(2 * nr);
+    take(4 * nr);
     return o;
   };
   while (elds > 0 && lds_for(elds) > 160 * 1024) elds /= 2;

@@ -59,7 +59,7 @@ def main():
         d, off, e = gen.frame(t)
         eng.step(d, off, e, None, out, cnt)
     torch.cuda.synchronize()
-    st = np.zeros((a.seqs, 32), np.uint64)
+    st = np.zeros((a.seqs, 64), np.uint64)
     L.bx_debug_stamps_host(eng._h, st.ctypes.data)
     st = st.astype(np.int64)
     d = np.diff(st[:, :13], axis=1)
@@ -81,6 +81,12 @@ def main():
         pre = st[:, 29] - st[:, 4]
         print(f"    assoc1 LAP init+fast path mean {pre.mean():.0f}, dijkstra mean "
               f"{(st[:, 5] - st[:, 29]).mean():.0f}")
+        print(f"    assoc1 LAP components mean {st[:, 30].mean():.1f}, max rows/component "
+              f"mean {st[:, 31].mean():.1f} max {st[:, 31].max()}, label iters mean "
+              f"{st[:, 32].mean():.1f} max {st[:, 32].max()}")
+        print(f"    assoc1 LAP labels {(st[:, 34] - st[:, 29]).mean():.0f}, lane solves "
+              f"{(st[:, 35] - st[:, 34]).mean():.0f}, rest {(st[:, 33] - st[:, 35]).mean():.0f}, "
+              f"after {(st[:, 5] - st[:, 33]).mean():.0f}")
     for k, name in enumerate(PHASES):
         print(f"  {name:18s} mean {d[:, k].mean():10.0f}  max {d[:, k].max():10.0f}  "
               f"share {d[:, k].mean() / tot.mean() * 100:5.1f}%")
