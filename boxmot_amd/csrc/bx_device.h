@@ -472,6 +472,8 @@ struct LapWS {
   int* coldeg;            // [C] finite-edge degree per column, then component labels per column
   uint16_t* roots;        // [R] rows left for the shortest-path phase, ascending
   int* rlab;              // [R] component label (smallest row index of the component)
+  int* colaux;            // [C] multi-edge rows per column (star detection)
+  int* colmin;            // [C] star components: winning row
   unsigned long long* dbg = nullptr;  // diagnostic counters (phase-timing builds only)
 };
 
@@ -655,52 +657,287 @@ __device__ __forceinline__ int lap_root_wave(int root, double L, const LapWS& w)
   return steps;
 }
 
+// Register-resident SSP for a component of m <= LAP_RM rows (ascending) and at most LAP_CM
+// columns, on one lane: the same successive-shortest-path steps as lap_root_lane, with the
+// component's columns kept sorted by column index (= the CSR edge order of every row, so the
+// relaxation and touch order are unchanged) and the argmin's ties broken by touch order.  No
+// LDS round trips on the dependent chain.  Returns false (nothing written) when the component
+// has more than LAP_CM columns.
+constexpr int LAP_RM = 3, LAP_CM = 6;
+// a[k] / a[k] = v on register arrays with a runtime k.  The per-element predicate goes through
+// an empty asm so the compiler cannot fold the select chain back into a dynamically indexed
+// (scratch-memory) array access.
+__device__ __forceinline__ bool ropaque(bool b) {
+  int x = b;
+  asm volatile("" : "+v"(x));
+  return x != 0;
+}
+template <int N, typename T>
+__device__ __forceinline__ T rsel(const T (&a)[N], int k) {
+  T r = a[0];
+#pragma unroll
+  for (int q = 1; q < N; q++) r = ropaque(q == k) ? a[q] : r;
+  return r;
+}
+template <int N, typename T>
+__device__ __forceinline__ void rput(T (&a)[N], int k, T v) {
+#pragma unroll
+  for (int q = 0; q < N; q++) a[q] = ropaque(q == k) ? v : a[q];
+}
+__device__ __forceinline__ bool lap_component_regs(const int (&rr)[LAP_RM], int m, double L,
+                                                   const LapWS& w, int& steps) {
+  constexpr int RM = LAP_RM, CM = LAP_CM;
+  int cols[CM];
+#pragma unroll
+  for (int q = 0; q < CM; q++) cols[q] = 0x7fffffff;
+  int nc = 0;
+  bool over = false;
+#pragma unroll
+  for (int q = 0; q < RM; q++) {
+    if (q >= m) break;
+    for (int e = w.row_ptr[rr[q]]; e < w.row_ptr[rr[q] + 1]; e++) {
+      int j;
+      double c;
+      lap_edge(w, e, j, c);
+      if (!(c < INF)) continue;
+      bool found = false;
+#pragma unroll
+      for (int t = 0; t < CM; t++) found |= cols[t] == j;
+      if (found) continue;
+      if (nc == CM) { over = true; continue; }
+      rput(cols, nc, j);
+      nc++;
+    }
+  }
+  if (over) return false;
+  // sort the column slots ascending (odd-even transposition network; empty slots = INT_MAX)
+#pragma unroll
+  for (int rd = 0; rd < CM; rd++)
+#pragma unroll
+    for (int t = rd & 1; t + 1 < CM; t += 2)
+      if (cols[t] > cols[t + 1]) { const int x = cols[t]; cols[t] = cols[t + 1]; cols[t + 1] = x; }
+  double cm[RM][CM];
+#pragma unroll
+  for (int q = 0; q < RM; q++)
+#pragma unroll
+    for (int t = 0; t < CM; t++) cm[q][t] = INF;
+#pragma unroll
+  for (int q = 0; q < RM; q++) {
+    if (q >= m) break;
+    for (int e = w.row_ptr[rr[q]]; e < w.row_ptr[rr[q] + 1]; e++) {
+      int j;
+      double c;
+      lap_edge(w, e, j, c);
+      if (!(c < INF)) continue;
+#pragma unroll
+      for (int t = 0; t < CM; t++)
+        if (cols[t] == j) cm[q][t] = c;
+    }
+  }
+  double u[RM], v[CM];
+  int c4r[RM], r4c[CM];
+#pragma unroll
+  for (int q = 0; q < RM; q++) { u[q] = 0.0; c4r[q] = -1; }
+#pragma unroll
+  for (int t = 0; t < CM; t++) { v[t] = 0.0; r4c[t] = -1; }
+#pragma unroll 1
+  for (int q0 = 0; q0 < m; q0++) {
+    double spc[CM];
+    int path[CM], rank[CM];
+    bool scanned[CM], touched[CM];
+#pragma unroll
+    for (int t = 0; t < CM; t++) {
+      spc[t] = INF; path[t] = -1; rank[t] = 0; scanned[t] = false; touched[t] = false;
+    }
+    double minVal = 0.0, dummy_best = INF;
+    int i = q0, dummy_row = -1, sink = -1, cnt = 0;
+    unsigned srmask = 0;
+    for (int it = 0; it <= RM; it++) {
+      const double ui = rsel(u, i);
+#pragma unroll
+      for (int t = 0; t < CM; t++) {
+        double c = cm[0][t];
+#pragma unroll
+        for (int q = 1; q < RM; q++) c = ropaque(q == i) ? cm[q][t] : c;
+        if (!(c < INF) || scanned[t]) continue;
+        const double r = minVal + (c - L) - ui - v[t];
+        if (r < spc[t]) {
+          spc[t] = r;
+          path[t] = i;
+          if (!touched[t]) { touched[t] = true; rank[t] = cnt++; }
+        }
+      }
+      const double dv = minVal - ui;
+      if (dv < dummy_best) { dummy_best = dv; dummy_row = i; }
+      double bv = INF;
+      int bs = -1, br = 0x7fffffff;
+#pragma unroll
+      for (int t = 0; t < CM; t++)
+        if (touched[t] && !scanned[t] && (spc[t] < bv || (spc[t] == bv && rank[t] < br))) {
+          bv = spc[t]; bs = t; br = rank[t];
+        }
+      if (dummy_best <= bv) { minVal = dummy_best; sink = -2; break; }
+      minVal = bv;
+      steps++;
+      rput(scanned, bs, true);
+      const int r4 = rsel(r4c, bs);
+      if (r4 < 0) { sink = bs; break; }
+      i = r4;
+      srmask |= 1u << i;
+    }
+    // dual updates (u of the root and of the visited rows; v of the scanned columns)
+#pragma unroll
+    for (int q = 0; q < RM; q++) {
+      if (ropaque(q == q0)) u[q] += minVal;
+      else if ((srmask >> q) & 1u) u[q] += minVal - rsel(spc, c4r[q]);
+    }
+#pragma unroll
+    for (int t = 0; t < CM; t++)
+      if (scanned[t]) v[t] -= minVal - spc[t];
+    // augment
+    int j;
+    if (sink == -2) {
+      j = rsel(c4r, dummy_row);
+      rput(c4r, dummy_row, -1);
+      if (dummy_row == q0) j = -1;
+    } else {
+      j = sink;
+    }
+    for (int it = 0; it <= RM && j >= 0; it++) {
+      const int r = rsel(path, j);
+      rput(r4c, j, r);
+      const int old = rsel(c4r, r);
+      rput(c4r, r, j);
+      if (r == q0) break;
+      j = old;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < RM; q++)
+    if (q < m) w.col4row[rr[q]] = (int16_t)(c4r[q] >= 0 ? rsel(cols, c4r[q]) : -1);
+#pragma unroll
+  for (int t = 0; t < CM; t++)
+    if (t < nc) w.row4col[cols[t]] = (int16_t)(r4c[t] >= 0 ? rsel(rr, r4c[t]) : -1);
+  return true;
+}
+
 constexpr int LAP_LANE_ROWS = 16;  // components up to this many rows are solved by one lane
 
-// Called by all 64 lanes of one wave.  R rows, C columns, limit L.
-__device__ __forceinline__ void lap_solve_wave(int R, int C, double L, const LapWS& w) {
-  const int lane = lane_id();
-  for (int k = lane; k < R; k += WAVE) { w.col4row[k] = -1; w.u[k] = 0.0; }
-  for (int k = lane; k < C; k += WAVE) {
+// Preparation, called by ALL threads of the workgroup (block-wide syncs): initialise, settle
+// single-edge and star components, and list the rows left for the searches (ascending) in
+// w.roots.  Returns that count (uniform).  `scan_tmp`: >= 4 ints of LDS for block_compact.
+__device__ __forceinline__ int lap_prepare_block(int R, int C, double L, const LapWS& w,
+                                                 int* scan_tmp) {
+  const int tid = threadIdx.x;
+  for (int k = tid; k < R; k += WG) { w.col4row[k] = -1; w.u[k] = 0.0; }
+  for (int k = tid; k < C; k += WG) {
     w.row4col[k] = -1; w.v[k] = 0.0; w.spc[k] = INF; w.colflag[k] = 0; w.coldeg[k] = 0;
+    w.colaux[k] = 0;
   }
-  wave_sync_lds();
-  const int E = w.row_ptr[R];
-  for (int e = lane; e < E; e += WAVE) {
-    int j;
-    double c;
-    lap_edge(w, e, j, c);
-    if (c < INF) atomicAdd(&w.coldeg[j], 1);
-  }
-  wave_sync_lds();
-  for (int r = lane; r < R; r += WAVE) {
-    int nf = 0, jj = -1;
-    double cc = 0.0;
+  __syncthreads();
+  auto row_scan = [&](int r, int& nf, int& jj, double& cc) {
+    nf = 0; jj = -1; cc = 0.0;
     for (int e = w.row_ptr[r]; e < w.row_ptr[r + 1]; e++) {
       int j;
       double c;
       lap_edge(w, e, j, c);
       if (c < INF) { nf++; jj = j; cc = c; }
     }
+  };
+  // finite-edge degree per column, and per column the rows with >= 2 finite edges
+  for (int r = tid; r < R; r += WG) {
+    int nf, jj;
+    double cc;
+    row_scan(r, nf, jj, cc);
+    if (nf == 0) continue;
+    for (int e = w.row_ptr[r]; e < w.row_ptr[r + 1]; e++) {
+      int j;
+      double c;
+      lap_edge(w, e, j, c);
+      if (!(c < INF)) continue;
+      atomicAdd(&w.coldeg[j], 1);
+      if (nf >= 2) atomicAdd(&w.colaux[j], 1);
+    }
+  }
+  __syncthreads();
+  // Single-edge components (a row whose only finite edge goes to a column no other row can
+  // reach) are matched directly: that is exactly the path SSP would find for them (gain L-c>0,
+  // potentials u = c-L, v = 0), and no other row can ever touch that row or column.
+  // A "star" component — one column whose every finite-edge row has no other finite edge — is
+  // also settled directly: rows taken in ascending order, a later row takes the column from
+  // its holder iff strictly cheaper (its search scans the column, then the holder's dummy wins
+  // exactly when c_new < c_holder), so the column ends with the cheapest row, ties to the
+  // smallest row index, and every other row unmatched.
+  auto okey = [](double c) {  // order-preserving double → u64
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, c);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+  };
+  unsigned long long* keyslot = (unsigned long long*)w.spc;  // spc is INF outside searches
+  int nstar = 0;
+  for (int r = tid; r < R; r += WG) {
+    int nf, jj;
+    double cc;
+    row_scan(r, nf, jj, cc);
     if (nf == 1 && w.coldeg[jj] == 1) {
       w.col4row[r] = (int16_t)jj;
       w.row4col[jj] = (int16_t)r;
       w.u[r] = cc - L;
+    } else if (nf == 1 && w.colaux[jj] == 0) {
+      keyslot[jj] = ~0ull;
+      w.colmin[jj] = 0x7fffffff;
+      nstar++;
     } else if (nf == 0) {
       w.col4row[r] = -2;  // only inadmissible candidates: its search would end at its dummy
     }
   }
-  wave_sync_lds();
-  // rows that still need a shortest-path search (have a finite edge, not fast-matched)
-  int nroots = 0;
-  for (int c = 0; c < R; c += WAVE) {
-    const int r = c + lane;
-    const bool need = r < R && w.col4row[r] == -1 && w.row_ptr[r + 1] > w.row_ptr[r];
-    const unsigned long long m = __ballot(need);
-    if (need) w.roots[nroots + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)r;
-    nroots += __popcll(m);
+  int tot;
+  block_scan_flag(nstar > 0, scan_tmp, tot);  // (also a block barrier)
+  if (tot) {
+    auto star = [&](int r, int& jj, double& cc) {
+      int nf;
+      row_scan(r, nf, jj, cc);
+      return nf == 1 && w.coldeg[jj] > 1 && w.colaux[jj] == 0;
+    };
+    for (int r = tid; r < R; r += WG) {
+      int jj;
+      double cc;
+      if (star(r, jj, cc)) atomicMin(&keyslot[jj], okey(cc));
+    }
+    __syncthreads();
+    for (int r = tid; r < R; r += WG) {
+      int jj;
+      double cc;
+      if (star(r, jj, cc) && okey(cc) == keyslot[jj]) atomicMin(&w.colmin[jj], r);
+    }
+    __syncthreads();
+    for (int r = tid; r < R; r += WG) {
+      int jj;
+      double cc;
+      if (!star(r, jj, cc)) continue;
+      if (w.colmin[jj] == r) {
+        w.col4row[r] = (int16_t)jj;
+        w.row4col[jj] = (int16_t)r;
+      } else {
+        w.col4row[r] = -2;  // settled unmatched
+      }
+    }
+    __syncthreads();
+    for (int r = tid; r < R; r += WG) {  // give the star columns back their INF
+      int jj;
+      double cc;
+      if (star(r, jj, cc)) w.spc[jj] = INF;
+    }
+    __syncthreads();
   }
-  wave_sync_lds();
+  // rows that still need a shortest-path search (have a finite edge, not settled), ascending
+  return block_compact(
+      R, [&](int r) { return w.col4row[r] == -1 && w.row_ptr[r + 1] > w.row_ptr[r]; },
+      [&](int r, int p) { w.roots[p] = (uint16_t)r; }, scan_tmp);
+}
+
+// The searches, called by all 64 lanes of ONE wave after lap_prepare_block.
+__device__ __forceinline__ void lap_solve_roots_wave(int R, int nroots, double L, const LapWS& w) {
+  const int lane = lane_id();
   int nsteps = 0, ncomp = 0, maxrows = 0, iters = 0;
   if (w.dbg && lane == 0) w.dbg[3] = __builtin_amdgcn_s_memtime();
   if (nroots > 0) {
@@ -757,6 +994,17 @@ __device__ __forceinline__ void lap_solve_wave(int R, int C, double L, const Lap
       ncomp++;
       maxrows = max(maxrows, nrows);
       if (nrows > LAP_LANE_ROWS) { big = true; continue; }
+      if (nrows <= LAP_RM) {  // register-resident solve when it fits
+        int rr[LAP_RM];
+        int n = 0;
+#pragma unroll
+        for (int t = 0; t < LAP_RM; t++) rr[t] = h;
+        for (int q = k; q < nroots && n < nrows; q++) {
+          const int r = w.roots[q];
+          if (w.rlab[r] == h) { rput(rr, n, r); n++; }
+        }
+        if (lap_component_regs(rr, nrows, L, w, nsteps)) continue;
+      }
       for (int q = k; q < nroots; q++) {
         const int r = w.roots[q];
         if (w.rlab[r] == h) nsteps += lap_root_lane(r, L, w);
@@ -797,6 +1045,14 @@ __device__ __forceinline__ void lap_solve_wave(int R, int C, double L, const Lap
     w.dbg[6] = iters;
     w.dbg[7] = __builtin_amdgcn_s_memtime();  // after labels+solve
   }
+}
+
+// Whole solve, called by ALL threads of the workgroup.
+__device__ __forceinline__ void lap_solve_block(int R, int C, double L, const LapWS& w,
+                                                int* scan_tmp) {
+  const int nroots = lap_prepare_block(R, C, L, w, scan_tmp);
+  if (wave_id() == 0) lap_solve_roots_wave(R, nroots, L, w);
+  __syncthreads();
 }
 
 }  // namespace bx

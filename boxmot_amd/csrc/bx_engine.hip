@@ -202,7 +202,7 @@ constexpr int NBIN = 64;  // x-bins of the candidate sweep (one wave scans them)
 // LDS carve-out of the association kernel (host and device agree on it).
 struct LdsA {
   size_t o_dbox, o_dboxf, o_dconf, o_tboxf, o_cbox, o_bin, o_bcol, o_u, o_v, o_spc, o_ecost, o_flags, o_fid,
-      o_rowptr, o_rlab, o_ints, o_act, o_lost, o_unconf, o_pool, o_rtr, o_lostl, o_refind, o_newt,
+      o_rowptr, o_rlab, o_colaux, o_colmin, o_ints, o_act, o_lost, o_unconf, o_pool, o_rtr, o_lostl, o_refind, o_newt,
       o_c4r, o_srl, o_roots, o_r4c, o_path, o_touch, o_cdeg, o_hd, o_sd, o_rem, o_ecol, o_mark,
       o_colf, o_dkind, total;
   __host__ __device__ LdsA(int T, int D, int elds) {
@@ -228,6 +228,8 @@ struct LdsA {
     o_rowptr = take(sizeof(int) * (T + 1));
     o_cdeg = take(4 * D);
     o_rlab = take(4 * T);
+    o_colaux = take(4 * D);
+    o_colmin = take(4 * D);
     o_ints = take(sizeof(int) * 64);
     o_act = take(2 * T);
     o_lost = take(2 * T);
@@ -812,6 +814,8 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
   W.colflag = (uint8_t*)(smem + Lo.o_colf); W.touched = (uint16_t*)(smem + Lo.o_touch);
   W.srlist = s_srl; W.coldeg = (int*)(smem + Lo.o_cdeg); W.roots = (uint16_t*)(smem + Lo.o_roots);
   W.rlab = (int*)(smem + Lo.o_rlab);
+  W.colaux = (int*)(smem + Lo.o_colaux);
+  W.colmin = (int*)(smem + Lo.o_colmin);
   uint16_t* e_gcol = P.gcol + (size_t)s * T * D;
   double* e_gcost = P.gcost + (size_t)s * T * D;
   auto put_edge = [&](int e, int col, double cost) {
@@ -997,7 +1001,7 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
 #ifdef BX_PHASE_TIMING
     W.dbg = (stamp == 4 && P.dbg) ? P.dbg + (size_t)s * BX_DBG_STRIDE + 26 : nullptr;
 #endif
-    if (wave_id() == 0) lap_solve_wave(R, C, L, W);
+    lap_solve_block(R, C, L, W, scan_tmp);
     __syncthreads();
   };
 
@@ -1022,46 +1026,57 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
         scan_tmp);
   };
 
-  // ---------------- P4/P5: first association: pool x high dets
-  BX_STAMP(3);
-  associate(s_pool, npool, s_hd, Dh, P.match_thresh, KIND == KIND_BYTE ? 1 : 2, 4);
-  BX_STAMP(5);
-  record_matches(s_pool, npool, s_hd, REID, true);
-  const int nref = block_compact(npool, [&](int k) { return (s_mark[s_pool[k]] & M_TMP) != 0; },
-                                 [&](int k, int p) { s_refind[p] = s_pool[k]; }, scan_tmp);
-  // remaining high dets (u_detection, ascending) — saved before the next solve reuses r4c
-  const int nrem = block_compact(Dh, [&](int j) { return s_r4c[j] < 0; },
-                                 [&](int j, int p) { s_rem[p] = s_hd[j]; }, scan_tmp);
-  for (int k = tid; k < nref; k += WG) s_mark[s_refind[k]] &= ~M_TMP;
-  // r_tracked = unmatched pool rows still Tracked
-  const int nrtr = block_compact(
-      npool, [&](int k) { return s_c4r[k] < 0 && st_of(s_flags[s_pool[k]]) == ST_TRACKED; },
-      [&](int k, int p) { s_rtr[p] = s_pool[k]; }, scan_tmp);
-
-  BX_STAMP(6);
-  // ---------------- P7: second association: r_tracked x low-confidence dets (IoU, 0.5)
-  associate(s_rtr, nrtr, s_sd, Ds, 0.5, 0, 7);
-  record_matches(s_rtr, nrtr, s_sd, false, false);  // second dets carry no features
-  const int nlostl = block_compact(
-      nrtr, [&](int k) { return s_c4r[k] < 0; },
-      [&](int k, int p) {
-        const int slot = s_rtr[k];
-        s_lostl[p] = (uint16_t)slot;
-        s_flags[slot] = (s_flags[slot] & ~F_STATE) | ST_LOST;  // mark_lost
-      },
-      scan_tmp);
-
-  // ---------------- P8: unconfirmed x remaining high dets (fused, 0.7)
-  BX_STAMP(8);
-  associate(s_unconf, nun, s_rem, nrem, 0.7, KIND == KIND_BYTE ? 1 : 3, 9);
-  BX_STAMP(10);
-  for (int i = tid; i < nun; i += WG) {
-    if (s_c4r[i] >= 0) continue;
-    const int slot = s_unconf[i];
-    s_flags[slot] = (s_flags[slot] & ~F_STATE) | ST_REMOVED;  // mark_removed
-    s_mark[slot] |= M_REMNOW;
+  // ---------------- P4..P8: the three associations (bytetrack.py:199-276, botsort.py:198-366)
+  //   0: strack_pool x high dets (fused / BoT first association), match_thresh
+  //   1: r_tracked x low-confidence dets, IoU, 0.5
+  //   2: unconfirmed x remaining high dets (fused), 0.7
+  // as ONE loop, so the candidate build and the solver exist once in the kernel's code
+  int nref = 0, nrem = 0, nrtr = 0, nlostl = 0;
+  for (int stage = 0; stage < 3; stage++) {
+    const uint16_t* rows = stage == 0 ? s_pool : stage == 1 ? s_rtr : s_unconf;
+    const int R = stage == 0 ? npool : stage == 1 ? nrtr : nun;
+    const uint16_t* cols = stage == 0 ? s_hd : stage == 1 ? s_sd : s_rem;
+    const int C = stage == 0 ? Dh : stage == 1 ? Ds : nrem;
+    const double L = stage == 0 ? P.match_thresh : stage == 1 ? 0.5 : 0.7;
+    const int mode = stage == 1 ? 0 : KIND == KIND_BYTE ? 1 : stage == 0 ? 2 : 3;
+    if (stage == 0) BX_STAMP(3);
+    if (stage == 1) BX_STAMP(6);
+    if (stage == 2) BX_STAMP(8);
+    associate(rows, R, cols, C, L, mode, stage == 0 ? 4 : stage == 1 ? 7 : 9);
+    if (stage == 0) BX_STAMP(5);
+    if (stage == 2) {
+      BX_STAMP(10);
+      for (int i = tid; i < nun; i += WG) {
+        if (s_c4r[i] >= 0) continue;
+        const int slot = s_unconf[i];
+        s_flags[slot] = (s_flags[slot] & ~F_STATE) | ST_REMOVED;  // mark_removed
+        s_mark[slot] |= M_REMNOW;
+      }
+    }
+    // second-stage dets carry no features
+    record_matches(rows, R, cols, REID && stage != 1, stage == 0);
+    if (stage == 0) {
+      nref = block_compact(npool, [&](int k) { return (s_mark[s_pool[k]] & M_TMP) != 0; },
+                           [&](int k, int p) { s_refind[p] = s_pool[k]; }, scan_tmp);
+      // remaining high dets (u_detection, ascending) — saved before the next solve reuses r4c
+      nrem = block_compact(Dh, [&](int j) { return s_r4c[j] < 0; },
+                           [&](int j, int p) { s_rem[p] = s_hd[j]; }, scan_tmp);
+      for (int k = tid; k < nref; k += WG) s_mark[s_refind[k]] &= ~M_TMP;
+      // r_tracked = unmatched pool rows still Tracked
+      nrtr = block_compact(
+          npool, [&](int k) { return s_c4r[k] < 0 && st_of(s_flags[s_pool[k]]) == ST_TRACKED; },
+          [&](int k, int p) { s_rtr[p] = s_pool[k]; }, scan_tmp);
+    } else if (stage == 1) {
+      nlostl = block_compact(
+          nrtr, [&](int k) { return s_c4r[k] < 0; },
+          [&](int k, int p) {
+            const int slot = s_rtr[k];
+            s_lostl[p] = (uint16_t)slot;
+            s_flags[slot] = (s_flags[slot] & ~F_STATE) | ST_LOST;  // mark_lost
+          },
+          scan_tmp);
+    }
   }
-  record_matches(s_unconf, nun, s_rem, REID, false);
 
   // ---------------- P9: new tracks from the detections left over (conf >= det/new thresh)
   const int nnew = block_compact(

@@ -127,6 +127,9 @@ __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int n
   int* cdeg = (int*)take(4 * nc);
   uint16_t* roots = (uint16_t*)take(2 * nr);
   int* rlab = (int*)take(4 * nr);
+  int* caux = (int*)take(4 * nc);
+  int* cmin = (int*)take(4 * nc);
+  int* scan_tmp = (int*)take(4 * 8);
   const int tid = threadIdx.x;
   for (int i = tid; i < nr; i += WG) {
     int cnt = 0;
@@ -153,8 +156,9 @@ __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int n
   W.path = path; W.colflag = colf; W.touched = touch; W.srlist = srl; W.coldeg = cdeg;
   W.roots = roots;
   W.rlab = rlab;
-  if (wave_id() == 0) lap_solve_wave(nr, nc, thr, W);
-  __syncthreads();
+  W.colaux = caux;
+  W.colmin = cmin;
+  lap_solve_block(nr, nc, thr, W, scan_tmp);
   for (int i = tid; i < nr; i += WG) x[i] = c4r[i];
   for (int j = tid; j < nc; j += WG) y[j] = r4c[j];
 }
@@ -265,6 +269,9 @@ int bx_linear_assignment(const double* cost, int nr, int nc, double thresh, int3
     take(2 * nr); take(2 * nc); take(2 * nc); take(2 * nc); take(2 * e); take(nc); take(4 * nc);
     take(2 * nr);
     take(4 * nr);
+    take(4 * nc);
+    take(4 * nc);
+    take(4 * 8);
     return o;
   };
   while (elds > 0 && lds_for(elds) > 160 * 1024) elds /= 2;

@@ -154,6 +154,30 @@ def test_linear_assignment_random_vs_oracle(torch_cuda, shape):
         np.testing.assert_array_equal(gub, oub)
 
 
+@pytest.mark.parametrize("shape,density", [((64, 64), 0.02), ((256, 128), 0.01),
+                                           ((256, 128), 0.03), ((128, 256), 0.02),
+                                           ((200, 200), 0.008)])
+def test_linear_assignment_sparse_components_vs_oracle(torch_cuda, shape, density):
+    """Sparse candidate graphs like the trackers' (many single-edge rows, stars — several
+    rows on one column — and small multi-edge components) against the oracle's dense solver."""
+    rng = np.random.default_rng(int(density * 1e4) + shape[0])
+    for rep in range(6):
+        thr = 0.8
+        c = np.ones(shape)
+        mask = rng.uniform(size=shape) < density
+        # stars: a few columns shared by several single-edge rows
+        for j in rng.choice(shape[1], size=max(1, shape[1] // 16), replace=False):
+            rows = rng.choice(shape[0], size=rng.integers(2, 5), replace=False)
+            mask[rows, :] = False
+            mask[rows, j] = True
+        c[mask] = rng.uniform(0, thr, mask.sum())
+        om, oua, oub = po.linear_assignment(c, thr)
+        gm, gua, gub = gpu_linear_assignment(torch_cuda, c, thr)
+        np.testing.assert_array_equal(gm, om)
+        np.testing.assert_array_equal(gua, oua)
+        np.testing.assert_array_equal(gub, oub)
+
+
 def test_linear_assignment_empty(torch_cuda):
     for shape in [(0, 4), (4, 0)]:
         m, ua, ub = gpu_linear_assignment(torch_cuda, np.zeros(shape), 0.5)
