@@ -72,7 +72,12 @@ struct RegRow {
     double s = 0.0;
 #pragma unroll
     for (int r = 0; r < REG_EPL; r++)
-      if (lane + 64 * r < F) { double d = (double)v[r]; s += d * d; }
+      if (lane + 64 * r < F) {
+        const double d = (double)v[r];
+        // a float's square is exact in fp64, so the fused form rounds identically to s + d*d
+        if constexpr (sizeof(FT) == 4) s = __builtin_fma(d, d, s);
+        else s += d * d;
+      }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
     if constexpr (sizeof(FT) == 4) return sqrtf((float)s);
@@ -314,8 +319,9 @@ __device__ __forceinline__ void det_measurement(const float* r, double* meas) {
 // float32 norm dn of (float)f2 that embedding_distance scales the det row by (matching.py:
 // 266-287).  Only the three norms are stored: every later use (K1c's cosine rows, K5's EMA)
 // recomputes f2 = (f / n1) / n2 elementwise from the input row, bit-identically.
-// Grid (n_seq, ceil(D/64)); each wave walks 16 detections of its block's 64, the next row's
-// load in flight while the current one is normalised.
+// Grid (n_seq, ceil(D/K1_DETS)); each wave walks its block's detections with stride 4, the
+// next row's load in flight while the current one is normalised.
+constexpr int K1_DETS = 8;  // detections per K1 block: 4 per wave keeps ~8 waves per SIMD busy
 template <typename FT, bool NPF>
 __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
                                                          const float* __restrict__ dets,
@@ -325,7 +331,7 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
   const int b = blockIdx.x, s = seq0 + b, w = wave_id(), lane = lane_id();
   const int F = P.F, D = P.D;
   const int d0 = det_off[b], N = min(det_off[b + 1] - d0, D);
-  const int k0 = blockIdx.y * 64, k1 = min(k0 + 64, N);
+  const int k0 = blockIdx.y * K1_DETS, k1 = min(k0 + K1_DETS, N);
   if (k0 >= N) return;  // block-uniform
   __shared__ unsigned long long s_hi;  // bit k - k0: detection k is high
   if (w == 0) {
@@ -517,11 +523,12 @@ __global__ __launch_bounds__(WG) void cosine_kernel(Dev P, int seq0, const int* 
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int q = 0; q < COS_CH; q += 2) {
+        // products of two floats are exact in fp64: fma rounds identically to acc + x*y
         const double x0 = (double)s_a[w][lane][q], x1 = (double)s_a[w][lane][q + 1];
         const double y0 = (double)s_b[w][lane][q], y1 = (double)s_b[w][lane][q + 1];
-        ab0 += x0 * y0; ab1 += x1 * y1;
-        aa0 += x0 * x0; aa1 += x1 * x1;
-        bb0 += y0 * y0; bb1 += y1 * y1;
+        ab0 = __builtin_fma(x0, y0, ab0); ab1 = __builtin_fma(x1, y1, ab1);
+        aa0 = __builtin_fma(x0, x0, aa0); aa1 = __builtin_fma(x1, x1, aa1);
+        bb0 = __builtin_fma(y0, y0, bb0); bb1 = __builtin_fma(y1, y1, bb1);
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -1334,7 +1341,7 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
 // new smooth_feat's numpy float32 norm (embedding_distance's track-side scale) is refreshed here,
 // while the row is in registers, for the next frame's K1c.  Grid (n_seq, FEAT_BLOCKS); one wave
 // per record.
-constexpr int FEAT_BLOCKS = 8;
+constexpr int FEAT_BLOCKS = 16;
 template <typename FT, bool NPF>
 __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
                                                      const int* __restrict__ det_off,
@@ -1631,7 +1638,7 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
     HIPCHK(hipGetLastError());                             \
     if (int rc_ = probe_end(stage)) return rc_;            \
   } while (0)
-  const int gy_det64 = (d.D + 63) / 64, gy_slot = (d.T + WG - 1) / WG;
+  const int gy_det64 = (d.D + K1_DETS - 1) / K1_DETS, gy_slot = (d.T + WG - 1) / WG;
   if (reid)
     BX_PROBED(BX_STAGE_DET_FEATURES,
               hipLaunchKernelGGL((det_feature_kernel<FT, NPF>), dim3(nseq, gy_det64), dim3(WG), 0,
