@@ -63,6 +63,19 @@ int bxo_id_count(const bxo_tracker *t);
 int bxo_frame_count(const bxo_tracker *t);
 void bxo_free(bxo_tracker *t);
 
+/* ----------------------------------------------------------------------------------------- */
+/* OCSort (trackers/ocsort/ocsort.py:195-439; XYSR KF xysr_kf.py; association.py) with the     */
+/* minimal patches P1-P5 of SURVEY.md Appendix A (see bxo_ocsort.c).                          */
+typedef struct bxo_ocsort bxo_ocsort;
+bxo_ocsort *bxo_ocsort_new(double min_conf, double det_thresh, int max_age, int min_hits,
+                           double asso_threshold, int delta_t, double inertia, int use_byte,
+                           double q_xy_scaling, double q_s_scaling);
+void bxo_ocsort_free(bxo_ocsort *o);
+int bxo_ocsort_id_count(bxo_ocsort *o);
+/* dets[n,6] float64 (float32-rounded); out[M,8]; returns M or -2 if out_cap is too small */
+int bxo_ocsort_update(bxo_ocsort *o, const double *dets, int n, double *out, int out_cap);
+double bxo_acos(double x);
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,6 +59,14 @@ def lib():
         L.bxo_id_count.argtypes = [C.c_void_p]
         L.bxo_frame_count.argtypes = [C.c_void_p]
         L.bxo_free.argtypes = [C.c_void_p]
+        L.bxo_ocsort_new.argtypes = [C.c_double, C.c_double, C.c_int, C.c_int, C.c_double,
+                                     C.c_int, C.c_double, C.c_int, C.c_double, C.c_double]
+        L.bxo_ocsort_new.restype = C.c_void_p
+        L.bxo_ocsort_free.argtypes = [C.c_void_p]
+        L.bxo_ocsort_id_count.argtypes = [C.c_void_p]
+        L.bxo_ocsort_update.argtypes = [C.c_void_p, _dp, C.c_int, _dp, C.c_int]
+        L.bxo_acos.argtypes = [C.c_double]
+        L.bxo_acos.restype = C.c_double
         _lib = L
     return _lib
 
@@ -156,6 +164,14 @@ class OracleTracker:
                 p.get("match_thresh", 0.8), p.get("proximity_thresh", 0.5),
                 p.get("appearance_thresh", 0.25), int(p.get("frame_rate", 30)),
                 int(bool(p.get("fuse_first_associate", False))), int(bool(p.get("with_reid", True))))
+        elif kind == "ocsort":  # YAML defaults (configs/trackers/ocsort.yaml)
+            self.h = L.bxo_ocsort_new(
+                p.get("min_conf", 0.1), p.get("det_thresh", 0.6), int(p.get("max_age", 30)),
+                int(p.get("min_hits", 3)), p.get("asso_threshold", 0.3), int(p.get("delta_t", 3)),
+                p.get("inertia", 0.1), int(bool(p.get("use_byte", False))),
+                p.get("Q_xy_scaling", 0.01), p.get("Q_s_scaling", 0.0001))
+            if p.get("asso_func", "iou") != "iou":
+                raise NotImplementedError("oracle OCSort: asso_func 'iou' only")
         else:
             raise KeyError(kind)
         self._cap = 1024
@@ -172,6 +188,15 @@ class OracleTracker:
                 embs = embs.astype(np.float32, copy=False)
             f = embs.shape[1]
             e_ptr = embs.ctypes.data_as(C.c_void_p)
+        if self.kind == "ocsort":
+            # BaseTracker.setup_decorator rounds dets to float32 (basetracker.py:122-128)
+            d32 = np.ascontiguousarray(dets.astype(np.float32).astype(np.float64))
+            cap = max(self._cap, 2 * n + 64)
+            out = np.zeros((cap, 8))
+            m = lib().bxo_ocsort_update(self.h, _d(d32), n, _d(out), cap)
+            if m < 0:
+                raise RuntimeError(f"oracle update failed ({m})")
+            return out[:m].copy()
         w = None if warp is None else _d(np.ascontiguousarray(warp, np.float64).reshape(6))
         while True:
             cap = max(self._cap, n + 16)
@@ -185,12 +210,14 @@ class OracleTracker:
 
     @property
     def id_count(self):
+        if self.kind == "ocsort":
+            return lib().bxo_ocsort_id_count(self.h)
         return lib().bxo_id_count(self.h)
 
     def __del__(self):
         h = getattr(self, "h", None)
         if h:
-            lib().bxo_free(h)
+            (lib().bxo_ocsort_free if self.kind == "ocsort" else lib().bxo_free)(h)
             self.h = None
 
 
