@@ -17,13 +17,14 @@ CSRC = PKG / "csrc"
 LIB_DIR = PKG / "lib"
 LIB_PATH = LIB_DIR / "libbxassoc.so"
 HEADER = REPO / "include" / "bxassoc.h"
+HEADER_OCS = REPO / "include" / "bxocsort.h"
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
     # numpy-identical rounding: no FMA contraction, IEEE f32 division/sqrt
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
 ]
-SOURCES = ["bx_engine.hip", "bx_ops.hip"]
+SOURCES = ["bx_engine.hip", "bx_ops.hip", "bx_ocsort.hip"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -32,7 +33,7 @@ class NativeUnavailable(RuntimeError):
 
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the HIP extension for gfx950 in-tree (boxmot_amd/lib/libbxassoc.so)."""
-    srcs = [CSRC / s for s in SOURCES] + [CSRC / "bx_device.h", HEADER]
+    srcs = [CSRC / s for s in SOURCES] + [CSRC / "bx_device.h", HEADER, HEADER_OCS]
     if not force and LIB_PATH.exists():
         t = LIB_PATH.stat().st_mtime
         if all(s.stat().st_mtime <= t for s in srcs):
@@ -63,7 +64,17 @@ class BxConfig(C.Structure):
     ]
 
 
-# every symbol include/bxassoc.h declares (checked by tests/test_native_abi.py)
+class BxOcsortConfig(C.Structure):
+    _fields_ = [
+        ("n_seq", C.c_int32), ("track_cap", C.c_int32), ("det_cap", C.c_int32),
+        ("min_conf", C.c_double), ("det_thresh", C.c_double), ("asso_threshold", C.c_double),
+        ("inertia", C.c_double), ("q_xy_scaling", C.c_double), ("q_s_scaling", C.c_double),
+        ("max_age", C.c_int32), ("min_hits", C.c_int32), ("delta_t", C.c_int32),
+        ("use_byte", C.c_int32),
+    ]
+
+
+# every symbol include/bxassoc.h and include/bxocsort.h declare (checked by tests/test_native_abi.py)
 EXPORTS = [
     "bx_last_error", "bx_device_count", "bx_engine_create", "bx_engine_destroy",
     "bx_engine_reset", "bx_engine_step", "bx_engine_update_host", "bx_engine_status",
@@ -71,6 +82,9 @@ EXPORTS = [
     "bx_engine_probe", "bx_engine_probe_read", "bx_engine_frame_stats_host",
     "bx_iou_batch", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
     "bx_kf_multi_predict", "bx_kf_update", "bx_kf_gating_distance", "bx_linear_assignment",
+    "bx_ocsort_create", "bx_ocsort_destroy", "bx_ocsort_reset", "bx_ocsort_step",
+    "bx_ocsort_update_host", "bx_ocsort_status", "bx_ocsort_counters_host",
+    "bx_ocsort_set_id_count", "bx_ocsort_tracks_host", "bx_ocsort_probe", "bx_ocsort_probe_read",
 ]
 
 _vp, _ip, _dp, _fp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_float)
@@ -99,6 +113,17 @@ _SIGS = {
     "bx_kf_update": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "bx_kf_gating_distance": ([C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, _vp], C.c_int),
     "bx_linear_assignment": ([_vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp], C.c_int),
+    "bx_ocsort_create": ([C.POINTER(BxOcsortConfig), C.POINTER(C.c_void_p)], C.c_int),
+    "bx_ocsort_destroy": ([_vp], C.c_int),
+    "bx_ocsort_reset": ([_vp, C.c_int, C.c_int, _vp], C.c_int),
+    "bx_ocsort_step": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_ocsort_update_host": ([_vp, C.c_int, _vp, C.c_int, _vp, _ip, _vp], C.c_int),
+    "bx_ocsort_status": ([_vp, _ip], C.c_int),
+    "bx_ocsort_counters_host": ([_vp, C.c_int, _ip, _ip, _ip], C.c_int),
+    "bx_ocsort_set_id_count": ([_vp, C.c_int, C.c_int, _vp], C.c_int),
+    "bx_ocsort_tracks_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _ip], C.c_int),
+    "bx_ocsort_probe": ([_vp, C.c_int], C.c_int),
+    "bx_ocsort_probe_read": ([_vp, _dp, _ip], C.c_int),
 }
 
 _lib = None

@@ -1696,6 +1696,10 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
 
 }  // namespace
 
+// shared by the other translation units of the library (bx_ocsort.hip) so that bx_last_error
+// reports their failures too
+int bx_record_error(int code, const char* msg) { return set_err(code, msg); }
+
 extern "C" {
 
 const char* bx_last_error(void) { return g_err.c_str(); }

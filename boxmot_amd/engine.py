@@ -175,6 +175,110 @@ class Engine:
                 "start_frame": sf[:n], "mean": mean[:n], "covariance": cov[:n]}
 
 
+@dataclass
+class OcsortParams:
+    """OcSort constructor parameters (ocsort.py:197-235 names; YAML defaults)."""
+
+    min_conf: float = 0.1
+    det_thresh: float = 0.6
+    max_age: int = 30
+    min_hits: int = 3
+    asso_threshold: float = 0.3
+    delta_t: int = 3
+    inertia: float = 0.1
+    use_byte: bool = False
+    Q_xy_scaling: float = 0.01
+    Q_s_scaling: float = 0.0001
+
+
+class OcsortEngine:
+    """Handle over ``bx_ocsort_*`` (include/bxocsort.h): ``n_seq`` OCSort sequences in HBM, one
+    kernel launch (one wave per sequence) per frame."""
+
+    def __init__(self, n_seq: int = 1, track_cap: int = 256, det_cap: int = 256,
+                 params: OcsortParams | None = None):
+        p = params or OcsortParams()
+        self.n_seq, self.track_cap, self.det_cap, self.params = n_seq, track_cap, det_cap, p
+        cfg = N.BxOcsortConfig(
+            n_seq=n_seq, track_cap=track_cap, det_cap=det_cap, min_conf=p.min_conf,
+            det_thresh=p.det_thresh, asso_threshold=p.asso_threshold, inertia=p.inertia,
+            q_xy_scaling=p.Q_xy_scaling, q_s_scaling=p.Q_s_scaling, max_age=int(p.max_age),
+            min_hits=int(p.min_hits), delta_t=int(p.delta_t), use_byte=int(bool(p.use_byte)))
+        self._L = N.load()
+        h = C.c_void_p()
+        N.check(self._L.bx_ocsort_create(C.byref(cfg), C.byref(h)), "bx_ocsort_create")
+        self._h = h
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.bx_ocsort_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, seq0: int = 0, nseq: int | None = None, stream=None):
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        N.check(self._L.bx_ocsort_reset(self._h, seq0, nseq, stream), "bx_ocsort_reset")
+
+    def step(self, dets, det_off, out, out_count, seq0: int = 0, nseq: int | None = None,
+             stream=None):
+        """One frame for sequences [seq0, seq0+nseq) from device tensors (see bx_ocsort_step)."""
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        if stream is None:
+            stream = _current_stream()
+        N.check(self._L.bx_ocsort_step(self._h, seq0, nseq, _ptr(dets), _ptr(det_off), _ptr(out),
+                                       _ptr(out_count), stream), "bx_ocsort_step")
+
+    def update_host(self, seq: int, dets: np.ndarray) -> np.ndarray:
+        d = np.ascontiguousarray(dets, dtype=np.float32).reshape(-1, 6)
+        n = d.shape[0]
+        out = np.empty((max(n, 1), 8), np.float64)
+        m = C.c_int(0)
+        N.check(self._L.bx_ocsort_update_host(self._h, seq, d.ctypes.data if n else None, n,
+                                              out.ctypes.data, C.byref(m), None),
+                "bx_ocsort_update_host")
+        return out[: m.value].copy()
+
+    def status(self) -> int:
+        s = C.c_int(0)
+        N.check(self._L.bx_ocsort_status(self._h, C.byref(s)), "bx_ocsort_status")
+        return s.value
+
+    def counters(self, seq: int = 0) -> dict:
+        fc, idc, nt = C.c_int(), C.c_int(), C.c_int()
+        N.check(self._L.bx_ocsort_counters_host(self._h, seq, C.byref(fc), C.byref(idc),
+                                                C.byref(nt)), "counters")
+        return {"frame_count": fc.value, "id_count": idc.value, "n_tracks": nt.value}
+
+    def set_id_count(self, seq: int, value: int):
+        N.check(self._L.bx_ocsort_set_id_count(self._h, seq, int(value), None), "set_id_count")
+
+    def tracks(self, seq: int = 0) -> dict:
+        """Host snapshot of the track list (list order): ids, XYSR means x [7], covariances."""
+        cap = self.track_cap
+        ids = np.zeros(cap, np.int32)
+        x = np.zeros((cap, 7))
+        P = np.zeros((cap, 7, 7))
+        n = C.c_int()
+        N.check(self._L.bx_ocsort_tracks_host(self._h, seq, cap, ids.ctypes.data, x.ctypes.data,
+                                              P.ctypes.data, C.byref(n)), "tracks")
+        k = min(n.value, cap)
+        return {"id": ids[:k], "x": x[:k], "P": P[:k]}
+
+    def probe(self, on: bool = True) -> None:
+        N.check(self._L.bx_ocsort_probe(self._h, int(bool(on))), "bx_ocsort_probe")
+
+    def probe_read(self):
+        t, n = C.c_double(), C.c_int()
+        N.check(self._L.bx_ocsort_probe_read(self._h, C.byref(t), C.byref(n)), "probe_read")
+        return t.value, n.value
+
+
 def _ptr(x):
     if x is None:
         return None

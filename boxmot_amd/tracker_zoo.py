@@ -15,6 +15,7 @@ TRACKER_CONFIGS = Path(__file__).resolve().parent / "configs" / "trackers"
 _ON_ENGINE = {
     "bytetrack": "boxmot_amd.trackers.bytetrack.ByteTrack",
     "botsort": "boxmot_amd.trackers.botsort.BotSort",
+    "ocsort": "boxmot_amd.trackers.ocsort.OcSort",
 }
 _REFERENCE_NAMES = ["strongsort", "ocsort", "bytetrack", "botsort", "deepocsort", "hybridsort",
                     "boosttrack"]

@@ -1,4 +1,5 @@
 from .botsort import BotSort
 from .bytetrack import ByteTrack
+from .ocsort import OcSort
 
-__all__ = ["ByteTrack", "BotSort"]
+__all__ = ["ByteTrack", "BotSort", "OcSort"]

@@ -1,0 +1,66 @@
+"""OCSort on the MI355X engine — drop-in for boxmot.trackers.ocsort.ocsort.OcSort
+(reference trackers/ocsort/ocsort.py:195-439).  Same constructor, same ``update`` contract and
+output rows; the whole frame (XYSR Kalman predict/update with ORU, IoU + direction-consistency
+costs, the legacy-lapx JV rounds, OCR/BYTE recovery, births and deaths) is one kernel launch.
+
+The fork's OCSort does not run as shipped; this follows it with the minimal patches P1-P5
+(SURVEY.md Appendix A), exactly as oracle/bxo_ocsort.c and the golden fixtures do.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..engine import OcsortEngine, OcsortParams
+from .basetracker import BaseTracker
+
+
+class OcSort(BaseTracker):
+    # KalmanBoxTracker.count is a class attribute shared by every instance and reset to 0 by
+    # each OcSort constructor (ocsort.py:61,115-116,244): mirrored here.
+    _id_count = 0
+
+    def __init__(self, per_class: bool = False, min_conf: float = 0.1, det_thresh: float = 0.2,
+                 max_age: int = 30, min_hits: int = 3, asso_threshold: float = 0.3,
+                 delta_t: int = 3, asso_func: str = "iou", inertia: float = 0.2,
+                 use_byte: bool = False, Q_xy_scaling: float = 0.01,
+                 Q_s_scaling: float = 0.0001, track_cap: int = 256, det_cap: int = 256):
+        super().__init__(max_age=max_age, per_class=per_class, asso_func=asso_func)
+        if asso_func != "iou":
+            raise NotImplementedError(f"OCSort asso_func {asso_func!r} is not on the engine "
+                                      "(the fork's OCSort path evaluates 'iou')")
+        self.min_conf = min_conf
+        self.max_age = max_age
+        self.min_hits = min_hits
+        self.asso_threshold = asso_threshold
+        self.frame_count = 0
+        self.det_thresh = det_thresh
+        self.delta_t = delta_t
+        self.inertia = inertia
+        self.use_byte = use_byte
+        self.Q_xy_scaling = Q_xy_scaling
+        self.Q_s_scaling = Q_s_scaling
+        OcSort._id_count = 0
+        self.engine = OcsortEngine(
+            n_seq=1, track_cap=track_cap, det_cap=det_cap,
+            params=OcsortParams(min_conf=min_conf, det_thresh=det_thresh, max_age=max_age,
+                                min_hits=min_hits, asso_threshold=asso_threshold,
+                                delta_t=delta_t, inertia=inertia, use_byte=use_byte,
+                                Q_xy_scaling=Q_xy_scaling, Q_s_scaling=Q_s_scaling))
+        self._engine_ids = 0
+
+    @BaseTracker.setup_decorator
+    @BaseTracker.per_class_decorator
+    def update(self, dets: np.ndarray, img: np.ndarray, embs: np.ndarray = None) -> np.ndarray:
+        self.check_inputs(dets, img)
+        if self._engine_ids != OcSort._id_count:
+            self.engine.set_id_count(0, OcSort._id_count)
+        self.frame_count += 1
+        out = self.engine.update_host(0, dets)
+        self._engine_ids = OcSort._id_count = self.engine.counters(0)["id_count"]
+        return out if out.shape[0] else np.array([])
+
+    @property
+    def active_tracks(self):
+        """Track list snapshot: ids and XYSR Kalman state (x [7], P [7, 7]) per track."""
+        snap = self.engine.tracks(0)
+        return [{"id": int(i), "x": x, "P": p} for i, x, p in zip(snap["id"], snap["x"], snap["P"])]

@@ -1,0 +1,86 @@
+/*
+ * bxocsort.h — C ABI of the OCSort engine in libbxassoc.so (MI355X, gfx950).
+ *
+ * Boundary: everything OcSort.update(dets, img) computes per frame — the XYSR Kalman predict
+ * and update of every track with the observation-centric re-update (ORU) of a track that
+ * reappears, the IoU + velocity-direction-consistency cost, the one-to-one fast path and the
+ * legacy lapx JV assignment, the optional BYTE round on low-confidence detections, the
+ * observation-centric recovery (OCR) round on last observations, track birth and death and the
+ * output rows — runs on the GPU, one wave64 workgroup per sequence, behind these entry points.
+ *
+ * Reference interfaces replaced (file:line in muntherr/boxmot @ /root/reference):
+ *   bx_ocsort_create/step/update_host  OcSort.__init__ / OcSort.update
+ *                                      boxmot/trackers/ocsort/ocsort.py:195-439
+ *     KalmanBoxTracker                 ocsort.py:56-192
+ *     KalmanFilterXYSR (ORU)           boxmot/motion/kalman_filters/aabb/xysr_kf.py:48-291
+ *     associate (enhanced)             boxmot/utils/association.py:377-536
+ *     linear_assignment (legacy lapx)  boxmot/utils/association.py:105-114
+ * The fork's OCSort does not run as shipped; the engine follows it with the minimal patches
+ * P1-P5 listed in SURVEY.md Appendix A (bit-identical to oracle/bxo_ocsort.c, pinned by the
+ * tests/golden/trk_ocsort_*.npz fixtures captured from the patched reference).
+ *
+ * Conventions as in bxassoc.h: device pointers unless a name ends in _host, asynchronous on
+ * `stream`, every function returns a bx_status (bx_last_error explains failures).
+ */
+#ifndef BXOCSORT_H
+#define BXOCSORT_H
+
+#include <stdint.h>
+
+#include "bxassoc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* OcSort constructor parameters (ocsort.py:197-235; YAML defaults in configs/trackers/ocsort.yaml:
+ * min_conf .1, det_thresh .6, max_age 30, min_hits 3, asso_threshold .3, delta_t 3, inertia .1,
+ * use_byte 0, Q_xy_scaling .01, Q_s_scaling 1e-4). asso_func is "iou" (the only one the fork's
+ * OCSort path evaluates). */
+typedef struct {
+    int32_t n_seq;      /* independent sequences held by this engine */
+    int32_t track_cap;  /* track slots per sequence */
+    int32_t det_cap;    /* max detections per frame per sequence */
+    double min_conf, det_thresh, asso_threshold, inertia, q_xy_scaling, q_s_scaling;
+    int32_t max_age, min_hits, delta_t, use_byte;
+} bx_ocsort_config;
+
+typedef struct bx_ocsort bx_ocsort;
+
+int bx_ocsort_create(const bx_ocsort_config *cfg, bx_ocsort **out);
+int bx_ocsort_destroy(bx_ocsort *e);
+/* Forget all tracks of sequences [seq0, seq0+nseq) (frame and id counters back to 0). */
+int bx_ocsort_reset(bx_ocsort *e, int seq0, int nseq, void *stream);
+/* One frame for sequences [seq0, seq0+nseq) — one kernel launch.
+ *   dets    [sum N][6] float32 (x1,y1,x2,y2,conf,cls)
+ *   det_off [nseq+1] int32 prefix offsets
+ *   out     [sum N][8] float64 rows [x1,y1,x2,y2,id,conf,cls,det_ind], sequence k from row
+ *           det_off[k], in the reference's (reversed track list) order
+ *   out_count [nseq] int32 */
+int bx_ocsort_step(bx_ocsort *e, int seq0, int nseq, const float *dets, const int32_t *det_off,
+                   double *out, int32_t *out_count, void *stream);
+/* Host-memory path for one sequence (the drop-in update): copies in, launches, copies out,
+ * synchronises.  out must hold n rows. */
+int bx_ocsort_update_host(bx_ocsort *e, int seq, const float *dets, int n, double *out,
+                          int *n_out, void *stream);
+/* Latched device status (BX_OK, BX_ERR_TRACK_OVERFLOW or BX_ERR_CAPACITY). */
+int bx_ocsort_status(bx_ocsort *e, int *status);
+int bx_ocsort_counters_host(bx_ocsort *e, int seq, int *frame_count, int *id_count,
+                            int *n_tracks);
+/* KalmanBoxTracker.count is class-global in the reference (ocsort.py:61,115-116,244); the
+ * Python drop-in mirrors it through this. */
+int bx_ocsort_set_id_count(bx_ocsort *e, int seq, int id_count, void *stream);
+/* Track list of a sequence in list order (host, synchronous): ids [cap], Kalman means x
+ * [cap][7] and covariances p [cap][49] (any may be NULL); *n = number of tracks. */
+int bx_ocsort_tracks_host(bx_ocsort *e, int seq, int cap, int32_t *ids, double *x, double *p,
+                          int *n);
+/* Timing probe (benchmarks): while on, every step records a HIP event pair around its kernel;
+ * probe_read synchronises and returns the summed milliseconds and launch count, then clears. */
+int bx_ocsort_probe(bx_ocsort *e, int on);
+int bx_ocsort_probe_read(bx_ocsort *e, double *total_ms, int *count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BXOCSORT_H */

@@ -72,6 +72,8 @@ bxo_ocsort *bxo_ocsort_new(double min_conf, double det_thresh, int max_age, int 
                            double q_xy_scaling, double q_s_scaling);
 void bxo_ocsort_free(bxo_ocsort *o);
 int bxo_ocsort_id_count(bxo_ocsort *o);
+/* track list in list order: ids [cap], XYSR means x [cap][7], covariances P [cap][49] */
+int bxo_ocsort_tracks(bxo_ocsort *o, int cap, int *ids, double *x, double *P);
 /* dets[n,6] float64 (float32-rounded); out[M,8]; returns M or -2 if out_cap is too small */
 int bxo_ocsort_update(bxo_ocsort *o, const double *dets, int n, double *out, int out_cap);
 double bxo_acos(double x);

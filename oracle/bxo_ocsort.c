@@ -628,6 +628,15 @@ void bxo_ocsort_free(bxo_ocsort *o) {
 
 int bxo_ocsort_id_count(bxo_ocsort *o) { return o->id_count; }
 
+int bxo_ocsort_tracks(bxo_ocsort *o, int cap, int *ids, double *x, double *P) {
+    for (int k = 0; k < o->ntr && k < cap; k++) {
+        if (ids) ids[k] = o->tr[k].id;
+        if (x) memcpy(x + 7 * k, o->tr[k].kf.s.x, sizeof(double) * 7);
+        if (P) memcpy(P + 49 * k, o->tr[k].kf.s.P, sizeof(double) * 49);
+    }
+    return o->ntr;
+}
+
 /* dets[n][6] float64 (already float32-rounded, as setup_decorator leaves them) */
 int bxo_ocsort_update(bxo_ocsort *o, const double *dets_in, int n, double *out, int out_cap) {
     o->frame_count++;

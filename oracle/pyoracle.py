@@ -65,6 +65,7 @@ def lib():
         L.bxo_ocsort_free.argtypes = [C.c_void_p]
         L.bxo_ocsort_id_count.argtypes = [C.c_void_p]
         L.bxo_ocsort_update.argtypes = [C.c_void_p, _dp, C.c_int, _dp, C.c_int]
+        L.bxo_ocsort_tracks.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.bxo_acos.argtypes = [C.c_double]
         L.bxo_acos.restype = C.c_double
         _lib = L
@@ -213,6 +214,15 @@ class OracleTracker:
         if self.kind == "ocsort":
             return lib().bxo_ocsort_id_count(self.h)
         return lib().bxo_id_count(self.h)
+
+    def ocsort_tracks(self):
+        """OCSort track list (list order): ids, XYSR means [n,7], covariances [n,7,7]."""
+        n = lib().bxo_ocsort_tracks(self.h, 0, None, None, None)
+        ids = np.zeros(max(n, 1), np.int32)
+        x = np.zeros((max(n, 1), 7))
+        P = np.zeros((max(n, 1), 7, 7))
+        lib().bxo_ocsort_tracks(self.h, n, ids.ctypes.data, x.ctypes.data, P.ctypes.data)
+        return {"id": ids[:n], "x": x[:n], "P": P[:n]}
 
     def __del__(self):
         h = getattr(self, "h", None)

@@ -186,11 +186,13 @@ def test_linear_assignment_empty(torch_cuda):
 
 # --------------------------------------------------------------------------- tracker level
 def make_dropin(kind, args):
-    from boxmot_amd import BotSort, ByteTrack
+    from boxmot_amd import BotSort, ByteTrack, OcSort
 
     if kind == "bytetrack":
         ByteTrack.clear_count()
         return ByteTrack(**args)
+    if kind == "ocsort":
+        return OcSort(**args)
     return BotSort(reid_weights=None, device="cuda", half=False, **args)
 
 
@@ -345,3 +347,79 @@ def test_capacity_errors(torch_cuda):
     eng.update_host(0, dets + np.array([200, 200, 200, 200, 0, 0]))  # 4 new → 8 live
     with pytest.raises(RuntimeError):
         eng.update_host(0, dets + np.array([400, 400, 400, 400, 0, 0]))  # would need 12 slots
+
+
+# ------------------------------------------------------------------------------------- OCSort
+def run_ocsort_batched(torch, scenes, n_frames, args, track_cap=256, det_cap=256):
+    from boxmot_amd.engine import OcsortEngine, OcsortParams
+
+    S = len(scenes)
+    eng = OcsortEngine(n_seq=S, track_cap=track_cap, det_cap=det_cap,
+                       params=OcsortParams(**args))
+    orcs = [po.OracleTracker("ocsort", **args) for _ in range(S)]
+    for t in range(1, n_frames + 1):
+        frames = [sc.frame(t)[0] for sc in scenes]
+        off = np.zeros(S + 1, np.int32)
+        off[1:] = np.cumsum([f.shape[0] for f in frames])
+        dets = np.concatenate(frames, 0).astype(np.float32)
+        out = torch.empty((max(int(off[-1]), 1), 8), dtype=torch.float64, device="cuda")
+        cnt = torch.empty(S, dtype=torch.int32, device="cuda")
+        eng.step(dev(torch, dets), dev(torch, off), out, cnt)
+        o, c = host(out), host(cnt)
+        for s in range(S):
+            np.testing.assert_array_equal(o[off[s]: off[s] + c[s]], orcs[s].update(frames[s]),
+                                          err_msg=f"seq {s} frame {t}")
+    assert eng.status() == 0
+    # Kalman state: bitwise the oracle's (and so within 1e-5 rel of the reference)
+    for s in range(S):
+        g, r = eng.tracks(s), orcs[s].ocsort_tracks()
+        np.testing.assert_array_equal(g["id"], r["id"])
+        np.testing.assert_array_equal(g["x"], r["x"])
+        np.testing.assert_array_equal(g["P"], r["P"])
+
+
+OCS_ARGS = dict(min_conf=0.1, det_thresh=0.6, max_age=30, min_hits=3, asso_threshold=0.3,
+                delta_t=3, inertia=0.1, use_byte=False, Q_xy_scaling=0.01, Q_s_scaling=0.0001)
+
+
+@pytest.mark.parametrize("variant", ["default", "byte", "short_age"])
+def test_ocsort_batched_vs_oracle(torch_cuda, variant):
+    """Several sequences per launch (grid / crowded layouts, low-confidence detections, missed
+    detections -> ORU re-updates, deaths) against the oracle, outputs and KF state bitwise."""
+    from boxmot_amd.synth import SyntheticScene
+
+    args = dict(OCS_ARGS)
+    if variant == "byte":
+        args.update(use_byte=True, det_thresh=0.5)
+    if variant == "short_age":
+        args.update(max_age=5, min_hits=1, delta_t=1, inertia=0.3)
+    scenes = [SyntheticScene(n_obj=12 + 9 * s, seed=300 + s,
+                             layout="crowded" if s % 2 else "grid", p_det=0.35 + 0.1 * (s % 3),
+                             conf_lo=0.2 if s % 3 == 0 else 0.55) for s in range(6)]
+    run_ocsort_batched(torch_cuda, scenes, 60, args)
+
+
+def test_ocsort_large_scene_vs_oracle(torch_cuda):
+    """A crowded 160-object sequence: assignment problems past the LDS cost budget (HBM path)."""
+    from boxmot_amd.synth import SyntheticScene
+
+    sc = SyntheticScene(n_obj=160, seed=17, layout="crowded", p_det=0.3, conf_lo=0.4)
+    run_ocsort_batched(torch_cuda, [sc], 30, dict(OCS_ARGS, use_byte=True, det_thresh=0.5))
+
+
+def test_ocsort_empty_frames_and_global_ids(torch_cuda):
+    from boxmot_amd import OcSort
+
+    img = np.zeros((720, 1280, 3), np.uint8)
+    a = OcSort(**OCS_ARGS)
+    orc = po.OracleTracker("ocsort", **OCS_ARGS)
+    d = np.array([[10, 10, 60, 120, 0.9, 0], [200, 50, 260, 170, 0.8, 2]], np.float32)
+    for t in range(6):
+        dd = d if t not in (2, 3) else np.empty((0, 6), np.float32)
+        o = np.asarray(a.update(dd, img), np.float64).reshape(-1, 8)
+        np.testing.assert_array_equal(o, orc.update(dd))
+    # the id counter is class-global: a second instance resets it, the first continues from it
+    b = OcSort(**OCS_ARGS)
+    ob = b.update(d, img)
+    assert ob.shape == (2, 8) and sorted(ob[:, 4]) == [1.0, 2.0]
+    assert OcSort._id_count == 2

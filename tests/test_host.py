@@ -25,7 +25,29 @@ def test_unknown_tracker_raises_keyerror(capsys):
     assert "No such tracker" in capsys.readouterr().out
 
 
-@pytest.mark.parametrize("name", ["ocsort", "strongsort", "boosttrack", "deepocsort"])
+def test_ocsort_yaml_defaults_reach_the_engine(monkeypatch):
+    """create_tracker('ocsort') passes the YAML defaults to the OcSort constructor; without a GPU
+    building the engine fails loudly (no CPU fallback)."""
+    import boxmot_amd._native as N
+    from boxmot_amd.trackers import ocsort as mod
+
+    seen = {}
+
+    class Probe:
+        def __init__(self, **kw):
+            seen.update(kw)
+            raise N.NativeUnavailable("no device")
+
+    monkeypatch.setattr(mod, "OcsortEngine", Probe)
+    with pytest.raises(N.NativeUnavailable):
+        create_tracker("ocsort")
+    p = seen["params"]
+    assert (p.det_thresh, p.max_age, p.min_hits, p.delta_t, p.inertia, p.use_byte) == \
+        (0.6, 30, 3, 3, 0.1, False)
+    assert (p.min_conf, p.Q_xy_scaling, p.Q_s_scaling, p.asso_threshold) == (0.1, 0.01, 1e-4, 0.3)
+
+
+@pytest.mark.parametrize("name", ["strongsort", "boosttrack", "deepocsort"])
 def test_not_yet_on_engine(name):
     with pytest.raises(NotImplementedError):
         create_tracker(name, evolve_param_dict={})
