@@ -43,7 +43,21 @@ CONFIGS = {
                                           appearance_thresh=0.25)),
     "bytetrack": ("bytetrack", 256, 0, dict(min_conf=0.1, track_thresh=0.6, match_thresh=0.9,
                                             track_buffer=30)),
+    # OCSort (configs[0]'s tracker, YAML defaults): ~20 tracks/frame like MOT17-mini, and the
+    # 256-track geometry of configs[1]; detection confidences span both BYTE splits
+    "ocsort": ("ocsort", 40, 0, dict(min_conf=0.1, det_thresh=0.6, max_age=30, min_hits=3,
+                                     asso_threshold=0.3, delta_t=3, inertia=0.1, use_byte=False,
+                                     Q_xy_scaling=0.01, Q_s_scaling=0.0001)),
+    "ocsort256": ("ocsort", 256, 0, dict(min_conf=0.1, det_thresh=0.6, max_age=30, min_hits=3,
+                                         asso_threshold=0.3, delta_t=3, inertia=0.1,
+                                         use_byte=False, Q_xy_scaling=0.01, Q_s_scaling=0.0001)),
 }
+OCS_CONF_LO = 0.3  # OCSort scenes: confidences U(0.3, 1) -> ~40% below det_thresh
+
+# OCSort per-launch algorithmic bytes: per live track the XYSR state (x[7], P[49] f64) read and
+# written plus its observation record (last_obs, velocity, k-previous box: 12 f64) read; per
+# detection one f32 row in; per output one f64 row out.
+OCS_TRACK_BYTES = 2 * 56 * 8 + 12 * 8
 
 KF_STATE = 576  # fp64 mean[8] + covariance[64] per track
 
@@ -80,7 +94,8 @@ def cpu_baseline(kind, n_obj, emb_dim, params, seconds=15.0, warm_frames=40):
     from boxmot_amd.synth import SyntheticScene
     from oracle import pyoracle as po
 
-    sc = SyntheticScene(n_obj=n_obj, seed=12345, emb_dim=emb_dim)
+    extra = dict(conf_lo=OCS_CONF_LO) if kind == "ocsort" else {}
+    sc = SyntheticScene(n_obj=n_obj, seed=12345, emb_dim=emb_dim, **extra)
     tr = po.OracleTracker(kind, **params)
     t = 0
     for _ in range(warm_frames):
@@ -142,18 +157,26 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from boxmot_amd.engine import Engine, EngineParams
+    from boxmot_amd.engine import Engine, EngineParams, OcsortEngine, OcsortParams
     from boxmot_amd.shard import gather_records, output_checksum, shard_sequences
     from boxmot_amd.synth import TorchSceneBatch
 
     kind, n_obj, F, params = CONFIGS[args.config]
     S = args.seqs
-    eng = Engine(kind, n_seq=S, track_cap=512, det_cap=256, emb_dim=F,
-                 params=EngineParams(**params))
-    stages = [s for s in Engine.STAGES
-              if F or s not in ("det_features", "gate", "cosine", "features")]
+    ocs = kind == "ocsort"
+    if ocs:
+        tcap = int(os.environ.get("BX_OCS_TRACK_CAP", max(64, 2 * n_obj)))
+        eng = OcsortEngine(n_seq=S, track_cap=tcap, det_cap=max(64, n_obj),
+                           params=OcsortParams(**params))
+        stages = []
+    else:
+        eng = Engine(kind, n_seq=S, track_cap=512, det_cap=256, emb_dim=F,
+                     params=EngineParams(**params))
+        stages = [s for s in Engine.STAGES
+                  if F or s not in ("det_features", "gate", "cosine", "features")]
     # this rank's shard: global sequences [rank*S, (rank+1)*S) — weak scaling, no exchange
-    gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev)
+    gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev,
+                          **(dict(conf_lo=OCS_CONF_LO) if ocs else {}))
     total = args.warmup + args.steps
     frames = [gen.frame(t) for t in range(1, total + 1)]  # resident in HBM before timing
     max_n = max(int(f[1][-1].item()) for f in frames)
@@ -164,7 +187,10 @@ def main():
 
     def step(k):
         d, off, e = frames[k]
-        eng.step(d, off, e, None, out, cnt, stream=stream.cuda_stream)
+        if ocs:
+            eng.step(d, off, out, cnt, stream=stream.cuda_stream)
+        else:
+            eng.step(d, off, e, None, out, cnt, stream=stream.cuda_stream)
 
     # warm-up; its last len(stages) steps time one stage each to find the dominant kernel
     stage_ms = {}
@@ -179,12 +205,13 @@ def main():
             stage_ms[stages[j]] = ms / max(n, 1)
             eng.probe(None)
     dominant = max(stage_ms, key=stage_ms.get) if stage_ms else (
-        "features" if F else "assoc")
+        "ocsort_frame" if ocs else ("features" if F else "assoc"))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    eng.probe(dominant)  # two event records per step around that stage's launch
+    # two event records per step around the dominant stage's launch (OCSort: its one kernel)
+    eng.probe(True if ocs else dominant)
     t0 = time.perf_counter()
     for k in range(args.warmup, total):
         step(k)
@@ -194,11 +221,13 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     dom_ms, dom_n = eng.probe_read()
-    eng.probe(None)
+    eng.probe(False if ocs else None)
     dom_ms /= max(dom_n, 1)
     if eng.status() != 0:
         raise RuntimeError(f"engine status {eng.status()} (capacity overflow)")
     units = eng.frame_stats()  # last timed frame, all sequences of this rank
+    if ocs:
+        units["dets"] = int(frames[total - 1][1][-1].item())
 
     # per-sequence records of this rank's shard: [global seq id, frames timed, dets timed,
     # rows of the last frame, checksum of the last frame, rank wall s, dominant-stage ms]
@@ -217,7 +246,11 @@ def main():
     if rank == 0:
         assert np.array_equal(np.sort(allrec[:, 0]), np.arange(S * world)), "shard gather"
         mean_d = float(allrec[:, 2].sum() / allrec[:, 1].sum())
-        per_launch = stage_bytes(dominant, units, F)
+        if ocs:
+            per_launch = (units["tracks"] * OCS_TRACK_BYTES + units["dets"] * 24 +
+                          units["outputs"] * 64)
+        else:
+            per_launch = stage_bytes(dominant, units, F)
         achieved = per_launch / (dom_ms * 1e-3) / 1e9
         traffic = load_traffic(args.config, dominant)
         line = {

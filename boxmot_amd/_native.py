@@ -85,6 +85,7 @@ EXPORTS = [
     "bx_ocsort_create", "bx_ocsort_destroy", "bx_ocsort_reset", "bx_ocsort_step",
     "bx_ocsort_update_host", "bx_ocsort_status", "bx_ocsort_counters_host",
     "bx_ocsort_set_id_count", "bx_ocsort_tracks_host", "bx_ocsort_probe", "bx_ocsort_probe_read",
+    "bx_ocsort_frame_stats_host",
 ]
 
 _vp, _ip, _dp, _fp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_float)
@@ -123,6 +124,7 @@ _SIGS = {
     "bx_ocsort_set_id_count": ([_vp, C.c_int, C.c_int, _vp], C.c_int),
     "bx_ocsort_tracks_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _ip], C.c_int),
     "bx_ocsort_probe": ([_vp, C.c_int], C.c_int),
+    "bx_ocsort_frame_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_ocsort_probe_read": ([_vp, _dp, _ip], C.c_int),
 }
 

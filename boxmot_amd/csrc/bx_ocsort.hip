@@ -45,11 +45,11 @@ struct OcsTrk {
   double sx[7], sP[49];         // freeze() snapshot (attr_saved)
   double hbox[4];               // last non-None entry of history_obs
   double last_obs[5];
-  double obs_box[OBS_KEEP][5];  // observations dict, newest OBS_KEEP entries
+  double obs_box[OBS_KEEP][5];  // observations dict: the entry of age a sits in slot a % 8
   double vel[2];
   double conf, cls;
   int obs_age[OBS_KEEP];
-  int n_obs, has_vel, id, tsu, hits, hit_streak, age, det_ind;
+  int last_age, has_vel, id, tsu, hits, hit_streak, age, det_ind;  // last_age < 0: no obs
   int observed, has_saved, hvalid, htail;
 };
 
@@ -64,7 +64,34 @@ struct OcsDev {
   double* tb;       // [S][T][TB]
   double* cost_g;   // [S][D*T] or null
   int* status;
+  unsigned long long* dbg;  // [S][OCS_DBG] phase stamps (diagnostic builds only, else null)
 };
+
+// Diagnostic phase stamps and counters (build with -DBX_PHASE_TIMING; never shipped): per
+// sequence, cycles accumulated per phase over all frames [0, 16) and event counters [16, 32).
+constexpr int OCS_DBG = 32;
+#ifdef BX_PHASE_TIMING
+#define OSTAMP(k)                                                                    \
+  do {                                                                               \
+    __syncthreads();                                                                 \
+    if (threadIdx.x == 0 && g.dbg) {                                                 \
+      const unsigned long long _now = __builtin_amdgcn_s_memtime();                  \
+      g.dbg[(size_t)seq * OCS_DBG + (k)] += _now - t_last;                           \
+      t_last = _now;                                                                 \
+    }                                                                                \
+  } while (0)
+#define OCOUNT(k, v)                                                                 \
+  do {                                                                               \
+    if (threadIdx.x == 0 && g.dbg) g.dbg[(size_t)seq * OCS_DBG + 16 + (k)] += (v);   \
+  } while (0)
+#else
+#define OSTAMP(k) \
+  do {            \
+  } while (0)
+#define OCOUNT(k, v) \
+  do {               \
+  } while (0)
+#endif
 
 // ------------------------------------------------------------------------------------------
 // fdlibm acos (oracle/bxo_ocsort.c bxo_acos)
@@ -113,138 +140,164 @@ __device__ double ocs_acos(double x) {
 }
 
 // ------------------------------------------------------------------------------------------
-// XYSR Kalman filter (xysr_kf.py), the oracle's kf_predict7 / inv4 / kf_update7_core.
-__device__ void kf_predict7(const OcsDev& g, double* x, double* P) {
-  for (int i = 0; i < 3; i++) x[i] = x[i] + x[i + 4];
-  double FP[49];
-  for (int i = 0; i < 7; i++)
-    for (int j = 0; j < 7; j++) FP[i * 7 + j] = i < 3 ? P[i * 7 + j] + P[(i + 4) * 7 + j] : P[i * 7 + j];
-  for (int i = 0; i < 7; i++)
-    for (int j = 0; j < 7; j++) {
-      const double m = j < 3 ? FP[i * 7 + j] + FP[i * 7 + j + 4] : FP[i * 7 + j];
-      double q = 0.0;
-      if (i == j) q = (i == 4 || i == 5) ? g.q_xy : (i == 6 ? g.q_s : 1.0);
-      P[i * 7 + j] = 1.0 * m + q;
-    }
+// XYSR Kalman filter (xysr_kf.py) on 8 lanes per track (an "octet"): lane r of the octet owns
+// row rr = min(r, 6) of the 7-state mean and covariance (lane 7 mirrors row 6 and never writes).
+// Every element is computed by one lane with the oracle's operation order (kf_predict7,
+// kf_update7_core in oracle/bxo_ocsort.c); shuffles only move operands between rows.
+__device__ __forceinline__ double osh(double v, int src) { return __shfl(v, src, 8); }
+
+struct KfRow {
+  double x, P[7];
+};
+
+__device__ __forceinline__ void row_load(const double* x, const double* P, int rr, KfRow& k) {
+  k.x = x[rr];
+#pragma unroll
+  for (int j = 0; j < 7; j++) k.P[j] = P[rr * 7 + j];
 }
 
-__device__ void inv4(const double* Ain, double* B) {
+__device__ __forceinline__ void row_store(double* x, double* P, int r, const KfRow& k) {
+  if (r < 7) {
+    x[r] = k.x;
+#pragma unroll
+    for (int j = 0; j < 7; j++) P[r * 7 + j] = k.P[j];
+  }
+}
+
+// x = F x ; P = 1.0 * (F P F') + Q  (F = I + e_i e_{i+4}' for i < 3)
+__device__ void kfo_predict(const OcsDev& g, int rr, KfRow& k) {
+  const int src = rr < 3 ? rr + 4 : rr;
+  const double x4 = osh(k.x, src);
+  k.x = rr < 3 ? k.x + x4 : k.x;
+  double FP[7];
+#pragma unroll
+  for (int j = 0; j < 7; j++) {
+    const double p4 = osh(k.P[j], src);
+    FP[j] = rr < 3 ? k.P[j] + p4 : k.P[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 7; j++) {
+    const double m = j < 3 ? FP[j] + FP[j + 4] : FP[j];
+    double q = 0.0;
+    if (rr == j) q = (rr == 4 || rr == 5) ? g.q_xy : (rr == 6 ? g.q_s : 1.0);
+    k.P[j] = 1.0 * m + q;
+  }
+}
+
+// np.linalg.inv of a 4x4 (oracle inv4: dgetf2 LU with partial pivoting, then dgetrs).  Row
+// swaps are written as predicated swaps over constant indices so both matrices stay in VGPRs.
+__device__ __forceinline__ void swap_rows4(double* M, int k, int p) {
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (i > k && i == p)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const double t = M[k * 4 + j];
+        M[k * 4 + j] = M[i * 4 + j];
+        M[i * 4 + j] = t;
+      }
+}
+
+__device__ __forceinline__ void inv4(const double* Ain, double* B) {
   double A[16];
   int piv[4];
+#pragma unroll
   for (int i = 0; i < 16; i++) A[i] = Ain[i];
+#pragma unroll
   for (int k = 0; k < 4; k++) {
     int p = k;
     double mx = fabs(A[k * 4 + k]);
+#pragma unroll
     for (int i = k + 1; i < 4; i++)
       if (fabs(A[i * 4 + k]) > mx) mx = fabs(A[i * 4 + k]), p = i;
     piv[k] = p;
-    if (p != k)
-      for (int j = 0; j < 4; j++) {
-        const double t = A[k * 4 + j];
-        A[k * 4 + j] = A[p * 4 + j];
-        A[p * 4 + j] = t;
-      }
+    swap_rows4(A, k, p);
     if (A[k * 4 + k] != 0.0) {
       if (fabs(A[k * 4 + k]) >= DBL_MIN) {
         const double r = 1.0 / A[k * 4 + k];
+#pragma unroll
         for (int i = k + 1; i < 4; i++) A[i * 4 + k] *= r;
       } else {
+#pragma unroll
         for (int i = k + 1; i < 4; i++) A[i * 4 + k] /= A[k * 4 + k];
       }
     }
+#pragma unroll
     for (int j = k + 1; j < 4; j++) {
       const double t = -A[k * 4 + j];
+#pragma unroll
       for (int i = k + 1; i < 4; i++) A[i * 4 + j] = A[i * 4 + j] + A[i * 4 + k] * t;
     }
   }
+#pragma unroll
   for (int i = 0; i < 16; i++) B[i] = (i % 5 == 0) ? 1.0 : 0.0;
-  for (int k = 0; k < 4; k++)
-    if (piv[k] != k)
-      for (int j = 0; j < 4; j++) {
-        const double t = B[k * 4 + j];
-        B[k * 4 + j] = B[piv[k] * 4 + j];
-        B[piv[k] * 4 + j] = t;
-      }
+#pragma unroll
+  for (int k = 0; k < 4; k++) swap_rows4(B, k, piv[k]);
+#pragma unroll
   for (int j = 0; j < 4; j++) {
+#pragma unroll
     for (int k = 0; k < 4; k++)
       if (B[k * 4 + j] != 0.0)
+#pragma unroll
         for (int i = k + 1; i < 4; i++) B[i * 4 + j] -= B[k * 4 + j] * A[i * 4 + k];
+#pragma unroll
     for (int k = 3; k >= 0; k--)
       if (B[k * 4 + j] != 0.0) {
         B[k * 4 + j] /= A[k * 4 + k];
+#pragma unroll
         for (int i = 0; i < k; i++) B[i * 4 + j] -= B[k * 4 + j] * A[i * 4 + k];
       }
   }
 }
 
-__device__ void kf_update7_core(double* x, double* P, const double* z) {
+// update with a measurement (R = diag(1,1,10,10), H = [I4 0], Joseph form); z uniform per octet
+__device__ void kfo_update(int rr, KfRow& k, const double* z) {
   const double Rd[4] = {1.0, 1.0, 10.0, 10.0};
-  double y[4], S[16], SI[16], K[28];
-  for (int k = 0; k < 4; k++) y[k] = z[k] - x[k];
+  double y[4], S[16], SI[16];
+#pragma unroll
+  for (int a = 0; a < 4; a++) y[a] = z[a] - osh(k.x, a);
+#pragma unroll
   for (int a = 0; a < 4; a++)
-    for (int b = 0; b < 4; b++) S[a * 4 + b] = P[a * 7 + b] + (a == b ? Rd[a] : 0.0);
-  inv4(S, SI);
-  for (int i = 0; i < 7; i++)
-    for (int b = 0; b < 4; b++) {
-      double acc = 0.0;
-      for (int a = 0; a < 4; a++) acc += P[i * 7 + a] * SI[a * 4 + b];
-      K[i * 4 + b] = acc;
-    }
-  for (int i = 0; i < 7; i++) {
+#pragma unroll
+    for (int b = 0; b < 4; b++) S[a * 4 + b] = osh(k.P[b], a) + (a == b ? Rd[a] : 0.0);
+  inv4(S, SI);  // every lane of the octet inverts the same S identically
+  double K[4];
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
     double acc = 0.0;
-    for (int b = 0; b < 4; b++) acc += K[i * 4 + b] * y[b];
-    x[i] = x[i] + acc;
+#pragma unroll
+    for (int a = 0; a < 4; a++) acc += k.P[a] * SI[a * 4 + b];
+    K[b] = acc;
   }
-  double IKH[49], A[49];
-  for (int i = 0; i < 7; i++)
-    for (int j = 0; j < 7; j++) IKH[i * 7 + j] = (i == j ? 1.0 : 0.0) - (j < 4 ? K[i * 4 + j] : 0.0);
-  for (int i = 0; i < 7; i++)
-    for (int j = 0; j < 7; j++) {
-      double acc = 0.0;
-      for (int k = 0; k < 7; k++) acc += IKH[i * 7 + k] * P[k * 7 + j];
-      A[i * 7 + j] = acc;
-    }
-  // P = A IKH' + K R K' (the Joseph form), written back row by row
-  for (int i = 0; i < 7; i++)
-    for (int j = 0; j < 7; j++) {
-      double acc = 0.0;
-      for (int k = 0; k < 7; k++) acc += A[i * 7 + k] * IKH[j * 7 + k];
-      double kr = 0.0;
-      for (int b = 0; b < 4; b++) kr += (K[i * 4 + b] * Rd[b]) * K[j * 4 + b];
-      P[i * 7 + j] = acc + kr;
-    }
-}
-
-// xysr_kf.py:211-291 with a measurement (the None branch is ocs_update_none)
-__device__ void kf_update7(const OcsDev& g, OcsTrk& t, const double* z) {
-  if (!t.observed && t.has_saved) {  // unfreeze (xysr_kf.py:183-209)
-    // new_history = history + [z]: the previous non-None entry is hbox, htail+1 steps back
-    const double b1[4] = {t.hbox[0], t.hbox[1], t.hbox[2], t.hbox[3]};
-    const int hv = t.hvalid, gap = t.htail + 1;
-    for (int i = 0; i < 7; i++) t.x[i] = t.sx[i];
-    for (int i = 0; i < 49; i++) t.P[i] = t.sP[i];
-    t.has_saved = 0;
-    if (hv) {
-      const double x1 = b1[0], y1 = b1[1], s1 = b1[2], r1 = b1[3];
-      const double w1 = sqrt(s1 * r1), h1 = sqrt(s1 / r1);
-      const double x2 = z[0], y2 = z[1], s2 = z[2], r2 = z[3];
-      const double w2 = sqrt(s2 * r2), h2 = sqrt(s2 / r2);
-      const double dx = (x2 - x1) / gap, dy = (y2 - y1) / gap;
-      const double dw = (w2 - w1) / gap, dh = (h2 - h1) / gap;
-      for (int i = 0; i < gap; i++) {
-        const double xx = x1 + (i + 1) * dx, yy = y1 + (i + 1) * dy;
-        const double ww = w1 + (i + 1) * dw, hh = h1 + (i + 1) * dh;
-        const double nb[4] = {xx, yy, ww * hh, ww / (double)hh};
-        kf_update7_core(t.x, t.P, nb);
-        if (i != gap - 1) kf_predict7(g, t.x, t.P);
-      }
-    }
+  {
+    double acc = 0.0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) acc += K[b] * y[b];
+    k.x = k.x + acc;
   }
-  t.observed = 1;
-  kf_update7_core(t.x, t.P, z);
-  for (int k = 0; k < 4; k++) t.hbox[k] = z[k];
-  t.htail = 0;
-  t.hvalid = 1;
+  double ikh[7], A[7];
+#pragma unroll
+  for (int c = 0; c < 7; c++) ikh[c] = (rr == c ? 1.0 : 0.0) - (c < 4 ? K[c] : 0.0);
+#pragma unroll
+  for (int j = 0; j < 7; j++) {
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < 7; c++) acc += ikh[c] * osh(k.P[j], c);
+    A[j] = acc;
+  }
+#pragma unroll
+  for (int j = 0; j < 7; j++) {
+    double Kj[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) Kj[b] = osh(K[b], j);
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < 7; c++) acc += A[c] * ((j == c ? 1.0 : 0.0) - (c < 4 ? Kj[c] : 0.0));
+    double kr = 0.0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) kr += (K[b] * Rd[b]) * Kj[b];
+    k.P[j] = acc + kr;
+  }
 }
 
 // ocsort.py:31-45
@@ -259,66 +312,107 @@ __device__ void x_to_bbox(const double* x, double* b) {
 
 __device__ double sum5(const double* b) { return (((b[0] + b[1]) + b[2]) + b[3]) + b[4]; }
 
-__device__ int obs_find(const OcsTrk& t, int age) {
-  for (int q = 0; q < t.n_obs; q++)
-    if (t.obs_age[q] == age) return q;
-  return -1;
+// The observations dict (ocsort.py:73,158) is read only at ages within delta_t <= 7 of the
+// current age, plus its newest key; keeping the entry of age a in slot a % 8 loses only entries
+// at least 8 ages older than a newer one, which no lookup reaches.
+// First hit of `want0 + i` for i < cnt (ascending), or -1; the probes are independent loads.
+__device__ __forceinline__ int obs_first(const OcsTrk& t, int want0, int cnt) {
+  int q = -1;
+  for (int i = cnt - 1; i >= 0; i--) {
+    const int want = want0 + i;
+    if (want >= 0 && t.obs_age[want & (OBS_KEEP - 1)] == want) q = want & (OBS_KEEP - 1);
+  }
+  return q;
 }
 
-// ocsort.py:136-171 (update with a detection row [x1,y1,x2,y2,conf] + cls)
-__device__ void ocs_update_det(const OcsDev& g, OcsTrk& t, const double* b5, double cls,
+// ocsort.py:136-171 (update with a detection row [x1,y1,x2,y2,conf] + cls), octet-wide: lane 0
+// keeps the track's bookkeeping, the octet runs the Kalman update (with the ORU replay of
+// xysr_kf.py:183-209 when the track was frozen)
+__device__ void ocs_update_det(const OcsDev& g, OcsTrk& t, int r, const double* b5, double cls,
                                int det_ind) {
-  t.det_ind = det_ind;
-  t.conf = b5[4];
-  t.cls = cls;
-  if (sum5(t.last_obs) >= 0) {
-    int q = -1;
-    for (int i = 0; i < g.delta_t && q < 0; i++) q = obs_find(t, t.age - (g.delta_t - i));
-    const double* prev = q >= 0 ? t.obs_box[q] : t.last_obs;
-    // ocsort.py:48-53 speed_direction
-    const double cx1 = (prev[0] + prev[2]) / 2.0, cy1 = (prev[1] + prev[3]) / 2.0;
-    const double cx2 = (b5[0] + b5[2]) / 2.0, cy2 = (b5[1] + b5[3]) / 2.0;
-    const double sy = cy2 - cy1, sx = cx2 - cx1;
-    const double norm = sqrt((cy2 - cy1) * (cy2 - cy1) + (cx2 - cx1) * (cx2 - cx1)) + 1e-6;
-    t.vel[0] = sy / norm;
-    t.vel[1] = sx / norm;
-    t.has_vel = 1;
-  }
-  for (int k = 0; k < 5; k++) t.last_obs[k] = b5[k];
-  if (t.n_obs > 0 && t.obs_age[t.n_obs - 1] == t.age) {
-    for (int k = 0; k < 5; k++) t.obs_box[t.n_obs - 1][k] = b5[k];
-  } else {
-    if (t.n_obs == OBS_KEEP) {
-      for (int q = 0; q + 1 < OBS_KEEP; q++) {
-        t.obs_age[q] = t.obs_age[q + 1];
-        for (int k = 0; k < 5; k++) t.obs_box[q][k] = t.obs_box[q + 1][k];
-      }
-      t.n_obs--;
+  const int rr = r < 7 ? r : 6;
+  const int observed = t.observed, has_saved = t.has_saved;
+  const int hv = t.hvalid, gap = t.htail + 1;
+  const double b1[4] = {t.hbox[0], t.hbox[1], t.hbox[2], t.hbox[3]};
+  if (r == 0) {
+    t.det_ind = det_ind;
+    t.conf = b5[4];
+    t.cls = cls;
+    if (sum5(t.last_obs) >= 0) {
+      const int q = obs_first(t, t.age - g.delta_t, g.delta_t);
+      const double* prev = q >= 0 ? t.obs_box[q] : t.last_obs;
+      // ocsort.py:48-53 speed_direction
+      const double cx1 = (prev[0] + prev[2]) / 2.0, cy1 = (prev[1] + prev[3]) / 2.0;
+      const double cx2 = (b5[0] + b5[2]) / 2.0, cy2 = (b5[1] + b5[3]) / 2.0;
+      const double sy = cy2 - cy1, sx = cx2 - cx1;
+      const double norm = sqrt((cy2 - cy1) * (cy2 - cy1) + (cx2 - cx1) * (cx2 - cx1)) + 1e-6;
+      t.vel[0] = sy / norm;
+      t.vel[1] = sx / norm;
+      t.has_vel = 1;
     }
-    t.obs_age[t.n_obs] = t.age;
-    for (int k = 0; k < 5; k++) t.obs_box[t.n_obs][k] = b5[k];
-    t.n_obs++;
+    for (int k = 0; k < 5; k++) t.last_obs[k] = b5[k];
+    const int slot = t.age & (OBS_KEEP - 1);  // observations[age] = bbox
+    t.obs_age[slot] = t.age;
+    for (int k = 0; k < 5; k++) t.obs_box[slot][k] = b5[k];
+    t.last_age = t.age;
+    t.tsu = 0;
+    t.hits++;
+    t.hit_streak++;
   }
-  t.tsu = 0;
-  t.hits++;
-  t.hit_streak++;
   // P1 xyxy2xysr
   const double w = b5[2] - b5[0], h = b5[3] - b5[1];
   const double z[4] = {b5[0] + w / 2.0, b5[1] + h / 2.0, w * h, w / (h + 1e-6)};
-  kf_update7(g, t, z);
+  KfRow k;
+  const bool unfreeze = !observed && has_saved;
+  if (unfreeze) {
+    // new_history = history + [z]: the previous non-None entry is hbox, htail+1 steps back;
+    // self.__dict__ = attr_saved restores (x, P); its history is overwritten by z below
+    row_load(t.sx, t.sP, rr, k);
+    if (hv) {
+      const double x1 = b1[0], y1 = b1[1], s1 = b1[2], r1 = b1[3];
+      const double w1 = sqrt(s1 * r1), h1 = sqrt(s1 / r1);
+      const double x2 = z[0], y2 = z[1], s2 = z[2], r2 = z[3];
+      const double w2 = sqrt(s2 * r2), h2 = sqrt(s2 / r2);
+      const double dx = (x2 - x1) / gap, dy = (y2 - y1) / gap;
+      const double dw = (w2 - w1) / gap, dh = (h2 - h1) / gap;
+      for (int i = 0; i < gap; i++) {
+        const double xx = x1 + (i + 1) * dx, yy = y1 + (i + 1) * dy;
+        const double ww = w1 + (i + 1) * dw, hh = h1 + (i + 1) * dh;
+        const double nb[4] = {xx, yy, ww * hh, ww / (double)hh};
+        kfo_update(rr, k, nb);
+        if (i != gap - 1) kfo_predict(g, rr, k);
+      }
+    }
+  } else {
+    row_load(t.x, t.P, rr, k);
+  }
+  kfo_update(rr, k, z);
+  row_store(t.x, t.P, r, k);
+  if (r == 0) {
+    if (unfreeze) t.has_saved = 0;
+    t.observed = 1;
+    for (int q = 0; q < 4; q++) t.hbox[q] = z[q];
+    t.htail = 0;
+    t.hvalid = 1;
+  }
 }
 
-// update(None): history_obs gets a None; the first miss after an observation freezes
-__device__ void ocs_update_none(const OcsDev& g, OcsTrk& t) {
-  t.det_ind = -1;
-  t.htail++;
-  if (t.htail >= g.max_obs) t.hvalid = 0;  // the box left the deque(maxlen=max_obs)
-  if (t.observed) {
-    t.has_saved = 1;
-    for (int i = 0; i < 7; i++) t.sx[i] = t.x[i];
-    for (int i = 0; i < 49; i++) t.sP[i] = t.P[i];
+// update(None), octet-wide: history_obs gets a None; the first miss after an observation
+// freezes (x, P)
+__device__ void ocs_update_none(const OcsDev& g, OcsTrk& t, int r) {
+  const int observed = t.observed;
+  if (observed && r < 7) {
+    t.sx[r] = t.x[r];
+#pragma unroll
+    for (int j = 0; j < 7; j++) t.sP[r * 7 + j] = t.P[r * 7 + j];
   }
-  t.observed = 0;
+  if (r == 0) {
+    t.det_ind = -1;
+    t.htail++;
+    if (t.htail >= g.max_obs) t.hvalid = 0;  // the box left the deque(maxlen=max_obs)
+    if (observed) t.has_saved = 1;
+    t.observed = 0;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -329,6 +423,7 @@ struct JvLds {
   int *x, *y, *matches, *freer, *pred, *col;
   int* sc;  // >= 8 ints of broadcast scratch
   double* sd;
+  unsigned long long* dc;  // diagnostic counters (timing builds) or null
 };
 
 __device__ __forceinline__ double cget(const double* C, int nr, int nc, int i, int j) {
@@ -339,6 +434,8 @@ __device__ double wave_min_d(double a) {
   for (int o = 32; o >= 1; o >>= 1) a = fmin(a, __shfl_xor(a, o));
   return a;
 }
+
+constexpr int JV_CH = 8;  // 64-position chunks of one relaxation (assignment sizes <= 512)
 
 __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
   const int n = nr > nc ? nr : nc;
@@ -397,6 +494,9 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
     }
   }
   __syncthreads();
+#ifdef BX_PHASE_TIMING
+  if (lane == 0 && w.dc) w.dc[0] += nfree;
+#endif
   // augmentation
   for (int f = 0; f < nfree; f++) {
     const int fr = w.freer[f];
@@ -409,61 +509,120 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
     int low = 0, up = 0, last = 0, endofpath = -1, found = 0;
     double mn = 0.0;
     do {
+#ifdef BX_PHASE_TIMING
+      if (lane == 0 && w.dc) w.dc[up == low ? 1 : 2] += 1;
+#endif
       if (up == low) {
-        // minimum scan over col[up..n): its swaps fix the later iteration order (lane 0)
-        if (lane == 0) {
-          last = low - 1;
-          mn = w.d[w.col[up++]];
-          for (int k = up; k < n; k++) {
-            const int j = w.col[k];
-            const double h = w.d[j];
-            if (h <= mn) {
-              if (h < mn) {
-                up = low;
-                mn = h;
-              }
-              w.col[k] = w.col[up];
-              w.col[up++] = j;
-            }
-          }
-          for (int k = low; k < up; k++)
-            if (w.y[w.col[k]] < 0) {
-              endofpath = w.col[k];
-              found = 1;
-              break;
-            }
-          w.sc[0] = last;
-          w.sc[1] = up;
-          w.sc[2] = endofpath;
-          w.sc[3] = found;
-          w.sd[0] = mn;
+        // Minimum scan.  The oracle's sequential scan gathers, in position order, every column
+        // at the minimum distance into col[low..up) and takes the first unassigned one as the
+        // path end.  When one exists the search ends here and the rest of the permutation it
+        // built is never read again (col is rebuilt for the next free row), so the lane-parallel
+        // path finds it directly; otherwise (or with NaN distances) the scan runs as written.
+        double m = INF;
+        bool bad = false;
+        for (int k = low + lane; k < n; k += OW) {
+          const double h = w.d[w.col[k]];
+          m = fmin(m, h);
+          bad |= isnan(h);
         }
-        __syncthreads();
-        last = w.sc[0];
-        up = w.sc[1];
-        endofpath = w.sc[2];
-        found = w.sc[3];
-        mn = w.sd[0];
-        __syncthreads();
+        m = wave_min_d(m);
+        bad = __any(bad) || !(m < INF);
+        int kg = -1, ke = -1;
+        if (!bad) {
+          for (int base = low; base < n && ke < 0; base += OW) {
+            const int k = base + lane;
+            bool G = false, E = false;
+            if (k < n) {
+              const int j = w.col[k];
+              G = w.d[j] == m;
+              E = G && w.y[j] < 0;
+            }
+            const unsigned long long gm = __ballot(G), em = __ballot(E);
+            if (kg < 0 && gm) kg = base + __ffsll((long long)gm) - 1;
+            if (em) ke = base + __ffsll((long long)em) - 1;
+          }
+        }
+#ifdef BX_PHASE_TIMING
+        if (lane == 0 && w.dc && ke < 0) w.dc[3] += 1;
+#endif
+        if (ke >= 0) {
+          last = low - 1;
+          mn = w.d[w.col[kg]];  // the first minimum, exactly as the sequential scan keeps it
+          endofpath = w.col[ke];
+          found = 1;
+        } else {
+          if (lane == 0) {
+            last = low - 1;
+            mn = w.d[w.col[up++]];
+            for (int k = up; k < n; k++) {
+              const int j = w.col[k];
+              const double h = w.d[j];
+              if (h <= mn) {
+                if (h < mn) {
+                  up = low;
+                  mn = h;
+                }
+                w.col[k] = w.col[up];
+                w.col[up++] = j;
+              }
+            }
+            for (int k = low; k < up; k++)
+              if (w.y[w.col[k]] < 0) {
+                endofpath = w.col[k];
+                found = 1;
+                break;
+              }
+            w.sc[0] = last;
+            w.sc[1] = up;
+            w.sc[2] = endofpath;
+            w.sc[3] = found;
+            w.sd[0] = mn;
+          }
+          __syncthreads();
+          last = w.sc[0];
+          up = w.sc[1];
+          endofpath = w.sc[2];
+          found = w.sc[3];
+          mn = w.sd[0];
+          __syncthreads();
+        }
       }
       if (!found) {
         const int j1 = w.col[low++];
         const int i = w.y[j1];
         const double h = cget(C, nr, nc, i, j1) - w.v[j1] - mn;
         // relaxation from row i over col[up..n) in chunks of 64 positions; the first column
-        // reached at distance mn that is unassigned ends the path (the oracle's break)
+        // reached at distance mn that is unassigned ends the path (the oracle's break).  Every
+        // operand of every chunk is loaded up front: a swap writes only positions up to the
+        // chunk in flight, and each column appears once, so later chunks read what the
+        // sequential loop would.
         const int up0 = up;
-        for (int base = up0; base < n && !found; base += OW) {
-          const int k = base + lane;
-          int j = -1;
-          double v2 = 0.0;
-          bool A = false, B = false, E = false;
+        int jc[JV_CH];
+        double v2c[JV_CH], dc[JV_CH];
+        bool yc[JV_CH];
+#pragma unroll
+        for (int c = 0; c < JV_CH; c++) {
+          const int k = up0 + c * OW + lane;
+          jc[c] = -1;
           if (k < n) {
-            j = w.col[k];
-            v2 = cget(C, nr, nc, i, j) - w.v[j] - h;
-            A = v2 < w.d[j];
+            const int j = w.col[k];
+            jc[c] = j;
+            v2c[c] = cget(C, nr, nc, i, j) - w.v[j] - h;
+            dc[c] = w.d[j];
+            yc[c] = w.y[j] < 0;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < JV_CH; c++) {
+          const int base = up0 + c * OW;
+          if (base >= n || found) break;
+          const int j = jc[c];
+          const double v2 = v2c[c];
+          bool A = false, B = false, E = false;
+          if (j >= 0) {
+            A = v2 < dc[c];
             B = A && v2 == mn;
-            E = B && w.y[j] < 0;
+            E = B && yc[c];
           }
           const unsigned long long em = __ballot(E);
           int kE = OW;
@@ -474,17 +633,17 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
           }
           if (em && lane == kE) w.pred[j] = i;
           unsigned long long hm = __ballot(B && !E && lane < kE);
-          __syncthreads();
-          while (hm) {  // the swaps, in position order
-            const int b = __ffsll((long long)hm) - 1;
-            hm &= hm - 1;
-            const int jb = __shfl(j, b);
-            if (lane == 0) {
-              w.col[base + b] = w.col[up];
-              w.col[up] = jb;
+          if (hm) {
+            while (hm) {  // the swaps, in position order (lane 0 owns col)
+              const int bb = __ffsll((long long)hm) - 1;
+              hm &= hm - 1;
+              const int jb = __shfl(j, bb);
+              if (lane == 0) {
+                w.col[base + bb] = w.col[up];
+                w.col[up] = jb;
+              }
+              up++;
             }
-            up++;
-            __syncthreads();
           }
           if (em) {
             endofpath = __shfl(j, kE);
@@ -604,6 +763,7 @@ __global__ void __launch_bounds__(OW)
   carve(g, lds_raw, L);
   const int lane = threadIdx.x;
   const int b = blockIdx.x, seq = seq0 + b;
+  L.jv.dc = g.dbg ? g.dbg + (size_t)seq * OCS_DBG + 24 : nullptr;
   const int r0 = det_off[b];
   int n = det_off[b + 1] - r0;
   if (n > g.D) {  // the host checks det_cap; a device-side overflow is latched, never run past
@@ -615,6 +775,9 @@ __global__ void __launch_bounds__(OW)
   int* order = g.order + (size_t)seq * g.T;
   double* tb = g.tb + (size_t)seq * g.T * TB;
   double* cost = g.cost_g ? g.cost_g + (size_t)seq * g.D * g.T : nullptr;
+#ifdef BX_PHASE_TIMING
+  unsigned long long t_last = __builtin_amdgcn_s_memtime();
+#endif
   const int frame = sq[SO_FRAME] + 1;
   const int id0 = sq[SO_IDS];
   const int nt0 = sq[SO_NTR];
@@ -630,47 +793,63 @@ __global__ void __launch_bounds__(OW)
   const int nh = wave_compact(
       n, [&](int i) { return L.dd[6 * i + 4] > g.det_thresh; }, [&](int i, int p) { L.hi[p] = i; });
 
-  // predict every track; tracks whose prediction has a NaN leave the list (ocsort.py:278-288)
+  const int oct = lane >> 3, r8 = lane & 7, rr8 = r8 < 7 ? r8 : 6;
+
+  // predict every track (an octet per track); tracks whose prediction has a NaN leave the list
+  // (ocsort.py:278-288).  tb row per kept track: box[4], k-previous obs[5], last_obs[5], vel[2]
   int nt = 0;
-  for (int c = 0; c < nt0; c += OW) {
-    const int p = c + lane;
-    double bx[4] = {0, 0, 0, 0};
-    int slot = -1;
+  for (int c = 0; c < nt0; c += 8) {
+    const int p = c + oct;
     bool keep = false;
+    int slot = -1;
+    double v0 = 0.0, v1 = 0.0;  // this lane's two tb entries: [r8] and [8 + r8]
     if (p < nt0) {
       slot = L.lst2[p];
       OcsTrk& t = trk[slot];
-      if ((t.x[6] + t.x[2]) <= 0) t.x[6] *= 0.0;
-      kf_predict7(g, t.x, t.P);
-      t.age++;
-      if (t.tsu > 0) t.hit_streak = 0;
-      t.tsu++;
-      x_to_bbox(t.x, bx);
-      keep = !(isnan(bx[0]) || isnan(bx[1]) || isnan(bx[2]) || isnan(bx[3]));
-    }
-    const unsigned long long m = __ballot(keep);
-    if (keep) {
-      const int q = nt + __popcll(m & ((1ull << lane) - 1ull));
-      L.lst[q] = slot;
-      double* r = tb + (size_t)q * TB;
-      const OcsTrk& t = trk[slot];
-      for (int k = 0; k < 4; k++) r[k] = bx[k];
-      // k_previous_obs (ocsort.py:17-28) -> r[4..8]; last_obs -> r[9..13]; velocity -> r[14..15]
-      if (t.n_obs == 0) {
-        for (int k = 0; k < 5; k++) r[4 + k] = -1.0;
-      } else {
-        int qq = -1;
-        for (int i = 0; i < g.delta_t && qq < 0; i++) qq = obs_find(t, t.age - (g.delta_t - i));
-        if (qq < 0) qq = t.n_obs - 1;
-        for (int k = 0; k < 5; k++) r[4 + k] = t.obs_box[qq][k];
+      KfRow k;
+      row_load(t.x, t.P, rr8, k);
+      if ((osh(k.x, 6) + osh(k.x, 2)) <= 0 && rr8 == 6) k.x *= 0.0;
+      kfo_predict(g, rr8, k);
+      row_store(t.x, t.P, r8, k);
+      const int age = t.age + 1;
+      if (r8 == 0) {
+        t.age = age;
+        if (t.tsu > 0) t.hit_streak = 0;
+        t.tsu++;
       }
-      for (int k = 0; k < 5; k++) r[9 + k] = t.last_obs[k];
-      r[14] = t.has_vel ? t.vel[0] : 0.0;
-      r[15] = t.has_vel ? t.vel[1] : 0.0;
+      double xs[4], bx[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) xs[q] = osh(k.x, q);
+      x_to_bbox(xs, bx);
+      keep = !(isnan(bx[0]) || isnan(bx[1]) || isnan(bx[2]) || isnan(bx[3]));
+      // k_previous_obs (ocsort.py:17-28) with the post-predict age
+      int qq = -1;
+      const int last_age = t.last_age;
+      if (last_age >= 0) {
+        qq = obs_first(t, age - g.delta_t, g.delta_t);
+        if (qq < 0) qq = last_age & (OBS_KEEP - 1);  // observations[max(keys)]
+      }
+      auto val = [&](int e) -> double {
+        if (e < 4) return e == 0 ? bx[0] : e == 1 ? bx[1] : e == 2 ? bx[2] : bx[3];
+        if (e < 9) return qq < 0 ? -1.0 : t.obs_box[qq][e - 4];
+        if (e < 14) return t.last_obs[e - 9];
+        return t.has_vel ? t.vel[e - 14] : 0.0;
+      };
+      v0 = val(r8);
+      v1 = val(8 + r8);
+    }
+    const unsigned long long m = __ballot(keep && r8 == 0);
+    if (keep) {
+      const int q = nt + __popcll(m & ((1ull << (lane & ~7)) - 1ull));
+      if (r8 == 0) L.lst[q] = slot;
+      double* row = tb + (size_t)q * TB;
+      row[r8] = v0;
+      row[8 + r8] = v1;
     }
     nt += __popcll(m);
   }
   __syncthreads();
+  OSTAMP(1);
 
   // ---- first association: enhanced_associate(high dets, predicted tracks) -----------------
   int nm = 0, nud = 0, nut = 0;
@@ -680,36 +859,38 @@ __global__ void __launch_bounds__(OW)
   } else {
     int nmi = 0;
     if (nh > 0) {
-      double* C = (nh * nt <= g.cost_lds) ? L.cost : cost;
-      for (int k = lane; k < g.N; k += OW) L.rowcnt[k] = L.colcnt[k] = 0;
+      // pass 1 (lane per track, dets broadcast from LDS): IoU > threshold counts for the
+      // one-to-one test.  A pair without overlap has IoU 0/U, never above a threshold >= 0, so
+      // only overlapping pairs divide.
+      for (int k = lane; k < g.N; k += OW) L.rowcnt[k] = 0;
       __syncthreads();
-      for (int q = lane; q < nh * nt; q += OW) {
-        const int d = q / nt, ti = q - d * nt;
-        const double* a = L.dd + 6 * L.hi[d];
-        const double* r = tb + (size_t)ti * TB;
-        const double o = iou_pair(a, r);
-        // speed_direction_batch (association.py:10-20) against the k-previous observation
-        const double* p = r + 4;
-        const double cx1 = (a[0] + a[2]) / 2.0, cy1 = (a[1] + a[3]) / 2.0;
-        const double cx2 = (p[0] + p[2]) / 2.0, cy2 = (p[1] + p[3]) / 2.0;
-        double dx = cx1 - cx2, dy = cy1 - cy2;
-        const double norm = sqrt(dx * dx + dy * dy) + 1e-6;
-        dx = dx / norm;
-        dy = dy / norm;
-        double c = r[15] * dx + r[14] * dy;
-        c = c < -1 ? -1 : (c > 1 ? 1 : c);
-        double ang = ocs_acos(c);
-        ang = (3.14159265358979323846 / 2.0 - fabs(ang)) / 3.14159265358979323846;
-        const double valid = p[4] < 0 ? 0.0 : 1.0;
-        const double mc = (valid * ang) * g.inertia;
-        C[q] = -(o + mc);
-        if (o > thr) {
-          atomicAdd(&L.rowcnt[d], 1);
-          atomicAdd(&L.colcnt[ti], 1);
-          L.rowcol[d] = ti;
+      for (int c = 0; c < nt; c += OW) {
+        const int ti = c + lane;
+        if (ti < nt) {
+          const double* bq = tb + (size_t)ti * TB;
+          const double b0 = bq[0], b1 = bq[1], b2 = bq[2], b3 = bq[3];
+          const double at = (b2 - b0) * (b3 - b1);
+          int cc = 0;
+          for (int d = 0; d < nh; d++) {
+            const double* a = L.dd + 6 * L.hi[d];
+            const double xx1 = fmax(a[0], b0), yy1 = fmax(a[1], b1);
+            const double xx2 = fmin(a[2], b2), yy2 = fmin(a[3], b3);
+            const double w = fmax(0.0, xx2 - xx1), h = fmax(0.0, yy2 - yy1);
+            const double wh = w * h;
+            if (wh > 0.0 || thr < 0.0) {
+              const double o = wh / ((a[2] - a[0]) * (a[3] - a[1]) + at - wh);
+              if (o > thr) {
+                atomicAdd(&L.rowcnt[d], 1);
+                L.rowcol[d] = ti;
+                cc++;
+              }
+            }
+          }
+          L.colcnt[ti] = cc;
         }
       }
       __syncthreads();
+      OSTAMP(2);
       int mr = 0, mcx = 0;
       for (int k = lane; k < nh; k += OW) mr = max(mr, L.rowcnt[k]);
       for (int k = lane; k < nt; k += OW) mcx = max(mcx, L.colcnt[k]);
@@ -724,9 +905,42 @@ __global__ void __launch_bounds__(OW)
               L.mi[2 * p] = d;
               L.mi[2 * p + 1] = L.rowcol[d];
             });
-      } else {  // P4: legacy linear_assignment(-total)
+      } else {
+        // pass 2: the full cost -(IoU + direction consistency) and P4's legacy
+        // linear_assignment of it
+        double* C = (nh * nt <= g.cost_lds) ? L.cost : cost;
+        for (int c = 0; c < nt; c += OW) {
+          const int ti = c + lane;
+          if (ti < nt) {
+            const double* r = tb + (size_t)ti * TB;
+            const double* p = r + 4;
+            const double cx2 = (p[0] + p[2]) / 2.0, cy2 = (p[1] + p[3]) / 2.0;
+            const double vy = r[14], vx = r[15];
+            const double valid = p[4] < 0 ? 0.0 : 1.0;
+            for (int d = 0; d < nh; d++) {
+              const double* a = L.dd + 6 * L.hi[d];
+              const double o = iou_pair(a, r);
+              // speed_direction_batch (association.py:10-20) against the k-previous obs
+              const double cx1 = (a[0] + a[2]) / 2.0, cy1 = (a[1] + a[3]) / 2.0;
+              double dx = cx1 - cx2, dy = cy1 - cy2;
+              const double norm = sqrt(dx * dx + dy * dy) + 1e-6;
+              dx = dx / norm;
+              dy = dy / norm;
+              double cth = vx * dx + vy * dy;
+              cth = cth < -1 ? -1 : (cth > 1 ? 1 : cth);
+              double ang = ocs_acos(cth);
+              ang = (3.14159265358979323846 / 2.0 - fabs(ang)) / 3.14159265358979323846;
+              const double mc = (valid * ang) * g.inertia;
+              C[d * nt + ti] = -(o + mc);
+            }
+          }
+        }
+        __syncthreads();
         nmi = legacy_lap(C, nh, nt, L.jv, L.mi);
+        OCOUNT(0, 1);
+        OCOUNT(1, nh > nt ? nh : nt);
       }
+      OSTAMP(3);
     }
     // P3: unmatched = absent from the candidate pairs, ascending; then the IoU validation with
     // rejected pairs appended in pair order (P5)
@@ -767,34 +981,71 @@ __global__ void __launch_bounds__(OW)
     }
     __syncthreads();
   }
-  for (int q = lane; q < nm; q += OW) {
-    const double* r = L.dd + 6 * L.hi[L.mm[2 * q]];
-    ocs_update_det(g, trk[L.lst[L.mm[2 * q + 1]]], r, r[5], L.hi[L.mm[2 * q]]);
+  for (int c = 0; c < nm; c += 8) {
+    const int q = c + oct;
+    if (q < nm) {
+      const double* r = L.dd + 6 * L.hi[L.mm[2 * q]];
+      ocs_update_det(g, trk[L.lst[L.mm[2 * q + 1]]], r8, r, r[5], L.hi[L.mm[2 * q]]);
+    }
   }
   __syncthreads();
+  OSTAMP(4);
+
+  // IoU matrix of detections (LDS rows `dsel`) x track boxes (tb rows `tsel`, offset `boff`):
+  // its maximum (overlapping pairs only divide: a threshold >= 0 never passes 0/U), and, when
+  // asked, the full matrix -IoU into C [nr][nc]
+  auto iou_max = [&](int nr, const int* dsel, const int* dmap, int nc, const int* tsel, int boff) {
+    double mx = -INF;
+    for (int c = 0; c < nc; c += OW) {
+      const int k = c + lane;
+      if (k < nc) {
+        const double* bq = tb + (size_t)tsel[k] * TB + boff;
+        const double b0 = bq[0], b1 = bq[1], b2 = bq[2], b3 = bq[3];
+        const double at = (b2 - b0) * (b3 - b1);
+        for (int d = 0; d < nr; d++) {
+          const double* a = L.dd + 6 * dsel[dmap ? dmap[d] : d];
+          const double xx1 = fmax(a[0], b0), yy1 = fmax(a[1], b1);
+          const double xx2 = fmin(a[2], b2), yy2 = fmin(a[3], b3);
+          const double w = fmax(0.0, xx2 - xx1), h = fmax(0.0, yy2 - yy1);
+          const double wh = w * h;
+          if (wh > 0.0 || thr < 0.0) mx = fmax(mx, wh / ((a[2] - a[0]) * (a[3] - a[1]) + at - wh));
+        }
+      }
+    }
+    for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+    return mx;
+  };
+  auto iou_fill = [&](double* C, int nr, const int* dsel, const int* dmap, int nc, const int* tsel,
+                      int boff) {
+    for (int c = 0; c < nc; c += OW) {
+      const int k = c + lane;
+      if (k < nc) {
+        const double* bq = tb + (size_t)tsel[k] * TB + boff;
+        for (int d = 0; d < nr; d++) C[d * nc + k] = -iou_pair(L.dd + 6 * dsel[dmap ? dmap[d] : d], bq);
+      }
+    }
+    __syncthreads();
+  };
 
   // ---- BYTE round on the low-confidence detections (ocsort.py:330-356) ---------------------
   if (g.use_byte && nl > 0 && nut > 0) {
-    double* C = (nl * nut <= g.cost_lds) ? L.cost : cost;
-    double mx = -INF;
-    for (int q = lane; q < nl * nut; q += OW) {
-      const int d = q / nut, k = q - d * nut;
-      const double o = iou_pair(L.dd + 6 * L.lo[d], tb + (size_t)L.ut[k] * TB);
-      C[q] = -o;
-      mx = fmax(mx, o);
-    }
-    for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-    __syncthreads();
+    const double mx = iou_max(nl, L.lo, nullptr, nut, L.ut, 0);
     if (mx > thr) {
+      double* C = (nl * nut <= g.cost_lds) ? L.cost : cost;
+      iou_fill(C, nl, L.lo, nullptr, nut, L.ut, 0);
       const int np_ = legacy_lap(C, nl, nut, L.jv, L.mi);
       for (int k = lane; k < g.N; k += OW) L.fl[k] = 0;
       __syncthreads();
-      for (int q = lane; q < np_; q += OW) {
-        const int dl = L.mi[2 * q], k = L.mi[2 * q + 1];
-        if (-C[dl * nut + k] < thr) continue;
-        const double* r = L.dd + 6 * L.lo[dl];
-        ocs_update_det(g, trk[L.lst[L.ut[k]]], r, r[5], L.lo[dl]);
-        L.fl[L.ut[k]] = 2;  // removed
+      for (int c = 0; c < np_; c += 8) {
+        const int q = c + oct;
+        if (q < np_) {
+          const int dl = L.mi[2 * q], k = L.mi[2 * q + 1];
+          if (!(-C[dl * nut + k] < thr)) {
+            const double* r = L.dd + 6 * L.lo[dl];
+            ocs_update_det(g, trk[L.lst[L.ut[k]]], r8, r, r[5], L.lo[dl]);
+            if (r8 == 0) L.fl[L.ut[k]] = 2;  // removed
+          }
+        }
       }
       __syncthreads();
       for (int k = lane; k < nut; k += OW)
@@ -802,33 +1053,37 @@ __global__ void __launch_bounds__(OW)
       __syncthreads();
       // np.setdiff1d: ascending, unique
       nut = wave_compact(nt, [&](int t) { return L.fl[t] == 1; }, [&](int t, int p) { L.ut[p] = t; });
+      OCOUNT(2, 1);
     }
   }
+  OSTAMP(5);
 
   // ---- OCR round on the last observations (ocsort.py:358-386) -------------------------------
   if (nud > 0 && nut > 0) {
-    double* C = (nud * nut <= g.cost_lds) ? L.cost : cost;
-    double mx = -INF;
-    for (int q = lane; q < nud * nut; q += OW) {
-      const int d = q / nut, k = q - d * nut;
-      const double o = iou_pair(L.dd + 6 * L.hi[L.ud[d]], tb + (size_t)L.ut[k] * TB + 9);
-      C[q] = -o;
-      mx = fmax(mx, o);
-    }
-    for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-    __syncthreads();
+    const double mx = iou_max(nud, L.hi, L.ud, nut, L.ut, 9);
+    OSTAMP(6);
     if (mx > thr) {
+      double* C = (nud * nut <= g.cost_lds) ? L.cost : cost;
+      iou_fill(C, nud, L.hi, L.ud, nut, L.ut, 9);
       const int np_ = legacy_lap(C, nud, nut, L.jv, L.mi);
+      OCOUNT(3, 1);
+      OCOUNT(4, nud > nut ? nud : nut);
       for (int k = lane; k < g.N; k += OW) L.rowcnt[k] = L.fl[k] = 0;
       __syncthreads();
-      for (int q = lane; q < np_; q += OW) {
-        const int a = L.mi[2 * q], k = L.mi[2 * q + 1];
-        if (-C[a * nut + k] < thr) continue;
-        const int di = L.ud[a], ti = L.ut[k];
-        const double* r = L.dd + 6 * L.hi[di];
-        ocs_update_det(g, trk[L.lst[ti]], r, r[5], L.hi[di]);
-        L.rowcnt[di] = 2;
-        L.fl[ti] = 2;
+      for (int c = 0; c < np_; c += 8) {
+        const int q = c + oct;
+        if (q < np_) {
+          const int a = L.mi[2 * q], k = L.mi[2 * q + 1];
+          if (!(-C[a * nut + k] < thr)) {
+            const int di = L.ud[a], ti = L.ut[k];
+            const double* r = L.dd + 6 * L.hi[di];
+            ocs_update_det(g, trk[L.lst[ti]], r8, r, r[5], L.hi[di]);
+            if (r8 == 0) {
+              L.rowcnt[di] = 2;
+              L.fl[ti] = 2;
+            }
+          }
+        }
       }
       __syncthreads();
       for (int k = lane; k < nud; k += OW)
@@ -840,49 +1095,59 @@ __global__ void __launch_bounds__(OW)
       nut = wave_compact(nt, [&](int t) { return L.fl[t] == 1; }, [&](int t, int p) { L.ut[p] = t; });
     }
   }
-  for (int k = lane; k < nut; k += OW) ocs_update_none(g, trk[L.lst[L.ut[k]]]);
+  OSTAMP(7);
+  for (int c = 0; c < nut; c += 8) {
+    const int k = c + oct;
+    if (k < nut) ocs_update_none(g, trk[L.lst[L.ut[k]]], r8);
+  }
 
   // ---- new tracks for the unmatched high detections (free slots ascending) ----------------
-  for (int s = lane; s < g.T; s += OW) L.fl[s] = 0;
+  for (int s2 = lane; s2 < g.T; s2 += OW) L.fl[s2] = 0;
   __syncthreads();
   for (int p = lane; p < nt; p += OW) L.fl[L.lst[p]] = 1;
   __syncthreads();
-  const int nfree = wave_compact(g.T, [&](int s) { return L.fl[s] == 0; }, [&](int s, int p) { L.lst2[p] = s; });
+  const int nfree = wave_compact(g.T, [&](int s2) { return L.fl[s2] == 0; }, [&](int s2, int p) { L.lst2[p] = s2; });
   int nnew = nud;
   if (nnew > nfree) {
     if (lane == 0) atomicExch(g.status, (int)BX_ERR_TRACK_OVERFLOW);
     nnew = nfree;
   }
-  for (int k = lane; k < nnew; k += OW) {
-    const int slot = L.lst2[k];
-    const double* r = L.dd + 6 * L.hi[L.ud[k]];
-    OcsTrk& t = trk[slot];
-    for (int i = 0; i < 7; i++) t.x[i] = 0.0;
-    for (int i = 0; i < 49; i++) t.P[i] = 0.0;
-    const double pd[7] = {10.0, 10.0, 10.0, 10.0, 10000.0, 10000.0, 10000.0};
-    for (int i = 0; i < 7; i++) t.P[i * 8] = pd[i];
-    const double w = r[2] - r[0], h = r[3] - r[1];
-    t.x[0] = r[0] + w / 2.0;
-    t.x[1] = r[1] + h / 2.0;
-    t.x[2] = w * h;
-    t.x[3] = w / (h + 1e-6);
-    t.observed = 0;
-    t.has_saved = 0;
-    t.hvalid = 0;
-    t.htail = 0;
-    t.id = id0 + k;
-    t.conf = r[4];
-    t.cls = r[5];
-    t.det_ind = L.hi[L.ud[k]];
-    for (int q = 0; q < 5; q++) t.last_obs[q] = -1.0;
-    t.n_obs = 0;
-    t.has_vel = 0;
-    t.vel[0] = t.vel[1] = 0.0;
-    t.tsu = t.hits = t.hit_streak = t.age = 0;
-    L.lst[nt + k] = slot;
+  for (int c = 0; c < nnew; c += 8) {
+    const int k = c + oct;
+    if (k < nnew) {
+      const int slot = L.lst2[k];
+      const double* r = L.dd + 6 * L.hi[L.ud[k]];
+      OcsTrk& t = trk[slot];
+      const double w = r[2] - r[0], h = r[3] - r[1];
+      const double z[4] = {r[0] + w / 2.0, r[1] + h / 2.0, w * h, w / (h + 1e-6)};
+      if (r8 < 7) {
+        t.x[r8] = r8 == 0 ? z[0] : r8 == 1 ? z[1] : r8 == 2 ? z[2] : r8 == 3 ? z[3] : 0.0;
+        const double pd = r8 < 4 ? 10.0 : 10000.0;
+#pragma unroll
+        for (int j = 0; j < 7; j++) t.P[r8 * 7 + j] = j == r8 ? pd : 0.0;
+      }
+      if (r8 == 0) {
+        t.observed = 0;
+        t.has_saved = 0;
+        t.hvalid = 0;
+        t.htail = 0;
+        t.id = id0 + k;
+        t.conf = r[4];
+        t.cls = r[5];
+        t.det_ind = L.hi[L.ud[k]];
+        for (int q = 0; q < 5; q++) t.last_obs[q] = -1.0;
+        t.last_age = -1;
+        for (int q = 0; q < OBS_KEEP; q++) t.obs_age[q] = -1;
+        t.has_vel = 0;
+        t.vel[0] = t.vel[1] = 0.0;
+        t.tsu = t.hits = t.hit_streak = t.age = 0;
+        L.lst[nt + k] = slot;
+      }
+    }
   }
   __syncthreads();
   const int ntr = nt + nnew;
+  OSTAMP(8);
 
   // ---- outputs in reversed list order, then deletion of the dead (ocsort.py:414-436) ---------
   double* orow = out + (size_t)r0 * 8;
@@ -912,6 +1177,10 @@ __global__ void __launch_bounds__(OW)
   const int nkeep = wave_compact(
       ntr, [&](int k) { return trk[L.lst[k]].tsu <= g.max_age; },
       [&](int k, int p) { order[p] = L.lst[k]; });
+  OSTAMP(9);
+  OCOUNT(5, nt);
+  OCOUNT(6, nh);
+  OCOUNT(7, 1);
   if (lane == 0) {
     out_count[b] = nout < n ? nout : n;
     sq[SO_FRAME] = frame;
@@ -976,8 +1245,8 @@ extern "C" {
 
 int bx_ocsort_create(const bx_ocsort_config* c, bx_ocsort** out) {
   if (!c || !out) return bx_record_error(BX_ERR_INVALID, "null argument");
-  if (c->n_seq <= 0 || c->track_cap <= 0 || c->det_cap <= 0 || c->track_cap > 4096 ||
-      c->det_cap > 4096)
+  if (c->n_seq <= 0 || c->track_cap <= 0 || c->det_cap <= 0 || c->track_cap > 512 ||
+      c->det_cap > 512)
     return bx_record_error(BX_ERR_INVALID, "n_seq/track_cap/det_cap out of range");
   if (c->delta_t < 1 || c->delta_t > OBS_KEEP - 1)
     return bx_record_error(BX_ERR_INVALID, "delta_t must be in [1, 7]");
@@ -1026,6 +1295,9 @@ int bx_ocsort_create(const bx_ocsort_config* c, bx_ocsort** out) {
   const size_t o_tb = carve_b(S * T * TB * sizeof(double));
   const size_t o_cg = need_g ? carve_b(S * (size_t)d.D * T * sizeof(double)) : 0;
   const size_t o_st = carve_b(sizeof(int) * 4);
+#ifdef BX_PHASE_TIMING
+  const size_t o_dbg = carve_b(S * OCS_DBG * sizeof(unsigned long long));
+#endif
   if (hipMalloc(&e->arena, off) != hipSuccess) {
     delete e;
     return bx_record_error(BX_ERR_HIP, "hipMalloc of the OCSort arena failed");
@@ -1038,6 +1310,11 @@ int bx_ocsort_create(const bx_ocsort_config* c, bx_ocsort** out) {
   d.tb = (double*)(base + o_tb);
   d.cost_g = need_g ? (double*)(base + o_cg) : nullptr;
   d.status = (int*)(base + o_st);
+#ifdef BX_PHASE_TIMING
+  d.dbg = (unsigned long long*)(base + o_dbg);
+#else
+  d.dbg = nullptr;
+#endif
   OCHK(hipFuncSetAttribute((const void*)ocsort_frame_kernel,
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->lds));
   OCHK(hipMalloc(&e->h_dets, sizeof(float) * 6 * d.D));
@@ -1150,6 +1427,35 @@ int bx_ocsort_tracks_host(bx_ocsort* e, int seq, int cap, int32_t* ids, double* 
     if (p) memcpy(p + 49 * k, t.P, sizeof(t.P));
   }
   *n = nt;
+  return BX_OK;
+}
+
+int bx_ocsort_frame_stats_host(bx_ocsort* e, int seq0, int nseq, int64_t* sums) {
+  if (!e || !sums || seq0 < 0 || nseq < 0 || seq0 + nseq > e->dev.S)
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ocsort_frame_stats_host");
+  std::vector<int> s((size_t)nseq * SQO);
+  OCHK(hipDeviceSynchronize());
+  if (nseq)
+    OCHK(hipMemcpy(s.data(), e->dev.seqst + (size_t)seq0 * SQO, sizeof(int) * s.size(),
+                   hipMemcpyDeviceToHost));
+  int64_t t = 0, o = 0, f = 0;
+  for (int k = 0; k < nseq; k++) {
+    t += s[(size_t)k * SQO + SO_NTR];
+    o += s[(size_t)k * SQO + SO_NOUT];
+    f = s[(size_t)k * SQO + SO_FRAME] > f ? s[(size_t)k * SQO + SO_FRAME] : f;
+  }
+  sums[0] = t;
+  sums[1] = o;
+  sums[2] = f;
+  return BX_OK;
+}
+
+// diagnostic (not in the public header): the phase stamps of every sequence, [S][OCS_DBG]
+int bx_ocsort_debug_host(bx_ocsort* e, unsigned long long* out) {
+  if (!e || !out || !e->dev.dbg) return bx_record_error(BX_ERR_INVALID, "not a timing build");
+  OCHK(hipDeviceSynchronize());
+  OCHK(hipMemcpy(out, e->dev.dbg, sizeof(unsigned long long) * OCS_DBG * e->dev.S,
+                 hipMemcpyDeviceToHost));
   return BX_OK;
 }
 

@@ -270,6 +270,13 @@ class OcsortEngine:
         k = min(n.value, cap)
         return {"id": ids[:k], "x": x[:k], "P": P[:k]}
 
+    def frame_stats(self, seq0: int = 0, nseq: int | None = None) -> dict:
+        """Last frame over sequences [seq0, seq0+nseq): live tracks, output rows, frame."""
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        a = (C.c_int64 * 3)()
+        N.check(self._L.bx_ocsort_frame_stats_host(self._h, seq0, nseq, a), "frame_stats")
+        return dict(zip(["tracks", "outputs", "frame"], [int(x) for x in a]))
+
     def probe(self, on: bool = True) -> None:
         N.check(self._L.bx_ocsort_probe(self._h, int(bool(on))), "bx_ocsort_probe")
 

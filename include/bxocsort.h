@@ -39,8 +39,8 @@ extern "C" {
  * OCSort path evaluates). */
 typedef struct {
     int32_t n_seq;      /* independent sequences held by this engine */
-    int32_t track_cap;  /* track slots per sequence */
-    int32_t det_cap;    /* max detections per frame per sequence */
+    int32_t track_cap;  /* track slots per sequence (<= 512) */
+    int32_t det_cap;    /* max detections per frame per sequence (<= 512) */
     double min_conf, det_thresh, asso_threshold, inertia, q_xy_scaling, q_s_scaling;
     int32_t max_age, min_hits, delta_t, use_byte;
 } bx_ocsort_config;
@@ -74,6 +74,9 @@ int bx_ocsort_set_id_count(bx_ocsort *e, int seq, int id_count, void *stream);
  * [cap][7] and covariances p [cap][49] (any may be NULL); *n = number of tracks. */
 int bx_ocsort_tracks_host(bx_ocsort *e, int seq, int cap, int32_t *ids, double *x, double *p,
                           int *n);
+/* Last-frame statistics over sequences [seq0, seq0+nseq) (host, synchronous): sums[3] =
+ * {tracks alive after the frame, output rows, max frame counter} — bench.py's unit counts. */
+int bx_ocsort_frame_stats_host(bx_ocsort *e, int seq0, int nseq, int64_t *sums);
 /* Timing probe (benchmarks): while on, every step records a HIP event pair around its kernel;
  * probe_read synchronises and returns the summed milliseconds and launch count, then clears. */
 int bx_ocsort_probe(bx_ocsort *e, int on);
