@@ -18,7 +18,8 @@ STAGE_OF = {"det_feature_kernel": "det_features", "predict_kernel": "predict",
             "gate_kernel": "gate", "cosine_kernel": "cosine", "cosine_kernel_any": "cosine",
             "assoc_kernel": "assoc", "update_kernel": "update",
             "cov_predict_kernel": "cov_predict", "cov_predict_gmc_kernel": "cov_predict",
-            "feature_kernel": "features", "finish_kernel": "finish"}
+            "feature_kernel": "features", "finish_kernel": "finish",
+            "ocsort_frame_kernel": "ocsort_frame"}
 
 
 def kname(full):
