@@ -18,6 +18,8 @@
  *   bx_kf_*                BaseKalmanFilter + XYAH/XYWH noise models
  *                          boxmot/motion/kalman_filters/aabb/base_kalman_filter.py:24-194,
  *                          xyah_kf.py:8-79, xywh_kf.py:8-66
+ *   bx_nn_cosine_distance  StrongSort NearestNeighborDistanceMetric.distance (cosine)
+ *                          boxmot/trackers/strongsort/sort/linear_assignment.py:468-618
  *   bx_linear_assignment   matching.enhanced_linear_assignment (lapx.lapjv extend_cost=True,
  *                          cost_limit=thresh)        boxmot/utils/matching.py:30-141
  *
@@ -141,6 +143,16 @@ int bx_kf_gating_distance(int kind, int n, const double *mean, const double *cov
                           const double *z, int nz, double *out, void *stream);
 /* lapx extend_cost + cost_limit semantics on a dense [nr][nc] cost: x [nr] (col or -1),
  * y [nc] (row or -1); matches are the pairs with x>=0 (all have cost < thresh). */
+/* StrongSort appearance metric (NearestNeighborDistanceMetric.distance with the cosine metric,
+ * trackers/strongsort/sort/linear_assignment.py:468-497,595-618): samples [G][F] float64 is every
+ * target's gallery packed by target (target t owns rows off[t]..off[t+1], off [T+1] int32 on the
+ * device, off[T] == G); feats [D][F] float64.  out [T][D] = min over the target's samples of
+ * 1 - clip(ŝ·d̂, -1, 1) with x̂ = x / (‖x‖ + 1e-8) (numpy's pairwise norm), 1e5 for a target
+ * without samples.  fp64 matrix cores (k-ordered fma chain, bitwise = the oracle).
+ * flags: BX_NN_SAMPLES_NORMALIZED = the samples are already x̂ (a gallery kept normalised). */
+#define BX_NN_SAMPLES_NORMALIZED 1
+int bx_nn_cosine_distance(const double *samples, int G, const int32_t *off, int T,
+                          const double *feats, int D, int F, int flags, double *out, void *stream);
 int bx_linear_assignment(const double *cost, int nr, int nc, double thresh, int32_t *x,
                          int32_t *y, void *stream);
 

@@ -64,6 +64,12 @@ int bxo_frame_count(const bxo_tracker *t);
 void bxo_free(bxo_tracker *t);
 
 /* ----------------------------------------------------------------------------------------- */
+/* StrongSort NearestNeighborDistanceMetric.distance, cosine (sort/linear_assignment.py:595-618):
+ * samples [off[T]][F] (target t owns rows off[t]..off[t+1]), feats [D][F] -> out [T][D] */
+int bxo_nn_cosine_distance(const double *samples, const int *off, int T, const double *feats,
+                           int D, int F, double *out);
+double bxo_np_norm_f64(const double *x, int n);
+
 /* OCSort (trackers/ocsort/ocsort.py:195-439; XYSR KF xysr_kf.py; association.py) with the     */
 /* minimal patches P1-P5 of SURVEY.md Appendix A (see bxo_ocsort.c).                          */
 typedef struct bxo_ocsort bxo_ocsort;

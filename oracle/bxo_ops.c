@@ -493,3 +493,76 @@ int bxo_linear_assignment(const double *cost, int nr, int nc, double thresh, int
     free(y);
     return 0;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* StrongSort NearestNeighborDistanceMetric.distance, cosine metric
+ * (trackers/strongsort/sort/linear_assignment.py:595-618 -> _nn_cosine_distance :468-497 ->
+ * _cosine_distance :382-413).  Rows are normalised as x / (np.linalg.norm(x, axis=1) + 1e-8)
+ * (numpy: sqrt of the pairwise sum of the squares, float64); the dot products are np.dot, a BLAS
+ * dgemm of unpinned order — restated here as the k-ascending fma chain that the engine's fp64
+ * MFMA (v_mfma_f64_16x16x4_f64, measured bitwise) computes; distance = 1 - clip(dot, -1, 1),
+ * minimum over the target's samples; a target without samples costs INFTY_COST = 1e5. */
+static double pairwise_sum_f64(const double *x, int n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int i = 0; i < n; i++) res += x[i];
+        return res;
+    }
+    if (n <= 128) {
+        double r[8];
+        for (int k = 0; k < 8; k++) r[k] = x[k];
+        int i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int k = 0; k < 8; k++) r[k] += x[i + k];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += x[i];
+        return res;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return pairwise_sum_f64(x, n2) + pairwise_sum_f64(x + n2, n - n2);
+}
+
+double bxo_np_norm_f64(const double *x, int n) {
+    double *sq = (double *)malloc(sizeof(double) * (n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) sq[i] = x[i] * x[i];
+    double s = pairwise_sum_f64(sq, n);
+    free(sq);
+    return sqrt(s);
+}
+
+static void normalise_rows(const double *x, int n, int f, double *y) {
+    for (int i = 0; i < n; i++) {
+        const double d = bxo_np_norm_f64(x + (size_t)i * f, f) + 1e-8;
+        for (int k = 0; k < f; k++) y[(size_t)i * f + k] = x[(size_t)i * f + k] / d;
+    }
+}
+
+int bxo_nn_cosine_distance(const double *samples, const int *off, int T, const double *feats,
+                           int D, int F, double *out) {
+    const int G = T > 0 ? off[T] : 0;
+    double *sh = (double *)malloc(sizeof(double) * ((size_t)G * F + 1));
+    double *dh = (double *)malloc(sizeof(double) * ((size_t)D * F + 1));
+    normalise_rows(samples, G, F, sh);
+    normalise_rows(feats, D, F, dh);
+    for (int t = 0; t < T; t++)
+        for (int d = 0; d < D; d++) {
+            if (off[t + 1] <= off[t]) {
+                out[(size_t)t * D + d] = 1e5;
+                continue;
+            }
+            double best = 0.0;
+            for (int s = off[t]; s < off[t + 1]; s++) {
+                const double *a = sh + (size_t)s * F, *b = dh + (size_t)d * F;
+                double acc = 0.0;
+                for (int k = 0; k < F; k++) acc = fma(a[k], b[k], acc);
+                const double c = acc < -1.0 ? -1.0 : (acc > 1.0 ? 1.0 : acc);
+                const double dist = 1.0 - c;
+                if (s == off[t] || dist < best) best = dist; /* np.min over the samples */
+            }
+            out[(size_t)t * D + d] = best;
+        }
+    free(sh);
+    free(dh);
+    return 0;
+}

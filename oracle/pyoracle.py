@@ -66,6 +66,9 @@ def lib():
         L.bxo_ocsort_id_count.argtypes = [C.c_void_p]
         L.bxo_ocsort_update.argtypes = [C.c_void_p, _dp, C.c_int, _dp, C.c_int]
         L.bxo_ocsort_tracks.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.bxo_nn_cosine_distance.argtypes = [_dp, _ip, C.c_int, _dp, C.c_int, C.c_int, _dp]
+        L.bxo_np_norm_f64.argtypes = [_dp, C.c_int]
+        L.bxo_np_norm_f64.restype = C.c_double
         L.bxo_acos.argtypes = [C.c_double]
         L.bxo_acos.restype = C.c_double
         _lib = L
@@ -97,6 +100,19 @@ def embedding_distance(trk, det):
     out = np.zeros((trk.shape[0], det.shape[0]))
     lib().bxo_embedding_distance(trk.ctypes.data_as(_fp), trk.shape[0], det.ctypes.data_as(_fp),
                                  det.shape[0], trk.shape[1], _d(out))
+    return out
+
+
+def nn_cosine_distance(samples, off, feats):
+    """StrongSort NN gallery distance: samples [G,F] f64 with per-target offsets off [T+1],
+    feats [D,F] -> [T,D]."""
+    samples = np.ascontiguousarray(samples, np.float64)
+    feats = np.ascontiguousarray(feats, np.float64)
+    off = np.ascontiguousarray(off, np.int32)
+    T, D = off.shape[0] - 1, feats.shape[0]
+    F = feats.shape[1] if feats.ndim == 2 else samples.shape[1]
+    out = np.zeros((T, D))
+    lib().bxo_nn_cosine_distance(_d(samples), off.ctypes.data_as(_ip), T, _d(feats), D, F, _d(out))
     return out
 
 

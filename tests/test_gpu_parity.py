@@ -423,3 +423,58 @@ def test_ocsort_empty_frames_and_global_ids(torch_cuda):
     ob = b.update(d, img)
     assert ob.shape == (2, 8) and sorted(ob[:, 4]) == [1.0, 2.0]
     assert OcSort._id_count == 2
+
+
+# ------------------------------------------------------------- StrongSort appearance metric
+def gpu_nn_cosine(torch, samples, off, feats, normalized=False):
+    from boxmot_amd import _native as N
+
+    L = N.load()
+    s = dev(torch, np.asarray(samples, np.float64).reshape(-1, feats.shape[1]))
+    o = dev(torch, np.asarray(off, np.int32))
+    f = dev(torch, np.asarray(feats, np.float64))
+    T, D, F = len(off) - 1, feats.shape[0], feats.shape[1]
+    out = torch.full((T, D), -7.0, dtype=torch.float64, device="cuda")
+    N.check(L.bx_nn_cosine_distance(s.data_ptr(), int(off[-1]), o.data_ptr(), T, f.data_ptr(), D,
+                                    F, 1 if normalized else 0, out.data_ptr(), None),
+            "bx_nn_cosine_distance")
+    return host(out)
+
+
+@pytest.mark.parametrize("case", ["small", "reid512", "reid2048"])
+def test_nn_cosine_distance_fixture(torch_cuda, case):
+    """Reference NearestNeighborDistanceMetric.distance (after partial_fit rounds): the fp64 MFMA
+    op equals the oracle bitwise and the reference within 1e-13 (np.dot's BLAS order)."""
+    fx = np.load(GOLDEN / "strongsort_ops.npz")
+    s, off, f, ref = (fx[f"{case}_{k}"] for k in ("samples", "off", "feats", "dist"))
+    got = gpu_nn_cosine(torch_cuda, s, off, f)
+    np.testing.assert_array_equal(got, po.nn_cosine_distance(s, off, f))
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-13)
+
+
+@pytest.mark.parametrize("F,T,D,smax", [(100, 37, 300, 9), (2048, 9, 513, 40), (16, 300, 5, 3),
+                                        (512, 70, 129, 150)])
+def test_nn_cosine_distance_random_vs_oracle(torch_cuda, F, T, D, smax):
+    """Ragged galleries (empty targets, tiles spanning several targets, F not a multiple of the
+    16-wide K chunk, D past one 256-wide column block): bitwise vs the oracle."""
+    rng = np.random.default_rng(F * 7 + T)
+    cnt = rng.integers(0, smax + 1, T)
+    cnt[0] = 0
+    off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int32)
+    base = rng.normal(size=(T, F))
+    s = np.repeat(base, cnt, 0) + 0.5 * rng.normal(size=(int(off[-1]), F))
+    s *= rng.uniform(0.2, 3.0, (s.shape[0], 1))
+    f = base[rng.integers(0, T, D)] + 0.5 * rng.normal(size=(D, F))
+    f[0] = s[0] if s.shape[0] else f[0]  # an exact match: distance 0 (clip at 1)
+    got = gpu_nn_cosine(torch_cuda, s, off, f)
+    np.testing.assert_array_equal(got, po.nn_cosine_distance(s, off, f))
+    # a gallery kept normalised (BX_NN_SAMPLES_NORMALIZED): samples used as given
+    sh = s / (np.linalg.norm(s, axis=1, keepdims=True) + 1e-8)
+    fh = f / (np.linalg.norm(f, axis=1, keepdims=True) + 1e-8)
+    got_n = gpu_nn_cosine(torch_cuda, sh, off, f, normalized=True)
+    for t in range(T):
+        if cnt[t] == 0:
+            assert np.all(got_n[t] == 1e5)
+        else:
+            ref = (1 - np.clip(sh[off[t]:off[t + 1]] @ fh.T, -1, 1)).min(0)
+            np.testing.assert_allclose(got_n[t], ref, rtol=0, atol=1e-13)

@@ -11,6 +11,8 @@ import pytest
 from oracle import pyoracle as po
 from tests.golden_util import compare_outputs, fixture_frames, fixture_tracker_args
 
+GOLDEN = __import__("pathlib").Path(__file__).parent / "golden"
+
 
 @pytest.fixture(scope="module")
 def K(golden_dir):
@@ -121,3 +123,18 @@ def test_acos_within_one_ulp_of_numpy():
     got = np.array([L.bxo_acos(float(x)) for x in xs])
     ref = np.arccos(xs)
     assert np.all(np.abs(got - ref) <= np.spacing(ref))
+
+
+@pytest.mark.parametrize("case", ["small", "reid512", "reid2048"])
+def test_nn_cosine_distance_vs_reference(case):
+    """StrongSort NearestNeighborDistanceMetric.distance (reference, captured after partial_fit
+    rounds with budget pruning) vs the oracle: the reference's np.dot is a BLAS dgemm of
+    unpinned order, the oracle the MFMA's k-ordered fma chain -> agreement to 1e-13; targets
+    without samples cost exactly 1e5."""
+    fx = np.load(GOLDEN / "strongsort_ops.npz")
+    s, off, f, ref = (fx[f"{case}_{k}"] for k in ("samples", "off", "feats", "dist"))
+    got = po.nn_cosine_distance(s, off, f)
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-13)
+    empty = np.diff(off) == 0
+    assert empty.any() and np.all(got[empty] == 1e5) and np.all(ref[empty] == 1e5)
