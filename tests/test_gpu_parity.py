@@ -453,10 +453,11 @@ def test_nn_cosine_distance_fixture(torch_cuda, case):
 
 
 @pytest.mark.parametrize("F,T,D,smax", [(100, 37, 300, 9), (2048, 9, 513, 40), (16, 300, 5, 3),
-                                        (512, 70, 129, 150)])
+                                        (512, 70, 129, 150), (64, 240, 300, 160)])
 def test_nn_cosine_distance_random_vs_oracle(torch_cuda, F, T, D, smax):
     """Ragged galleries (empty targets, tiles spanning several targets, F not a multiple of the
-    16-wide K chunk, D past one 256-wide column block): bitwise vs the oracle."""
+    16-wide K chunk, D past one 256-wide column block; the last case is large enough for the
+    128 x 256 tile, the others run the 64 x 64 one): bitwise vs the oracle."""
     rng = np.random.default_rng(F * 7 + T)
     cnt = rng.integers(0, smax + 1, T)
     cnt[0] = 0
