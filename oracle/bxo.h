@@ -84,6 +84,28 @@ int bxo_ocsort_tracks(bxo_ocsort *o, int cap, int *ids, double *x, double *P);
 int bxo_ocsort_update(bxo_ocsort *o, const double *dets, int n, double *out, int out_cap);
 double bxo_acos(double x);
 
+/* BoostTrack / BoostTrack++ (trackers/boosttrack/boosttrack.py:123-456, assoc.py,            */
+/* kalmanfilter.py), as shipped (see bxo_boost.c for the fixed orders).                        */
+typedef struct {
+    int max_age, min_hits;
+    double det_thresh, iou_threshold, min_box_area, aspect_ratio_thresh;
+    double lambda_iou, lambda_mhd, lambda_shape, dlo_boost_coef;
+    int use_ecc, use_dlo_boost, use_duo_boost, s_sim_corr, use_rich_s, use_sb, use_vt, with_reid;
+} bxo_boost_params;
+typedef struct bxo_boost bxo_boost;
+bxo_boost *bxo_boost_new(const bxo_boost_params *p);
+void bxo_boost_free(bxo_boost *b);
+int bxo_boost_id_count(const bxo_boost *b);
+void bxo_boost_set_id_count(bxo_boost *b, int c);
+/* track list in list order: ids [cap], means x [cap][8], covariances P [cap][64] */
+int bxo_boost_tracks(const bxo_boost *b, int cap, int *ids, double *x, double *P);
+/* dets[n,6] float64 (float32-rounded); embs [n][emb_dim] float64 or NULL; warp[6] 2x3 CMC
+ * affine (NULL = identity).  out[M,8]; returns M, -2 if out_cap is too small. */
+int bxo_boost_update(bxo_boost *b, const double *dets, int n, const double *embs, int emb_dim,
+                     const double *warp, double *out, int out_cap);
+double bxo_exp(double x);
+double bxo_pow15(double x);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,12 +21,41 @@ _ip = C.POINTER(C.c_int)
 
 
 def build(force: bool = False) -> Path:
-    srcs = [HERE / n for n in ("bxo_ops.c", "bxo_track.c", "bxo.h", "bxo_internal.h")]
+    srcs = [HERE / n for n in ("bxo_ops.c", "bxo_track.c", "bxo_ocsort.c", "bxo_boost.c", "bxo.h",
+                               "bxo_internal.h")]
     if force or not LIB_PATH.exists() or any(
         s.stat().st_mtime > LIB_PATH.stat().st_mtime for s in srcs
     ):
         subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
     return LIB_PATH
+
+
+class BoostParams(C.Structure):
+    """bxo_boost_params (oracle/bxo.h)."""
+
+    _fields_ = [("max_age", C.c_int), ("min_hits", C.c_int), ("det_thresh", C.c_double),
+                ("iou_threshold", C.c_double), ("min_box_area", C.c_double),
+                ("aspect_ratio_thresh", C.c_double), ("lambda_iou", C.c_double),
+                ("lambda_mhd", C.c_double), ("lambda_shape", C.c_double),
+                ("dlo_boost_coef", C.c_double), ("use_ecc", C.c_int), ("use_dlo_boost", C.c_int),
+                ("use_duo_boost", C.c_int), ("s_sim_corr", C.c_int), ("use_rich_s", C.c_int),
+                ("use_sb", C.c_int), ("use_vt", C.c_int), ("with_reid", C.c_int)]
+
+
+# BoostTrack.__init__ defaults (boosttrack.py:154-181)
+BOOST_DEFAULTS = dict(max_age=60, min_hits=3, det_thresh=0.6, iou_threshold=0.3, use_ecc=True,
+                      min_box_area=10, aspect_ratio_thresh=1.6, lambda_iou=0.5, lambda_mhd=0.25,
+                      lambda_shape=0.25, use_dlo_boost=True, use_duo_boost=True,
+                      dlo_boost_coef=0.65, s_sim_corr=False, use_rich_s=False, use_sb=False,
+                      use_vt=False, with_reid=False)
+
+
+def boost_params(**p):
+    q = dict(BOOST_DEFAULTS)
+    q.update({k: v for k, v in p.items() if k in BOOST_DEFAULTS})
+    return BoostParams(**{k: (type(getattr(BoostParams, k)) is not None and
+                              (float(v) if isinstance(BOOST_DEFAULTS[k], float) else int(v)))
+                          for k, v in q.items()})
 
 
 _lib = None
@@ -71,6 +100,18 @@ def lib():
         L.bxo_np_norm_f64.restype = C.c_double
         L.bxo_acos.argtypes = [C.c_double]
         L.bxo_acos.restype = C.c_double
+        L.bxo_boost_new.argtypes = [C.POINTER(BoostParams)]
+        L.bxo_boost_new.restype = C.c_void_p
+        L.bxo_boost_free.argtypes = [C.c_void_p]
+        L.bxo_boost_id_count.argtypes = [C.c_void_p]
+        L.bxo_boost_set_id_count.argtypes = [C.c_void_p, C.c_int]
+        L.bxo_boost_tracks.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.bxo_boost_update.argtypes = [C.c_void_p, _dp, C.c_int, C.c_void_p, C.c_int, _dp, _dp,
+                                       C.c_int]
+        L.bxo_exp.argtypes = [C.c_double]
+        L.bxo_exp.restype = C.c_double
+        L.bxo_pow15.argtypes = [C.c_double]
+        L.bxo_pow15.restype = C.c_double
         _lib = L
     return _lib
 
@@ -189,6 +230,9 @@ class OracleTracker:
                 p.get("Q_xy_scaling", 0.01), p.get("Q_s_scaling", 0.0001))
             if p.get("asso_func", "iou") != "iou":
                 raise NotImplementedError("oracle OCSort: asso_func 'iou' only")
+        elif kind == "boosttrack":
+            self._bp = boost_params(**p)
+            self.h = L.bxo_boost_new(C.byref(self._bp))
         else:
             raise KeyError(kind)
         self._cap = 1024
@@ -215,6 +259,18 @@ class OracleTracker:
                 raise RuntimeError(f"oracle update failed ({m})")
             return out[:m].copy()
         w = None if warp is None else _d(np.ascontiguousarray(warp, np.float64).reshape(6))
+        if self.kind == "boosttrack":
+            d32 = np.ascontiguousarray(dets.astype(np.float32).astype(np.float64))
+            ep, fd = None, 0
+            if embs is not None and n and self._bp.with_reid:
+                e64 = np.ascontiguousarray(embs, np.float64)
+                ep, fd = e64.ctypes.data_as(C.c_void_p), e64.shape[1]
+            cap = max(self._cap, 2 * n + 64)
+            out = np.zeros((cap, 8))
+            m = lib().bxo_boost_update(self.h, _d(d32), n, ep, fd, w, _d(out), cap)
+            if m < 0:
+                raise RuntimeError(f"oracle update failed ({m})")
+            return out[:m].copy()
         while True:
             cap = max(self._cap, n + 16)
             out = np.zeros((cap, 8))
@@ -229,6 +285,8 @@ class OracleTracker:
     def id_count(self):
         if self.kind == "ocsort":
             return lib().bxo_ocsort_id_count(self.h)
+        if self.kind == "boosttrack":
+            return lib().bxo_boost_id_count(self.h)
         return lib().bxo_id_count(self.h)
 
     def ocsort_tracks(self):
@@ -243,7 +301,8 @@ class OracleTracker:
     def __del__(self):
         h = getattr(self, "h", None)
         if h:
-            (lib().bxo_ocsort_free if self.kind == "ocsort" else lib().bxo_free)(h)
+            free = {"ocsort": lib().bxo_ocsort_free, "boosttrack": lib().bxo_boost_free}
+            free.get(self.kind, lib().bxo_free)(h)
             self.h = None
 
 

@@ -101,16 +101,39 @@ def test_linear_assignment_empty():
 def test_tracker_fixture(path):
     fx = np.load(path)
     kind, args = fixture_tracker_args(fx)
-    if kind != "ocsort":
+    if kind not in ("ocsort", "boosttrack"):
         assert int(fx["lap_degenerate"]) == 0
-    # (OCSort's full-matching LAP ties on zero-IoU pairs by construction; its fixtures were
-    # captured with the restated lapx JV resolving them — make_golden.use_restated_lapx_jv)
+    # (OCSort's and BoostTrack's full-matching LAP (extend_cost, no cost_limit) can tie on
+    # zero-cost pairs; their fixtures were captured with the restated lapx JV resolving ties —
+    # make_golden.use_restated_lapx_jv)
     tr = po.OracleTracker(kind, **args)
     rows = []
     for f, d, e in fixture_frames(fx):
         o = tr.update(d, e)
         rows.append(np.concatenate([np.full((o.shape[0], 1), f), o], 1))
-    compare_outputs(np.concatenate(rows, 0), fx["outputs"], box_atol=1e-9)
+    compare_outputs(np.concatenate(rows, 0), fx["outputs"], box_atol=1e-9,
+                    conf_atol=1e-9 if kind == "boosttrack" else None)
+
+
+def test_exp_pow_within_one_ulp_of_numpy():
+    """BoostTrack's np.exp (MhDist softmax, shape similarity) and max_s ** 1.5: oracle and engine
+    share fdlibm's exp and a compensated x*sqrt(x) (fixed, reproducible algorithms) which stay
+    within 1 ulp of numpy's."""
+    rng = np.random.default_rng(1)
+    xs = np.concatenate([rng.uniform(-40, 15, 40000), rng.uniform(-1e-3, 1e-3, 2000),
+                         [0.0, -0.0, 1.0, -1.0, 13.2767, 0.34657359027997264, 700.0, -745.0]])
+    L = po.lib()
+    got = np.array([L.bxo_exp(float(x)) for x in xs])
+    ref = np.exp(xs)
+    assert np.all(np.abs(got - ref) <= np.spacing(ref))
+    ys = np.concatenate([rng.uniform(0, 1, 40000), [0.0, 1.0, 0.25, 1e-300, 4.0]])
+    got = np.array([L.bxo_pow15(float(y)) for y in ys])
+    ref = ys ** 1.5
+    assert np.all(np.abs(got - ref) <= np.spacing(ref))
+    # numpy's array power is not correctly rounded; glibc's pow (<= 0.52 ulp) nearly is, and so
+    # is the compensated form
+    import math
+    assert np.mean(got == np.array([math.pow(float(y), 1.5) for y in ys])) > 0.999
 
 
 def test_acos_within_one_ulp_of_numpy():
