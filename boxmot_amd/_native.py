@@ -18,13 +18,14 @@ LIB_DIR = PKG / "lib"
 LIB_PATH = LIB_DIR / "libbxassoc.so"
 HEADER = REPO / "include" / "bxassoc.h"
 HEADER_OCS = REPO / "include" / "bxocsort.h"
+HEADER_BOOST = REPO / "include" / "bxboost.h"
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
     # numpy-identical rounding: no FMA contraction, IEEE f32 division/sqrt
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
 ]
-SOURCES = ["bx_engine.hip", "bx_ops.hip", "bx_ocsort.hip", "bx_nn.hip"]
+SOURCES = ["bx_engine.hip", "bx_ops.hip", "bx_ocsort.hip", "bx_nn.hip", "bx_boost.hip"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -33,7 +34,8 @@ class NativeUnavailable(RuntimeError):
 
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the HIP extension for gfx950 in-tree (boxmot_amd/lib/libbxassoc.so)."""
-    srcs = [CSRC / s for s in SOURCES] + [CSRC / "bx_device.h", HEADER, HEADER_OCS]
+    srcs = [CSRC / s for s in SOURCES] + [CSRC / "bx_device.h", CSRC / "bx_jv.h", HEADER,
+                                          HEADER_OCS, HEADER_BOOST]
     if not force and LIB_PATH.exists():
         t = LIB_PATH.stat().st_mtime
         if all(s.stat().st_mtime <= t for s in srcs):
@@ -74,7 +76,20 @@ class BxOcsortConfig(C.Structure):
     ]
 
 
-# every symbol include/bxassoc.h and include/bxocsort.h declare (checked by tests/test_native_abi.py)
+class BxBoostConfig(C.Structure):
+    _fields_ = [
+        ("n_seq", C.c_int32), ("track_cap", C.c_int32), ("det_cap", C.c_int32),
+        ("emb_dim", C.c_int32), ("max_age", C.c_int32), ("min_hits", C.c_int32),
+        ("det_thresh", C.c_double), ("iou_threshold", C.c_double), ("min_box_area", C.c_double),
+        ("aspect_ratio_thresh", C.c_double), ("lambda_iou", C.c_double),
+        ("lambda_mhd", C.c_double), ("lambda_shape", C.c_double), ("dlo_boost_coef", C.c_double),
+        ("use_ecc", C.c_int32), ("use_dlo_boost", C.c_int32), ("use_duo_boost", C.c_int32),
+        ("s_sim_corr", C.c_int32), ("use_rich_s", C.c_int32), ("use_sb", C.c_int32),
+        ("use_vt", C.c_int32), ("with_reid", C.c_int32),
+    ]
+
+
+# every symbol include/bxassoc.h, include/bxocsort.h and include/bxboost.h declare (checked by tests/test_native_abi.py)
 EXPORTS = [
     "bx_last_error", "bx_device_count", "bx_engine_create", "bx_engine_destroy",
     "bx_engine_reset", "bx_engine_step", "bx_engine_update_host", "bx_engine_status",
@@ -85,7 +100,10 @@ EXPORTS = [
     "bx_nn_cosine_distance", "bx_ocsort_create", "bx_ocsort_destroy", "bx_ocsort_reset", "bx_ocsort_step",
     "bx_ocsort_update_host", "bx_ocsort_status", "bx_ocsort_counters_host",
     "bx_ocsort_set_id_count", "bx_ocsort_tracks_host", "bx_ocsort_probe", "bx_ocsort_probe_read",
-    "bx_ocsort_frame_stats_host",
+    "bx_ocsort_frame_stats_host", "bx_boost_create", "bx_boost_destroy", "bx_boost_reset",
+    "bx_boost_step", "bx_boost_update_host", "bx_boost_status", "bx_boost_counters_host",
+    "bx_boost_set_id_count", "bx_boost_tracks_host", "bx_boost_frame_stats_host",
+    "bx_boost_probe", "bx_boost_probe_read",
 ]
 
 _vp, _ip, _dp, _fp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_float)
@@ -128,6 +146,18 @@ _SIGS = {
     "bx_ocsort_probe": ([_vp, C.c_int], C.c_int),
     "bx_ocsort_frame_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_ocsort_probe_read": ([_vp, _dp, _ip], C.c_int),
+    "bx_boost_create": ([C.POINTER(BxBoostConfig), C.POINTER(C.c_void_p)], C.c_int),
+    "bx_boost_destroy": ([_vp], C.c_int),
+    "bx_boost_reset": ([_vp, C.c_int, C.c_int, _vp], C.c_int),
+    "bx_boost_step": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_boost_update_host": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp, _vp, _ip, _vp], C.c_int),
+    "bx_boost_status": ([_vp, _ip], C.c_int),
+    "bx_boost_counters_host": ([_vp, C.c_int, _ip, _ip, _ip], C.c_int),
+    "bx_boost_set_id_count": ([_vp, C.c_int, C.c_int, _vp], C.c_int),
+    "bx_boost_tracks_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _ip], C.c_int),
+    "bx_boost_frame_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
+    "bx_boost_probe": ([_vp, C.c_int], C.c_int),
+    "bx_boost_probe_read": ([_vp, _dp, _ip], C.c_int),
 }
 
 _lib = None

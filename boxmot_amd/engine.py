@@ -286,6 +286,153 @@ class OcsortEngine:
         return t.value, n.value
 
 
+@dataclass
+class BoostParams:
+    """BoostTrack constructor parameters (boosttrack.py:154-181 names; YAML defaults)."""
+
+    max_age: int = 60
+    min_hits: int = 3
+    det_thresh: float = 0.6
+    iou_threshold: float = 0.3
+    use_ecc: bool = True
+    min_box_area: float = 10
+    aspect_ratio_thresh: float = 1.6
+    lambda_iou: float = 0.5
+    lambda_mhd: float = 0.25
+    lambda_shape: float = 0.25
+    use_dlo_boost: bool = True
+    use_duo_boost: bool = True
+    dlo_boost_coef: float = 0.65
+    s_sim_corr: bool = False
+    use_rich_s: bool = True
+    use_sb: bool = True
+    use_vt: bool = True
+    with_reid: bool = True
+
+
+class BoostEngine:
+    """Handle over ``bx_boost_*`` (include/bxboost.h): ``n_seq`` BoostTrack sequences in HBM;
+    per frame a ReID contraction (fp64 MFMA), the frame kernel (one wave per sequence) and the
+    embedding update."""
+
+    def __init__(self, n_seq: int = 1, track_cap: int = 256, det_cap: int = 256,
+                 emb_dim: int = 0, params: BoostParams | None = None):
+        p = params or BoostParams()
+        if p.with_reid and emb_dim <= 0:
+            raise ValueError("with_reid BoostTrack needs emb_dim > 0")
+        self.n_seq, self.track_cap, self.det_cap, self.params = n_seq, track_cap, det_cap, p
+        self.emb_dim = emb_dim if p.with_reid else 0
+        cfg = N.BxBoostConfig(
+            n_seq=n_seq, track_cap=track_cap, det_cap=det_cap, emb_dim=self.emb_dim,
+            max_age=int(p.max_age), min_hits=int(p.min_hits), det_thresh=float(p.det_thresh),
+            iou_threshold=float(p.iou_threshold), min_box_area=float(p.min_box_area),
+            aspect_ratio_thresh=float(p.aspect_ratio_thresh), lambda_iou=float(p.lambda_iou),
+            lambda_mhd=float(p.lambda_mhd), lambda_shape=float(p.lambda_shape),
+            dlo_boost_coef=float(p.dlo_boost_coef), use_ecc=int(bool(p.use_ecc)),
+            use_dlo_boost=int(bool(p.use_dlo_boost)), use_duo_boost=int(bool(p.use_duo_boost)),
+            s_sim_corr=int(bool(p.s_sim_corr)), use_rich_s=int(bool(p.use_rich_s)),
+            use_sb=int(bool(p.use_sb)), use_vt=int(bool(p.use_vt)),
+            with_reid=int(bool(p.with_reid)))
+        self._L = N.load()
+        h = C.c_void_p()
+        N.check(self._L.bx_boost_create(C.byref(cfg), C.byref(h)), "bx_boost_create")
+        self._h = h
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.bx_boost_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, seq0: int = 0, nseq: int | None = None, stream=None):
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        N.check(self._L.bx_boost_reset(self._h, seq0, nseq, stream), "bx_boost_reset")
+
+    def step(self, dets, det_off, embs, warps, out, out_count, seq0: int = 0,
+             nseq: int | None = None, stream=None):
+        """One frame for sequences [seq0, seq0+nseq) from device tensors (see bx_boost_step)."""
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        if stream is None:
+            stream = _current_stream()
+        N.check(self._L.bx_boost_step(self._h, seq0, nseq, _ptr(dets), _ptr(det_off), _ptr(embs),
+                                      _ptr(warps), _ptr(out), _ptr(out_count), stream),
+                "bx_boost_step")
+
+    def update_host(self, seq: int, dets: np.ndarray, embs: np.ndarray | None = None,
+                    warp: np.ndarray | None = None) -> np.ndarray:
+        d = np.ascontiguousarray(dets, dtype=np.float32).reshape(-1, 6)
+        n = d.shape[0]
+        e = None
+        if self.emb_dim:
+            if n and embs is None:
+                raise ValueError("with_reid BoostTrack needs embeddings")
+            if n:
+                e = np.ascontiguousarray(embs, dtype=np.float64).reshape(n, -1)
+                if e.shape[1] != self.emb_dim:
+                    raise ValueError(f"embedding dim {e.shape[1]} != engine emb_dim {self.emb_dim}")
+        w = None if warp is None else np.ascontiguousarray(warp, np.float64).reshape(6)
+        out = np.empty((max(n, 1), 8), np.float64)
+        m = C.c_int(0)
+        N.check(self._L.bx_boost_update_host(
+            self._h, seq, d.ctypes.data if n else None, n, None if e is None else e.ctypes.data,
+            None if w is None else w.ctypes.data, out.ctypes.data, C.byref(m), None),
+            "bx_boost_update_host")
+        return out[: m.value].copy()
+
+    def status(self) -> int:
+        s = C.c_int(0)
+        N.check(self._L.bx_boost_status(self._h, C.byref(s)), "bx_boost_status")
+        return s.value
+
+    def counters(self, seq: int = 0) -> dict:
+        fc, idc, nt = C.c_int(), C.c_int(), C.c_int()
+        N.check(self._L.bx_boost_counters_host(self._h, seq, C.byref(fc), C.byref(idc),
+                                               C.byref(nt)), "counters")
+        return {"frame_count": fc.value, "id_count": idc.value, "n_tracks": nt.value}
+
+    def set_id_count(self, seq: int, value: int):
+        N.check(self._L.bx_boost_set_id_count(self._h, seq, int(value), None), "set_id_count")
+
+    def tracks(self, seq: int = 0) -> dict:
+        """Host snapshot of the track list (list order): ids, means x [8], covariances [8, 8],
+        embeddings [F] (with_reid)."""
+        cap = self.track_cap
+        ids = np.zeros(cap, np.int32)
+        x = np.zeros((cap, 8))
+        P = np.zeros((cap, 8, 8))
+        E = np.zeros((cap, max(self.emb_dim, 1)))
+        n = C.c_int()
+        N.check(self._L.bx_boost_tracks_host(self._h, seq, cap, ids.ctypes.data, x.ctypes.data,
+                                             P.ctypes.data, E.ctypes.data if self.emb_dim else None,
+                                             C.byref(n)), "tracks")
+        k = min(n.value, cap)
+        snap = {"id": ids[:k], "x": x[:k], "P": P[:k]}
+        if self.emb_dim:
+            snap["emb"] = E[:k]
+        return snap
+
+    def frame_stats(self, seq0: int = 0, nseq: int | None = None) -> dict:
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        a = (C.c_int64 * 6)()
+        N.check(self._L.bx_boost_frame_stats_host(self._h, seq0, nseq, a), "frame_stats")
+        return dict(zip(["dets", "kept", "tracks", "outputs", "records", "frame"],
+                        [int(x) for x in a]))
+
+    def probe(self, stage: int = 1) -> None:
+        N.check(self._L.bx_boost_probe(self._h, int(stage)), "bx_boost_probe")
+
+    def probe_read(self):
+        t, n = C.c_double(), C.c_int()
+        N.check(self._L.bx_boost_probe_read(self._h, C.byref(t), C.byref(n)), "probe_read")
+        return t.value, n.value
+
+
 def _ptr(x):
     if x is None:
         return None

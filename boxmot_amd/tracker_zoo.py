@@ -16,6 +16,7 @@ _ON_ENGINE = {
     "bytetrack": "boxmot_amd.trackers.bytetrack.ByteTrack",
     "botsort": "boxmot_amd.trackers.botsort.BotSort",
     "ocsort": "boxmot_amd.trackers.ocsort.OcSort",
+    "boosttrack": "boxmot_amd.trackers.boosttrack.BoostTrack",
 }
 _REFERENCE_NAMES = ["strongsort", "ocsort", "bytetrack", "botsort", "deepocsort", "hybridsort",
                     "boosttrack"]

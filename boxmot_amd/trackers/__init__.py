@@ -1,5 +1,6 @@
+from .boosttrack import BoostTrack
 from .botsort import BotSort
 from .bytetrack import ByteTrack
 from .ocsort import OcSort
 
-__all__ = ["ByteTrack", "BotSort", "OcSort"]
+__all__ = ["ByteTrack", "BotSort", "OcSort", "BoostTrack"]

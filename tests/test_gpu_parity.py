@@ -186,13 +186,16 @@ def test_linear_assignment_empty(torch_cuda):
 
 # --------------------------------------------------------------------------- tracker level
 def make_dropin(kind, args):
-    from boxmot_amd import BotSort, ByteTrack, OcSort
+    from boxmot_amd import BoostTrack, BotSort, ByteTrack, OcSort
 
     if kind == "bytetrack":
         ByteTrack.clear_count()
         return ByteTrack(**args)
     if kind == "ocsort":
         return OcSort(**args)
+    if kind == "boosttrack":
+        BoostTrack._id_count = 0  # fixtures were captured with the class counter reset
+        return BoostTrack(reid_weights=None, device="cuda", half=False, **args)
     return BotSort(reid_weights=None, device="cuda", half=False, **args)
 
 
@@ -210,7 +213,8 @@ def test_tracker_fixture_parity(torch_cuda, path):
         oo = orc.update(d, e)
         np.testing.assert_array_equal(o, oo, err_msg=f"frame {f}: GPU != oracle")
         rows.append(np.concatenate([np.full((o.shape[0], 1), f), o], 1))
-    compare_outputs(np.concatenate(rows, 0), fx["outputs"], box_atol=1e-9)
+    compare_outputs(np.concatenate(rows, 0), fx["outputs"], box_atol=1e-9,
+                    conf_atol=1e-9 if kind == "boosttrack" else None)
 
 
 def run_batched(torch, kind, scenes, n_frames, args, emb_dim=0, seq_frames=None):
@@ -479,3 +483,130 @@ def test_nn_cosine_distance_random_vs_oracle(torch_cuda, F, T, D, smax):
         else:
             ref = (1 - np.clip(sh[off[t]:off[t + 1]] @ fh.T, -1, 1)).min(0)
             np.testing.assert_allclose(got_n[t], ref, rtol=0, atol=1e-13)
+
+
+# ----------------------------------------------------------------------------------- BoostTrack
+BOOST_ARGS = dict(max_age=60, min_hits=3, det_thresh=0.6, iou_threshold=0.3, use_ecc=True,
+                  min_box_area=10, aspect_ratio_thresh=1.6, lambda_iou=0.5, lambda_mhd=0.25,
+                  lambda_shape=0.25, use_dlo_boost=True, use_duo_boost=True, dlo_boost_coef=0.65,
+                  s_sim_corr=False, use_rich_s=True, use_sb=True, use_vt=True, with_reid=True)
+
+
+def run_boost_batched(torch, scenes, n_frames, args, emb_dim, track_cap=256, det_cap=256,
+                      warps=None):
+    """BoostEngine with len(scenes) sequences per launch vs one oracle per sequence: outputs and
+    the track state (ids, Kalman mean/covariance, embeddings) bitwise."""
+    from boxmot_amd.engine import BoostEngine, BoostParams
+
+    S = len(scenes)
+    eng = BoostEngine(n_seq=S, track_cap=track_cap, det_cap=det_cap, emb_dim=emb_dim,
+                      params=BoostParams(**args))
+    orcs = [po.OracleTracker("boosttrack", **args) for _ in range(S)]
+    reid = args["with_reid"]
+    for t in range(1, n_frames + 1):
+        frames = [sc.frame(t) for sc in scenes]
+        off = np.zeros(S + 1, np.int32)
+        off[1:] = np.cumsum([f[0].shape[0] for f in frames])
+        dets = np.concatenate([f[0] for f in frames], 0).astype(np.float32)
+        de = None
+        if reid:
+            de = dev(torch, np.concatenate([f[1] for f in frames], 0).astype(np.float64))
+        w = None if warps is None else dev(torch, np.stack([warps(s, t) for s in range(S)]))
+        out = torch.empty((max(int(off[-1]), 1), 8), dtype=torch.float64, device="cuda")
+        cnt = torch.empty(S, dtype=torch.int32, device="cuda")
+        eng.step(dev(torch, dets), dev(torch, off), de, w, out, cnt)
+        o, c = host(out), host(cnt)
+        for s in range(S):
+            ref = orcs[s].update(frames[s][0], frames[s][1] if reid else None,
+                                 None if warps is None else warps(s, t))
+            np.testing.assert_array_equal(o[off[s]: off[s] + c[s]], ref,
+                                          err_msg=f"seq {s} frame {t}")
+    assert eng.status() == 0
+    for s in range(S):
+        g = eng.tracks(s)
+        L = po.lib()
+        n = L.bxo_boost_tracks(orcs[s].h, 0, None, None, None)
+        ids = np.zeros(max(n, 1), np.int32)
+        x = np.zeros((max(n, 1), 8))
+        P = np.zeros((max(n, 1), 8, 8))
+        L.bxo_boost_tracks(orcs[s].h, n, ids.ctypes.data, x.ctypes.data, P.ctypes.data)
+        np.testing.assert_array_equal(g["id"], ids[:n])
+        np.testing.assert_array_equal(g["x"], x[:n])
+        np.testing.assert_array_equal(g["P"], P[:n])
+    return eng
+
+
+@pytest.mark.parametrize("variant", ["plusplus", "plain", "v2_sb", "vt_noreid"])
+def test_boosttrack_batched_vs_oracle(torch_cuda, variant):
+    """Several sequences per launch (grid / crowded layouts, low-confidence detections for the
+    DLO/DUO boosts, misses, deaths) against the oracle, outputs and Kalman state bitwise."""
+    from boxmot_amd.synth import SyntheticScene
+
+    args = dict(BOOST_ARGS)
+    emb = 64
+    if variant == "plain":
+        args.update(use_rich_s=False, use_sb=False, use_vt=False, with_reid=False)
+    if variant == "v2_sb":
+        args.update(s_sim_corr=True, use_vt=False, det_thresh=0.5, max_age=8, min_hits=1)
+    if variant == "vt_noreid":
+        args.update(use_sb=False, with_reid=False, use_ecc=False)
+    if not args["with_reid"]:
+        emb = 0
+    scenes = [SyntheticScene(n_obj=12 + 9 * s, seed=500 + s, emb_dim=emb or 0,
+                             emb_dtype=np.float64, layout="crowded" if s % 2 else "grid",
+                             p_det=0.4 + 0.1 * (s % 3), conf_lo=0.2 if s % 3 == 0 else 0.4)
+              for s in range(6)]
+    run_boost_batched(torch_cuda, scenes, 60, args, emb)
+
+
+def test_boosttrack_large_scene_vs_oracle(torch_cuda):
+    """A crowded 160-object sequence with 512-d ReID: cost matrices past the LDS budget (HBM
+    path), several MFMA output tiles per sequence, LAP solves."""
+    from boxmot_amd.synth import SyntheticScene
+
+    sc = SyntheticScene(n_obj=160, seed=23, layout="crowded", p_det=0.5, conf_lo=0.3,
+                        emb_dim=512, emb_dtype=np.float64)
+    run_boost_batched(torch_cuda, [sc], 25, dict(BOOST_ARGS), 512)
+
+
+def test_boosttrack_warp_and_embeddings(torch_cuda):
+    """Non-identity camera warps per sequence (camera_update) and the embedding EMA state."""
+    from boxmot_amd.synth import SyntheticScene
+
+    scenes = [SyntheticScene(n_obj=20 + 5 * s, seed=700 + s, emb_dim=96, emb_dtype=np.float64,
+                             conf_lo=0.3) for s in range(3)]
+
+    def warp(s, t):
+        a = 0.002 * np.sin(0.3 * t + s)
+        return np.array([[1.0 + a, -a, 1.5 * s - 0.5], [a, 1.0 - a, 0.25 * t % 2.0]])
+
+    eng = run_boost_batched(torch_cuda, scenes, 40, dict(BOOST_ARGS), 96, warps=warp)
+    snap = eng.tracks(0)
+    norms = np.linalg.norm(snap["emb"], axis=1)
+    assert snap["emb"].shape[1] == 96 and np.all(norms > 0)
+
+
+def test_boosttrack_dropin_empty_frames_and_global_ids(torch_cuda):
+    from boxmot_amd import BoostTrack, create_tracker
+
+    img = np.zeros((720, 1280, 3), np.uint8)
+    BoostTrack._id_count = 0
+    args = dict(BOOST_ARGS, with_reid=False)
+    a = BoostTrack(**args)
+    orc = po.OracleTracker("boosttrack", **args)
+    d = np.array([[10, 10, 60, 120, 0.9, 0], [200, 50, 260, 170, 0.8, 2]], np.float32)
+    for t in range(6):
+        dd = d if t not in (2, 3) else np.empty((0, 6), np.float32)
+        o = a.update(dd, img)
+        assert o.shape[1] == 8
+        np.testing.assert_array_equal(o, orc.update(dd))
+    # the id counter is class-global and never reset: a second instance continues it
+    b = BoostTrack(**args)
+    ob = b.update(d, img)
+    assert ob.shape == (2, 8) and sorted(ob[:, 4]) == [3.0, 4.0]
+    # the plugin path (YAML defaults = BoostTrack++ with ReID) takes embeddings
+    t = create_tracker("boosttrack")
+    e = np.random.default_rng(0).standard_normal((2, 32))
+    assert t.update(d, img, e).shape[1] == 8
+    with pytest.raises(AssertionError):
+        t.update(d, img, e[:1])

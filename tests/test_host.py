@@ -47,10 +47,26 @@ def test_ocsort_yaml_defaults_reach_the_engine(monkeypatch):
     assert (p.min_conf, p.Q_xy_scaling, p.Q_s_scaling, p.asso_threshold) == (0.1, 0.01, 1e-4, 0.3)
 
 
-@pytest.mark.parametrize("name", ["strongsort", "boosttrack", "deepocsort"])
+@pytest.mark.parametrize("name", ["strongsort", "deepocsort"])
 def test_not_yet_on_engine(name):
     with pytest.raises(NotImplementedError):
         create_tracker(name, evolve_param_dict={})
+
+
+def test_boosttrack_yaml_defaults_match_reference_constructor_names():
+    """configs/trackers/boosttrack.yaml keys are BoostTrack.__init__ parameters (plugin path)."""
+    import inspect
+
+    import yaml
+
+    from boxmot_amd import BoostTrack, get_tracker_config
+
+    cfg = yaml.safe_load(open(get_tracker_config("boosttrack")))
+    params = inspect.signature(BoostTrack.__init__).parameters
+    assert set(cfg) <= set(params)
+    d = {k: v["default"] for k, v in cfg.items()}
+    assert d["use_rich_s"] and d["use_sb"] and d["use_vt"] and d["with_reid"]  # BoostTrack++
+    assert (d["max_age"], d["min_hits"], d["det_thresh"]) == (60, 3, 0.6)
 
 
 def test_synthetic_scene_is_deterministic_per_frame():
