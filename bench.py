@@ -5,7 +5,8 @@ A step = one frame of every sequence this rank holds, advanced by one `Engine.st
 pipeline of kernels).  Workload (BASELINE.json configs[2], the north_star's
 256-track x 128-det x 512-d target): BoT-SORT on synthetic grid scenes of 256 objects detected
 w.p. 0.5 (~128 dets/frame, all above track_high_thresh) with 512-d float32 embeddings;
-`--config bytetrack` runs configs[1] (ByteTrack, IoU only).  Each rank holds `--seqs` independent
+`--config bytetrack` runs configs[1] (ByteTrack, IoU only); `--config boosttrack` the C5 tracker
+(BoostTrack++ with 512-d float64 ReID on MOT17-sized scenes: 60 objects, ~30 dets/frame).  Each rank holds `--seqs` independent
 sequences (weak scaling: the sequence count per GPU is fixed as N grows; no per-frame
 collective).  Inputs for every timed frame are generated on the GPU and resident in HBM before
 the timed region.
@@ -51,8 +52,15 @@ CONFIGS = {
     "ocsort256": ("ocsort", 256, 0, dict(min_conf=0.1, det_thresh=0.6, max_age=30, min_hits=3,
                                          asso_threshold=0.3, delta_t=3, inertia=0.1,
                                          use_byte=False, Q_xy_scaling=0.01, Q_s_scaling=0.0001)),
+    # BoostTrack++ (configs[4]'s tracker, YAML defaults) on MOT17-ablation-sized sequences
+    # (T ~ 20-40 live tracks, D ~ 30 dets, 512-d ReID)
+    "boosttrack": ("boosttrack", 60, 512, dict(
+        max_age=60, min_hits=3, det_thresh=0.6, iou_threshold=0.3, use_ecc=True,
+        min_box_area=10, aspect_ratio_thresh=1.6, lambda_iou=0.5, lambda_mhd=0.25,
+        lambda_shape=0.25, use_dlo_boost=True, use_duo_boost=True, dlo_boost_coef=0.65,
+        s_sim_corr=False, use_rich_s=True, use_sb=True, use_vt=True, with_reid=True)),
 }
-OCS_CONF_LO = 0.3  # OCSort scenes: confidences U(0.3, 1) -> ~40% below det_thresh
+OCS_CONF_LO = 0.3  # OCSort / BoostTrack scenes: confidences U(0.3, 1) -> ~40% below det_thresh
 
 # OCSort per-launch algorithmic bytes: per live track the XYSR state (x[7], P[49] f64) read and
 # written plus its observation record (last_obs, velocity, k-previous box: 12 f64) read; per
@@ -88,13 +96,30 @@ def stage_bytes(stage, u, F, es=4):
     }[stage]
 
 
+def boost_stage_bytes(stage, u, F):
+    """Algorithmic HBM bytes of one BoostTrack launch from the frame's unit counts
+    summed over sequences: dets, kept, tracks (entering the frame), outputs, records, pairs."""
+    return {
+        # every detection's and live track's f64 embedding read once, one f64 entry per pair out
+        "embcost": (u["dets"] + u["tracks"]) * F * 8 + u["pairs"] * 8,
+        # Kalman state (x[8], P[64] + scalars, 616 B) read + written per track, f32 det rows in,
+        # the pair's ReID entry read, output rows + update records out
+        "frame": u["tracks"] * 2 * 616 + u["dets"] * 24 + u["pairs"] * 8 + u["outputs"] * 64 +
+                 u["records"] * 16,
+        # detection row + track embedding read, track embedding written, per record
+        "feature": u["records"] * 3 * F * 8,
+    }[stage]
+
+
 def cpu_baseline(kind, n_obj, emb_dim, params, seconds=15.0, warm_frames=40):
     """Time the C oracle (port of the reference semantics, 1 thread) on one sequence of the
     same workload: frames/s over a bounded sample after `warm_frames` of warm-up."""
     from boxmot_amd.synth import SyntheticScene
     from oracle import pyoracle as po
 
-    extra = dict(conf_lo=OCS_CONF_LO) if kind == "ocsort" else {}
+    extra = dict(conf_lo=OCS_CONF_LO) if kind in ("ocsort", "boosttrack") else {}
+    if kind == "boosttrack":
+        extra["emb_dtype"] = np.float64
     sc = SyntheticScene(n_obj=n_obj, seed=12345, emb_dim=emb_dim, **extra)
     tr = po.OracleTracker(kind, **params)
     t = 0
@@ -157,14 +182,20 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from boxmot_amd.engine import Engine, EngineParams, OcsortEngine, OcsortParams
+    from boxmot_amd.engine import (BoostEngine, BoostParams, Engine, EngineParams, OcsortEngine,
+                                   OcsortParams)
     from boxmot_amd.shard import gather_records, output_checksum, shard_sequences
     from boxmot_amd.synth import TorchSceneBatch
 
     kind, n_obj, F, params = CONFIGS[args.config]
     S = args.seqs
     ocs = kind == "ocsort"
-    if ocs:
+    bst = kind == "boosttrack"
+    if bst:
+        eng = BoostEngine(n_seq=S, track_cap=128, det_cap=max(64, n_obj), emb_dim=F,
+                          params=BoostParams(**params))
+        stages = list(BoostEngine.STAGES)
+    elif ocs:
         tcap = int(os.environ.get("BX_OCS_TRACK_CAP", max(64, 2 * n_obj)))
         eng = OcsortEngine(n_seq=S, track_cap=tcap, det_cap=max(64, n_obj),
                            params=OcsortParams(**params))
@@ -176,9 +207,11 @@ def main():
                   if F or s not in ("det_features", "gate", "cosine", "features")]
     # this rank's shard: global sequences [rank*S, (rank+1)*S) — weak scaling, no exchange
     gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev,
-                          **(dict(conf_lo=OCS_CONF_LO) if ocs else {}))
+                          **(dict(conf_lo=OCS_CONF_LO) if ocs or bst else {}))
     total = args.warmup + args.steps
     frames = [gen.frame(t) for t in range(1, total + 1)]  # resident in HBM before timing
+    if bst:  # BoostTrack consumes float64 embeddings (the dtype `boxmot eval` loads)
+        frames = [(d, o, e.double()) for d, o, e in frames]
     max_n = max(int(f[1][-1].item()) for f in frames)
     out = torch.empty((max_n, 8), dtype=torch.float64, device=dev)
     cnt = torch.empty(S, dtype=torch.int32, device=dev)
@@ -189,6 +222,8 @@ def main():
         d, off, e = frames[k]
         if ocs:
             eng.step(d, off, out, cnt, stream=stream.cuda_stream)
+        elif bst:
+            eng.step(d, off, e, None, out, cnt, stream=stream.cuda_stream)
         else:
             eng.step(d, off, e, None, out, cnt, stream=stream.cuda_stream)
 
@@ -228,6 +263,7 @@ def main():
     units = eng.frame_stats()  # last timed frame, all sequences of this rank
     if ocs:
         units["dets"] = int(frames[total - 1][1][-1].item())
+    emb_bytes = 8 if bst else 4
 
     # per-sequence records of this rank's shard: [global seq id, frames timed, dets timed,
     # rows of the last frame, checksum of the last frame, rank wall s, dominant-stage ms]
@@ -249,6 +285,8 @@ def main():
         if ocs:
             per_launch = (units["tracks"] * OCS_TRACK_BYTES + units["dets"] * 24 +
                           units["outputs"] * 64)
+        elif bst:
+            per_launch = boost_stage_bytes(dominant, units, F)
         else:
             per_launch = stage_bytes(dominant, units, F)
         achieved = per_launch / (dom_ms * 1e-3) / 1e9
@@ -262,7 +300,8 @@ def main():
             "config": {"workload": f"{args.config}: {S} sequences/GPU x {n_obj} tracks x "
                                    f"~{mean_d:.0f} dets" + (f" x {F}-d ReID" if F else ""),
                        "tracker": kind, "n_seq_per_gpu": S, "n_tracks": n_obj,
-                       "n_dets_mean": round(mean_d, 1), "feat_dim": F, "emb_dtype": "f32",
+                       "n_dets_mean": round(mean_d, 1), "feat_dim": F,
+                       "emb_dtype": "f64" if emb_bytes == 8 else "f32",
                        "parallelism": f"seq-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -67,7 +67,34 @@ struct BstDev {
   double* rec_a;          // [S][D] EMA weight alpha, < 0: newborn copy          (reid)
   const double* conf_tab; // [ntab] 0.9 ** k (get_confidence)
   int* status;
+  unsigned long long* dbg;  // [S][BST_DBG] phase stamps (diagnostic builds only, else null)
 };
+
+// Diagnostic phase stamps and counters (build with -DBX_PHASE_TIMING; never shipped): per
+// sequence, cycles accumulated per phase over all frames [0, 16) and event counters [16, 32).
+constexpr int BST_DBG = 32;
+#ifdef BX_PHASE_TIMING
+#define BSTAMP(k)                                                                    \
+  do {                                                                               \
+    __syncthreads();                                                                 \
+    if (threadIdx.x == 0 && g.dbg) {                                                 \
+      const unsigned long long _now = __builtin_amdgcn_s_memtime();                  \
+      g.dbg[(size_t)seq * BST_DBG + (k)] += _now - t_last;                           \
+      t_last = _now;                                                                 \
+    }                                                                                \
+  } while (0)
+#define BCOUNT(k, v)                                                                 \
+  do {                                                                               \
+    if (threadIdx.x == 0 && g.dbg) g.dbg[(size_t)seq * BST_DBG + 16 + (k)] += (v);   \
+  } while (0)
+#else
+#define BSTAMP(k) \
+  do {            \
+  } while (0)
+#define BCOUNT(k, v) \
+  do {               \
+  } while (0)
+#endif
 
 // ------------------------------------------------------------------------------------------
 // fdlibm exp (oracle/bxo_boost.c bxo_exp)
@@ -192,10 +219,11 @@ __device__ __forceinline__ double shape_sim(const double* a, const double* b, in
   return bst_exp(-(fabs(dw - tw) / mw + fabs(dh - th) / mh));
 }
 
-// get_mh_dist_matrix entry (boosttrack.py:356-369); r = tb row (x at +6, 1/diag(P) at +10)
+// get_mh_dist_matrix entry (boosttrack.py:356-369); det = LDS row (convert_bbox_to_z at +7),
+// r = tb row (x at +6, 1/diag(P) at +10)
+constexpr int DDW = 11;  // doubles per detection row: x1 y1 x2 y2 conf cls det_ind z[4]
 __device__ __forceinline__ double mh_dist(const double* det, const double* r) {
-  double z[4];
-  bbox_to_z(det, z);
+  const double* z = det + 7;
   double s = 0.0;
 #pragma unroll
   for (int q = 0; q < 4; q++) {
@@ -279,7 +307,8 @@ __device__ __forceinline__ void okf_update(int r, double& xr, double (&Pr)[8], c
 
 // ------------------------------------------------------------------------------------------
 struct BstLds {
-  double* dd;    // [D][7] detections of the frame (float32 values as f64, conf boosted, det_ind)
+  double* dd;    // [D][DDW] detections of the frame (float32 values as f64, conf boosted,
+                 // det_ind, convert_bbox_to_z)
   double* cost;  // [cost_lds]
   double* colsum;  // [T]
   int *kd, *bi;    // [D] kept detections, DUO boost candidates
@@ -295,7 +324,7 @@ __device__ void carve(const BstDev& g, char* base, BstLds& L) {
   auto takeD = [&](size_t n) { double* p = (double*)(base + o); o += n * 8; return p; };
   auto takeI = [&](size_t n) { int* p = (int*)(base + o); o += ((n * 4 + 7) / 8) * 8; return p; };
   const int N = g.N, D = g.D, T = g.T;
-  L.dd = takeD((size_t)D * 7);
+  L.dd = takeD((size_t)D * DDW);
   L.cost = takeD(g.cost_lds);
   L.colsum = takeD(T);
   L.jv.v = takeD(N);
@@ -325,7 +354,7 @@ __device__ void carve(const BstDev& g, char* base, BstLds& L) {
 
 size_t lds_bytes(int D, int T, int N, int cost_lds) {
   auto dI = [](size_t n) { return ((n * 4 + 7) / 8) * 8; };
-  return (size_t)D * 7 * 8 + (size_t)cost_lds * 8 + (size_t)T * 8 + 2 * (size_t)N * 8 + 2 * 8 +
+  return (size_t)D * DDW * 8 + (size_t)cost_lds * 8 + (size_t)T * 8 + 2 * (size_t)N * 8 + 2 * 8 +
          2 * dI(D) + 2 * dI(T) + 2 * dI(2 * N) + 2 * dI(D + T) + 4 * dI(N) + 6 * dI(N) + dI(8);
 }
 
@@ -338,6 +367,7 @@ __global__ void __launch_bounds__(OW)
   carve(g, lds_raw, L);
   const int lane = threadIdx.x;
   const int b = blockIdx.x, seq = seq0 + b;
+  L.jv.dc = g.dbg ? g.dbg + (size_t)seq * BST_DBG + 24 : nullptr;
   const int r0 = det_off[b];
   int n = det_off[b + 1] - r0;
   if (n > g.D) {  // the host checks det_cap; a device-side overflow is latched, never run past
@@ -355,12 +385,20 @@ __global__ void __launch_bounds__(OW)
   const int nt = sq[SB_NTR];
   const double thr = g.iou_thr;
   const double det_thresh = g.det_thresh;
+#ifdef BX_PHASE_TIMING
+  unsigned long long t_last = __builtin_amdgcn_s_memtime();
+#endif
 
   // detections (x1,y1,x2,y2,conf,cls, det_ind = input row) and the track list
-  for (int q = lane; q < n * 6; q += OW) L.dd[(q / 6) * 7 + q % 6] = (double)dets[(size_t)r0 * 6 + q];
-  for (int i = lane; i < n; i += OW) L.dd[7 * i + 6] = (double)i;
+  for (int q = lane; q < n * 6; q += OW) L.dd[(q / 6) * DDW + q % 6] = (double)dets[(size_t)r0 * 6 + q];
+  __syncthreads();
+  for (int i = lane; i < n; i += OW) {
+    L.dd[DDW * i + 6] = (double)i;
+    bbox_to_z(L.dd + DDW * i, L.dd + DDW * i + 7);
+  }
   for (int p = lane; p < nt; p += OW) L.lst[p] = order[p];
   __syncthreads();
+  BSTAMP(0);
 
   // ---- CMC warp (camera_update, boosttrack.py:81-103) + predict (:105-111), octet per track;
   // tb row: box[4], get_confidence, time_since_update, x[0..3], 1/diag(P)[0..3]
@@ -414,6 +452,7 @@ __global__ void __launch_bounds__(OW)
     }
   }
   __syncthreads();
+  BSTAMP(1);
 
   // ---- DLO confidence boost (boosttrack.py:413-456) ----------------------------------------
   if (g.use_dlo && n > 0 && nt > 0) {
@@ -425,7 +464,7 @@ __global__ void __launch_bounds__(OW)
           double cs = 0.0;
           for (int d = 0; d < n; d++) {
             bool m;
-            const double e = mh_num(mh_dist(L.dd + 7 * d, rw), m);
+            const double e = mh_num(mh_dist(L.dd + DDW * d, rw), m);
             cs = d == 0 ? e : cs + e;
           }
           L.colsum[t] = cs;
@@ -436,7 +475,7 @@ __global__ void __launch_bounds__(OW)
     for (int d0 = 0; d0 < n; d0 += OW) {  // lane per detection
       const int d = d0 + lane;
       if (d < n) {
-        const double* a = L.dd + 7 * d;
+        const double* a = L.dd + DDW * d;
         double max_s = 0.0;
         bool vt = false;
         for (int t = 0; t < nt; t++) {
@@ -465,18 +504,19 @@ __global__ void __launch_bounds__(OW)
           }
           if (g.use_vt && vt) c = nmax(c, det_thresh + 1e-5);
         }
-        L.dd[7 * d + 4] = c;
+        L.dd[DDW * d + 4] = c;
       }
     }
     __syncthreads();
   }
 
+  BSTAMP(2);
   // ---- DUO confidence boost (boosttrack.py:371-411) ----------------------------------------
   if (g.use_duo && n > 0 && nt > 0) {
     const int nb = wave_compact(
         n,
         [&](int d) {
-          const double* a = L.dd + 7 * d;
+          const double* a = L.dd + DDW * d;
           double m = 0.0;
           for (int t = 0; t < nt; t++) {
             const double v = mh_dist(a, tb + (size_t)t * TBB);
@@ -488,10 +528,10 @@ __global__ void __launch_bounds__(OW)
     if (nb > 0) {
       // bdiou = iou(boost, boost) - eye: row maxima -> remaining (<= .3) / args (> .3)
       for (int i = lane; i < nb; i += OW) {
-        const double* a = L.dd + 7 * L.bi[i];
+        const double* a = L.dd + DDW * L.bi[i];
         double m = 0.0;
         for (int j = 0; j < nb; j++) {
-          const double v = iou_b(a, L.dd + 7 * L.bi[j]) - (i == j ? 1.0 : 0.0);
+          const double v = iou_b(a, L.dd + DDW * L.bi[j]) - (i == j ? 1.0 : 0.0);
           m = j == 0 ? v : nmax(m, v);
         }
         L.fl[i] = (m <= 0.3 ? 1 : 0) | (m > 0.3 ? 2 : 0);
@@ -500,24 +540,25 @@ __global__ void __launch_bounds__(OW)
       // an overlapping candidate stays if it holds the maximum confidence of its overlaps
       for (int i = lane; i < nb; i += OW) {
         if (!(L.fl[i] & 2)) continue;
-        const double* a = L.dd + 7 * L.bi[i];
+        const double* a = L.dd + DDW * L.bi[i];
         double cm = a[4];
         for (int j = 0; j < nb; j++) {
           if (!(L.fl[j] & 2)) continue;
-          const double* bj = L.dd + 7 * L.bi[j];
+          const double* bj = L.dd + DDW * L.bi[j];
           if (iou_b(a, bj) - (i == j ? 1.0 : 0.0) > 0.3) cm = nmax(cm, bj[4]);
         }
         if (a[4] == cm) L.fl[i] |= 4;
       }
       __syncthreads();
       for (int i = lane; i < nb; i += OW)
-        if (L.fl[i] & 5) L.dd[7 * L.bi[i] + 4] = det_thresh + 1e-4;
+        if (L.fl[i] & 5) L.dd[DDW * L.bi[i] + 4] = det_thresh + 1e-4;
       __syncthreads();
     }
   }
 
+  BSTAMP(3);
   // ---- detections kept for the association (boosttrack.py:262-266) ------------------------
-  const int nk = wave_compact(n, [&](int d) { return L.dd[7 * d + 4] >= det_thresh; },
+  const int nk = wave_compact(n, [&](int d) { return L.dd[DDW * d + 4] >= det_thresh; },
                               [&](int d, int p) { L.kd[p] = d; });
 
   // ---- associate (assoc.py:156-200) ---------------------------------------------------------
@@ -538,7 +579,7 @@ __global__ void __launch_bounds__(OW)
           double cs = 0.0;
           for (int i = 0; i < nk; i++) {
             bool m;
-            const double e = mh_num(mh_dist(L.dd + 7 * L.kd[i], rw), m);
+            const double e = mh_num(mh_dist(L.dd + DDW * L.kd[i], rw), m);
             cs = i == 0 ? e : cs + e;
           }
           L.colsum[t] = cs;
@@ -546,6 +587,7 @@ __global__ void __launch_bounds__(OW)
       }
       for (int k = lane; k < nk; k += OW) L.rowcnt[k] = 0;
       __syncthreads();
+      BSTAMP(4);
       // the cost matrix (stored negated for lapjv(-cost)), lane per track; counts of entries
       // above the threshold per row/column for match()'s one-to-one test
       for (int t0 = 0; t0 < nt; t0 += OW) {
@@ -555,7 +597,7 @@ __global__ void __launch_bounds__(OW)
           int cc = 0;
           for (int i = 0; i < nk; i++) {
             const int d = L.kd[i];
-            const double* a = L.dd + 7 * d;
+            const double* a = L.dd + DDW * d;
             const double o = iou_b(a, rw);
             double cst = o;
             double cf = a[4] * rw[4];
@@ -577,6 +619,7 @@ __global__ void __launch_bounds__(OW)
         }
       }
       __syncthreads();
+      BSTAMP(5);
       int mr = 0, mc = 0;
       for (int k = lane; k < nk; k += OW) mr = max(mr, L.rowcnt[k]);
       for (int k = lane; k < nt; k += OW) mc = max(mc, L.colcnt[k]);
@@ -593,7 +636,10 @@ __global__ void __launch_bounds__(OW)
             });
       } else {  // lap.lapjv(-cost, extend_cost=True) -> [[y[i], i] for i in x if i >= 0]
         nmi = legacy_lap(C, nk, nt, L.jv, L.mi);
+        BCOUNT(0, 1);
+        BCOUNT(1, nk > nt ? nk : nt);
       }
+      BSTAMP(6);
     }
     // linear_assignment (assoc.py:117-153): unmatched = absent from the pairs, ascending; then
     // the validation, rejected pairs appended in pair order
@@ -614,7 +660,7 @@ __global__ void __launch_bounds__(OW)
         i = L.mi[2 * q];
         t = L.mi[2 * q + 1];
         const int d = L.kd[i];
-        const double o = iou_b(L.dd + 7 * d, tb + (size_t)t * TBB);
+        const double o = iou_b(L.dd + DDW * d, tb + (size_t)t * TBB);
         ok = o >= thr || (ec ? (o >= thr / 2 && ec[(size_t)d * g.T + t] >= 0.75) : false);
         rej = !ok;
       }
@@ -637,6 +683,10 @@ __global__ void __launch_bounds__(OW)
     __syncthreads();
   }
 
+  BSTAMP(7);
+  BCOUNT(2, nk);
+  BCOUNT(3, nt);
+  BCOUNT(4, 1);
   // ---- matched updates (boosttrack.py:297-306), octet per pair ------------------------------
   int* rec = g.reid ? g.rec + (size_t)seq * g.D * 2 : nullptr;
   double* rec_a = g.reid ? g.rec_a + (size_t)seq * g.D : nullptr;
@@ -645,7 +695,7 @@ __global__ void __launch_bounds__(OW)
     if (q < nm) {
       const int d = L.kd[L.mm[2 * q]];
       const int slot = L.lst[L.mm[2 * q + 1]];
-      const double* a = L.dd + 7 * d;
+      const double* a = L.dd + DDW * d;
       BstTrk& t = trk[slot];
       double xr = t.x[r], Pr[8];
 #pragma unroll
@@ -674,6 +724,7 @@ __global__ void __launch_bounds__(OW)
   }
   __syncthreads();
 
+  BSTAMP(8);
   // ---- births for the unmatched detections (boosttrack.py:308-312), free slots ascending ----
   for (int s2 = lane; s2 < g.T; s2 += OW) L.fl[s2] = 0;
   __syncthreads();
@@ -690,7 +741,7 @@ __global__ void __launch_bounds__(OW)
     if (k < nnew) {
       const int slot = L.lst2[k];
       const int d = L.kd[L.ud[k]];
-      const double* a = L.dd + 7 * d;
+      const double* a = L.dd + DDW * d;
       BstTrk& t = trk[slot];
       double z[4];
       bbox_to_z(a, z);
@@ -714,6 +765,7 @@ __global__ void __launch_bounds__(OW)
   }
   __syncthreads();
   const int ntr = nt + nnew;
+  BSTAMP(9);
 
   // ---- outputs in list order + filter_outputs (boosttrack.py:314-341), then deaths ----------
   double* orow = out + (size_t)r0 * 8;
@@ -744,6 +796,7 @@ __global__ void __launch_bounds__(OW)
   const int nkeep = wave_compact(
       ntr, [&](int k) { return trk[L.lst[k]].tsu <= g.max_age; },
       [&](int k, int p) { order[p] = L.lst[k]; });
+  BSTAMP(10);
   if (lane == 0) {
     out_count[b] = nout < n ? nout : n;
     sq[SB_FRAME] = frame;
@@ -1014,6 +1067,9 @@ int bx_boost_create(const bx_boost_config* c, bx_boost** out) {
   const size_t o_reca = d.reid ? carve_b(S * D * sizeof(double)) : 0;
   const size_t o_tab = carve_b(tab.size() * sizeof(double));
   const size_t o_st = carve_b(sizeof(int) * 4);
+#ifdef BX_PHASE_TIMING
+  const size_t o_dbg = carve_b(S * BST_DBG * sizeof(unsigned long long));
+#endif
   if (hipMalloc(&e->arena, off) != hipSuccess) {
     delete e;
     return bx_record_error(BX_ERR_HIP, "hipMalloc of the BoostTrack arena failed");
@@ -1031,6 +1087,11 @@ int bx_boost_create(const bx_boost_config* c, bx_boost** out) {
   d.rec_a = d.reid ? (double*)(base + o_reca) : nullptr;
   d.conf_tab = (const double*)(base + o_tab);
   d.status = (int*)(base + o_st);
+#ifdef BX_PHASE_TIMING
+  d.dbg = (unsigned long long*)(base + o_dbg);
+#else
+  d.dbg = nullptr;
+#endif
   BCHK(hipMemcpy(base + o_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
   BCHK(hipFuncSetAttribute((const void*)boost_frame_kernel,
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->lds));
@@ -1171,9 +1232,10 @@ int bx_boost_frame_stats_host(bx_boost* e, int seq0, int nseq, int64_t* sums) {
   if (nseq)
     BCHK(hipMemcpy(s.data(), e->dev.seqst + (size_t)seq0 * SQB, sizeof(int) * s.size(),
                    hipMemcpyDeviceToHost));
-  int64_t a[6] = {0, 0, 0, 0, 0, 0};
+  int64_t a[7] = {0, 0, 0, 0, 0, 0, 0};
   for (int k = 0; k < nseq; k++) {
     const int* q = s.data() + (size_t)k * SQB;
+    a[6] += (int64_t)q[SB_NDET] * q[SB_NT0];
     a[0] += q[SB_NDET];
     a[1] += q[SB_NKEEP];
     a[2] += q[SB_NT0];
@@ -1181,7 +1243,16 @@ int bx_boost_frame_stats_host(bx_boost* e, int seq0, int nseq, int64_t* sums) {
     a[4] += q[SB_NREC];
     a[5] = q[SB_FRAME] > a[5] ? q[SB_FRAME] : a[5];
   }
-  for (int k = 0; k < 6; k++) sums[k] = a[k];
+  for (int k = 0; k < 7; k++) sums[k] = a[k];
+  return BX_OK;
+}
+
+// diagnostic (not in the public header): the phase stamps of every sequence, [S][BST_DBG]
+int bx_boost_debug_host(bx_boost* e, unsigned long long* out) {
+  if (!e || !out || !e->dev.dbg) return bx_record_error(BX_ERR_INVALID, "not a timing build");
+  BCHK(hipDeviceSynchronize());
+  BCHK(hipMemcpy(out, e->dev.dbg, sizeof(unsigned long long) * BST_DBG * e->dev.S,
+                 hipMemcpyDeviceToHost));
   return BX_OK;
 }
 

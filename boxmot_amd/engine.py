@@ -419,13 +419,18 @@ class BoostEngine:
 
     def frame_stats(self, seq0: int = 0, nseq: int | None = None) -> dict:
         nseq = self.n_seq - seq0 if nseq is None else nseq
-        a = (C.c_int64 * 6)()
+        a = (C.c_int64 * 7)()
         N.check(self._L.bx_boost_frame_stats_host(self._h, seq0, nseq, a), "frame_stats")
-        return dict(zip(["dets", "kept", "tracks", "outputs", "records", "frame"],
+        return dict(zip(["dets", "kept", "tracks", "outputs", "records", "frame", "pairs"],
                         [int(x) for x in a]))
 
-    def probe(self, stage: int = 1) -> None:
-        N.check(self._L.bx_boost_probe(self._h, int(stage)), "bx_boost_probe")
+    STAGES = ["embcost", "frame", "feature"]
+
+    def probe(self, stage) -> None:
+        """Time one stage per step (name from STAGES or index); None = off."""
+        idx = -1 if stage is None else (self.STAGES.index(stage) if isinstance(stage, str)
+                                        else int(stage))
+        N.check(self._L.bx_boost_probe(self._h, idx), "bx_boost_probe")
 
     def probe_read(self):
         t, n = C.c_double(), C.c_int()

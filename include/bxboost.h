@@ -84,9 +84,10 @@ int bx_boost_set_id_count(bx_boost *e, int seq, int id_count, void *stream);
  * covariances P [cap][64], embeddings emb [cap][emb_dim] (any may be NULL); *n = tracks. */
 int bx_boost_tracks_host(bx_boost *e, int seq, int cap, int32_t *ids, double *x, double *p,
                          double *emb, int *n);
-/* Last-frame statistics over sequences [seq0, seq0+nseq) (host, synchronous): sums[6] =
+/* Last-frame statistics over sequences [seq0, seq0+nseq) (host, synchronous): sums[7] =
  * {detections, detections kept after the boosts, tracks entering the frame, output rows,
- * embedding-update records, max frame counter} — bench.py's unit counts. */
+ * embedding-update records, max frame counter, sum of detections x tracks (the ReID
+ * contraction's entries)} — bench.py's unit counts. */
 int bx_boost_frame_stats_host(bx_boost *e, int seq0, int nseq, int64_t *sums);
 /* Timing probe (benchmarks): stage 0 = ReID contraction, 1 = frame kernel, 2 = embedding
  * update; -1 = off.  While on, every step records a HIP event pair around that stage's launch;

@@ -19,7 +19,8 @@ STAGE_OF = {"det_feature_kernel": "det_features", "predict_kernel": "predict",
             "assoc_kernel": "assoc", "update_kernel": "update",
             "cov_predict_kernel": "cov_predict", "cov_predict_gmc_kernel": "cov_predict",
             "feature_kernel": "features", "finish_kernel": "finish",
-            "ocsort_frame_kernel": "ocsort_frame"}
+            "ocsort_frame_kernel": "ocsort_frame", "boost_embcost_kernel": "embcost",
+            "boost_frame_kernel": "frame", "boost_feature_kernel": "feature"}
 
 
 def kname(full):
