@@ -106,6 +106,28 @@ int bxo_boost_update(bxo_boost *b, const double *dets, int n, const double *embs
 double bxo_exp(double x);
 double bxo_pow15(double x);
 
+/* StrongSort, the fork's "enhanced" tracker (trackers/strongsort/strongsort.py:17-232, sort/...)
+ * with P6, handle_occlusions=False and the born-Confirmed switch (see bxo_strongsort.c). */
+typedef struct {
+    double min_conf, max_cos_dist, max_iou_dist;
+    int max_age, n_init, nn_budget;
+    double mc_lambda, ema_alpha, conf_thresh_high, conf_thresh_low, id_preservation_weight;
+    int crowd_detection, born_confirmed;
+} bxo_ss_params;
+typedef struct bxo_ss bxo_ss;
+bxo_ss *bxo_ss_new(const bxo_ss_params *p);
+void bxo_ss_free(bxo_ss *s);
+int bxo_ss_next_id(const bxo_ss *s);
+int bxo_ss_tracks(const bxo_ss *s, int cap, int *ids, int *state, double *mean, double *cov);
+/* dets[n,6] float64; embs [n][F] float64 (required when a detection passes min_conf); warp[6]
+ * 2x3 CMC affine (NULL = identity).  out [M][10] (x1,y1,x2,y2,id,conf,cls,det_ind,quality,
+ * occlusion=0); returns M, -2 if out_cap is too small, -4 without embeddings. */
+int bxo_ss_update(bxo_ss *s, const double *dets, int n, const double *embs, int F,
+                  const double *warp, double *out, int out_cap);
+/* scipy.optimize.linear_sum_assignment restated: pairs (rows[k], cols[k]) sorted by row;
+ * returns the count (-1 if infeasible). */
+int bxo_lsap(const double *cost, int nr, int nc, int *rows, int *cols);
+
 #ifdef __cplusplus
 }
 #endif

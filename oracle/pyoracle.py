@@ -21,8 +21,8 @@ _ip = C.POINTER(C.c_int)
 
 
 def build(force: bool = False) -> Path:
-    srcs = [HERE / n for n in ("bxo_ops.c", "bxo_track.c", "bxo_ocsort.c", "bxo_boost.c", "bxo.h",
-                               "bxo_internal.h")]
+    srcs = [HERE / n for n in ("bxo_ops.c", "bxo_track.c", "bxo_ocsort.c", "bxo_boost.c",
+                               "bxo_strongsort.c", "bxo.h", "bxo_internal.h")]
     if force or not LIB_PATH.exists() or any(
         s.stat().st_mtime > LIB_PATH.stat().st_mtime for s in srcs
     ):
@@ -40,6 +40,42 @@ class BoostParams(C.Structure):
                 ("dlo_boost_coef", C.c_double), ("use_ecc", C.c_int), ("use_dlo_boost", C.c_int),
                 ("use_duo_boost", C.c_int), ("s_sim_corr", C.c_int), ("use_rich_s", C.c_int),
                 ("use_sb", C.c_int), ("use_vt", C.c_int), ("with_reid", C.c_int)]
+
+
+class SsParams(C.Structure):
+    """bxo_ss_params (oracle/bxo.h)."""
+
+    _fields_ = [("min_conf", C.c_double), ("max_cos_dist", C.c_double),
+                ("max_iou_dist", C.c_double), ("max_age", C.c_int), ("n_init", C.c_int),
+                ("nn_budget", C.c_int), ("mc_lambda", C.c_double), ("ema_alpha", C.c_double),
+                ("conf_thresh_high", C.c_double), ("conf_thresh_low", C.c_double),
+                ("id_preservation_weight", C.c_double), ("crowd_detection", C.c_int),
+                ("born_confirmed", C.c_int)]
+
+
+# StrongSort.__init__ defaults (strongsort.py:43-66)
+SS_DEFAULTS = dict(min_conf=0.1, max_cos_dist=0.15, max_iou_dist=0.7, max_age=50, n_init=2,
+                   nn_budget=150, mc_lambda=0.995, ema_alpha=0.9, conf_thresh_high=0.7,
+                   conf_thresh_low=0.3, id_preservation_weight=0.1, crowd_detection=True,
+                   born_confirmed=True)
+
+
+def ss_params(**p):
+    q = dict(SS_DEFAULTS)
+    q.update({k: v for k, v in p.items() if k in SS_DEFAULTS})
+    return SsParams(**{k: (float(v) if isinstance(SS_DEFAULTS[k], float) else int(v))
+                       for k, v in q.items()})
+
+
+def lsap(cost):
+    """scipy.optimize.linear_sum_assignment restated (rows, cols)."""
+    c = np.ascontiguousarray(cost, np.float64)
+    nr, nc = c.shape
+    k = max(1, min(nr, nc))
+    r = np.zeros(k, np.int32)
+    cc = np.zeros(k, np.int32)
+    n = lib().bxo_lsap(_d(c), nr, nc, r.ctypes.data_as(_ip), cc.ctypes.data_as(_ip))
+    return r[:max(n, 0)], cc[:max(n, 0)]
 
 
 # BoostTrack.__init__ defaults (boosttrack.py:154-181)
@@ -108,6 +144,15 @@ def lib():
         L.bxo_boost_tracks.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.bxo_boost_update.argtypes = [C.c_void_p, _dp, C.c_int, C.c_void_p, C.c_int, _dp, _dp,
                                        C.c_int]
+        L.bxo_ss_new.argtypes = [C.POINTER(SsParams)]
+        L.bxo_ss_new.restype = C.c_void_p
+        L.bxo_ss_free.argtypes = [C.c_void_p]
+        L.bxo_ss_next_id.argtypes = [C.c_void_p]
+        L.bxo_ss_tracks.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p]
+        L.bxo_ss_update.argtypes = [C.c_void_p, _dp, C.c_int, C.c_void_p, C.c_int, _dp, _dp,
+                                    C.c_int]
+        L.bxo_lsap.argtypes = [_dp, C.c_int, C.c_int, _ip, _ip]
         L.bxo_exp.argtypes = [C.c_double]
         L.bxo_exp.restype = C.c_double
         L.bxo_pow15.argtypes = [C.c_double]
@@ -233,6 +278,11 @@ class OracleTracker:
         elif kind == "boosttrack":
             self._bp = boost_params(**p)
             self.h = L.bxo_boost_new(C.byref(self._bp))
+        elif kind == "strongsort":
+            if p.get("handle_occlusions", False):
+                raise NotImplementedError("oracle StrongSort: handle_occlusions=False only")
+            self._sp = ss_params(**p)
+            self.h = L.bxo_ss_new(C.byref(self._sp))
         else:
             raise KeyError(kind)
         self._cap = 1024
@@ -259,6 +309,17 @@ class OracleTracker:
                 raise RuntimeError(f"oracle update failed ({m})")
             return out[:m].copy()
         w = None if warp is None else _d(np.ascontiguousarray(warp, np.float64).reshape(6))
+        if self.kind == "strongsort":  # no setup_decorator: dets stay float64
+            ep, fd = None, 0
+            if embs is not None and n:
+                e64 = np.ascontiguousarray(embs, np.float64)
+                ep, fd = e64.ctypes.data_as(C.c_void_p), e64.shape[1]
+            cap = max(self._cap, 2 * n + 64)
+            out = np.zeros((cap, 10))
+            m = lib().bxo_ss_update(self.h, _d(dets), n, ep, fd, w, _d(out), cap)
+            if m < 0:
+                raise RuntimeError(f"oracle update failed ({m})")
+            return out[:m].copy()
         if self.kind == "boosttrack":
             d32 = np.ascontiguousarray(dets.astype(np.float32).astype(np.float64))
             ep, fd = None, 0
@@ -287,6 +348,8 @@ class OracleTracker:
             return lib().bxo_ocsort_id_count(self.h)
         if self.kind == "boosttrack":
             return lib().bxo_boost_id_count(self.h)
+        if self.kind == "strongsort":
+            return lib().bxo_ss_next_id(self.h) - 1
         return lib().bxo_id_count(self.h)
 
     def ocsort_tracks(self):
@@ -301,7 +364,8 @@ class OracleTracker:
     def __del__(self):
         h = getattr(self, "h", None)
         if h:
-            free = {"ocsort": lib().bxo_ocsort_free, "boosttrack": lib().bxo_boost_free}
+            free = {"ocsort": lib().bxo_ocsort_free, "boosttrack": lib().bxo_boost_free,
+                    "strongsort": lib().bxo_ss_free}
             free.get(self.kind, lib().bxo_free)(h)
             self.h = None
 

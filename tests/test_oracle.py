@@ -111,8 +111,34 @@ def test_tracker_fixture(path):
     for f, d, e in fixture_frames(fx):
         o = tr.update(d, e)
         rows.append(np.concatenate([np.full((o.shape[0], 1), f), o], 1))
-    compare_outputs(np.concatenate(rows, 0), fx["outputs"], box_atol=1e-9,
+    got = np.concatenate(rows, 0)
+    compare_outputs(got, fx["outputs"], box_atol=1e-9,
                     conf_atol=1e-9 if kind == "boosttrack" else None)
+    if kind == "strongsort":  # [M, 10]: + track quality score, occlusion level (0: no handler)
+        np.testing.assert_allclose(got[:, 9], fx["outputs"][:, 9], rtol=0, atol=1e-12)
+        np.testing.assert_array_equal(got[:, 10], fx["outputs"][:, 10])
+
+
+def test_lsap_matches_scipy_including_ties():
+    """StrongSort's scipy.optimize.linear_sum_assignment (sort/linear_assignment.py:70) is
+    restated exactly — Crouse's shortest augmenting path with its tie rules — so even tied
+    (thresholded) cost matrices give scipy's pairs."""
+    from scipy.optimize import linear_sum_assignment
+
+    rng = np.random.default_rng(0)
+    for trial in range(1500):
+        nr, nc = (int(v) for v in rng.integers(1, 10, 2))
+        if trial % 3 == 0:
+            c = rng.integers(0, 3, (nr, nc)).astype(float)
+        elif trial % 3 == 1:
+            c = rng.uniform(0, 1, (nr, nc))
+            c[c > 0.6] = 0.70001  # min_cost_matching's `cost > max_distance -> max + 1e-5`
+        else:
+            c = rng.uniform(0, 1, (nr, nc))
+        r, k = linear_sum_assignment(c)
+        r2, k2 = po.lsap(c)
+        np.testing.assert_array_equal(r, r2)
+        np.testing.assert_array_equal(k, k2)
 
 
 def test_exp_pow_within_one_ulp_of_numpy():
