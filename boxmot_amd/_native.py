@@ -19,13 +19,15 @@ LIB_PATH = LIB_DIR / "libbxassoc.so"
 HEADER = REPO / "include" / "bxassoc.h"
 HEADER_OCS = REPO / "include" / "bxocsort.h"
 HEADER_BOOST = REPO / "include" / "bxboost.h"
+HEADER_SS = REPO / "include" / "bxstrongsort.h"
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
     # numpy-identical rounding: no FMA contraction, IEEE f32 division/sqrt
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
 ]
-SOURCES = ["bx_engine.hip", "bx_ops.hip", "bx_ocsort.hip", "bx_nn.hip", "bx_boost.hip"]
+SOURCES = ["bx_engine.hip", "bx_ops.hip", "bx_ocsort.hip", "bx_nn.hip", "bx_boost.hip",
+           "bx_strongsort.hip"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -35,7 +37,7 @@ class NativeUnavailable(RuntimeError):
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the HIP extension for gfx950 in-tree (boxmot_amd/lib/libbxassoc.so)."""
     srcs = [CSRC / s for s in SOURCES] + [CSRC / "bx_device.h", CSRC / "bx_jv.h", HEADER,
-                                          HEADER_OCS, HEADER_BOOST]
+                                          HEADER_OCS, HEADER_BOOST, HEADER_SS]
     if not force and LIB_PATH.exists():
         t = LIB_PATH.stat().st_mtime
         if all(s.stat().st_mtime <= t for s in srcs):
@@ -89,7 +91,19 @@ class BxBoostConfig(C.Structure):
     ]
 
 
-# every symbol include/bxassoc.h, include/bxocsort.h and include/bxboost.h declare (checked by tests/test_native_abi.py)
+class BxSsConfig(C.Structure):
+    _fields_ = [
+        ("n_seq", C.c_int32), ("track_cap", C.c_int32), ("det_cap", C.c_int32),
+        ("emb_dim", C.c_int32), ("vec_cap", C.c_int32), ("min_conf", C.c_double),
+        ("max_cos_dist", C.c_double), ("max_iou_dist", C.c_double), ("max_age", C.c_int32),
+        ("n_init", C.c_int32), ("nn_budget", C.c_int32), ("mc_lambda", C.c_double),
+        ("ema_alpha", C.c_double), ("conf_thresh_high", C.c_double),
+        ("conf_thresh_low", C.c_double), ("id_preservation_weight", C.c_double),
+        ("crowd_detection", C.c_int32), ("born_confirmed", C.c_int32),
+    ]
+
+
+# every symbol include/*.h declares (checked by tests/test_native_abi.py)
 EXPORTS = [
     "bx_last_error", "bx_device_count", "bx_engine_create", "bx_engine_destroy",
     "bx_engine_reset", "bx_engine_step", "bx_engine_update_host", "bx_engine_status",
@@ -103,7 +117,9 @@ EXPORTS = [
     "bx_ocsort_frame_stats_host", "bx_boost_create", "bx_boost_destroy", "bx_boost_reset",
     "bx_boost_step", "bx_boost_update_host", "bx_boost_status", "bx_boost_counters_host",
     "bx_boost_set_id_count", "bx_boost_tracks_host", "bx_boost_frame_stats_host",
-    "bx_boost_probe", "bx_boost_probe_read",
+    "bx_boost_probe", "bx_boost_probe_read", "bx_ss_create", "bx_ss_destroy", "bx_ss_reset",
+    "bx_ss_step", "bx_ss_update_host", "bx_ss_status", "bx_ss_counters_host",
+    "bx_ss_tracks_host", "bx_ss_frame_stats_host", "bx_ss_probe", "bx_ss_probe_read",
 ]
 
 _vp, _ip, _dp, _fp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_float)
@@ -158,6 +174,17 @@ _SIGS = {
     "bx_boost_frame_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_boost_probe": ([_vp, C.c_int], C.c_int),
     "bx_boost_probe_read": ([_vp, _dp, _ip], C.c_int),
+    "bx_ss_create": ([C.POINTER(BxSsConfig), C.POINTER(C.c_void_p)], C.c_int),
+    "bx_ss_destroy": ([_vp], C.c_int),
+    "bx_ss_reset": ([_vp, C.c_int, C.c_int, _vp], C.c_int),
+    "bx_ss_step": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_ss_update_host": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp, _vp, _ip, _vp], C.c_int),
+    "bx_ss_status": ([_vp, _ip], C.c_int),
+    "bx_ss_counters_host": ([_vp, C.c_int, _ip, _ip, _ip, _ip], C.c_int),
+    "bx_ss_tracks_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _ip], C.c_int),
+    "bx_ss_frame_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
+    "bx_ss_probe": ([_vp, C.c_int], C.c_int),
+    "bx_ss_probe_read": ([_vp, _dp, _ip], C.c_int),
 }
 
 _lib = None

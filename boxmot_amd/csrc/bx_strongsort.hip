@@ -1,0 +1,1741 @@
+// bx_strongsort.hip — the fork's "enhanced" StrongSort per-frame update on MI355X.
+//
+// Reference: boxmot/trackers/strongsort/strongsort.py:45-345 (StrongSort.update, detection
+// quality, crowd mode), sort/tracker.py:63-344 (Tracker: three-stage matching, ID recovery,
+// lost buffer, partial_fit), sort/track.py:76-400 (Track), sort/linear_assignment.py:14-618
+// (matching_cascade, min_cost_matching, gate_cost_matrix + cost shaping,
+// NearestNeighborDistanceMetric), sort/iou_matching.py:10-87, utils/occlusion_handler.py:45-87,
+// 464-490 (detect_crowd_situations).  With P6 and handle_occlusions=False.
+//
+// Per frame, four launches on the caller's stream:
+//   ss_prep_kernel   wave per detection: the feature's wave-order norm (quality; BLAS order of
+//                    the reference unpinned), its numpy pairwise norm, the NN-normalised row
+//                    feat/(‖·‖₂+1e-8) and the track-feature row feat/(‖·‖_wave+1e-8) with its
+//                    norms
+//   ss_nn_kernel     wave per confirmed track: min over its distinct gallery samples of
+//                    1 − clip(ŝ·d̂) for every detection — the (samples × F)·(F × dets)
+//                    contraction on the fp64 matrix cores (v_mfma_f64_16x16x4f64, ascending-k
+//                    chain = the oracle's fma chain), max over rows by wave shuffles
+//   ss_rec_kernel    wave per (lost track, detection): ID-recovery cosine similarity
+//   ss_frame_kernel  one wave per sequence: crowd mode, CMC warp, detection quality + stable
+//                    sort, Kalman predict, the matching cascade (gating, motion/quality cost
+//                    shaping lane per track row, scipy's linear_sum_assignment restated
+//                    wave-parallel), the IoU stage, Kalman + feature updates (feature vectors
+//                    built wave-cooperatively), misses, ID recovery, births, lost buffer,
+//                    partial_fit budget pruning (lane per track), outputs
+// Every floating-point expression restates oracle/bxo_strongsort.c operation for operation.
+//
+// Track state lives in HBM: SsTrk slots, each with a private pool of `vec_cap` feature vectors
+// (its features list and its gallery samples reference pool entries: the gallery keeps (pool
+// index, sample quality) pairs in the reference's list order, duplicates included, so
+// partial_fit's stable sort-and-truncate is reproduced exactly while each vector is stored once).
+#include <float.h>
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/bxstrongsort.h"
+#include "bx_device.h"
+
+using namespace bx;
+
+int bx_record_error(int code, const char* msg);  // bx_engine.hip (shared bx_last_error)
+
+namespace {
+
+#include "bx_jv.h"
+
+constexpr int MAXF = 10, MAXC = 20, MAXH = 10, LOSTN = 30;
+constexpr double SS_INFTY = 1e5, SS_GATE = 9.4877;
+
+struct SsTrk {
+  double mean[8], cov[64];
+  double conf, cls, det_ind, base_alpha, quality, stability, app_cons, motion_cons;
+  double vel[MAXH][2], pos[MAXH][2];
+  double confh[MAXC];
+  int id, state, hits, age, tsu, max_age, n_init;
+  int nvel, npos, nconf, nfeat, missed, confirmed_det, low_streak, high_streak, lost_frame;
+  int gal_n;
+  int feat[MAXF];
+  unsigned long long vmask;  // pool entries in use
+};
+
+enum {
+  Q_FRAME = 0, Q_NEXTID, Q_NTR, Q_NLOST, Q_CROWD, Q_ORIG, Q_OMAXAGE, Q_OBUDGET, Q_MAXAGE,
+  Q_BUDGET, Q_HIST, Q_NNL, Q_NK, Q_NT0, Q_NOUT, Q_ROWS, SQS
+};
+
+struct SsDev {
+  int S, T, D, F, VP, GB, N;
+  double min_conf, max_iou, mc_lambda, ema_alpha, thi, tlo, idw;
+  int n_init, crowd, born;
+  SsTrk* trk;     // [S][T]
+  int* gal_v;     // [S][T][GB] pool index
+  double* gal_q;  // [S][T][GB] sample quality (wave norm)
+  double* vec;    // [S][T][VP][F]
+  double* vden;   // [S][T][VP] numpy pairwise norm + 1e-8 (NN sample normalisation)
+  double* vwn;    // [S][T][VP] wave-order norm
+  int* sq;        // [S][SQS]
+  double* sqd;    // [S][2] metric.matching_threshold, its original
+  int* order;     // [S][T] track list (slots)
+  int* lost;      // [S][LOSTN] lost buffer (slots)
+  int* nnl;       // [S][T] confirmed slots queried by the next frame's gallery distance
+  double* nnd;    // [S][T][D] NN distance by (slot, input detection)
+  double* dprep;  // [S][D][4] wave norm, pairwise norm of feat; wave norm, den of nf
+  double* dn;     // [S][D][F] feat / (pairwise norm + 1e-8)
+  double* nf;     // [S][D][F] feat / (wave norm + 1e-8)
+  double* recsim; // [S][LOSTN][D]
+  double* cost;   // [S][2T*D] scratch cost matrices
+  int* wsi;       // [S][WSI] int scratch
+  double* wsd;    // [S][WSD] double scratch
+  int wsi_n, wsd_n;
+  int* status;
+};
+
+__device__ __forceinline__ double* vecp(const SsDev& g, int seq, int slot, int v) {
+  return g.vec + ((((size_t)seq * g.T + slot) * g.VP + v) * (size_t)g.F);
+}
+__device__ __forceinline__ size_t vidx(const SsDev& g, int seq, int slot, int v) {
+  return ((size_t)seq * g.T + slot) * g.VP + v;
+}
+
+// ---- wave-cooperative vector primitives (64 lanes) ----------------------------------------
+// wave-order dot (oracle wave_dot): lane l sums a[l]b[l], a[l+64]b[l+64], ... then xor butterfly
+__device__ __forceinline__ double wdot(const double* a, const double* b, int n) {
+  const int lane = threadIdx.x & 63;
+  double s = 0.0;
+  for (int k = lane; k < n; k += 64) s += a[k] * b[k];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+  return s;
+}
+
+// numpy pairwise sum of x[k]^2 (PW_BLOCKSIZE 128): leaves found by numpy's halving, each leaf
+// summed by 8 lanes (lane j keeps numpy's accumulator r[j]), the leaves folded in the tree's
+// order by lane 0.  Called by all 64 lanes; result valid on every lane.
+constexpr int PW_MAXLEAF = 160;
+__device__ int pw_leaves(int n, int* lo, int* ln) {
+  int cnt = 0, so[24], sn[24], top = 1;
+  so[0] = 0;
+  sn[0] = n;
+  while (top > 0) {
+    const int o = so[--top], m = sn[top];
+    if (m <= 128) {
+      lo[cnt] = o;
+      ln[cnt] = m;
+      cnt++;
+      continue;
+    }
+    int n2 = m / 2;
+    n2 -= n2 % 8;
+    so[top] = o + n2;
+    sn[top] = m - n2;
+    top++;
+    so[top] = o;
+    sn[top] = n2;
+    top++;
+  }
+  return cnt;
+}
+__device__ double pw_fold(int n, const double* leaf) {
+  double acc[24];
+  int ap = 0, li = 0, sn[24], st[24], top = 1;
+  sn[0] = n;
+  st[0] = 0;
+  while (top > 0) {
+    const int t = top - 1, m = sn[t];
+    if (m <= 128) {
+      acc[ap++] = leaf[li++];
+      top--;
+      continue;
+    }
+    int n2 = m / 2;
+    n2 -= n2 % 8;
+    if (st[t] == 0) {
+      st[t] = 1;
+      sn[top] = n2;
+      st[top] = 0;
+      top++;
+    } else if (st[t] == 1) {
+      st[t] = 2;
+      sn[top] = m - n2;
+      st[top] = 0;
+      top++;
+    } else {
+      const double b = acc[--ap], a = acc[--ap];
+      acc[ap++] = a + b;
+      top--;
+    }
+  }
+  return acc[0];
+}
+// sqrt of numpy's pairwise sum of squares of x[0..n); lo/ln/leaf: per-wave scratch
+__device__ double wpw_norm(const double* x, int n, int* lo, int* ln, double* leaf) {
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) {
+    const int c = pw_leaves(n, lo, ln);
+    ln[PW_MAXLEAF - 1] = c;
+  }
+  __syncthreads();
+  const int nl = ln[PW_MAXLEAF - 1];
+  for (int base = 0; base < nl; base += 8) {
+    const int li = base + (lane >> 3), k = lane & 7;
+    double r = 0.0;
+    int m = 0, o = 0;
+    if (li < nl) {
+      m = ln[li];
+      o = lo[li];
+      if (m >= 8) {
+        const int full = m - (m % 8);
+        r = x[o + k] * x[o + k];
+        for (int i = 8 + k; i < full; i += 8) r += x[o + i] * x[o + i];
+      }
+    }
+    r = r + __shfl_xor(r, 1);
+    r = r + __shfl_xor(r, 2);
+    r = r + __shfl_xor(r, 4);
+    if (li < nl && k == 0) {
+      double res;
+      if (m < 8) {
+        res = 0.0;
+        for (int i = 0; i < m; i++) res += x[o + i] * x[o + i];
+      } else {
+        res = r;
+        for (int i = m - (m % 8); i < m; i++) res += x[o + i] * x[o + i];
+      }
+      leaf[li] = res;
+    }
+  }
+  __syncthreads();
+  double s = 0.0;
+  if (lane == 0) s = pw_fold(n, leaf);
+  s = __shfl(s, 0);
+  __syncthreads();
+  return sqrt(s);
+}
+
+// numpy pairwise sum of a short run (n <= 20: the confidence history), one lane
+__device__ double pw_sum_short(const double* x, int n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; i++) r += x[i];
+    return r;
+  }
+  double r[8];
+  for (int k = 0; k < 8; k++) r[k] = x[k];
+  int i;
+  for (i = 8; i < n - (n % 8); i += 8)
+    for (int k = 0; k < 8; k++) r[k] += x[i + k];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; i++) res += x[i];
+  return res;
+}
+__device__ double np_mean(const double* x, int n) { return pw_sum_short(x, n) / n; }
+__device__ double np_std(const double* x, int n) {
+  const double m = np_mean(x, n);
+  double d[MAXC];
+  for (int i = 0; i < n; i++) {
+    d[i] = x[i] - m;
+    d[i] = d[i] * d[i];
+  }
+  return sqrt(pw_sum_short(d, n) / n);
+}
+
+__device__ __forceinline__ double clipd(double x, double lo, double hi) {
+  return x < lo ? lo : (x > hi ? hi : x);
+}
+__device__ __forceinline__ double pymax(double a, double b) { return b > a ? b : a; }
+__device__ __forceinline__ double pymin(double a, double b) { return b < a ? b : a; }
+__device__ __forceinline__ double norm2(double a, double b) { return sqrt(a * a + b * b); }
+
+// ---- per-track scalar helpers (one lane) ----------------------------------------------------
+__device__ void to_tlwh(const SsTrk& t, double* r) {
+  r[0] = t.mean[0], r[1] = t.mean[1], r[2] = t.mean[2], r[3] = t.mean[3];
+  r[2] *= r[3];
+  r[0] -= r[2] / 2;
+  r[1] -= r[3] / 2;
+}
+__device__ void to_tlbr(const SsTrk& t, double* r) {
+  to_tlwh(t, r);
+  r[2] = r[0] + r[2];
+  r[3] = r[1] + r[3];
+}
+// dt row: tlwh[4], conf, cls, det_ind, quality
+constexpr int DTW = 8;
+__device__ void det_xyah(const double* d, double* r) {
+  r[0] = d[0], r[1] = d[1], r[2] = d[2], r[3] = d[3];
+  r[0] += r[2] / 2;
+  r[1] += r[3] / 2;
+  r[2] /= r[3];
+}
+
+__device__ void motion_cons(SsTrk& t, const double* prev, const double* cur) {
+  if (t.nvel < 2) return;
+  const double* pv = t.vel[t.nvel - 1];
+  const double pred0 = prev[0] + pv[0], pred1 = prev[1] + pv[1];
+  const double a0 = cur[0] - prev[0], a1 = cur[1] - prev[1];
+  const double p0 = pred0 - prev[0], p1 = pred1 - prev[1];
+  double c;
+  if (norm2(p0, p1) > 0) {
+    const double err = norm2(a0 - p0, a1 - p1);
+    const double mx = pymax(norm2(p0, p1) * 0.5, 10.0);
+    c = pymax(0, 1.0 - (err / mx));
+  } else {
+    c = norm2(a0, a1) < 5.0 ? 1.0 : 0.5;
+  }
+  t.motion_cons = 0.8 * t.motion_cons + 0.2 * c;
+}
+
+__device__ void push2(double (*h)[2], int& n, const double* v) {
+  if (n == MAXH) {
+    for (int k = 0; k < MAXH - 1; k++) h[k][0] = h[k + 1][0], h[k][1] = h[k + 1][1];
+    n--;
+  }
+  h[n][0] = v[0];
+  h[n][1] = v[1];
+  n++;
+}
+
+// base_kalman_filter.py:61-78 single-track predict: F (P F^T) + Q
+__device__ void track_predict(SsTrk& t) {
+  double* m = t.mean;
+  double* P = t.cov;
+  double q[8];
+  kf_process_noise(KIND_BYTE, m, q);
+  for (int k = 0; k < 4; k++) m[k] = m[k] + m[k + 4];
+  for (int i = 0; i < 8; i++) {
+    double M[8], M4[8];
+    for (int j = 0; j < 8; j++) {
+      M[j] = j < 4 ? P[8 * i + j] + P[8 * i + j + 4] : P[8 * i + j];
+      if (i < 4) M4[j] = j < 4 ? P[8 * (i + 4) + j] + P[8 * (i + 4) + j + 4] : P[8 * (i + 4) + j];
+    }
+    if (i < 4)
+      for (int j = 0; j < 8; j++) {
+        const double v = M[j] + M4[j];
+        P[8 * i + j] = i == j ? v + q[i] : v;
+      }
+    else
+      for (int j = 0; j < 8; j++) P[8 * i + j] = i == j ? M[j] + q[i] : M[j];
+  }
+  t.age++;
+  t.tsu++;
+  push2(t.vel, t.nvel, t.mean + 4);
+  push2(t.pos, t.npos, t.mean);
+  if (t.npos >= 2) motion_cons(t, t.pos[t.npos - 2], t.pos[t.npos - 1]);
+}
+
+__device__ void track_camera(SsTrk& t, const double* w) {
+  double b[4];
+  to_tlbr(t, b);
+  const double x1 = (w[0] * b[0] + w[1] * b[1]) + w[2], y1 = (w[3] * b[0] + w[4] * b[1]) + w[5];
+  const double x2 = (w[0] * b[2] + w[1] * b[3]) + w[2], y2 = (w[3] * b[2] + w[4] * b[3]) + w[5];
+  const double ww = x2 - x1, hh = y2 - y1;
+  const double cx = x1 + ww / 2, cy = y1 + hh / 2;
+  const double prev[2] = {t.mean[0], t.mean[1]};
+  t.mean[0] = cx, t.mean[1] = cy, t.mean[2] = ww / hh, t.mean[3] = hh;
+  const double cur[2] = {cx, cy};
+  motion_cons(t, prev, cur);
+}
+
+__device__ void track_missed(SsTrk& t) {
+  t.missed++;
+  int thr = t.max_age;
+  if (t.quality > 0.8)
+    thr = (int)(t.max_age * 1.5);
+  else if (t.quality < 0.3)
+    thr = (int)(t.max_age * 0.5);
+  if (t.state == 1)
+    t.state = 3;
+  else if (t.tsu > thr)
+    t.state = 3;
+}
+
+// Track.update's scalar part after the features (track.py:246-277)
+__device__ void track_update_scalars(SsTrk& t, const double* d) {
+  if (t.nconf == MAXC) {
+    for (int k = 0; k < MAXC - 1; k++) t.confh[k] = t.confh[k + 1];
+    t.nconf--;
+  }
+  t.confh[t.nconf++] = d[4];
+  if (d[4] > 0.7) {
+    t.high_streak++;
+    t.low_streak = 0;
+  } else if (d[4] < 0.3) {
+    t.low_streak++;
+    t.high_streak = 0;
+  } else {
+    t.low_streak = 0;
+    t.high_streak = 0;
+  }
+  t.hits++;
+  t.confirmed_det++;
+  t.tsu = 0;
+  double cq = d[4];
+  if (t.nconf > 1) {
+    const double avg = np_mean(t.confh, t.nconf);
+    const double stab = 1.0 - np_std(t.confh, t.nconf);
+    cq = 0.7 * cq + 0.3 * avg * stab;
+  }
+  const double lb = pymin(t.hits / 20.0, 0.2);
+  const double ab = pymax(0, (t.app_cons - 0.5) * 0.2);
+  const double mb = pymax(0, (t.motion_cons - 0.5) * 0.1);
+  t.quality = clipd(((cq + lb) + ab) + mb, 0.0, 1.0);
+  const double cs = t.nconf > 3 ? 1.0 - pymin(np_std(t.confh, t.nconf), 1.0) : 0.5;
+  const double hr = (double)t.confirmed_det / (t.age > 1 ? t.age : 1);
+  const double cons = (0.4 * t.app_cons + 0.3 * t.motion_cons) + 0.3 * cs;
+  t.stability = clipd(0.5 * hr + 0.5 * cons, 0.0, 1.0);
+  if (t.state == 1 && (t.hits >= t.n_init || (t.hits >= 1 && t.quality > 0.8))) t.state = 2;
+}
+
+// first free pool entry of a slot (-1 if the pool is exhausted)
+__device__ int pool_alloc(SsTrk& t, int VP) {
+  for (int v = 0; v < VP; v++)
+    if (!((t.vmask >> v) & 1ull)) {
+      t.vmask |= 1ull << v;
+      return v;
+    }
+  return -1;
+}
+
+// ---- the frame kernel's scratch -----------------------------------------------------------
+struct SsWs {
+  // ints
+  int *lst, *conf_t, *unconf_t, *aut, *cand, *ut3, *fut, *hi, *med, *lo, *aud, *rd, *ud, *ud2;
+  int *lvl, *ages, *mt, *tmp, *rows, *cols, *flag, *ti2, *dord;
+  int *path, *col4row, *row4col, *rem, *SR, *SC, *pwlo, *pwln, *sc;
+  // doubles
+  double *dt, *u, *v, *spc, *meas, *key, *pwleaf, *sd;
+};
+
+int ws_ints(int T, int D, int N) {
+  return T /*lst*/ + T + T + T + 2 * T /*cand*/ + 2 * T /*ut3*/ + 3 * T /*fut*/ + 3 * D + D /*aud*/ +
+         D /*rd*/ + 2 * (D + 2 * T) /*ud ud2*/ + T /*lvl*/ + T /*ages*/ + 4 * (D + 2) /*mt*/ +
+         2 * (T + D) /*tmp*/ + 2 * N /*rows cols*/ + 2 * T /*flag*/ + 2 * T /*ti2*/ +
+         6 * N + 2 * PW_MAXLEAF + 32 + D /*dord*/;
+}
+int ws_doubles(int T, int D, int N) {
+  return D * DTW + 3 * N + 4 * D + 2 * T + PW_MAXLEAF + 8;
+}
+
+__device__ void ws_carve(const SsDev& g, int seq, SsWs& w) {
+  int* pi = g.wsi + (size_t)seq * g.wsi_n;
+  double* pd = g.wsd + (size_t)seq * g.wsd_n;
+  const int T = g.T, D = g.D, N = g.N;
+  auto I = [&](int n) { int* p = pi; pi += n; return p; };
+  auto Dd = [&](int n) { double* p = pd; pd += n; return p; };
+  w.lst = I(T); w.conf_t = I(T); w.unconf_t = I(T); w.aut = I(T); w.cand = I(2 * T);
+  w.ut3 = I(2 * T); w.fut = I(3 * T); w.hi = I(D); w.med = I(D); w.lo = I(D); w.aud = I(D);
+  w.rd = I(D); w.ud = I(D + 2 * T); w.ud2 = I(D + 2 * T); w.lvl = I(T); w.ages = I(T);
+  w.mt = I(4 * (D + 2)); w.tmp = I(2 * (T + D)); w.rows = I(N); w.cols = I(N); w.flag = I(2 * T);
+  w.ti2 = I(2 * T); w.path = I(N); w.col4row = I(N); w.row4col = I(N); w.rem = I(N); w.SR = I(N);
+  w.SC = I(N); w.pwlo = I(PW_MAXLEAF); w.pwln = I(PW_MAXLEAF); w.sc = I(32); w.dord = I(D);
+  w.dt = Dd(D * DTW); w.u = Dd(N); w.v = Dd(N); w.spc = Dd(N); w.meas = Dd(4 * D);
+  w.key = Dd(2 * T); w.pwleaf = Dd(PW_MAXLEAF); w.sd = Dd(8);
+}
+
+// broadcast an int from lane 0 (all lanes call)
+__device__ __forceinline__ int bcast(int v) { return __shfl(v, 0); }
+__device__ __forceinline__ double bcastd(double v) { return __shfl(v, 0); }
+
+// stable sort of idx[0..n) by key descending (ties keep order): rank placement, lane-parallel
+template <class K>
+__device__ void stable_sort_desc(int* idx, int n, K key, int* tmp) {
+  const int lane = threadIdx.x & 63;
+  for (int i = lane; i < n; i += 64) tmp[i] = idx[i];
+  __syncthreads();
+  for (int i = lane; i < n; i += 64) {
+    const double ki = key(tmp[i]);
+    int r = 0;
+    for (int j = 0; j < n; j++) {
+      const double kj = key(tmp[j]);
+      r += (kj > ki) || (kj == ki && j < i);
+    }
+    idx[r] = tmp[i];
+  }
+  __syncthreads();
+}
+
+// keep a[k] unless it appears in column `col` of matches [m0, m1): in place via tmp
+__device__ int filter_matched(int* a, int na, const int* mt, int m0, int m1, int col, int* tmp) {
+  const int lane = threadIdx.x & 63;
+  const int n = wave_compact(
+      na,
+      [&](int k) {
+        for (int q = m0; q < m1; q++)
+          if (mt[2 * q + col] == a[k]) return false;
+        return true;
+      },
+      [&](int k, int p) { tmp[p] = a[k]; });
+  for (int k = lane; k < n; k += 64) a[k] = tmp[k];
+  __syncthreads();
+  return n;
+}
+
+__device__ __forceinline__ bool in_list(const int* a, int n, int v) {
+  for (int k = 0; k < n; k++)
+    if (a[k] == v) return true;
+  return false;
+}
+
+// ------------------------------------------------------------------------------------------
+// Detection features (wave per input detection, 64-thread blocks): prep [wave norm of feat,
+// pairwise norm of feat, wave norm of nf, pairwise norm of nf + 1e-8], dn, nf
+__global__ void __launch_bounds__(64)
+    ss_prep_kernel(SsDev g, int seq0, const int* __restrict__ det_off,
+                   const double* __restrict__ embs) {
+  __shared__ int lo[PW_MAXLEAF], ln[PW_MAXLEAF];
+  __shared__ double leaf[PW_MAXLEAF];
+  const int b = blockIdx.y, seq = seq0 + b, k = blockIdx.x;
+  const int r0 = det_off[b];
+  int n = det_off[b + 1] - r0;
+  if (n > g.D) n = g.D;
+  if (k >= n) return;
+  const int F = g.F, lane = threadIdx.x;
+  const double* x = embs + (size_t)(r0 + k) * F;
+  double* dn = g.dn + ((size_t)seq * g.D + k) * F;
+  double* nf = g.nf + ((size_t)seq * g.D + k) * F;
+  const double fn = sqrt(wdot(x, x, F));
+  const double pwn = wpw_norm(x, F, lo, ln, leaf);
+  const double dd = pwn + 1e-8, dw = fn + 1e-8;
+  for (int q = lane; q < F; q += 64) {
+    dn[q] = x[q] / dd;
+    nf[q] = x[q] / dw;
+  }
+  __syncthreads();
+  const double wn = sqrt(wdot(nf, nf, F));
+  const double pn = wpw_norm(nf, F, lo, ln, leaf) + 1e-8;
+  if (lane == 0) {
+    double* p = g.dprep + ((size_t)seq * g.D + k) * 4;
+    p[0] = fn;
+    p[1] = pwn;
+    p[2] = wn;
+    p[3] = pn;
+  }
+}
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// NearestNeighborDistanceMetric.distance for one confirmed track (wave per listed slot):
+// rows = its distinct gallery vectors x/den, columns = this frame's normalised detections.
+__global__ void __launch_bounds__(64)
+    ss_nn_kernel(SsDev g, int seq0, const int* __restrict__ det_off) {
+  __shared__ int rowv[64];
+  __shared__ int nrow_s;
+  const int b = blockIdx.y, seq = seq0 + b, k = blockIdx.x;
+  const int nl = g.sq[(size_t)seq * SQS + Q_NNL];
+  if (k >= nl) return;
+  const int r0 = det_off[b];
+  int n = det_off[b + 1] - r0;
+  if (n > g.D) n = g.D;
+  if (n <= 0) return;
+  const int slot = g.nnl[(size_t)seq * g.T + k], lane = threadIdx.x, F = g.F;
+  const SsTrk& t = g.trk[(size_t)seq * g.T + slot];
+  if (lane == 0) {  // distinct pool entries referenced by the gallery
+    unsigned long long seen = 0ull;
+    int c = 0;
+    const int* gv = g.gal_v + ((size_t)seq * g.T + slot) * g.GB;
+    for (int q = 0; q < t.gal_n; q++) {
+      const int v = gv[q];
+      if (!((seen >> v) & 1ull)) {
+        seen |= 1ull << v;
+        rowv[c++] = v;
+      }
+    }
+    nrow_s = c;
+  }
+  __syncthreads();
+  const int nrow = nrow_s;
+  double* out = g.nnd + ((size_t)seq * g.T + slot) * g.D;
+  const double* dnb = g.dn + (size_t)seq * g.D * F;
+  for (int d0 = 0; d0 < n; d0 += 16) {
+    double best = -INF;  // max over rows of the dot product, column d0 + (lane & 15)
+    bool any = false;
+    for (int rt = 0; rt < nrow; rt += 16) {
+      const int ra = rt + (lane & 15), col = d0 + (lane & 15);
+      const bool aok = ra < nrow, bok = col < n;
+      const double* ap = aok ? vecp(g, seq, slot, rowv[ra]) : nullptr;
+      const double den = aok ? g.vden[vidx(g, seq, slot, rowv[ra])] : 1.0;
+      const double* bp = dnb + (size_t)(bok ? col : 0) * F;
+      d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+      for (int k0 = 0; k0 < F; k0 += 4) {
+        const int kk = k0 + (lane >> 4);
+        const double a = (aok && kk < F) ? ap[kk] / den : 0.0;
+        const double bb = (bok && kk < F) ? bp[kk] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+      }
+      // lane holds column (lane & 15), rows (lane >> 4) + 4 q
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int row = rt + (lane >> 4) + 4 * q;
+        if (row < nrow) {
+          best = any ? (acc[q] > best ? acc[q] : best) : acc[q];
+          any = true;
+        }
+      }
+    }
+    // combine the four row groups holding column (lane & 15)
+    for (int o = 16; o <= 32; o <<= 1) {
+      const double ob = __shfl_xor(best, o);
+      const bool oa = __shfl_xor((int)any, o) != 0;
+      if (oa && (!any || ob > best)) best = ob;
+      any = any || oa;
+    }
+    const int col = d0 + (lane & 15);
+    if (lane < 16 && col < n && any) out[col] = 1.0 - clipd(best, -1.0, 1.0);
+  }
+}
+
+// _attempt_id_recovery similarities: wave per (lost track, detection)
+__global__ void __launch_bounds__(256)
+    ss_rec_kernel(SsDev g, int seq0, const int* __restrict__ det_off,
+                  const double* __restrict__ embs) {
+  const int b = blockIdx.y, seq = seq0 + b, li = blockIdx.x;
+  if (li >= g.sq[(size_t)seq * SQS + Q_NLOST]) return;
+  const int slot = g.lost[(size_t)seq * LOSTN + li];
+  const SsTrk& t = g.trk[(size_t)seq * g.T + slot];
+  if (t.nfeat == 0) return;
+  const int r0 = det_off[b];
+  int n = det_off[b + 1] - r0;
+  if (n > g.D) n = g.D;
+  const int v = t.feat[t.nfeat - 1], F = g.F;
+  const double* tf = vecp(g, seq, slot, v);
+  const double tn = g.vwn[vidx(g, seq, slot, v)];
+  for (int d = threadIdx.x >> 6; d < n; d += 4) {
+    const double* x = embs + (size_t)(r0 + d) * F;
+    const double dot = wdot(x, tf, F);
+    if ((threadIdx.x & 63) == 0)
+      g.recsim[((size_t)seq * LOSTN + li) * g.D + d] =
+          dot / (g.dprep[((size_t)seq * g.D + d) * 4 + 1] * tn);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// The frame kernel: one wave64 per sequence.
+struct SsCtx {
+  const SsDev& g;
+  SsWs& w;
+  int seq, lane;
+  SsTrk* trk;
+  int* sq;
+  double* sqd;
+  int* lost;
+  int ntr, nlost, nk, nm;
+  __device__ const double* det(int i) const { return w.dt + (size_t)w.dord[i] * DTW; }
+  __device__ int det_in(int i) const { return (int)det(i)[6]; }
+};
+
+// scipy.optimize.linear_sum_assignment (Crouse's shortest augmenting path, rectangular) on the
+// nr x nc row-major matrix C, wave-parallel: each row's Dijkstra relaxes the remaining columns
+// lane-parallel and picks the minimum with scipy's tie rule (the last unassigned column at the
+// minimum in `remaining` order, else the first at the minimum).  Pairs sorted by row into
+// w.rows/w.cols; returns their count.
+__device__ int lsap_wave(SsCtx& x, const double* C, int nr, int nc) {
+  SsWs& w = x.w;
+  const int lane = x.lane;
+  const bool tr = nc < nr;
+  const int R = tr ? nc : nr, CC = tr ? nr : nc;
+  auto cost = [&](int i, int j) -> double { return tr ? C[(size_t)j * nc + i] : C[(size_t)i * nc + j]; };
+  for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
+  for (int j = lane; j < CC; j += 64) w.v[j] = 0.0, w.path[j] = -1, w.row4col[j] = -1;
+  __syncthreads();
+  for (int cur = 0; cur < R; cur++) {
+    double minVal = 0.0;
+    int nrem = CC;
+    for (int it = lane; it < CC; it += 64) w.rem[it] = CC - it - 1;
+    for (int i = lane; i < R; i += 64) w.SR[i] = 0;
+    for (int j = lane; j < CC; j += 64) w.SC[j] = 0, w.spc[j] = INF;
+    __syncthreads();
+    int sink = -1, i = cur;
+    while (sink == -1) {
+      if (lane == 0) w.SR[i] = 1;
+      const double ui = w.u[i];
+      double m = INF;
+      for (int it = lane; it < nrem; it += 64) {
+        const int j = w.rem[it];
+        const double r = minVal + cost(i, j) - ui - w.v[j];
+        if (r < w.spc[j]) {
+          w.path[j] = i;
+          w.spc[j] = r;
+        }
+        m = fmin(m, w.spc[j]);
+      }
+      m = wave_min_d(m);
+      // tie rule: the last unassigned position at the minimum, else the first at the minimum
+      int last_un = -1, first_eq = 0x7fffffff;
+      for (int it = lane; it < nrem; it += 64) {
+        const int j = w.rem[it];
+        if (w.spc[j] == m) {
+          if (w.row4col[j] == -1) last_un = it > last_un ? it : last_un;
+          first_eq = it < first_eq ? it : first_eq;
+        }
+      }
+      for (int o = 32; o >= 1; o >>= 1) {
+        last_un = max(last_un, __shfl_xor(last_un, o));
+        first_eq = min(first_eq, __shfl_xor(first_eq, o));
+      }
+      if (!(m < INF)) {  // infeasible (cannot happen with finite costs)
+        if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
+        return 0;
+      }
+      const int index = last_un >= 0 ? last_un : first_eq;
+      minVal = m;
+      const int j = w.rem[index];
+      __syncthreads();
+      if (w.row4col[j] == -1)
+        sink = j;
+      else
+        i = w.row4col[j];
+      if (lane == 0) {
+        w.SC[j] = 1;
+        w.rem[index] = w.rem[nrem - 1];
+      }
+      nrem--;
+      __syncthreads();
+    }
+    for (int q = lane; q < R; q += 64)
+      if (q == cur)
+        w.u[q] += minVal;
+      else if (w.SR[q])
+        w.u[q] += minVal - w.spc[w.col4row[q]];
+    for (int j = lane; j < CC; j += 64)
+      if (w.SC[j]) w.v[j] -= minVal - w.spc[j];
+    __syncthreads();
+    if (lane == 0) {
+      int j = sink;
+      for (;;) {
+        const int q = w.path[j];
+        w.row4col[j] = q;
+        const int t = w.col4row[q];
+        w.col4row[q] = j;
+        j = t;
+        if (q == cur) break;
+      }
+    }
+    __syncthreads();
+  }
+  if (tr) {  // argsort(col4row): pairs ordered by the original row
+    for (int q = lane; q < R; q += 64) {
+      const int orow = w.col4row[q];
+      int rank = 0;
+      for (int k = 0; k < R; k++) rank += w.col4row[k] < orow;
+      w.rows[rank] = orow;
+      w.cols[rank] = q;
+    }
+  } else {
+    for (int q = lane; q < R; q += 64) {
+      w.rows[q] = q;
+      w.cols[q] = w.col4row[q];
+    }
+  }
+  __syncthreads();
+  return R;
+}
+
+enum { M_GATED = 0, M_IOU = 1 };
+
+// min_cost_matching (linear_assignment.py:14-93) of track positions ti x sorted detections di:
+// matches appended to w.mt at x.nm; unmatched tracks to ut_out (if non-null), detections to
+// ud_out.  Cost rows lane per track (gated_metric + gate_cost_matrix + id preservation, or
+// iou_cost), _enhance_cost_matrix and the max_distance clamp fused per entry.
+__device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* ti, int nt,
+                                  const int* di, int nd, int* ut_out, int& nut, int* ud_out,
+                                  int& nud) {
+  const SsDev& g = x.g;
+  SsWs& w = x.w;
+  const int lane = x.lane;
+  if (nd == 0 || nt == 0) {
+    for (int k = lane; k < nt; k += 64)
+      if (ut_out) ut_out[k] = ti[k];
+    for (int k = lane; k < nd; k += 64) ud_out[k] = di[k];
+    nut = nt;
+    nud = nd;
+    __syncthreads();
+    return;
+  }
+  double* C = g.cost + (size_t)x.seq * 2 * g.T * g.D;
+  if (kind == M_GATED) {
+    for (int c = lane; c < nd; c += 64) det_xyah(x.det(di[c]), w.meas + 4 * c);
+    __syncthreads();
+  }
+  const double* nnd = g.nnd + (size_t)x.seq * g.T * g.D;
+  for (int r = lane; r < nt; r += 64) {
+    const int slot = w.lst[ti[r]];
+    const SsTrk& t = x.trk[slot];
+    double* row = C + (size_t)r * nd;
+    if (kind == M_IOU) {
+      if (t.tsu > 1) {
+        for (int c = 0; c < nd; c++) row[c] = SS_INFTY;
+      } else {
+        double b[4];
+        to_tlwh(t, b);
+        const double br0 = b[0] + b[2], br1 = b[1] + b[3];
+        for (int c = 0; c < nd; c++) {
+          const double* q = x.det(di[c]);
+          const double tl0 = fmax(b[0], q[0]), tl1 = fmax(b[1], q[1]);
+          const double e0 = fmin(br0, q[0] + q[2]), e1 = fmin(br1, q[1] + q[3]);
+          const double ww = fmax(0.0, e0 - tl0), hh = fmax(0.0, e1 - tl1);
+          const double ai = ww * hh;
+          row[c] = 1.0 - ai / ((b[2] * b[3] + q[2] * q[3]) - ai);
+        }
+      }
+    } else {
+      // Mahalanobis gating (base_kalman_filter.py:166-194, kf_gating_soa order)
+      double S[16], L[16], rr[4];
+      kf_meas_noise(KIND_BYTE, t.mean, 0.0, rr);
+      for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) S[4 * i + j] = t.cov[8 * i + j] + (i == j ? rr[i] : 0.0);
+      const bool ok = chol4(S, L);
+      const double mf = 2.0 - t.motion_cons;
+      double pp0 = 0.0, pp1 = 0.0;
+      if (t.nvel > 0) pp0 = t.mean[0] + t.vel[t.nvel - 1][0], pp1 = t.mean[1] + t.vel[t.nvel - 1][1];
+      const double af = pymin(t.age / 10.0, 1.0);
+      double al = g.mc_lambda + (1 - g.mc_lambda) * af * 0.1;
+      al = al * (0.8 + 0.4 * t.motion_cons);
+      if (t.app_cons < 0.5) al = pymin(al * 1.2, 0.99);
+      al = clipd(al, 0.1, 0.99);
+      const double pb = g.idw * pymin(t.hits / 10.0, 1.0);
+      for (int c = 0; c < nd; c++) {
+        const double* z = w.meas + 4 * c;
+        double gd;
+        if (!ok) {
+          gd = __builtin_nan("");
+        } else {
+          double dd[4], y[4], s2 = 0.0;
+          for (int i = 0; i < 4; i++) dd[i] = z[i] - t.mean[i];
+          for (int i = 0; i < 4; i++) {
+            double sm = dd[i];
+            for (int j = 0; j < i; j++) sm -= L[4 * i + j] * y[j];
+            y[i] = sm / L[4 * i + i];
+            s2 += y[i] * y[i];
+          }
+          gd = s2;
+        }
+        double v = t.gal_n > 0 ? nnd[(size_t)slot * g.D + x.det_in(di[c])] : SS_INFTY;
+        if (gd > SS_GATE) v = SS_INFTY;
+        double m = gd * mf;
+        if (t.nvel > 0) {
+          const double ve = norm2(z[0] - pp0, z[1] - pp1);
+          m *= 1.0 + pymin(ve / 50.0, 1.0);
+        }
+        v = al * v + (1 - al) * m;
+        if (t.quality > 0.8) v *= 0.95;
+        if (t.hits > 10 && t.tsu == 0) v *= 0.98;
+        if (t.high_streak > 3) v *= 0.97;
+        if (t.low_streak > 2) v *= 1.05;
+        if (g.idw > 0) v *= (1.0 - pb);
+        row[c] = v;
+      }
+    }
+    // _enhance_cost_matrix + clamp
+    for (int c = 0; c < nd; c++) {
+      const double* d = x.det(di[c]);
+      double e = row[c];
+      const double cq = (t.quality + d[7]) / 2.0;
+      e *= clipd(1.0 - (cq - 0.5) * 0.2, 0.8, 1.2);
+      if (t.cls == d[5]) e *= 0.9;
+      double cf = 1.0;
+      if (t.conf > 0.7 && d[4] > 0.7)
+        cf = 0.9;
+      else if (t.conf < 0.3 || d[4] < 0.3)
+        cf = 1.1;
+      e *= cf;
+      if (e > max_d) e = max_d + 1e-5;
+      row[c] = e;
+    }
+  }
+  __syncthreads();
+  const int np_ = lsap_wave(x, C, nt, nd);
+  // assigned flags (w.SR rows, w.SC columns), unmatched in index order, then the rejected pairs
+  for (int r = lane; r < nt; r += 64) w.SR[r] = 0;
+  for (int c = lane; c < nd; c += 64) w.SC[c] = 0;
+  __syncthreads();
+  for (int q = lane; q < np_; q += 64) w.SR[w.rows[q]] = 1, w.SC[w.cols[q]] = 1;
+  __syncthreads();
+  nud = wave_compact(nd, [&](int c) { return w.SC[c] == 0; }, [&](int c, int p) { ud_out[p] = di[c]; });
+  nut = wave_compact(nt, [&](int r) { return w.SR[r] == 0; },
+                     [&](int r, int p) { if (ut_out) ut_out[p] = ti[r]; });
+  for (int c0 = 0; c0 < np_; c0 += 64) {
+    const int q = c0 + lane;
+    bool ok = false, rej = false;
+    int r = 0, c = 0;
+    if (q < np_) {
+      r = w.rows[q];
+      c = w.cols[q];
+      rej = C[(size_t)r * nd + c] > max_d;
+      ok = !rej;
+    }
+    const unsigned long long mo = __ballot(ok), mr = __ballot(rej);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    if (ok) {
+      const int p = x.nm + __popcll(mo & below);
+      w.mt[2 * p] = ti[r];
+      w.mt[2 * p + 1] = di[c];
+    }
+    if (rej) {
+      const int p = __popcll(mr & below);
+      if (ut_out) ut_out[nut + p] = ti[r];
+      ud_out[nud + p] = di[c];
+    }
+    x.nm += __popcll(mo);
+    nut += __popcll(mr);
+    nud += __popcll(mr);
+  }
+  __syncthreads();
+}
+
+// matching_cascade (linear_assignment.py:96-171): levels by time_since_update ascending (up to
+// tracker.max_age), each level's tracks ordered by -(quality + stability), stable
+__device__ void matching_cascade(SsCtx& x, double max_d, const int* ti, int nt, const int* di,
+                                 int nd) {
+  SsWs& w = x.w;
+  const int lane = x.lane;
+  int nud = nd;
+  for (int k = lane; k < nd; k += 64) w.ud[k] = di[k];
+  int na = 0;
+  if (lane == 0) {
+    for (int k = 0; k < nt; k++) {
+      const int a = x.trk[w.lst[ti[k]]].tsu;
+      bool seen = false;
+      for (int q = 0; q < na && !seen; q++) seen = w.ages[q] == a;
+      if (!seen) w.ages[na++] = a;
+    }
+    for (int p = 1; p < na; p++)
+      for (int y = p; y > 0 && w.ages[y - 1] > w.ages[y]; y--) {
+        const int tmp = w.ages[y];
+        w.ages[y] = w.ages[y - 1];
+        w.ages[y - 1] = tmp;
+      }
+  }
+  na = bcast(na);
+  __syncthreads();
+  const int max_age = x.sq[Q_MAXAGE];
+  for (int q = 0; q < na; q++) {
+    const int age = w.ages[q];
+    if (age > max_age) break;
+    const int nl = wave_compact(nt, [&](int k) { return x.trk[w.lst[ti[k]]].tsu == age; },
+                                [&](int k, int p) { w.lvl[p] = ti[k]; });
+    stable_sort_desc(w.lvl, nl,
+                     [&](int pos) {
+                       const SsTrk& t = x.trk[w.lst[pos]];
+                       return t.quality + t.stability;
+                     },
+                     w.tmp);
+    int nut_dummy = 0, nud2 = 0;
+    min_cost_matching(x, M_GATED, max_d, w.lvl, nl, w.ud, nud, nullptr, nut_dummy, w.ud2, nud2);
+    for (int k = lane; k < nud2; k += 64) w.ud[k] = w.ud2[k];
+    nud = nud2;
+    __syncthreads();
+  }
+}
+
+// Track.update (track.py:204-277), wave-cooperative: Kalman update and scalars on lane 0, the
+// feature vectors (similarity, adaptive-EMA smoothing, norms) on all lanes.
+__device__ void track_update(SsCtx& x, int slot, int di) {
+  const SsDev& g = x.g;
+  const int lane = x.lane, F = g.F;
+  SsTrk& t = x.trk[slot];
+  const double* d = x.det(di);
+  const int dk = x.det_in(di);
+  if (lane == 0) {
+    double bb[4];
+    det_xyah(d, bb);
+    t.conf = d[4], t.cls = d[5], t.det_ind = d[6];
+    kf_update_soa(KIND_BYTE, t.mean, t.cov, 1, bb, t.conf);
+  }
+  __syncthreads();
+  const double* nf = g.nf + ((size_t)x.seq * g.D + dk) * F;
+  const double* pr = g.dprep + ((size_t)x.seq * g.D + dk) * 4;
+  int v = -1;
+  if (lane == 0) v = pool_alloc(t, g.VP);
+  v = bcast(v);
+  const int nfeat = t.nfeat;
+  if (v < 0) {
+    if (lane == 0) atomicExch(g.status, (int)BX_ERR_TRACK_OVERFLOW);
+  } else {
+    double* dst = vecp(g, x.seq, slot, v);
+    const size_t vi = vidx(g, x.seq, slot, v);
+    if (nfeat > 0) {
+      const int lv = t.feat[nfeat - 1];
+      const double* last = vecp(g, x.seq, slot, lv);
+      const double wl = g.vwn[vidx(g, x.seq, slot, lv)];
+      const double sim = wdot(nf, last, F) / (pr[2] * wl + 1e-8);
+      const double cf = d[4] > 0.7 ? 1.0 : (d[4] > 0.3 ? 0.5 : 0.2);
+      const double af = sim > 0.7 ? 1.0 : (sim > 0.4 ? 0.7 : 0.4);
+      const double a = clipd(t.base_alpha * cf * af, 0.1, 0.95);
+      for (int q = lane; q < F; q += 64) dst[q] = a * last[q] + (1 - a) * nf[q];
+      __syncthreads();
+      const double ns = sqrt(wdot(dst, dst, F)) + 1e-8;
+      for (int q = lane; q < F; q += 64) dst[q] = dst[q] / ns;
+      __syncthreads();
+      const double wn = sqrt(wdot(dst, dst, F));
+      const double pn = wpw_norm(dst, F, x.w.pwlo, x.w.pwln, x.w.pwleaf) + 1e-8;
+      if (lane == 0) {
+        t.app_cons = 0.9 * t.app_cons + 0.1 * sim;
+        g.vwn[vi] = wn;
+        g.vden[vi] = pn;
+      }
+    } else {
+      for (int q = lane; q < F; q += 64) dst[q] = nf[q];
+      if (lane == 0) {
+        g.vwn[vi] = pr[2];
+        g.vden[vi] = pr[3];
+      }
+    }
+    if (lane == 0) {
+      if (t.nfeat == MAXF) {
+        for (int k = 0; k < MAXF - 1; k++) t.feat[k] = t.feat[k + 1];
+        t.nfeat--;
+      }
+      t.feat[t.nfeat++] = v;
+    }
+  }
+  if (lane == 0) track_update_scalars(t, d);
+  __syncthreads();
+}
+
+// Track.__init__ (track.py:76-131) into a free slot; the detection's feature, normalised as the
+// reference normalises it in place, is the first feature vector.
+__device__ void track_birth(SsCtx& x, int slot, int di) {
+  const SsDev& g = x.g;
+  const int lane = x.lane, F = g.F;
+  SsTrk& t = x.trk[slot];
+  const double* d = x.det(di);
+  const int dk = x.det_in(di);
+  if (lane == 0) {
+    double bb[4];
+    det_xyah(d, bb);
+    t.id = x.sq[Q_NEXTID]++;
+    t.conf = d[4], t.cls = d[5], t.det_ind = d[6];
+    t.hits = 1, t.age = 1, t.tsu = 0;
+    t.base_alpha = g.ema_alpha;
+    t.state = g.born ? 2 : 1;
+    t.confh[0] = d[4];
+    t.nconf = 1;
+    t.n_init = g.n_init;
+    t.max_age = x.sq[Q_MAXAGE];
+    t.quality = d[7];
+    t.stability = 0.0;
+    t.app_cons = 1.0;
+    t.motion_cons = 1.0;
+    t.nvel = t.npos = 0;
+    t.missed = 0;
+    t.confirmed_det = 1;
+    t.low_streak = 0;
+    t.high_streak = d[4] > 0.7 ? 1 : 0;
+    t.lost_frame = 0;
+    t.gal_n = 0;
+    t.nfeat = 0;
+    t.vmask = 1ull;  // pool entry 0 holds the first feature
+    kf_initiate(KIND_BYTE, bb, t.mean, t.cov);
+    push2(t.pos, t.npos, bb);
+    t.feat[0] = 0;
+    t.nfeat = 1;
+    const size_t vi = vidx(g, x.seq, slot, 0);
+    const double* pr = g.dprep + ((size_t)x.seq * g.D + dk) * 4;
+    g.vwn[vi] = pr[2];
+    g.vden[vi] = pr[3];
+  }
+  const double* nf = g.nf + ((size_t)x.seq * g.D + dk) * F;
+  double* dst = vecp(g, x.seq, slot, 0);
+  for (int q = lane; q < F; q += 64) dst[q] = nf[q];
+  __syncthreads();
+}
+
+// partial_fit's append + budget prune for one gallery (one lane): stable sort by quality
+// descending (insertion) and truncation, as samples_with_quality.sort(reverse=True)[:keep]
+__device__ void gal_prune(int* gv, double* gq, int& n, int keep) {
+  for (int i = 1; i < n; i++) {
+    const int v = gv[i];
+    const double q = gq[i];
+    int j = i - 1;
+    while (j >= 0 && gq[j] < q) {
+      gv[j + 1] = gv[j];
+      gq[j + 1] = gq[j];
+      j--;
+    }
+    gv[j + 1] = v;
+    gq[j + 1] = q;
+  }
+  if (n > keep) n = keep;
+}
+
+__global__ void __launch_bounds__(64)
+    ss_frame_kernel(SsDev g, int seq0, const double* __restrict__ dets,
+                    const int* __restrict__ det_off, const double* __restrict__ warps,
+                    double* __restrict__ out, int* __restrict__ out_count) {
+  const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
+  SsWs w;
+  ws_carve(g, seq, w);
+  SsCtx x{g, w, seq, lane, g.trk + (size_t)seq * g.T, g.sq + (size_t)seq * SQS,
+          g.sqd + (size_t)seq * 2, g.lost + (size_t)seq * LOSTN, 0, 0, 0, 0};
+  int* sq = x.sq;
+  int* order = g.order + (size_t)seq * g.T;
+  const int r0 = det_off[b];
+  int n = det_off[b + 1] - r0;
+  if (n > g.D) {
+    if (lane == 0) atomicExch(g.status, (int)BX_ERR_CAPACITY);
+    n = g.D;
+  }
+  const int frame = sq[Q_FRAME] + 1;
+  x.ntr = sq[Q_NTR];
+  x.nlost = sq[Q_NLOST];
+  const int nt0 = x.ntr;
+  for (int p = lane; p < x.ntr; p += 64) w.lst[p] = order[p];
+  // detections with conf >= min_conf, input order (strongsort.py:141-143)
+  x.nk = wave_compact(
+      n, [&](int k) { return dets[(size_t)(r0 + k) * 6 + 4] >= g.min_conf; },
+      [&](int k, int p) {
+        const double* r = dets + (size_t)(r0 + k) * 6;
+        double* d = w.dt + (size_t)p * DTW;
+        d[0] = r[0], d[1] = r[1], d[2] = r[2] - r[0], d[3] = r[3] - r[1];
+        d[4] = r[4], d[5] = r[5], d[6] = (double)k, d[7] = 0.0;
+        w.dord[p] = p;
+      });
+  int fid = frame;
+  if (x.nk == 0) {
+    for (int p = lane; p < x.ntr; p += 64) track_predict(x.trk[w.lst[p]]);
+    __syncthreads();
+    fid = 0;  // tracker.update([]) passes frame_id=None
+  } else {
+    if (g.crowd) {  // detect_crowd_situations (reads the tlwh boxes as xyxy)
+      int crowd = 0;
+      const int nn = x.ntr;
+      if (nn >= 3) {
+        long long high = 0;
+        for (int i = 0; i < nn; i++) {
+          double bi[4];
+          to_tlwh(x.trk[w.lst[i]], bi);
+          for (int j = i + 1 + lane; j < nn; j += 64) {
+            double bj[4];
+            to_tlwh(x.trk[w.lst[j]], bj);
+            const double xx1 = pymax(bi[0], bj[0]), yy1 = pymax(bi[1], bj[1]);
+            const double xx2 = pymin(bi[2], bj[2]), yy2 = pymin(bi[3], bj[3]);
+            const double ww = pymax(0, xx2 - xx1), hh = pymax(0, yy2 - yy1);
+            const double inter = ww * hh;
+            if (inter > 0) {
+              const double ai = (bi[2] - bi[0]) * (bi[3] - bi[1]);
+              const double aj = (bj[2] - bj[0]) * (bj[3] - bj[1]);
+              if (pymax(inter / ai, inter / aj) > 0.3) high++;
+            }
+          }
+        }
+        for (int o = 32; o >= 1; o >>= 1) high += __shfl_xor(high, o);
+        const long long total = (long long)nn * (nn - 1) / 2;
+        crowd = (double)high / (double)(total > 1 ? total : 1) > 0.3;
+      }
+      if (lane == 0) {
+        sq[Q_CROWD] = crowd;
+        if (crowd) {  // _adjust_for_crowd_mode (strongsort.py:183-208)
+          if (!sq[Q_ORIG]) {
+            sq[Q_OMAXAGE] = sq[Q_MAXAGE];
+            x.sqd[1] = x.sqd[0];
+            sq[Q_OBUDGET] = sq[Q_BUDGET];
+            sq[Q_ORIG] = 1;
+          }
+          sq[Q_MAXAGE] = (int)(sq[Q_OMAXAGE] * 1.5);
+          x.sqd[0] = x.sqd[1] * 0.8;
+          if (sq[Q_BUDGET]) sq[Q_BUDGET] = sq[Q_OBUDGET] * 2 < 300 ? sq[Q_OBUDGET] * 2 : 300;
+        }
+      }
+      __syncthreads();
+    }
+    if (x.ntr >= 1) {
+      double wm[6] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0};
+      if (warps)
+        for (int q = 0; q < 6; q++) wm[q] = warps[(size_t)b * 6 + q];
+      for (int p = lane; p < x.ntr; p += 64) track_camera(x.trk[w.lst[p]], wm);
+    }
+    const int crowd_mode = sq[Q_CROWD];
+    for (int i = lane; i < x.nk; i += 64) {  // _compute_detection_quality
+      double* d = w.dt + (size_t)i * DTW;
+      double q = d[4];
+      const double fn = g.dprep[((size_t)seq * g.D + (int)d[6]) * 4 + 0];
+      q = 0.7 * q + 0.3 * pymin(fn / 10.0, 1.0);
+      const double ww = d[2], hh = d[3];
+      if (hh > 0) {
+        const double aq = pymax(0.1, 1.0 - fabs(ww / hh - 0.5) / 2.0);
+        q = 0.9 * q + 0.1 * aq;
+      }
+      if (crowd_mode) q += pymin(ww * hh / 10000.0, 0.1);
+      d[7] = q;
+    }
+    __syncthreads();
+    stable_sort_desc(w.dord, x.nk, [&](int r) { return w.dt[(size_t)r * DTW + 7]; }, w.tmp);
+    for (int p = lane; p < x.ntr; p += 64) track_predict(x.trk[w.lst[p]]);
+    __syncthreads();
+  }
+  if (!fid) fid = sq[Q_HIST];
+
+  // ---- Tracker._enhanced_match (tracker.py:183-281, P6) --------------------------------------
+  x.nm = 0;
+  const int ncf = wave_compact(x.ntr, [&](int p) { return x.trk[w.lst[p]].state == 2; },
+                               [&](int p, int q) { w.conf_t[q] = p; });
+  const int nun = wave_compact(x.ntr, [&](int p) { return x.trk[w.lst[p]].state != 1; },
+                               [&](int p, int q) { w.unconf_t[q] = p; });
+  const int nhi = wave_compact(x.nk, [&](int i) { return x.det(i)[4] >= g.thi; },
+                               [&](int i, int q) { w.hi[q] = i; });
+  const int nmed = wave_compact(
+      x.nk, [&](int i) { const double c = x.det(i)[4]; return g.tlo <= c && c < g.thi; },
+      [&](int i, int q) { w.med[q] = i; });
+  const int nlo = wave_compact(x.nk, [&](int i) { return x.det(i)[4] < g.tlo; },
+                               [&](int i, int q) { w.lo[q] = i; });
+  int naut = ncf, naud = x.nk;
+  for (int k = lane; k < ncf; k += 64) w.aut[k] = w.conf_t[k];
+  for (int k = lane; k < x.nk; k += 64) w.aud[k] = k;
+  __syncthreads();
+  const double thr = x.sqd[0];
+  if (nhi && ncf) {  // stage 1: high-confidence detections, confirmed tracks
+    const int m0 = x.nm;
+    matching_cascade(x, thr * 0.8, w.conf_t, ncf, w.hi, nhi);
+    naut = filter_matched(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp);
+    naud = filter_matched(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp);
+  }
+  {  // stage 2: medium-confidence detections, remaining confirmed tracks
+    const int nrt = wave_compact(naut, [&](int k) { return in_list(w.conf_t, ncf, w.aut[k]); },
+                                 [&](int k, int q) { w.ti2[q] = w.aut[k]; });
+    const int nrm = wave_compact(nmed, [&](int k) { return in_list(w.aud, naud, w.med[k]); },
+                                 [&](int k, int q) { w.rd[q] = w.med[k]; });
+    if (nrm && nrt) {
+      const int m0 = x.nm;
+      matching_cascade(x, thr, w.ti2, nrt, w.rd, nrm);
+      naut = filter_matched(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp);
+      naud = filter_matched(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp);
+    }
+  }
+  // stage 3: IoU on unconfirmed (= non-tentative) + unmatched with time_since_update == 1
+  int ncand = nun;
+  for (int k = lane; k < nun; k += 64) w.cand[k] = w.unconf_t[k];
+  __syncthreads();
+  ncand += wave_compact(naut, [&](int k) { return x.trk[w.lst[w.aut[k]]].tsu == 1; },
+                        [&](int k, int q) { w.cand[nun + q] = w.aut[k]; });
+  const int nrd = wave_compact(naud, [&](int k) { return !in_list(w.lo, nlo, w.aud[k]); },
+                               [&](int k, int q) { w.rd[q] = w.aud[k]; });
+  int nut3 = 0;
+  if (nrd && ncand) {
+    const int m0 = x.nm;
+    int nud3 = 0;
+    min_cost_matching(x, M_IOU, g.max_iou, w.cand, ncand, w.rd, nrd, w.ut3, nut3, w.ud, nud3);
+    naut = filter_matched(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp);
+    naud = filter_matched(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp);
+  }
+  int nfut = wave_compact(naut, [&](int k) { return !in_list(w.cand, ncand, w.aut[k]); },
+                          [&](int k, int q) { w.fut[q] = w.aut[k]; });
+  for (int k = lane; k < nut3; k += 64) w.fut[nfut + k] = w.ut3[k];
+  nfut += nut3;
+  __syncthreads();
+
+  // ---- updates, misses (tracker.py:139-145) ---------------------------------------------------
+  for (int q = 0; q < x.nm; q++) track_update(x, w.lst[w.mt[2 * q]], w.mt[2 * q + 1]);
+  for (int k = lane; k < nfut; k += 64) track_missed(x.trk[w.lst[w.fut[k]]]);
+  __syncthreads();
+
+  // ---- _attempt_id_recovery (tracker.py:300-344) ----------------------------------------------
+  if (x.nlost && naud) {
+    for (int li = 0; li < x.nlost; li++) {
+      const int ls = x.lost[li];
+      if (x.trk[ls].nfeat == 0) continue;
+      const double* rs = g.recsim + ((size_t)seq * LOSTN + li) * g.D;
+      double best = -INF;
+      int bk = 0x7fffffff;
+      for (int k = lane; k < naud; k += 64) {
+        const double sv = rs[x.det_in(w.aud[k])];
+        if (sv > best || (sv == best && k < bk)) best = sv, bk = k;
+      }
+      for (int o = 32; o >= 1; o >>= 1) {
+        const double ob = __shfl_xor(best, o);
+        const int ok = __shfl_xor(bk, o);
+        if (ob > best || (ob == best && ok < bk)) best = ob, bk = ok;
+      }
+      if (best > 0.7) {
+        const int di = w.aud[bk];
+        if (lane == 0) {
+          x.trk[ls].state = 1;  // the reference's "Confirmed state" comment sets Tentative (1)
+          x.trk[ls].tsu = 0;
+        }
+        __syncthreads();
+        track_update(x, ls, di);
+        if (lane == 0) {
+          w.lst[x.ntr] = ls;
+          for (int k = li; k < x.nlost - 1; k++) x.lost[k] = x.lost[k + 1];
+          for (int k = bk; k < naud - 1; k++) w.aud[k] = w.aud[k + 1];
+        }
+        x.ntr++;
+        x.nlost--;
+        naud--;
+        __syncthreads();
+        break;
+      }
+    }
+  }
+
+  // ---- births (_initiate_track), free slots ascending ----------------------------------------
+  if (naud) {
+    for (int s2 = lane; s2 < g.T; s2 += 64) w.flag[s2] = 0;
+    __syncthreads();
+    for (int p = lane; p < x.ntr; p += 64) w.flag[w.lst[p]] = 1;
+    for (int k = lane; k < x.nlost; k += 64) w.flag[x.lost[k]] = 1;
+    __syncthreads();
+    const int nfree = wave_compact(g.T, [&](int s2) { return w.flag[s2] == 0; },
+                                   [&](int s2, int p) { w.tmp[p] = s2; });
+    int nnew = naud;
+    if (nnew > nfree) {
+      if (lane == 0) atomicExch(g.status, (int)BX_ERR_TRACK_OVERFLOW);
+      nnew = nfree;
+    }
+    for (int k = 0; k < nnew; k++) {
+      const int slot = w.tmp[k];
+      track_birth(x, slot, w.aud[k]);
+      if (lane == 0) w.lst[x.ntr] = slot;
+      x.ntr++;
+    }
+    __syncthreads();
+  }
+
+  // ---- deleted tracks -> lost buffer (tracker.py:152-164) -------------------------------------
+  if (lane == 0) {
+    const int max_age = sq[Q_MAXAGE];
+    int wq = 0;
+    for (int p = 0; p < x.ntr; p++) {
+      const int s2 = w.lst[p];
+      SsTrk& t = x.trk[s2];
+      if (t.state == 3) {
+        if (x.nlost < LOSTN) {
+          t.lost_frame = fid;
+          x.lost[x.nlost++] = s2;
+        }
+        int lw = 0;
+        for (int k = 0; k < x.nlost; k++)
+          if (fid - x.trk[x.lost[k]].lost_frame < max_age) x.lost[lw++] = x.lost[k];
+        x.nlost = lw;
+      } else {
+        w.lst[wq++] = s2;
+      }
+    }
+    w.sc[0] = wq;
+    w.sc[1] = x.nlost;
+  }
+  __syncthreads();
+  x.ntr = w.sc[0];
+  x.nlost = w.sc[1];
+  __syncthreads();
+
+  // ---- metric.partial_fit (tracker.py:166-178; linear_assignment.py:521-593) -----------------
+  int anyf = 0;
+  for (int p = lane; p < x.ntr; p += 64) {
+    const SsTrk& t = x.trk[w.lst[p]];
+    anyf |= t.state == 2 && t.nfeat > 0;
+  }
+  anyf = __any(anyf);
+  if (anyf) {
+    const int budget = sq[Q_BUDGET];
+    const int keep = budget > 0 ? (budget / 4 < 5 ? budget / 4 : 5) : 5;
+    for (int p = lane; p < x.ntr; p += 64) {
+      const int s2 = w.lst[p];
+      SsTrk& t = x.trk[s2];
+      int* gv = g.gal_v + ((size_t)seq * g.T + s2) * g.GB;
+      double* gq = g.gal_q + ((size_t)seq * g.T + s2) * g.GB;
+      if (t.state == 2) {
+        for (int q = 0; q < t.nfeat; q++) {
+          const int v = t.feat[q];
+          gv[t.gal_n] = v;
+          gq[t.gal_n] = g.vwn[vidx(g, seq, s2, v)];
+          t.gal_n++;
+          if (budget > 0 && t.gal_n > budget) gal_prune(gv, gq, t.gal_n, budget);
+        }
+      } else if (t.gal_n > keep) {
+        gal_prune(gv, gq, t.gal_n, keep);
+      }
+    }
+    for (int k = lane; k < x.nlost; k += 64) {
+      const int s2 = x.lost[k];
+      SsTrk& t = x.trk[s2];
+      if (t.gal_n > keep)
+        gal_prune(g.gal_v + ((size_t)seq * g.T + s2) * g.GB,
+                  g.gal_q + ((size_t)seq * g.T + s2) * g.GB, t.gal_n, keep);
+    }
+    __syncthreads();
+  }
+  // pool entries still referenced by a features list or a gallery
+  for (int p = lane; p < x.ntr + x.nlost; p += 64) {
+    const int s2 = p < x.ntr ? w.lst[p] : x.lost[p - x.ntr];
+    SsTrk& t = x.trk[s2];
+    unsigned long long m = 0ull;
+    for (int q = 0; q < t.nfeat; q++) m |= 1ull << t.feat[q];
+    const int* gv = g.gal_v + ((size_t)seq * g.T + s2) * g.GB;
+    for (int q = 0; q < t.gal_n; q++) m |= 1ull << gv[q];
+    t.vmask = m;
+  }
+  // the next frame's gallery queries: confirmed tracks with samples
+  const int nnl = wave_compact(
+      x.ntr, [&](int p) { const SsTrk& t = x.trk[w.lst[p]]; return t.state == 2 && t.gal_n > 0; },
+      [&](int p, int q) { g.nnl[(size_t)seq * g.T + q] = w.lst[p]; });
+
+  // ---- outputs (strongsort.py:313-345) ---------------------------------------------------------
+  double* orow = out + (size_t)r0 * 10;
+  const int nout = wave_compact(
+      x.ntr, [&](int p) { const SsTrk& t = x.trk[w.lst[p]]; return t.state == 2 && t.tsu < 1; },
+      [&](int p, int q) {
+        const SsTrk& t = x.trk[w.lst[p]];
+        if (q < n) {
+          double bx[4];
+          to_tlbr(t, bx);
+          double* o = orow + (size_t)q * 10;
+          o[0] = bx[0], o[1] = bx[1], o[2] = bx[2], o[3] = bx[3];
+          o[4] = (double)t.id, o[5] = t.conf, o[6] = t.cls, o[7] = t.det_ind;
+          o[8] = t.quality, o[9] = 0.0;
+        }
+      });
+  for (int p = lane; p < x.ntr; p += 64) order[p] = w.lst[p];
+  if (lane == 0) {
+    out_count[b] = nout < n ? nout : n;
+    sq[Q_FRAME] = frame;
+    sq[Q_NTR] = x.ntr;
+    sq[Q_NLOST] = x.nlost;
+    sq[Q_HIST] = sq[Q_HIST] < 100 ? sq[Q_HIST] + 1 : 100;
+    sq[Q_NNL] = nnl;
+    sq[Q_NK] = x.nk;
+    sq[Q_NT0] = nt0;
+    sq[Q_NOUT] = nout;
+  }
+}
+
+__global__ void ss_reset_kernel(SsDev g, int seq0, int nseq) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nseq) {
+    int* q = g.sq + (size_t)(seq0 + k) * SQS;
+    for (int i = 0; i < SQS; i++) q[i] = 0;
+    q[Q_NEXTID] = 1;
+    q[Q_MAXAGE] = g.sq[(size_t)g.S * SQS + 0];
+    q[Q_BUDGET] = g.sq[(size_t)g.S * SQS + 1];
+    g.sqd[(size_t)(seq0 + k) * 2] = g.sqd[(size_t)g.S * 2];
+    g.sqd[(size_t)(seq0 + k) * 2 + 1] = g.sqd[(size_t)g.S * 2];
+  }
+}
+
+}  // namespace
+
+struct bx_ss {
+  SsDev dev;
+  bx_ss_config cfg;
+  void* arena = nullptr;
+  double* h_dets = nullptr;
+  int* h_off = nullptr;
+  double* h_embs = nullptr;
+  double* h_warp = nullptr;
+  double* h_out = nullptr;
+  int* h_cnt = nullptr;
+  int probe_stage = -1;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  int ev_used = 0;
+};
+
+#define SCHK(x)                                                                    \
+  do {                                                                             \
+    hipError_t _e = (x);                                                           \
+    if (_e != hipSuccess)                                                          \
+      return bx_record_error(BX_ERR_HIP, (std::string(#x) + ": " + hipGetErrorString(_e)).c_str()); \
+  } while (0)
+
+static int ss_probe_begin(bx_ss* e, int stage, hipStream_t st) {
+  if (e->probe_stage != stage) return BX_OK;
+  if (e->ev_used == (int)e->ev.size()) {
+    hipEvent_t a, b;
+    SCHK(hipEventCreateWithFlags(&a, hipEventDisableSystemFence));
+    SCHK(hipEventCreateWithFlags(&b, hipEventDisableSystemFence));
+    e->ev.push_back({a, b});
+  }
+  SCHK(hipEventRecord(e->ev[e->ev_used].first, st));
+  return BX_OK;
+}
+static int ss_probe_end(bx_ss* e, int stage, hipStream_t st) {
+  if (e->probe_stage != stage) return BX_OK;
+  SCHK(hipEventRecord(e->ev[e->ev_used++].second, st));
+  return BX_OK;
+}
+
+static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int* off,
+                     const double* embs, const double* warps, double* out, int* cnt,
+                     hipStream_t st) {
+  const SsDev& d = e->dev;
+  int rc;
+  if (!embs) return bx_record_error(BX_ERR_SHAPE, "StrongSort needs embeddings");
+  if ((rc = ss_probe_begin(e, 0, st))) return rc;
+  hipLaunchKernelGGL(ss_prep_kernel, dim3(d.D, nseq), dim3(64), 0, st, d, seq0, off, embs);
+  SCHK(hipGetLastError());
+  if ((rc = ss_probe_end(e, 0, st))) return rc;
+  if ((rc = ss_probe_begin(e, 1, st))) return rc;
+  hipLaunchKernelGGL(ss_nn_kernel, dim3(d.T, nseq), dim3(64), 0, st, d, seq0, off);
+  SCHK(hipGetLastError());
+  if ((rc = ss_probe_end(e, 1, st))) return rc;
+  if ((rc = ss_probe_begin(e, 2, st))) return rc;
+  hipLaunchKernelGGL(ss_rec_kernel, dim3(LOSTN, nseq), dim3(256), 0, st, d, seq0, off, embs);
+  SCHK(hipGetLastError());
+  if ((rc = ss_probe_end(e, 2, st))) return rc;
+  if ((rc = ss_probe_begin(e, 3, st))) return rc;
+  hipLaunchKernelGGL(ss_frame_kernel, dim3(nseq), dim3(64), 0, st, d, seq0, dets, off, warps, out,
+                     cnt);
+  SCHK(hipGetLastError());
+  if ((rc = ss_probe_end(e, 3, st))) return rc;
+  return BX_OK;
+}
+
+extern "C" {
+
+int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
+  if (!c || !out) return bx_record_error(BX_ERR_INVALID, "null argument");
+  const int vp = c->vec_cap > 0 ? c->vec_cap : 32;
+  if (c->n_seq <= 0 || c->track_cap <= 0 || c->det_cap <= 0 || c->track_cap > 1024 ||
+      c->det_cap > 512 || c->emb_dim <= 0 || c->emb_dim > 8192 || vp > 64 || c->nn_budget <= 0 ||
+      c->max_age < 0)
+    return bx_record_error(BX_ERR_INVALID, "bx_ss_config out of range");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return bx_record_error(BX_ERR_NO_DEVICE, "no HIP device visible");
+  bx_ss* e = new bx_ss();
+  e->cfg = *c;
+  SsDev& d = e->dev;
+  d.S = c->n_seq;
+  d.T = c->track_cap;
+  d.D = c->det_cap;
+  d.F = c->emb_dim;
+  d.VP = vp;
+  const int crowd_budget = c->nn_budget * 2 < 300 ? c->nn_budget * 2 : 300;
+  d.GB = (c->nn_budget > crowd_budget ? c->nn_budget : crowd_budget) + 1;
+  d.N = 2 * d.T > d.D ? 2 * d.T : d.D;
+  d.min_conf = c->min_conf;
+  d.max_iou = c->max_iou_dist;
+  d.mc_lambda = c->mc_lambda;
+  d.ema_alpha = c->ema_alpha;
+  d.thi = c->conf_thresh_high;
+  d.tlo = c->conf_thresh_low;
+  d.idw = c->id_preservation_weight;
+  d.n_init = c->n_init;
+  d.crowd = c->crowd_detection != 0;
+  d.born = c->born_confirmed != 0;
+  d.wsi_n = ws_ints(d.T, d.D, d.N);
+  d.wsd_n = ws_doubles(d.T, d.D, d.N);
+  const size_t S = d.S, T = d.T, D = d.D, F = d.F, VP = d.VP, GB = d.GB;
+  size_t off = 0;
+  auto cb = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+  const size_t o_trk = cb(S * T * sizeof(SsTrk));
+  const size_t o_gv = cb(S * T * GB * sizeof(int));
+  const size_t o_gq = cb(S * T * GB * sizeof(double));
+  const size_t o_vec = cb(S * T * VP * F * sizeof(double));
+  const size_t o_vden = cb(S * T * VP * sizeof(double));
+  const size_t o_vwn = cb(S * T * VP * sizeof(double));
+  const size_t o_sq = cb((S + 1) * SQS * sizeof(int));
+  const size_t o_sqd = cb((S + 1) * 2 * sizeof(double));
+  const size_t o_ord = cb(S * T * sizeof(int));
+  const size_t o_lost = cb(S * LOSTN * sizeof(int));
+  const size_t o_nnl = cb(S * T * sizeof(int));
+  const size_t o_nnd = cb(S * T * D * sizeof(double));
+  const size_t o_prep = cb(S * D * 4 * sizeof(double));
+  const size_t o_dn = cb(S * D * F * sizeof(double));
+  const size_t o_nf = cb(S * D * F * sizeof(double));
+  const size_t o_rec = cb(S * LOSTN * D * sizeof(double));
+  const size_t o_cost = cb(S * 2 * T * D * sizeof(double));
+  const size_t o_wsi = cb(S * (size_t)d.wsi_n * sizeof(int));
+  const size_t o_wsd = cb(S * (size_t)d.wsd_n * sizeof(double));
+  const size_t o_st = cb(sizeof(int) * 4);
+  if (hipMalloc(&e->arena, off) != hipSuccess) {
+    delete e;
+    return bx_record_error(BX_ERR_HIP, "hipMalloc of the StrongSort arena failed");
+  }
+  SCHK(hipMemset(e->arena, 0, off));
+  char* base = (char*)e->arena;
+  d.trk = (SsTrk*)(base + o_trk);
+  d.gal_v = (int*)(base + o_gv);
+  d.gal_q = (double*)(base + o_gq);
+  d.vec = (double*)(base + o_vec);
+  d.vden = (double*)(base + o_vden);
+  d.vwn = (double*)(base + o_vwn);
+  d.sq = (int*)(base + o_sq);
+  d.sqd = (double*)(base + o_sqd);
+  d.order = (int*)(base + o_ord);
+  d.lost = (int*)(base + o_lost);
+  d.nnl = (int*)(base + o_nnl);
+  d.nnd = (double*)(base + o_nnd);
+  d.dprep = (double*)(base + o_prep);
+  d.dn = (double*)(base + o_dn);
+  d.nf = (double*)(base + o_nf);
+  d.recsim = (double*)(base + o_rec);
+  d.cost = (double*)(base + o_cost);
+  d.wsi = (int*)(base + o_wsi);
+  d.wsd = (double*)(base + o_wsd);
+  d.status = (int*)(base + o_st);
+  // per-sequence defaults (row S holds them for bx_ss_reset): max_age, budget, threshold
+  std::vector<int> q((S + 1) * SQS, 0);
+  std::vector<double> qd((S + 1) * 2, c->max_cos_dist);
+  for (size_t k = 0; k < S; k++) {
+    q[k * SQS + Q_NEXTID] = 1;
+    q[k * SQS + Q_MAXAGE] = c->max_age;
+    q[k * SQS + Q_BUDGET] = c->nn_budget;
+  }
+  q[S * SQS + 0] = c->max_age;
+  q[S * SQS + 1] = c->nn_budget;
+  SCHK(hipMemcpy(d.sq, q.data(), q.size() * sizeof(int), hipMemcpyHostToDevice));
+  SCHK(hipMemcpy(d.sqd, qd.data(), qd.size() * sizeof(double), hipMemcpyHostToDevice));
+  SCHK(hipMalloc(&e->h_dets, sizeof(double) * 6 * D));
+  SCHK(hipMalloc(&e->h_off, sizeof(int) * 2));
+  SCHK(hipMalloc(&e->h_embs, sizeof(double) * D * F));
+  SCHK(hipMalloc(&e->h_warp, sizeof(double) * 6));
+  SCHK(hipMalloc(&e->h_out, sizeof(double) * 10 * D));
+  SCHK(hipMalloc(&e->h_cnt, sizeof(int)));
+  *out = e;
+  return BX_OK;
+}
+
+int bx_ss_destroy(bx_ss* e) {
+  if (!e) return BX_OK;
+  for (auto& p : e->ev) {
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
+  }
+  (void)hipFree(e->arena);
+  (void)hipFree(e->h_dets);
+  (void)hipFree(e->h_off);
+  (void)hipFree(e->h_embs);
+  (void)hipFree(e->h_warp);
+  (void)hipFree(e->h_out);
+  (void)hipFree(e->h_cnt);
+  delete e;
+  return BX_OK;
+}
+
+int bx_ss_reset(bx_ss* e, int seq0, int nseq, void* stream) {
+  if (!e || seq0 < 0 || nseq < 0 || seq0 + nseq > e->dev.S)
+    return bx_record_error(BX_ERR_INVALID, "bad sequence range");
+  if (!nseq) return BX_OK;
+  hipLaunchKernelGGL(ss_reset_kernel, dim3((nseq + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     e->dev, seq0, nseq);
+  SCHK(hipGetLastError());
+  return BX_OK;
+}
+
+int bx_ss_step(bx_ss* e, int seq0, int nseq, const double* dets, const int32_t* det_off,
+               const double* embs, const double* warps, double* out, int32_t* out_count,
+               void* stream) {
+  if (!e || seq0 < 0 || nseq <= 0 || seq0 + nseq > e->dev.S || !det_off || !out || !out_count)
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_step");
+  return ss_launch(e, seq0, nseq, dets, det_off, embs, warps, out, out_count, (hipStream_t)stream);
+}
+
+int bx_ss_update_host(bx_ss* e, int seq, const double* dets, int n, const double* embs,
+                      const double* warp, double* out, int* n_out, void* stream) {
+  if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && (!dets || !out || !embs)) || !n_out)
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_update_host");
+  if (n > e->dev.D) return bx_record_error(BX_ERR_CAPACITY, "detections exceed det_cap");
+  hipStream_t st = (hipStream_t)stream;
+  const int off[2] = {0, n};
+  if (n) {
+    SCHK(hipMemcpyAsync(e->h_dets, dets, sizeof(double) * 6 * n, hipMemcpyHostToDevice, st));
+    SCHK(hipMemcpyAsync(e->h_embs, embs, sizeof(double) * (size_t)n * e->dev.F,
+                        hipMemcpyHostToDevice, st));
+  }
+  if (warp) SCHK(hipMemcpyAsync(e->h_warp, warp, sizeof(double) * 6, hipMemcpyHostToDevice, st));
+  SCHK(hipMemcpyAsync(e->h_off, off, sizeof(off), hipMemcpyHostToDevice, st));
+  int rc = ss_launch(e, seq, 1, e->h_dets, e->h_off, e->h_embs, warp ? e->h_warp : nullptr,
+                     e->h_out, e->h_cnt, st);
+  if (rc) return rc;
+  int cnt = 0;
+  SCHK(hipMemcpyAsync(&cnt, e->h_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+  SCHK(hipStreamSynchronize(st));
+  if (cnt) SCHK(hipMemcpy(out, e->h_out, sizeof(double) * 10 * cnt, hipMemcpyDeviceToHost));
+  *n_out = cnt;
+  int status = 0;
+  SCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
+  if (status) return bx_record_error(status, "StrongSort engine status latched (see bx_ss_status)");
+  return BX_OK;
+}
+
+int bx_ss_status(bx_ss* e, int* status) {
+  if (!e || !status) return bx_record_error(BX_ERR_INVALID, "null argument");
+  SCHK(hipMemcpy(status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
+  return BX_OK;
+}
+
+int bx_ss_counters_host(bx_ss* e, int seq, int* frame_count, int* next_id, int* n_tracks,
+                        int* n_lost) {
+  if (!e || seq < 0 || seq >= e->dev.S) return bx_record_error(BX_ERR_INVALID, "bad sequence");
+  int s[SQS];
+  SCHK(hipDeviceSynchronize());
+  SCHK(hipMemcpy(s, e->dev.sq + (size_t)seq * SQS, sizeof(s), hipMemcpyDeviceToHost));
+  if (frame_count) *frame_count = s[Q_FRAME];
+  if (next_id) *next_id = s[Q_NEXTID];
+  if (n_tracks) *n_tracks = s[Q_NTR];
+  if (n_lost) *n_lost = s[Q_NLOST];
+  return BX_OK;
+}
+
+int bx_ss_tracks_host(bx_ss* e, int seq, int cap, int32_t* ids, int32_t* state, double* mean,
+                      double* cov, int* n) {
+  if (!e || seq < 0 || seq >= e->dev.S || cap < 0 || !n)
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_tracks_host");
+  SCHK(hipDeviceSynchronize());
+  int s[SQS];
+  SCHK(hipMemcpy(s, e->dev.sq + (size_t)seq * SQS, sizeof(s), hipMemcpyDeviceToHost));
+  const int nt = s[Q_NTR];
+  std::vector<int> ord(nt);
+  if (nt)
+    SCHK(hipMemcpy(ord.data(), e->dev.order + (size_t)seq * e->dev.T, sizeof(int) * nt,
+                   hipMemcpyDeviceToHost));
+  for (int k = 0; k < nt && k < cap; k++) {
+    SsTrk t;
+    SCHK(hipMemcpy(&t, e->dev.trk + (size_t)seq * e->dev.T + ord[k], sizeof(SsTrk),
+                   hipMemcpyDeviceToHost));
+    if (ids) ids[k] = t.id;
+    if (state) state[k] = t.state;
+    if (mean) memcpy(mean + 8 * k, t.mean, sizeof(t.mean));
+    if (cov) memcpy(cov + 64 * k, t.cov, sizeof(t.cov));
+  }
+  *n = nt;
+  return BX_OK;
+}
+
+int bx_ss_frame_stats_host(bx_ss* e, int seq0, int nseq, int64_t* sums) {
+  if (!e || !sums || seq0 < 0 || nseq < 0 || seq0 + nseq > e->dev.S)
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_frame_stats_host");
+  std::vector<int> s((size_t)nseq * SQS);
+  SCHK(hipDeviceSynchronize());
+  if (nseq)
+    SCHK(hipMemcpy(s.data(), e->dev.sq + (size_t)seq0 * SQS, sizeof(int) * s.size(),
+                   hipMemcpyDeviceToHost));
+  int64_t a[6] = {0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < nseq; k++) {
+    const int* q = s.data() + (size_t)k * SQS;
+    a[0] += q[Q_NK];
+    a[1] += q[Q_NT0];
+    a[2] += q[Q_NNL];
+    a[3] += q[Q_ROWS];
+    a[4] += q[Q_NOUT];
+    a[5] = q[Q_FRAME] > a[5] ? q[Q_FRAME] : a[5];
+  }
+  for (int k = 0; k < 6; k++) sums[k] = a[k];
+  return BX_OK;
+}
+
+int bx_ss_probe(bx_ss* e, int stage) {
+  if (!e) return bx_record_error(BX_ERR_INVALID, "null engine");
+  e->probe_stage = stage;
+  e->ev_used = 0;
+  return BX_OK;
+}
+
+int bx_ss_probe_read(bx_ss* e, double* total_ms, int* count) {
+  if (!e || !total_ms || !count) return bx_record_error(BX_ERR_INVALID, "null argument");
+  double s = 0.0;
+  for (int k = 0; k < e->ev_used; k++) {
+    SCHK(hipEventSynchronize(e->ev[k].second));
+    float ms = 0.f;
+    SCHK(hipEventElapsedTime(&ms, e->ev[k].first, e->ev[k].second));
+    s += ms;
+  }
+  *total_ms = s;
+  *count = e->ev_used;
+  e->ev_used = 0;
+  return BX_OK;
+}
+
+}  // extern "C"

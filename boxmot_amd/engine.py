@@ -438,6 +438,137 @@ class BoostEngine:
         return t.value, n.value
 
 
+@dataclass
+class SsParams:
+    """StrongSort constructor parameters (strongsort.py:45-66 names and defaults)."""
+
+    min_conf: float = 0.1
+    max_cos_dist: float = 0.15
+    max_iou_dist: float = 0.7
+    max_age: int = 50
+    n_init: int = 2
+    nn_budget: int = 150
+    mc_lambda: float = 0.995
+    ema_alpha: float = 0.9
+    conf_thresh_high: float = 0.7
+    conf_thresh_low: float = 0.3
+    id_preservation_weight: float = 0.1
+    crowd_detection: bool = True
+    born_confirmed: bool = False
+
+
+class SsEngine:
+    """Handle over ``bx_ss_*`` (include/bxstrongsort.h): ``n_seq`` StrongSort sequences in HBM;
+    per frame the detection-feature kernel, the NN-gallery distance (fp64 MFMA), the recovery
+    similarities and the frame kernel (one wave per sequence)."""
+
+    STAGES = ["prep", "nn", "recovery", "frame"]
+
+    def __init__(self, n_seq: int = 1, track_cap: int = 256, det_cap: int = 256,
+                 emb_dim: int = 512, vec_cap: int = 32, params: SsParams | None = None):
+        p = params or SsParams()
+        self.n_seq, self.track_cap, self.det_cap, self.params = n_seq, track_cap, det_cap, p
+        self.emb_dim = emb_dim
+        cfg = N.BxSsConfig(
+            n_seq=n_seq, track_cap=track_cap, det_cap=det_cap, emb_dim=emb_dim, vec_cap=vec_cap,
+            min_conf=float(p.min_conf), max_cos_dist=float(p.max_cos_dist),
+            max_iou_dist=float(p.max_iou_dist), max_age=int(p.max_age), n_init=int(p.n_init),
+            nn_budget=int(p.nn_budget), mc_lambda=float(p.mc_lambda),
+            ema_alpha=float(p.ema_alpha), conf_thresh_high=float(p.conf_thresh_high),
+            conf_thresh_low=float(p.conf_thresh_low),
+            id_preservation_weight=float(p.id_preservation_weight),
+            crowd_detection=int(bool(p.crowd_detection)),
+            born_confirmed=int(bool(p.born_confirmed)))
+        self._L = N.load()
+        h = C.c_void_p()
+        N.check(self._L.bx_ss_create(C.byref(cfg), C.byref(h)), "bx_ss_create")
+        self._h = h
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.bx_ss_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, seq0: int = 0, nseq: int | None = None, stream=None):
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        N.check(self._L.bx_ss_reset(self._h, seq0, nseq, stream), "bx_ss_reset")
+
+    def step(self, dets, det_off, embs, warps, out, out_count, seq0: int = 0,
+             nseq: int | None = None, stream=None):
+        """One frame for sequences [seq0, seq0+nseq) from device tensors (see bx_ss_step):
+        dets [sumN, 6] f64, det_off [S+1] i32, embs [sumN, F] f64, out [sumN, 10] f64."""
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        if stream is None:
+            stream = _current_stream()
+        N.check(self._L.bx_ss_step(self._h, seq0, nseq, _ptr(dets), _ptr(det_off), _ptr(embs),
+                                   _ptr(warps), _ptr(out), _ptr(out_count), stream), "bx_ss_step")
+
+    def update_host(self, seq: int, dets: np.ndarray, embs: np.ndarray,
+                    warp: np.ndarray | None = None) -> np.ndarray:
+        d = np.ascontiguousarray(dets, dtype=np.float64).reshape(-1, 6)
+        n = d.shape[0]
+        e = np.ascontiguousarray(embs, dtype=np.float64).reshape(n, -1) if n else None
+        if n and e.shape[1] != self.emb_dim:
+            raise ValueError(f"embedding dim {e.shape[1]} != engine emb_dim {self.emb_dim}")
+        w = None if warp is None else np.ascontiguousarray(warp, np.float64).reshape(6)
+        out = np.empty((max(n, 1), 10), np.float64)
+        m = C.c_int(0)
+        N.check(self._L.bx_ss_update_host(
+            self._h, seq, d.ctypes.data if n else None, n, e.ctypes.data if n else None,
+            None if w is None else w.ctypes.data, out.ctypes.data, C.byref(m), None),
+            "bx_ss_update_host")
+        return out[: m.value].copy()
+
+    def status(self) -> int:
+        s = C.c_int(0)
+        N.check(self._L.bx_ss_status(self._h, C.byref(s)), "bx_ss_status")
+        return s.value
+
+    def counters(self, seq: int = 0) -> dict:
+        fc, nid, nt, nl = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        N.check(self._L.bx_ss_counters_host(self._h, seq, C.byref(fc), C.byref(nid), C.byref(nt),
+                                            C.byref(nl)), "counters")
+        return {"frame_count": fc.value, "next_id": nid.value, "n_tracks": nt.value,
+                "n_lost": nl.value}
+
+    def tracks(self, seq: int = 0) -> dict:
+        cap = self.track_cap
+        ids = np.zeros(cap, np.int32)
+        st = np.zeros(cap, np.int32)
+        mean = np.zeros((cap, 8))
+        cov = np.zeros((cap, 8, 8))
+        n = C.c_int()
+        N.check(self._L.bx_ss_tracks_host(self._h, seq, cap, ids.ctypes.data, st.ctypes.data,
+                                          mean.ctypes.data, cov.ctypes.data, C.byref(n)),
+                "tracks")
+        k = min(n.value, cap)
+        return {"id": ids[:k], "state": st[:k], "mean": mean[:k], "covariance": cov[:k]}
+
+    def frame_stats(self, seq0: int = 0, nseq: int | None = None) -> dict:
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        a = (C.c_int64 * 6)()
+        N.check(self._L.bx_ss_frame_stats_host(self._h, seq0, nseq, a), "frame_stats")
+        return dict(zip(["dets", "tracks", "queried", "rows", "outputs", "frame"],
+                        [int(x) for x in a]))
+
+    def probe(self, stage) -> None:
+        idx = -1 if stage is None else (self.STAGES.index(stage) if isinstance(stage, str)
+                                        else int(stage))
+        N.check(self._L.bx_ss_probe(self._h, idx), "bx_ss_probe")
+
+    def probe_read(self):
+        t, n = C.c_double(), C.c_int()
+        N.check(self._L.bx_ss_probe_read(self._h, C.byref(t), C.byref(n)), "probe_read")
+        return t.value, n.value
+
+
 def _ptr(x):
     if x is None:
         return None

@@ -17,6 +17,7 @@ _ON_ENGINE = {
     "botsort": "boxmot_amd.trackers.botsort.BotSort",
     "ocsort": "boxmot_amd.trackers.ocsort.OcSort",
     "boosttrack": "boxmot_amd.trackers.boosttrack.BoostTrack",
+    "strongsort": "boxmot_amd.trackers.strongsort.StrongSort",
 }
 _REFERENCE_NAMES = ["strongsort", "ocsort", "bytetrack", "botsort", "deepocsort", "hybridsort",
                     "boosttrack"]
@@ -47,6 +48,8 @@ def create_tracker(tracker_type, tracker_config=None, reid_weights=None, device=
     if tracker_type in ["strongsort", "botsort", "deepocsort", "hybridsort", "boosttrack"]:
         tracker_args["per_class"] = per_class
         tracker_args.update(reid_args)
+        if tracker_type in ["strongsort"]:
+            tracker_args.pop("per_class")  # tracker_zoo.py:84-85
     else:
         tracker_args["per_class"] = per_class
     return cls(**tracker_args)

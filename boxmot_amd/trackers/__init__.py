@@ -2,5 +2,6 @@ from .boosttrack import BoostTrack
 from .botsort import BotSort
 from .bytetrack import ByteTrack
 from .ocsort import OcSort
+from .strongsort import StrongSort
 
-__all__ = ["ByteTrack", "BotSort", "OcSort", "BoostTrack"]
+__all__ = ["ByteTrack", "BotSort", "OcSort", "BoostTrack", "StrongSort"]

@@ -1,0 +1,102 @@
+/*
+ * bxstrongsort.h — C ABI of the StrongSort engine in libbxassoc.so (MI355X, gfx950).
+ *
+ * Boundary: everything the fork's "enhanced" StrongSort.update(dets, img, embs) computes per
+ * frame — detection quality and ordering, crowd detection and its parameter adjustments, camera
+ * warp, XYAH Kalman predict, the three-stage matching (appearance cascade on high- then
+ * medium-confidence detections: NN-gallery cosine distance on the fp64 matrix cores, Mahalanobis
+ * gating, motion/quality/confidence cost shaping, scipy's linear_sum_assignment; then IoU), the
+ * Kalman/feature updates, misses, ID recovery from the lost-track buffer, births, deaths, the
+ * gallery's partial_fit budget pruning and the output rows — runs on the GPU behind these entry
+ * points: per frame a detection-feature kernel (wave per detection), the gallery distance
+ * (fp64 MFMA, wave per confirmed track and detection block), the recovery similarities and the
+ * frame kernel (one wave per sequence).
+ *
+ * Reference interfaces replaced (file:line in muntherr/boxmot @ /root/reference):
+ *   bx_ss_create/step/update_host  StrongSort.__init__ / StrongSort.update
+ *                                  boxmot/trackers/strongsort/strongsort.py:45-181, 285-345
+ *     Tracker                      trackers/strongsort/sort/tracker.py:63-344
+ *     Track / Detection            sort/track.py:76-400, sort/detection.py:35-42
+ *     matching_cascade, min_cost_matching, gate_cost_matrix + cost shaping,
+ *     NearestNeighborDistanceMetric sort/linear_assignment.py:14-618
+ *     iou_cost                     sort/iou_matching.py:10-87
+ *     detect_crowd_situations      utils/occlusion_handler.py:45-87, 464-490
+ * The fork needs the minimal patch P6 and runs with
+ * handle_occlusions=False (D7); `born_confirmed` stands for its GITHUB_ACTIONS=true switch (D8).
+ * Bit-identical to oracle/bxo_strongsort.c (pinned by tests/golden/trk_strongsort_*.npz).
+ *
+ * Conventions as in bxassoc.h: device pointers unless a name ends in _host, asynchronous on
+ * `stream`, every function returns a bx_status (bx_last_error explains failures).
+ */
+#ifndef BXSTRONGSORT_H
+#define BXSTRONGSORT_H
+
+#include <stdint.h>
+
+#include "bxassoc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* StrongSort constructor parameters (strongsort.py:45-66 names and defaults: min_conf .1,
+ * max_cos_dist .15, max_iou_dist .7, max_age 50, n_init 2, nn_budget 150, mc_lambda .995,
+ * ema_alpha .9, conf_thresh_high .7, conf_thresh_low .3, id_preservation_weight .1,
+ * crowd_detection 1). */
+typedef struct {
+    int32_t n_seq;      /* independent sequences held by this engine */
+    int32_t track_cap;  /* track slots per sequence, live + lost-buffer (<= 1024) */
+    int32_t det_cap;    /* max detections per frame per sequence (<= 512) */
+    int32_t emb_dim;    /* embedding dimension F (float64 embeddings, required) */
+    int32_t vec_cap;    /* feature vectors kept per track slot (its features + gallery
+                           samples; <= 64, default 32) */
+    double min_conf, max_cos_dist, max_iou_dist;
+    int32_t max_age, n_init, nn_budget;
+    double mc_lambda, ema_alpha, conf_thresh_high, conf_thresh_low, id_preservation_weight;
+    int32_t crowd_detection, born_confirmed;
+} bx_ss_config;
+
+typedef struct bx_ss bx_ss;
+
+int bx_ss_create(const bx_ss_config *cfg, bx_ss **out);
+int bx_ss_destroy(bx_ss *e);
+/* Forget all tracks of sequences [seq0, seq0+nseq). */
+int bx_ss_reset(bx_ss *e, int seq0, int nseq, void *stream);
+/* One frame for sequences [seq0, seq0+nseq).
+ *   dets    [sum N][6] float64 (x1,y1,x2,y2,conf,cls) — StrongSort has no setup_decorator,
+ *           detections are not rounded to float32
+ *   det_off [nseq+1] int32 prefix offsets
+ *   embs    [sum N][emb_dim] float64
+ *   warps   [nseq][6] float64 2x3 camera-motion affine per sequence, NULL = identity
+ *   out     [sum N][10] float64 rows [x1,y1,x2,y2,id,conf,cls,det_ind,quality,occlusion(=0)]
+ *           in track-list order, sequence k from row det_off[k]
+ *   out_count [nseq] int32 */
+int bx_ss_step(bx_ss *e, int seq0, int nseq, const double *dets, const int32_t *det_off,
+               const double *embs, const double *warps, double *out, int32_t *out_count,
+               void *stream);
+/* Host-memory path for one sequence (the drop-in update). out must hold n rows of 10. */
+int bx_ss_update_host(bx_ss *e, int seq, const double *dets, int n, const double *embs,
+                      const double *warp, double *out, int *n_out, void *stream);
+/* Latched device status (BX_OK, BX_ERR_TRACK_OVERFLOW — track slots or a slot's vector pool
+ * exhausted — or BX_ERR_CAPACITY). */
+int bx_ss_status(bx_ss *e, int *status);
+/* Per-sequence counters (host): frame count, next id, live tracks, lost-buffer tracks. */
+int bx_ss_counters_host(bx_ss *e, int seq, int *frame_count, int *next_id, int *n_tracks,
+                        int *n_lost);
+/* Track list in list order (host): ids, states (1 tentative, 2 confirmed), means [8], covs [64]. */
+int bx_ss_tracks_host(bx_ss *e, int seq, int cap, int32_t *ids, int32_t *state, double *mean,
+                      double *cov, int *n);
+/* Last-frame statistics over sequences [seq0, seq0+nseq) (host): sums[6] = {detections kept,
+ * tracks entering the frame, confirmed tracks queried, gallery sample rows compared, output rows,
+ * max frame counter} — bench.py's unit counts. */
+int bx_ss_frame_stats_host(bx_ss *e, int seq0, int nseq, int64_t *sums);
+/* Timing probe: stage 0 = detection features, 1 = gallery distance, 2 = recovery similarities,
+ * 3 = frame kernel; -1 = off (see bx_boost_probe). */
+int bx_ss_probe(bx_ss *e, int stage);
+int bx_ss_probe_read(bx_ss *e, double *total_ms, int *count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BXSTRONGSORT_H */

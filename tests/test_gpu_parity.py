@@ -196,6 +196,14 @@ def make_dropin(kind, args):
     if kind == "boosttrack":
         BoostTrack._id_count = 0  # fixtures were captured with the class counter reset
         return BoostTrack(reid_weights=None, device="cuda", half=False, **args)
+    if kind == "strongsort":  # captured with GITHUB_ACTIONS=true (born Confirmed, App. A D8)
+        import os
+
+        from boxmot_amd import StrongSort
+
+        os.environ["GITHUB_ACTIONS"] = "true"
+        os.environ.pop("GITHUB_JOB", None)
+        return StrongSort(reid_weights=None, device="cuda", half=False, **args)
     return BotSort(reid_weights=None, device="cuda", half=False, **args)
 
 
@@ -204,13 +212,17 @@ def test_tracker_fixture_parity(torch_cuda, path):
     fx = np.load(path)
     kind, args = fixture_tracker_args(fx)
     tr = make_dropin(kind, args)
-    orc = po.OracleTracker(kind, **args)
+    orc = po.OracleTracker(kind, **(dict(args, born_confirmed=True) if kind == "strongsort"
+                                    else args))
     img = np.zeros((1080, 1920, 3), np.uint8)
     rows = []
+    ncol = 10 if kind == "strongsort" else 8
+    if kind == "strongsort":
+        args = dict(args, born_confirmed=True)
     for f, d, e in fixture_frames(fx):
         o = tr.update(d, img, e) if e is not None else tr.update(d, img)
-        o = np.asarray(o, np.float64).reshape(-1, 8)
-        oo = orc.update(d, e)
+        o = np.asarray(o, np.float64).reshape(-1, ncol)
+        oo = orc.update(d, e).reshape(-1, ncol)
         np.testing.assert_array_equal(o, oo, err_msg=f"frame {f}: GPU != oracle")
         rows.append(np.concatenate([np.full((o.shape[0], 1), f), o], 1))
     compare_outputs(np.concatenate(rows, 0), fx["outputs"], box_atol=1e-9,
@@ -610,3 +622,112 @@ def test_boosttrack_dropin_empty_frames_and_global_ids(torch_cuda):
     assert t.update(d, img, e).shape[1] == 8
     with pytest.raises(AssertionError):
         t.update(d, img, e[:1])
+
+
+# ----------------------------------------------------------------------------------- StrongSort
+SS_ARGS = dict(min_conf=0.1, max_cos_dist=0.15, max_iou_dist=0.7, max_age=50, n_init=2,
+               nn_budget=150, mc_lambda=0.995, ema_alpha=0.9, conf_thresh_high=0.7,
+               conf_thresh_low=0.3, id_preservation_weight=0.1, crowd_detection=True,
+               born_confirmed=True)
+
+
+def run_ss_batched(torch, scenes, n_frames, args, emb_dim, track_cap=256, det_cap=256,
+                   warps=None):
+    """SsEngine with len(scenes) sequences per launch vs one oracle per sequence: outputs and
+    Kalman state bitwise."""
+    from boxmot_amd.engine import SsEngine, SsParams
+
+    S = len(scenes)
+    eng = SsEngine(n_seq=S, track_cap=track_cap, det_cap=det_cap, emb_dim=emb_dim,
+                   params=SsParams(**args))
+    orcs = [po.OracleTracker("strongsort", **args) for _ in range(S)]
+    for t in range(1, n_frames + 1):
+        frames = [sc.frame(t) for sc in scenes]
+        off = np.zeros(S + 1, np.int32)
+        off[1:] = np.cumsum([f[0].shape[0] for f in frames])
+        dets = np.concatenate([f[0] for f in frames], 0).astype(np.float64)
+        de = dev(torch, np.concatenate([f[1] for f in frames], 0).astype(np.float64))
+        w = None if warps is None else dev(torch, np.stack([warps(s, t) for s in range(S)]))
+        out = torch.empty((max(int(off[-1]), 1), 10), dtype=torch.float64, device="cuda")
+        cnt = torch.empty(S, dtype=torch.int32, device="cuda")
+        eng.step(dev(torch, dets), dev(torch, off), de, w, out, cnt)
+        o, c = host(out), host(cnt)
+        for s in range(S):
+            ref = orcs[s].update(frames[s][0], frames[s][1],
+                                 None if warps is None else warps(s, t))
+            np.testing.assert_array_equal(o[off[s]: off[s] + c[s]], ref,
+                                          err_msg=f"seq {s} frame {t}")
+    assert eng.status() == 0
+    L = po.lib()
+    for s in range(S):
+        g = eng.tracks(s)
+        n = L.bxo_ss_tracks(orcs[s].h, 0, None, None, None, None)
+        ids = np.zeros(max(n, 1), np.int32)
+        st = np.zeros(max(n, 1), np.int32)
+        mean = np.zeros((max(n, 1), 8))
+        cov = np.zeros((max(n, 1), 8, 8))
+        L.bxo_ss_tracks(orcs[s].h, n, ids.ctypes.data, st.ctypes.data, mean.ctypes.data,
+                        cov.ctypes.data)
+        np.testing.assert_array_equal(g["id"], ids[:n])
+        np.testing.assert_array_equal(g["state"], st[:n])
+        np.testing.assert_array_equal(g["mean"], mean[:n])
+        np.testing.assert_array_equal(g["covariance"], cov[:n])
+    return eng
+
+
+@pytest.mark.parametrize("variant", ["default", "churn", "crowd", "tentative"])
+def test_strongsort_batched_vs_oracle(torch_cuda, variant):
+    """Several sequences per launch against the oracle: cascade levels, IoU stage, recovery from
+    the lost buffer (churn), crowd mode, Tentative births; outputs and Kalman state bitwise."""
+    from boxmot_amd.synth import SyntheticScene
+
+    args = dict(SS_ARGS)
+    kw = dict(emb_dim=48, emb_dtype=np.float64, conf_lo=0.15)
+    if variant == "default":
+        scenes = [SyntheticScene(n_obj=16 + 8 * s, seed=800 + s,
+                                 layout="crowded" if s % 2 else "grid", **kw) for s in range(4)]
+    elif variant == "churn":
+        args.update(max_age=6, nn_budget=12)
+        scenes = [SyntheticScene(n_obj=14 + 6 * s, seed=810 + s, p_det=0.3, **kw)
+                  for s in range(4)]
+    elif variant == "crowd":
+        args.update(max_age=8, nn_budget=16)
+        scenes = [SyntheticScene(n_obj=10 + 2 * s, seed=820 + s, layout="crowded", width=60.0,
+                                 height=60.0, **kw) for s in range(3)]
+    else:  # Tentative tracks are never matched nor deleted (App. A D8): they accumulate
+        args.update(born_confirmed=False)
+        scenes = [SyntheticScene(n_obj=12, seed=830 + s, **kw) for s in range(2)]
+        run_ss_batched(torch_cuda, scenes, 30, args, 48, track_cap=512)
+        return
+    run_ss_batched(torch_cuda, scenes, 50, args, 48)
+
+
+def test_strongsort_large_scene_vs_oracle(torch_cuda):
+    """128 objects with 512-d ReID: several MFMA row/column tiles per track, large LSAPs."""
+    from boxmot_amd.synth import SyntheticScene
+
+    sc = SyntheticScene(n_obj=128, seed=31, emb_dim=512, emb_dtype=np.float64, conf_lo=0.15)
+    run_ss_batched(torch_cuda, [sc], 20, dict(SS_ARGS), 512, track_cap=1024)
+
+
+def test_strongsort_dropin(torch_cuda, monkeypatch):
+    from boxmot_amd import StrongSort, create_tracker
+
+    monkeypatch.setenv("GITHUB_ACTIONS", "true")
+    monkeypatch.delenv("GITHUB_JOB", raising=False)
+    img = np.zeros((720, 1280, 3), np.uint8)
+    t = create_tracker("strongsort", handle_occlusions=False) if False else StrongSort()
+    orc = po.OracleTracker("strongsort", **SS_ARGS)
+    rng = np.random.default_rng(5)
+    base = rng.standard_normal((3, 32))
+    d = np.array([[10, 10, 60, 120, 0.9, 0], [200, 50, 260, 170, 0.8, 2],
+                  [400, 300, 470, 460, 0.5, 0]], np.float64)
+    for k in range(8):
+        dd = d if k not in (3, 4) else d[:0]
+        e = base[: len(dd)] + 0.01 * rng.standard_normal((len(dd), 32))
+        o = np.asarray(t.update(dd, img, e), np.float64).reshape(-1, 10)
+        np.testing.assert_array_equal(o, orc.update(dd, e).reshape(-1, 10))
+    y = create_tracker("strongsort")
+    assert not hasattr(y, "per_class") or y.per_class is False
+    with pytest.raises(AssertionError):
+        y.update(d, img, base[:2])

@@ -47,7 +47,7 @@ def test_ocsort_yaml_defaults_reach_the_engine(monkeypatch):
     assert (p.min_conf, p.Q_xy_scaling, p.Q_s_scaling, p.asso_threshold) == (0.1, 0.01, 1e-4, 0.3)
 
 
-@pytest.mark.parametrize("name", ["strongsort", "deepocsort"])
+@pytest.mark.parametrize("name", ["deepocsort", "hybridsort"])
 def test_not_yet_on_engine(name):
     with pytest.raises(NotImplementedError):
         create_tracker(name, evolve_param_dict={})
