@@ -59,7 +59,19 @@ CONFIGS = {
         min_box_area=10, aspect_ratio_thresh=1.6, lambda_iou=0.5, lambda_mhd=0.25,
         lambda_shape=0.25, use_dlo_boost=True, use_duo_boost=True, dlo_boost_coef=0.65,
         s_sim_corr=False, use_rich_s=True, use_sb=True, use_vt=True, with_reid=True)),
+    # StrongSort (configs[3]'s tracker, constructor defaults, born Confirmed): many MOT-sized
+    # sequences with 512-d ReID, and the C4 geometry (1000 tracks x ~500 dets x 2048-d) as one
+    # sequence
+    "strongsort": ("strongsort", 48, 512, dict(
+        min_conf=0.1, max_cos_dist=0.15, max_iou_dist=0.7, max_age=50, n_init=2, nn_budget=150,
+        mc_lambda=0.995, ema_alpha=0.9, conf_thresh_high=0.7, conf_thresh_low=0.3,
+        id_preservation_weight=0.1, crowd_detection=True, born_confirmed=True)),
+    "strongsort_c4": ("strongsort", 1000, 2048, dict(
+        min_conf=0.1, max_cos_dist=0.15, max_iou_dist=0.7, max_age=50, n_init=2, nn_budget=150,
+        mc_lambda=0.995, ema_alpha=0.9, conf_thresh_high=0.7, conf_thresh_low=0.3,
+        id_preservation_weight=0.1, crowd_detection=True, born_confirmed=True)),
 }
+DEFAULT_SEQS = {"strongsort": 256, "strongsort_c4": 1}
 OCS_CONF_LO = 0.3  # OCSort / BoostTrack scenes: confidences U(0.3, 1) -> ~40% below det_thresh
 
 # OCSort per-launch algorithmic bytes: per live track the XYSR state (x[7], P[49] f64) read and
@@ -111,14 +123,31 @@ def boost_stage_bytes(stage, u, F):
     }[stage]
 
 
+def ss_stage_bytes(stage, u, F):
+    """Algorithmic HBM bytes of one StrongSort launch from the frame's unit
+    counts summed over sequences: dets (kept), tracks, queried (confirmed tracks with a gallery),
+    rows (distinct gallery samples compared), outputs."""
+    return {
+        # embedding row in, NN-normalised and track-normalised rows out
+        "prep": u["dets"] * 3 * F * 8,
+        # every compared sample row and every detection row read once, one distance per
+        # (queried track, detection) out
+        "nn": (u["rows"] + u["dets"]) * F * 8 + u["queried"] * (u["dets"] // max(u["seqs"], 1)) * 8,
+        # the feature row of each lost track and the detection rows
+        "recovery": u["dets"] * F * 8,
+        # track records (mean, cov, histories: ~1.2 kB) read + written, detection rows
+        "frame": u["tracks"] * 2 * 1200 + u["dets"] * 64 + u["outputs"] * 80,
+    }[stage]
+
+
 def cpu_baseline(kind, n_obj, emb_dim, params, seconds=15.0, warm_frames=40):
     """Time the C oracle (port of the reference semantics, 1 thread) on one sequence of the
     same workload: frames/s over a bounded sample after `warm_frames` of warm-up."""
     from boxmot_amd.synth import SyntheticScene
     from oracle import pyoracle as po
 
-    extra = dict(conf_lo=OCS_CONF_LO) if kind in ("ocsort", "boosttrack") else {}
-    if kind == "boosttrack":
+    extra = dict(conf_lo=OCS_CONF_LO) if kind in ("ocsort", "boosttrack", "strongsort") else {}
+    if kind in ("boosttrack", "strongsort"):
         extra["emb_dtype"] = np.float64
     sc = SyntheticScene(n_obj=n_obj, seed=12345, emb_dim=emb_dim, **extra)
     tr = po.OracleTracker(kind, **params)
@@ -160,7 +189,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", choices=list(CONFIGS), default="botsort")
-    ap.add_argument("--seqs", type=int, default=1024, help="sequences per GPU")
+    ap.add_argument("--seqs", type=int, default=None,
+                    help="sequences per GPU (default 1024; strongsort 256, strongsort_c4 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -183,15 +213,21 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from boxmot_amd.engine import (BoostEngine, BoostParams, Engine, EngineParams, OcsortEngine,
-                                   OcsortParams)
+                                   OcsortParams, SsEngine, SsParams)
     from boxmot_amd.shard import gather_records, output_checksum, shard_sequences
     from boxmot_amd.synth import TorchSceneBatch
 
     kind, n_obj, F, params = CONFIGS[args.config]
-    S = args.seqs
+    S = args.seqs if args.seqs is not None else DEFAULT_SEQS.get(args.config, 1024)
     ocs = kind == "ocsort"
     bst = kind == "boosttrack"
-    if bst:
+    sss = kind == "strongsort"
+    if sss:
+        eng = SsEngine(n_seq=S, track_cap=min(1024, max(96, 2 * n_obj)),
+                       det_cap=min(1024, max(64, n_obj)), emb_dim=F, vec_cap=64,
+                       params=SsParams(**params))
+        stages = list(SsEngine.STAGES)
+    elif bst:
         eng = BoostEngine(n_seq=S, track_cap=128, det_cap=max(64, n_obj), emb_dim=F,
                           params=BoostParams(**params))
         stages = list(BoostEngine.STAGES)
@@ -207,13 +243,15 @@ def main():
                   if F or s not in ("det_features", "gate", "cosine", "features")]
     # this rank's shard: global sequences [rank*S, (rank+1)*S) — weak scaling, no exchange
     gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev,
-                          **(dict(conf_lo=OCS_CONF_LO) if ocs or bst else {}))
+                          **(dict(conf_lo=OCS_CONF_LO) if ocs or bst or sss else {}))
     total = args.warmup + args.steps
     frames = [gen.frame(t) for t in range(1, total + 1)]  # resident in HBM before timing
     if bst:  # BoostTrack consumes float64 embeddings (the dtype `boxmot eval` loads)
         frames = [(d, o, e.double()) for d, o, e in frames]
+    if sss:  # StrongSort: float64 detections (no setup_decorator rounding) and embeddings
+        frames = [(d.double(), o, e.double()) for d, o, e in frames]
     max_n = max(int(f[1][-1].item()) for f in frames)
-    out = torch.empty((max_n, 8), dtype=torch.float64, device=dev)
+    out = torch.empty((max_n, 10 if kind == "strongsort" else 8), dtype=torch.float64, device=dev)
     cnt = torch.empty(S, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream()
     torch.cuda.synchronize()
@@ -222,7 +260,7 @@ def main():
         d, off, e = frames[k]
         if ocs:
             eng.step(d, off, out, cnt, stream=stream.cuda_stream)
-        elif bst:
+        elif bst or sss:
             eng.step(d, off, e, None, out, cnt, stream=stream.cuda_stream)
         else:
             eng.step(d, off, e, None, out, cnt, stream=stream.cuda_stream)
@@ -263,7 +301,9 @@ def main():
     units = eng.frame_stats()  # last timed frame, all sequences of this rank
     if ocs:
         units["dets"] = int(frames[total - 1][1][-1].item())
-    emb_bytes = 8 if bst else 4
+    emb_bytes = 8 if bst or sss else 4
+    if sss:
+        units["seqs"] = S
 
     # per-sequence records of this rank's shard: [global seq id, frames timed, dets timed,
     # rows of the last frame, checksum of the last frame, rank wall s, dominant-stage ms]
@@ -287,6 +327,8 @@ def main():
                           units["outputs"] * 64)
         elif bst:
             per_launch = boost_stage_bytes(dominant, units, F)
+        elif sss:
+            per_launch = ss_stage_bytes(dominant, units, F)
         else:
             per_launch = stage_bytes(dominant, units, F)
         achieved = per_launch / (dom_ms * 1e-3) / 1e9
@@ -312,7 +354,9 @@ def main():
                          "stage_ms_warmup": {k: round(v, 4) for k, v in stage_ms.items()}},
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        # (strongsort_c4: one oracle frame of 1000 tracks x 150 samples x ~500 dets x 2048-d is
+        # minutes of single-thread CPU — no bounded sample fits; reported separately)
+        if world == 1 and not args.no_cpu_baseline and args.config != "strongsort_c4":
             line["cpu_baseline"] = cpu_baseline(kind, n_obj, F, params, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if dist:

@@ -57,14 +57,15 @@ struct SsTrk {
   double confh[MAXC];
   int id, state, hits, age, tsu, max_age, n_init;
   int nvel, npos, nconf, nfeat, missed, confirmed_det, low_streak, high_streak, lost_frame;
-  int gal_n;
+  int gal_n, gal_sp;          // gallery length, its sorted prefix (partial_fit's last sort)
   int feat[MAXF];
-  unsigned long long vmask;  // pool entries in use
+  unsigned long long vmask;  // pool entries in use (features or gallery)
+  unsigned long long gmask;  // pool entries referenced by the gallery
 };
 
 enum {
   Q_FRAME = 0, Q_NEXTID, Q_NTR, Q_NLOST, Q_CROWD, Q_ORIG, Q_OMAXAGE, Q_OBUDGET, Q_MAXAGE,
-  Q_BUDGET, Q_HIST, Q_NNL, Q_NK, Q_NT0, Q_NOUT, Q_ROWS, SQS
+  Q_BUDGET, Q_HIST, Q_NNL, Q_NK, Q_NT0, Q_NOUT, Q_ROWS, Q_ROWSL, SQS
 };
 
 struct SsDev {
@@ -88,9 +89,11 @@ struct SsDev {
   double* nf;     // [S][D][F] feat / (wave norm + 1e-8)
   double* recsim; // [S][LOSTN][D]
   double* cost;   // [S][2T*D] scratch cost matrices
+  int* gcnt;      // [S][T][VP] gallery references per pool entry
   int* wsi;       // [S][WSI] int scratch
   double* wsd;    // [S][WSD] double scratch
   int wsi_n, wsd_n;
+  int ws_lds;     // 1: the frame kernel's workspace lives in LDS
   int* status;
 };
 
@@ -419,9 +422,13 @@ int ws_doubles(int T, int D, int N) {
   return D * DTW + 3 * N + 4 * D + 2 * T + PW_MAXLEAF + 8;
 }
 
-__device__ void ws_carve(const SsDev& g, int seq, SsWs& w) {
+__device__ void ws_carve(const SsDev& g, int seq, SsWs& w, char* lds) {
   int* pi = g.wsi + (size_t)seq * g.wsi_n;
   double* pd = g.wsd + (size_t)seq * g.wsd_n;
+  if (g.ws_lds) {  // doubles first (8-byte alignment), then ints
+    pd = (double*)lds;
+    pi = (int*)(lds + (size_t)g.wsd_n * 8);
+  }
   const int T = g.T, D = g.D, N = g.N;
   auto I = [&](int n) { int* p = pi; pi += n; return p; };
   auto Dd = [&](int n) { double* p = pd; pd += n; return p; };
@@ -533,17 +540,14 @@ __global__ void __launch_bounds__(64)
   const int slot = g.nnl[(size_t)seq * g.T + k], lane = threadIdx.x, F = g.F;
   const SsTrk& t = g.trk[(size_t)seq * g.T + slot];
   if (lane == 0) {  // distinct pool entries referenced by the gallery
-    unsigned long long seen = 0ull;
+    unsigned long long m = t.gmask;
     int c = 0;
-    const int* gv = g.gal_v + ((size_t)seq * g.T + slot) * g.GB;
-    for (int q = 0; q < t.gal_n; q++) {
-      const int v = gv[q];
-      if (!((seen >> v) & 1ull)) {
-        seen |= 1ull << v;
-        rowv[c++] = v;
-      }
+    while (m) {
+      rowv[c++] = __ffsll((long long)m) - 1;
+      m &= m - 1;
     }
     nrow_s = c;
+    atomicAdd(g.sq + (size_t)seq * SQS + Q_ROWS, c);
   }
   __syncthreads();
   const int nrow = nrow_s;
@@ -1026,6 +1030,8 @@ __device__ void track_birth(SsCtx& x, int slot, int di) {
     t.high_streak = d[4] > 0.7 ? 1 : 0;
     t.lost_frame = 0;
     t.gal_n = 0;
+    t.gal_sp = 0;
+    t.gmask = 0ull;
     t.nfeat = 0;
     t.vmask = 1ull;  // pool entry 0 holds the first feature
     kf_initiate(KIND_BYTE, bb, t.mean, t.cov);
@@ -1040,13 +1046,17 @@ __device__ void track_birth(SsCtx& x, int slot, int di) {
   const double* nf = g.nf + ((size_t)x.seq * g.D + dk) * F;
   double* dst = vecp(g, x.seq, slot, 0);
   for (int q = lane; q < F; q += 64) dst[q] = nf[q];
+  for (int q = lane; q < g.VP; q += 64) g.gcnt[vidx(g, x.seq, slot, q)] = 0;
   __syncthreads();
 }
 
-// partial_fit's append + budget prune for one gallery (one lane): stable sort by quality
-// descending (insertion) and truncation, as samples_with_quality.sort(reverse=True)[:keep]
-__device__ void gal_prune(int* gv, double* gq, int& n, int keep) {
-  for (int i = 1; i < n; i++) {
+// partial_fit's budget prune for one gallery (one lane): samples_with_quality.sort(reverse=True)
+// [:keep] — a stable sort by quality descending, done as an insertion sort over the unsorted
+// tail [sp, n) (the prefix is sorted since the last prune), then truncation; gallery reference
+// counts and the gallery mask follow the dropped entries.
+__device__ void gal_prune(SsTrk& t, int* gv, double* gq, int* cnt, int keep) {
+  const int n = t.gal_n;
+  for (int i = t.gal_sp > 1 ? t.gal_sp : 1; i < n; i++) {
     const int v = gv[i];
     const double q = gq[i];
     int j = i - 1;
@@ -1058,16 +1068,20 @@ __device__ void gal_prune(int* gv, double* gq, int& n, int keep) {
     gv[j + 1] = v;
     gq[j + 1] = q;
   }
-  if (n > keep) n = keep;
+  for (int k = keep; k < n; k++)
+    if (--cnt[gv[k]] == 0) t.gmask &= ~(1ull << gv[k]);
+  t.gal_n = n > keep ? keep : n;
+  t.gal_sp = t.gal_n;
 }
 
 __global__ void __launch_bounds__(64)
     ss_frame_kernel(SsDev g, int seq0, const double* __restrict__ dets,
                     const int* __restrict__ det_off, const double* __restrict__ warps,
                     double* __restrict__ out, int* __restrict__ out_count) {
+  extern __shared__ __align__(16) char ss_lds[];
   const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
   SsWs w;
-  ws_carve(g, seq, w);
+  ws_carve(g, seq, w, ss_lds);
   SsCtx x{g, w, seq, lane, g.trk + (size_t)seq * g.T, g.sq + (size_t)seq * SQS,
           g.sqd + (size_t)seq * 2, g.lost + (size_t)seq * LOSTN, 0, 0, 0, 0};
   int* sq = x.sq;
@@ -1079,6 +1093,10 @@ __global__ void __launch_bounds__(64)
     n = g.D;
   }
   const int frame = sq[Q_FRAME] + 1;
+  if (lane == 0) {  // gallery rows compared by this frame's ss_nn_kernel (a statistic)
+    sq[Q_ROWSL] = sq[Q_ROWS];
+    sq[Q_ROWS] = 0;
+  }
   x.ntr = sq[Q_NTR];
   x.nlost = sq[Q_NLOST];
   const int nt0 = x.ntr;
@@ -1336,24 +1354,27 @@ __global__ void __launch_bounds__(64)
       SsTrk& t = x.trk[s2];
       int* gv = g.gal_v + ((size_t)seq * g.T + s2) * g.GB;
       double* gq = g.gal_q + ((size_t)seq * g.T + s2) * g.GB;
+      int* cnt = g.gcnt + vidx(g, seq, s2, 0);
       if (t.state == 2) {
         for (int q = 0; q < t.nfeat; q++) {
           const int v = t.feat[q];
           gv[t.gal_n] = v;
           gq[t.gal_n] = g.vwn[vidx(g, seq, s2, v)];
           t.gal_n++;
-          if (budget > 0 && t.gal_n > budget) gal_prune(gv, gq, t.gal_n, budget);
+          cnt[v]++;
+          t.gmask |= 1ull << v;
+          if (budget > 0 && t.gal_n > budget) gal_prune(t, gv, gq, cnt, budget);
         }
       } else if (t.gal_n > keep) {
-        gal_prune(gv, gq, t.gal_n, keep);
+        gal_prune(t, gv, gq, cnt, keep);
       }
     }
     for (int k = lane; k < x.nlost; k += 64) {
       const int s2 = x.lost[k];
       SsTrk& t = x.trk[s2];
       if (t.gal_n > keep)
-        gal_prune(g.gal_v + ((size_t)seq * g.T + s2) * g.GB,
-                  g.gal_q + ((size_t)seq * g.T + s2) * g.GB, t.gal_n, keep);
+        gal_prune(t, g.gal_v + ((size_t)seq * g.T + s2) * g.GB,
+                  g.gal_q + ((size_t)seq * g.T + s2) * g.GB, g.gcnt + vidx(g, seq, s2, 0), keep);
     }
     __syncthreads();
   }
@@ -1361,10 +1382,8 @@ __global__ void __launch_bounds__(64)
   for (int p = lane; p < x.ntr + x.nlost; p += 64) {
     const int s2 = p < x.ntr ? w.lst[p] : x.lost[p - x.ntr];
     SsTrk& t = x.trk[s2];
-    unsigned long long m = 0ull;
+    unsigned long long m = t.gmask;
     for (int q = 0; q < t.nfeat; q++) m |= 1ull << t.feat[q];
-    const int* gv = g.gal_v + ((size_t)seq * g.T + s2) * g.GB;
-    for (int q = 0; q < t.gal_n; q++) m |= 1ull << gv[q];
     t.vmask = m;
   }
   // the next frame's gallery queries: confirmed tracks with samples
@@ -1474,8 +1493,9 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 2, st))) return rc;
   if ((rc = ss_probe_begin(e, 3, st))) return rc;
-  hipLaunchKernelGGL(ss_frame_kernel, dim3(nseq), dim3(64), 0, st, d, seq0, dets, off, warps, out,
-                     cnt);
+  const size_t lds = d.ws_lds ? (size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4 : 0;
+  hipLaunchKernelGGL(ss_frame_kernel, dim3(nseq), dim3(64), lds, st, d, seq0, dets, off, warps,
+                     out, cnt);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 3, st))) return rc;
   return BX_OK;
@@ -1487,7 +1507,7 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   if (!c || !out) return bx_record_error(BX_ERR_INVALID, "null argument");
   const int vp = c->vec_cap > 0 ? c->vec_cap : 32;
   if (c->n_seq <= 0 || c->track_cap <= 0 || c->det_cap <= 0 || c->track_cap > 1024 ||
-      c->det_cap > 512 || c->emb_dim <= 0 || c->emb_dim > 8192 || vp > 64 || c->nn_budget <= 0 ||
+      c->det_cap > 1024 || c->emb_dim <= 0 || c->emb_dim > 8192 || vp > 64 || c->nn_budget <= 0 ||
       c->max_age < 0)
     return bx_record_error(BX_ERR_INVALID, "bx_ss_config out of range");
   int ndev = 0;
@@ -1516,6 +1536,9 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   d.born = c->born_confirmed != 0;
   d.wsi_n = ws_ints(d.T, d.D, d.N);
   d.wsd_n = ws_doubles(d.T, d.D, d.N);
+  // the frame kernel's workspace in LDS when it fits beside ~3 other workgroups per CU
+  const size_t ws_bytes = (size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4;
+  d.ws_lds = ws_bytes <= 48 * 1024 ? 1 : 0;
   const size_t S = d.S, T = d.T, D = d.D, F = d.F, VP = d.VP, GB = d.GB;
   size_t off = 0;
   auto cb = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
@@ -1536,6 +1559,7 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   const size_t o_nf = cb(S * D * F * sizeof(double));
   const size_t o_rec = cb(S * LOSTN * D * sizeof(double));
   const size_t o_cost = cb(S * 2 * T * D * sizeof(double));
+  const size_t o_gcnt = cb(S * T * VP * sizeof(int));
   const size_t o_wsi = cb(S * (size_t)d.wsi_n * sizeof(int));
   const size_t o_wsd = cb(S * (size_t)d.wsd_n * sizeof(double));
   const size_t o_st = cb(sizeof(int) * 4);
@@ -1562,6 +1586,7 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   d.nf = (double*)(base + o_nf);
   d.recsim = (double*)(base + o_rec);
   d.cost = (double*)(base + o_cost);
+  d.gcnt = (int*)(base + o_gcnt);
   d.wsi = (int*)(base + o_wsi);
   d.wsd = (double*)(base + o_wsd);
   d.status = (int*)(base + o_st);
@@ -1577,6 +1602,10 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   q[S * SQS + 1] = c->nn_budget;
   SCHK(hipMemcpy(d.sq, q.data(), q.size() * sizeof(int), hipMemcpyHostToDevice));
   SCHK(hipMemcpy(d.sqd, qd.data(), qd.size() * sizeof(double), hipMemcpyHostToDevice));
+  if (d.ws_lds)
+    SCHK(hipFuncSetAttribute((const void*)ss_frame_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)((size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4)));
   SCHK(hipMalloc(&e->h_dets, sizeof(double) * 6 * D));
   SCHK(hipMalloc(&e->h_off, sizeof(int) * 2));
   SCHK(hipMalloc(&e->h_embs, sizeof(double) * D * F));
@@ -1708,7 +1737,7 @@ int bx_ss_frame_stats_host(bx_ss* e, int seq0, int nseq, int64_t* sums) {
     a[0] += q[Q_NK];
     a[1] += q[Q_NT0];
     a[2] += q[Q_NNL];
-    a[3] += q[Q_ROWS];
+    a[3] += q[Q_ROWSL];
     a[4] += q[Q_NOUT];
     a[5] = q[Q_FRAME] > a[5] ? q[Q_FRAME] : a[5];
   }

@@ -33,8 +33,10 @@ def shard_sequences(frame_counts, world: int, rank: int):
 
 
 def output_checksum(rows: np.ndarray) -> float:
-    """Order-sensitive checksum of an output stream (ids, det_ind and boxes)."""
-    r = np.asarray(rows, np.float64).reshape(-1, 8)
+    """Order-sensitive checksum of an output stream (ids, det_ind and boxes); rows have 8
+    columns (10 for StrongSort, whose extra quality/occlusion columns are ignored)."""
+    r = np.asarray(rows, np.float64)
+    r = r.reshape(-1, r.shape[-1] if r.ndim == 2 else 8)
     w = np.arange(1, r.shape[0] + 1, dtype=np.float64)
     return float((r[:, 4] * w).sum() + (r[:, 7] * 0.5 * w).sum() + r[:, :4].sum() * 1e-3)
 

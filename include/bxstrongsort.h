@@ -46,7 +46,7 @@ extern "C" {
 typedef struct {
     int32_t n_seq;      /* independent sequences held by this engine */
     int32_t track_cap;  /* track slots per sequence, live + lost-buffer (<= 1024) */
-    int32_t det_cap;    /* max detections per frame per sequence (<= 512) */
+    int32_t det_cap;    /* max detections per frame per sequence (<= 1024) */
     int32_t emb_dim;    /* embedding dimension F (float64 embeddings, required) */
     int32_t vec_cap;    /* feature vectors kept per track slot (its features + gallery
                            samples; <= 64, default 32) */
