@@ -74,7 +74,8 @@ class BxOcsortConfig(C.Structure):
         ("min_conf", C.c_double), ("det_thresh", C.c_double), ("asso_threshold", C.c_double),
         ("inertia", C.c_double), ("q_xy_scaling", C.c_double), ("q_s_scaling", C.c_double),
         ("max_age", C.c_int32), ("min_hits", C.c_int32), ("delta_t", C.c_int32),
-        ("use_byte", C.c_int32),
+        ("use_byte", C.c_int32), ("asso_kind", C.c_int32), ("frame_w", C.c_double),
+        ("frame_h", C.c_double),
     ]
 
 
@@ -109,11 +110,11 @@ EXPORTS = [
     "bx_engine_reset", "bx_engine_step", "bx_engine_update_host", "bx_engine_status",
     "bx_engine_counters_host", "bx_engine_set_id_count", "bx_engine_tracks_host",
     "bx_engine_probe", "bx_engine_probe_read", "bx_engine_frame_stats_host",
-    "bx_iou_batch", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
+    "bx_iou_batch", "bx_pairwise_cost", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
     "bx_kf_multi_predict", "bx_kf_update", "bx_kf_gating_distance", "bx_linear_assignment",
     "bx_nn_cosine_distance", "bx_ocsort_create", "bx_ocsort_destroy", "bx_ocsort_reset", "bx_ocsort_step",
     "bx_ocsort_update_host", "bx_ocsort_status", "bx_ocsort_counters_host",
-    "bx_ocsort_set_id_count", "bx_ocsort_tracks_host", "bx_ocsort_probe", "bx_ocsort_probe_read",
+    "bx_ocsort_set_id_count", "bx_ocsort_set_frame_size", "bx_ocsort_tracks_host", "bx_ocsort_probe", "bx_ocsort_probe_read",
     "bx_ocsort_frame_stats_host", "bx_boost_create", "bx_boost_destroy", "bx_boost_reset",
     "bx_boost_step", "bx_boost_update_host", "bx_boost_status", "bx_boost_counters_host",
     "bx_boost_set_id_count", "bx_boost_tracks_host", "bx_boost_frame_stats_host",
@@ -141,6 +142,8 @@ _SIGS = {
     "bx_engine_tracks_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip,
                                _ip], C.c_int),
     "bx_iou_batch": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp], C.c_int),
+    "bx_pairwise_cost": ([C.c_int, _vp, C.c_int, C.c_int, _vp, C.c_int, C.c_int, C.c_double,
+                          C.c_double, _vp, _vp], C.c_int),
     "bx_fuse_score": ([_vp, C.c_int, C.c_int, _vp, _vp], C.c_int),
     "bx_embedding_distance": ([_vp, C.c_int, _vp, C.c_int, C.c_int, _vp, _vp], C.c_int),
     "bx_kf_initiate": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
@@ -158,6 +161,7 @@ _SIGS = {
     "bx_ocsort_status": ([_vp, _ip], C.c_int),
     "bx_ocsort_counters_host": ([_vp, C.c_int, _ip, _ip, _ip], C.c_int),
     "bx_ocsort_set_id_count": ([_vp, C.c_int, C.c_int, _vp], C.c_int),
+    "bx_ocsort_set_frame_size": ([_vp, C.c_int, C.c_double, C.c_double, _vp], C.c_int),
     "bx_ocsort_tracks_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _ip], C.c_int),
     "bx_ocsort_probe": ([_vp, C.c_int], C.c_int),
     "bx_ocsort_frame_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),

@@ -60,6 +60,98 @@ __device__ __forceinline__ double iou_pair(const double* b1, const double* b2) {
   double wh = w * h;
   return wh / ((b1[2] - b1[0]) * (b1[3] - b1[1]) + (b2[2] - b2[0]) * (b2[3] - b2[1]) - wh);
 }
+// fdlibm s_atan.c (the algorithm oracle/bxo_ops.c restates as bxo_atan); within 1 ulp of
+// np.arctan, bit-identical to the oracle.
+__device__ inline double bx_atan(double x) {
+  constexpr double hi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,
+                            9.82793723247329054082e-01, 1.57079632679489655800e+00};
+  constexpr double lo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17,
+                            1.39033110312309984516e-17, 6.12323399573676603587e-17};
+  const int hx = __double2hiint(x);
+  const int ix = hx & 0x7fffffff;
+  int id;
+  if (ix >= 0x44100000) {
+    if (ix > 0x7ff00000 || (ix == 0x7ff00000 && __double2loint(x) != 0)) return x + x;
+    return hx > 0 ? hi[3] + lo[3] : -hi[3] - lo[3];
+  }
+  if (ix < 0x3fdc0000) {
+    if (ix < 0x3e200000) return x;
+    id = -1;
+  } else {
+    x = fabs(x);
+    if (ix < 0x3ff30000) {
+      if (ix < 0x3fe60000) {
+        id = 0;
+        x = (2.0 * x - 1.0) / (2.0 + x);
+      } else {
+        id = 1;
+        x = (x - 1.0) / (x + 1.0);
+      }
+    } else if (ix < 0x40038000) {
+      id = 2;
+      x = (x - 1.5) / (1.0 + 1.5 * x);
+    } else {
+      id = 3;
+      x = -1.0 / x;
+    }
+  }
+  const double z = x * x, w = z * z;
+  const double s1 = z * (3.33333333333329318027e-01 +
+                         w * (1.42857142725034663711e-01 +
+                              w * (9.09088713343650656196e-02 +
+                                   w * (6.66107313738753120669e-02 +
+                                        w * (4.97687799461593236017e-02 + w * 1.62858201153657823623e-02)))));
+  const double s2 = w * (-1.99999999998764832476e-01 +
+                         w * (-1.11111104054623557880e-01 +
+                              w * (-7.69187620504482999495e-02 +
+                                   w * (-5.83357013379057348645e-02 + w * -3.65315727442169155270e-02))));
+  if (id < 0) return x - x * (s1 + s2);
+  const double r = hi[id] - ((x * (s1 + s2) - lo[id]) - x);
+  return hx < 0 ? -r : r;
+}
+
+// AssociationFunction registry (utils/iou.py:79-346), numpy's operation order per mode.
+// kind: 0 iou, 1 hmiou, 2 giou, 3 diou, 4 ciou, 5 centroid (frame size w, h).
+enum { ASSO_IOU = 0, ASSO_HMIOU = 1, ASSO_GIOU = 2, ASSO_DIOU = 3, ASSO_CIOU = 4,
+       ASSO_CENTROID = 5 };
+__device__ inline double asso_pair(int kind, const double* a, const double* b, double fw,
+                                   double fh) {
+  if (kind == ASSO_IOU) return iou_pair(a, b);
+  const double xx1 = fmax(a[0], b[0]), yy1 = fmax(a[1], b[1]);
+  const double xx2 = fmin(a[2], b[2]), yy2 = fmin(a[3], b[3]);
+  const double iw = fmax(0.0, xx2 - xx1), ih = fmax(0.0, yy2 - yy1);
+  const double wh = iw * ih;
+  const double area1 = (a[2] - a[0]) * (a[3] - a[1]), area2 = (b[2] - b[0]) * (b[3] - b[1]);
+  const double ex = fmax(a[2], b[2]) - fmin(a[0], b[0]);  // enclosing box
+  const double ey = fmax(a[3], b[3]) - fmin(a[1], b[1]);
+  const double cx1 = (a[0] + a[2]) / 2.0, cy1 = (a[1] + a[3]) / 2.0;
+  const double cx2 = (b[0] + b[2]) / 2.0, cy2 = (b[1] + b[3]) / 2.0;
+  const double dx = cx1 - cx2, dy = cy1 - cy2;
+  switch (kind) {
+    case ASSO_HMIOU:  // :79-127
+      return (wh / ((area1 + area2 - wh) + 1e-10)) * (ih / fmax(1e-10, ey));
+    case ASSO_GIOU: {  // :129-169
+      const double uni = area1 + area2 - wh;
+      const double enc = ex * ey;
+      return ((wh / uni - (enc - uni) / enc) + 1.0) / 2.0;
+    }
+    case ASSO_DIOU:  // :266-307
+      return ((wh / (area1 + area2 - wh) - (dx * dx + dy * dy) / (ex * ex + ey * ey)) + 1) / 2.0;
+    case ASSO_CIOU: {  // :199-264
+      const double eps = 1e-7;
+      const double iou = wh / (((area1 + area2) - wh) + eps);
+      const double outer = (ex * ex + ey * ey) + eps;
+      const double h1 = (a[3] - a[1]) + eps, h2 = (b[3] - b[1]) + eps;
+      const double d = bx_atan((b[2] - b[0]) / h2) - bx_atan((a[2] - a[0]) / h1);
+      const double pi = 3.141592653589793;
+      const double v = (4 / (pi * pi)) * (d * d);
+      const double alpha = v / (((1 - iou) + v) + eps);
+      return (((iou - (dx * dx + dy * dy) / outer) + alpha * v) + 1) / 2.0;
+    }
+    default:  // ASSO_CENTROID :171-184
+      return 1 - sqrt(dx * dx + dy * dy) / sqrt(fw * fw + fh * fh);
+  }
+}
 // Positive-area intersection.  A pair that fails this has IoU exactly 0 (cost 1 or 2 after
 // fuse_score), which is never admissible for a cost_limit <= 1.
 __device__ __forceinline__ bool boxes_intersect(const double* b1, const double* b2) {

@@ -56,6 +56,8 @@ struct OcsDev {
   int S, T, D, N;  // N = max(T, D): largest assignment problem
   double min_conf, det_thresh, asso_threshold, inertia, q_xy, q_s;
   int max_age, min_hits, delta_t, use_byte, max_obs;
+  int asso_kind;    // ASSO_* (BaseTracker asso_func): iou unless configured otherwise
+  double* fsz;      // [S][2] frame (w, h) per sequence, for the centroid mode
   int cost_lds;     // doubles of LDS for a cost matrix (larger ones go to `cost_g`)
   OcsTrk* trk;      // [S][T]
   int* seqst;       // [S][SQO]
@@ -497,6 +499,8 @@ __global__ void __launch_bounds__(OW)
   const int id0 = sq[SO_IDS];
   const int nt0 = sq[SO_NTR];
   const double thr = g.asso_threshold;
+  const int ak = g.asso_kind;
+  const double fw = g.fsz[2 * seq], fh = g.fsz[2 * seq + 1];
 
   // detections (setup_decorator's float32 rounding is the input format) and the splits
   for (int q = lane; q < n * 6; q += OW) L.dd[q] = (double)dets[(size_t)r0 * 6 + q];
@@ -592,8 +596,10 @@ __global__ void __launch_bounds__(OW)
             const double xx2 = fmin(a[2], b2), yy2 = fmin(a[3], b3);
             const double w = fmax(0.0, xx2 - xx1), h = fmax(0.0, yy2 - yy1);
             const double wh = w * h;
-            if (wh > 0.0 || thr < 0.0) {
-              const double o = wh / ((a[2] - a[0]) * (a[3] - a[1]) + at - wh);
+            // the other registry modes score disjoint pairs too: no shortcut for them
+            if (wh > 0.0 || thr < 0.0 || ak != ASSO_IOU) {
+              const double o = ak == ASSO_IOU ? wh / ((a[2] - a[0]) * (a[3] - a[1]) + at - wh)
+                                              : asso_pair(ak, a, bq, fw, fh);
               if (o > thr) {
                 atomicAdd(&L.rowcnt[d], 1);
                 L.rowcol[d] = ti;
@@ -634,7 +640,7 @@ __global__ void __launch_bounds__(OW)
             const double valid = p[4] < 0 ? 0.0 : 1.0;
             for (int d = 0; d < nh; d++) {
               const double* a = L.dd + 6 * L.hi[d];
-              const double o = iou_pair(a, r);
+              const double o = asso_pair(ak, a, r, fw, fh);
               // speed_direction_batch (association.py:10-20) against the k-previous obs
               const double cx1 = (a[0] + a[2]) / 2.0, cy1 = (a[1] + a[3]) / 2.0;
               double dx = cx1 - cx2, dy = cy1 - cy2;
@@ -675,7 +681,7 @@ __global__ void __launch_bounds__(OW)
       if (q < nmi) {
         d = L.mi[2 * q];
         ti = L.mi[2 * q + 1];
-        ok = iou_pair(L.dd + 6 * L.hi[d], tb + (size_t)ti * TB) >= thr;
+        ok = asso_pair(ak, L.dd + 6 * L.hi[d], tb + (size_t)ti * TB, fw, fh) >= thr;
         rej = !ok;
       }
       const unsigned long long mo = __ballot(ok), mr = __ballot(rej);
@@ -723,7 +729,10 @@ __global__ void __launch_bounds__(OW)
           const double xx2 = fmin(a[2], b2), yy2 = fmin(a[3], b3);
           const double w = fmax(0.0, xx2 - xx1), h = fmax(0.0, yy2 - yy1);
           const double wh = w * h;
-          if (wh > 0.0 || thr < 0.0) mx = fmax(mx, wh / ((a[2] - a[0]) * (a[3] - a[1]) + at - wh));
+          if (ak != ASSO_IOU)
+            mx = fmax(mx, asso_pair(ak, a, bq, fw, fh));
+          else if (wh > 0.0 || thr < 0.0)
+            mx = fmax(mx, wh / ((a[2] - a[0]) * (a[3] - a[1]) + at - wh));
         }
       }
     }
@@ -736,7 +745,8 @@ __global__ void __launch_bounds__(OW)
       const int k = c + lane;
       if (k < nc) {
         const double* bq = tb + (size_t)tsel[k] * TB + boff;
-        for (int d = 0; d < nr; d++) C[d * nc + k] = -iou_pair(L.dd + 6 * dsel[dmap ? dmap[d] : d], bq);
+        for (int d = 0; d < nr; d++)
+          C[d * nc + k] = -asso_pair(ak, L.dd + 6 * dsel[dmap ? dmap[d] : d], bq, fw, fh);
       }
     }
     __syncthreads();
@@ -986,6 +996,11 @@ int bx_ocsort_create(const bx_ocsort_config* c, bx_ocsort** out) {
   d.min_hits = c->min_hits;
   d.delta_t = c->delta_t;
   d.use_byte = c->use_byte;
+  if (c->asso_kind < ASSO_IOU || c->asso_kind > ASSO_CENTROID) {
+    delete e;
+    return bx_record_error(BX_ERR_INVALID, "unknown asso_kind");
+  }
+  d.asso_kind = c->asso_kind;
   // basetracker.py:59-62: max_obs = 50, or max_age + 5 when max_age >= 50
   d.max_obs = c->max_age >= 50 ? c->max_age + 5 : 50;
   // LDS: the fixed part plus as much cost matrix as keeps ~4 workgroups per CU resident
@@ -1010,6 +1025,7 @@ int bx_ocsort_create(const bx_ocsort_config* c, bx_ocsort** out) {
   const size_t o_tb = carve_b(S * T * TB * sizeof(double));
   const size_t o_cg = need_g ? carve_b(S * (size_t)d.D * T * sizeof(double)) : 0;
   const size_t o_st = carve_b(sizeof(int) * 4);
+  const size_t o_fsz = carve_b(S * 2 * sizeof(double));
 #ifdef BX_PHASE_TIMING
   const size_t o_dbg = carve_b(S * OCS_DBG * sizeof(unsigned long long));
 #endif
@@ -1025,6 +1041,15 @@ int bx_ocsort_create(const bx_ocsort_config* c, bx_ocsort** out) {
   d.tb = (double*)(base + o_tb);
   d.cost_g = need_g ? (double*)(base + o_cg) : nullptr;
   d.status = (int*)(base + o_st);
+  d.fsz = (double*)(base + o_fsz);
+  {
+    std::vector<double> f(2 * S);
+    for (size_t k = 0; k < S; k++) {
+      f[2 * k] = c->frame_w;
+      f[2 * k + 1] = c->frame_h;
+    }
+    OCHK(hipMemcpy(d.fsz, f.data(), sizeof(double) * 2 * S, hipMemcpyHostToDevice));
+  }
 #ifdef BX_PHASE_TIMING
   d.dbg = (unsigned long long*)(base + o_dbg);
 #else
@@ -1117,6 +1142,15 @@ int bx_ocsort_set_id_count(bx_ocsort* e, int seq, int id_count, void* stream) {
   if (!e || seq < 0 || seq >= e->dev.S) return bx_record_error(BX_ERR_INVALID, "bad sequence");
   OCHK(hipMemcpyAsync(e->dev.seqst + (size_t)seq * SQO + SO_IDS, &id_count, sizeof(int),
                       hipMemcpyHostToDevice, (hipStream_t)stream));
+  OCHK(hipStreamSynchronize((hipStream_t)stream));
+  return BX_OK;
+}
+
+int bx_ocsort_set_frame_size(bx_ocsort* e, int seq, double w, double h, void* stream) {
+  if (!e || seq < 0 || seq >= e->dev.S) return bx_record_error(BX_ERR_INVALID, "bad sequence");
+  const double f[2] = {w, h};
+  OCHK(hipMemcpyAsync(e->dev.fsz + 2 * (size_t)seq, f, sizeof(f), hipMemcpyHostToDevice,
+                      (hipStream_t)stream));
   OCHK(hipStreamSynchronize((hipStream_t)stream));
   return BX_OK;
 }

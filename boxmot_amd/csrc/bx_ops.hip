@@ -10,13 +10,11 @@
 
 using namespace bx;
 
+int bx_record_error(int code, const char* msg);  // bx_engine.hip (shared bx_last_error)
+
 namespace {
 
-thread_local std::string g_op_err;
-int op_err(int code, const char* msg) {
-  g_op_err = msg;
-  return code;
-}
+int op_err(int code, const char* msg) { return bx_record_error(code, msg); }
 #define OPCHK(x)                                                  \
   do {                                                            \
     hipError_t _e = (x);                                          \
@@ -29,6 +27,16 @@ __global__ void iou_kernel(const double* a, int na, const double* b, int nb, dou
        k += (size_t)gridDim.x * blockDim.x) {
     const int i = (int)(k / nb), j = (int)(k % nb);
     out[k] = iou_pair(a + 4 * i, b + 4 * j);
+  }
+}
+
+__global__ void pairwise_kernel(int kind, const double* a, int na, int lda, const double* b,
+                                int nb, int ldb, double fw, double fh, double* out) {
+  const size_t n = (size_t)na * nb;
+  for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n;
+       k += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(k / nb), j = (int)(k % nb);
+    out[k] = asso_pair(kind, a + (size_t)lda * i, b + (size_t)ldb * j, fw, fh);
   }
 }
 
@@ -177,6 +185,19 @@ int bx_iou_batch(const double* a, int na, const double* b, int nb, double* out, 
   if (!na || !nb) return BX_OK;
   hipLaunchKernelGGL(iou_kernel, dim3(grid_for((size_t)na * nb)), dim3(256), 0,
                      (hipStream_t)stream, a, na, b, nb, out);
+  OPCHK(hipGetLastError());
+  return BX_OK;
+}
+
+int bx_pairwise_cost(int kind, const double* a, int na, int lda, const double* b, int nb,
+                     int ldb, double w, double h, double* out, void* stream) {
+  if (kind < BX_ASSO_IOU || kind > BX_ASSO_CENTROID)
+    return op_err(BX_ERR_INVALID, "unknown association kind");
+  if (na < 0 || nb < 0) return op_err(BX_ERR_INVALID, "negative size");
+  if (!na || !nb) return BX_OK;
+  if (lda < 4 || ldb < 4) return op_err(BX_ERR_INVALID, "row stride below 4");
+  hipLaunchKernelGGL(pairwise_kernel, dim3(grid_for((size_t)na * nb)), dim3(256), 0,
+                     (hipStream_t)stream, kind, a, na, lda, b, nb, ldb, w, h, out);
   OPCHK(hipGetLastError());
   return BX_OK;
 }

@@ -175,6 +175,14 @@ class Engine:
                 "start_frame": sf[:n], "mean": mean[:n], "covariance": cov[:n]}
 
 
+def _asso_kind(name: str) -> int:
+    from .iou import KINDS
+
+    if name not in KINDS:
+        raise ValueError(f"Invalid association mode: {name}. Choose from {list(KINDS)}")
+    return KINDS[name]
+
+
 @dataclass
 class OcsortParams:
     """OcSort constructor parameters (ocsort.py:197-235 names; YAML defaults)."""
@@ -189,6 +197,9 @@ class OcsortParams:
     use_byte: bool = False
     Q_xy_scaling: float = 0.01
     Q_s_scaling: float = 0.0001
+    asso_func: str = "iou"      # utils/iou.py registry mode (BaseTracker asso_func)
+    frame_w: float = 1920.0     # centroid normalisation until set_frame_size latches the image
+    frame_h: float = 1080.0
 
 
 class OcsortEngine:
@@ -203,7 +214,8 @@ class OcsortEngine:
             n_seq=n_seq, track_cap=track_cap, det_cap=det_cap, min_conf=p.min_conf,
             det_thresh=p.det_thresh, asso_threshold=p.asso_threshold, inertia=p.inertia,
             q_xy_scaling=p.Q_xy_scaling, q_s_scaling=p.Q_s_scaling, max_age=int(p.max_age),
-            min_hits=int(p.min_hits), delta_t=int(p.delta_t), use_byte=int(bool(p.use_byte)))
+            min_hits=int(p.min_hits), delta_t=int(p.delta_t), use_byte=int(bool(p.use_byte)),
+            asso_kind=_asso_kind(p.asso_func), frame_w=float(p.frame_w), frame_h=float(p.frame_h))
         self._L = N.load()
         h = C.c_void_p()
         N.check(self._L.bx_ocsort_create(C.byref(cfg), C.byref(h)), "bx_ocsort_create")
@@ -257,6 +269,10 @@ class OcsortEngine:
 
     def set_id_count(self, seq: int, value: int):
         N.check(self._L.bx_ocsort_set_id_count(self._h, seq, int(value), None), "set_id_count")
+
+    def set_frame_size(self, seq: int, w: float, h: float):
+        N.check(self._L.bx_ocsort_set_frame_size(self._h, seq, float(w), float(h), None),
+                "set_frame_size")
 
     def tracks(self, seq: int = 0) -> dict:
         """Host snapshot of the track list (list order): ids, XYSR means x [7], covariances."""

@@ -79,6 +79,12 @@ class BaseTracker:
                     self._first_dets_processed = True
             if not self._first_frame_processed and img is not None:
                 self.h, self.w = img.shape[0:2]
+                # basetracker.py:140-147: the association function is chosen here, so an
+                # unknown asso_func raises ValueError on the first update
+                from ..iou import AssociationFunction
+
+                self.asso_func = AssociationFunction(
+                    w=self.w, h=self.h, asso_mode=self.asso_func_name).asso_func
                 self._first_frame_processed = True
             rest = args[2:]
             if "embs" in kwargs:

@@ -1,7 +1,7 @@
 """OCSort on the MI355X engine — drop-in for boxmot.trackers.ocsort.ocsort.OcSort
 (reference trackers/ocsort/ocsort.py:195-439).  Same constructor, same ``update`` contract and
-output rows; the whole frame (XYSR Kalman predict/update with ORU, IoU + direction-consistency
-costs, the legacy-lapx JV rounds, OCR/BYTE recovery, births and deaths) is one kernel launch.
+output rows; the whole frame (XYSR Kalman predict/update with ORU, asso_func (iou, hmiou, giou,
+diou, ciou or centroid) + direction-consistency costs, the legacy-lapx JV rounds, OCR/BYTE recovery, births and deaths) is one kernel launch.
 
 The fork's OCSort does not run as shipped; this follows it with the minimal patches P1-P5
 (SURVEY.md Appendix A), exactly as oracle/bxo_ocsort.c and the golden fixtures do.
@@ -11,6 +11,7 @@ from __future__ import annotations
 import numpy as np
 
 from ..engine import OcsortEngine, OcsortParams
+from ..iou import KINDS
 from .basetracker import BaseTracker
 
 
@@ -25,9 +26,6 @@ class OcSort(BaseTracker):
                  use_byte: bool = False, Q_xy_scaling: float = 0.01,
                  Q_s_scaling: float = 0.0001, track_cap: int = 256, det_cap: int = 256):
         super().__init__(max_age=max_age, per_class=per_class, asso_func=asso_func)
-        if asso_func != "iou":
-            raise NotImplementedError(f"OCSort asso_func {asso_func!r} is not on the engine "
-                                      "(the fork's OCSort path evaluates 'iou')")
         self.min_conf = min_conf
         self.max_age = max_age
         self.min_hits = min_hits
@@ -45,13 +43,19 @@ class OcSort(BaseTracker):
             params=OcsortParams(min_conf=min_conf, det_thresh=det_thresh, max_age=max_age,
                                 min_hits=min_hits, asso_threshold=asso_threshold,
                                 delta_t=delta_t, inertia=inertia, use_byte=use_byte,
-                                Q_xy_scaling=Q_xy_scaling, Q_s_scaling=Q_s_scaling))
+                                Q_xy_scaling=Q_xy_scaling, Q_s_scaling=Q_s_scaling,
+                                asso_func=asso_func if asso_func in KINDS else "iou"))
         self._engine_ids = 0
+        self._frame_latched = False
 
     @BaseTracker.setup_decorator
     @BaseTracker.per_class_decorator
     def update(self, dets: np.ndarray, img: np.ndarray, embs: np.ndarray = None) -> np.ndarray:
         self.check_inputs(dets, img)
+        if not self._frame_latched and self._first_frame_processed:
+            # the engine's asso_func / centroid frame size follow BaseTracker's first-frame latch
+            self.engine.set_frame_size(0, self.w, self.h)
+            self._frame_latched = True
         if self._engine_ids != OcSort._id_count:
             self.engine.set_id_count(0, OcSort._id_count)
         self.frame_count += 1

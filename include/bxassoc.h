@@ -13,6 +13,8 @@
  *                          BotSort.update            boxmot/trackers/botsort/botsort.py:94-166
  *                          (+ per-frame glue         botsort.py:168-411, botsort_utils.py:1-81)
  *   bx_iou_batch           AssociationFunction.iou_batch   boxmot/utils/iou.py:50-67
+ *   bx_pairwise_cost       AssociationFunction.{iou,hmiou,giou,diou,ciou,centroid}_batch
+ *                          boxmot/utils/iou.py:50-307, registry :320-346
  *   bx_fuse_score          matching.enhanced_fuse_score    boxmot/utils/matching.py:488-555
  *   bx_embedding_distance  matching.enhanced_embedding_distance  boxmot/utils/matching.py:230-316
  *   bx_kf_*                BaseKalmanFilter + XYAH/XYWH noise models
@@ -130,6 +132,15 @@ int bx_engine_tracks_host(bx_engine *e, int seq, int cap, int32_t *ids, int32_t 
 
 /* ---------------------------- op-level kernels (device pointers) ---------------------------- */
 int bx_iou_batch(const double *a, int na, const double *b, int nb, double *out, void *stream);
+/* AssociationFunction registry (utils/iou.py:79-346, _get_asso_func :320-346): out[i][j] =
+ * <kind>_batch(a, b)[i][j] for rows of stride lda / ldb (>= 4, xyxy first).  centroid
+ * normalises by the frame diagonal sqrt(w^2 + h^2) (AssociationFunction(w, h), :36-49); the
+ * other kinds ignore w, h.  giou's assert (enclosing box of positive size, :163) is the
+ * caller's; the OBB modes (iou_obb, centroid_obb) are not provided. */
+enum { BX_ASSO_IOU = 0, BX_ASSO_HMIOU = 1, BX_ASSO_GIOU = 2, BX_ASSO_DIOU = 3, BX_ASSO_CIOU = 4,
+       BX_ASSO_CENTROID = 5 };
+int bx_pairwise_cost(int kind, const double *a, int na, int lda, const double *b, int nb, int ldb,
+                     double w, double h, double *out, void *stream);
 int bx_fuse_score(double *cost, int nr, int nc, const double *confs, void *stream);
 /* float32 features, numpy float32 norms, scipy cdist-cosine summation order, clipped at 0 */
 int bx_embedding_distance(const float *trk, int nt, const float *det, int nd, int f, double *out,

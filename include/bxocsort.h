@@ -35,14 +35,17 @@ extern "C" {
 
 /* OcSort constructor parameters (ocsort.py:197-235; YAML defaults in configs/trackers/ocsort.yaml:
  * min_conf .1, det_thresh .6, max_age 30, min_hits 3, asso_threshold .3, delta_t 3, inertia .1,
- * use_byte 0, Q_xy_scaling .01, Q_s_scaling 1e-4). asso_func is "iou" (the only one the fork's
- * OCSort path evaluates). */
+ * use_byte 0, Q_xy_scaling .01, Q_s_scaling 1e-4).  asso_kind is BaseTracker's asso_func
+ * (basetracker.py:140-147; BX_ASSO_* of bxassoc.h, iou by default); centroid normalises by the
+ * sequence's frame size, frame_w x frame_h until bx_ocsort_set_frame_size latches another. */
 typedef struct {
     int32_t n_seq;      /* independent sequences held by this engine */
     int32_t track_cap;  /* track slots per sequence (<= 512) */
     int32_t det_cap;    /* max detections per frame per sequence (<= 512) */
     double min_conf, det_thresh, asso_threshold, inertia, q_xy_scaling, q_s_scaling;
     int32_t max_age, min_hits, delta_t, use_byte;
+    int32_t asso_kind;
+    double frame_w, frame_h;
 } bx_ocsort_config;
 
 typedef struct bx_ocsort bx_ocsort;
@@ -72,6 +75,8 @@ int bx_ocsort_counters_host(bx_ocsort *e, int seq, int *frame_count, int *id_cou
 int bx_ocsort_set_id_count(bx_ocsort *e, int seq, int id_count, void *stream);
 /* Track list of a sequence in list order (host, synchronous): ids [cap], Kalman means x
  * [cap][7] and covariances p [cap][49] (any may be NULL); *n = number of tracks. */
+/* Frame size (w, h) of a sequence — BaseTracker latches img.shape on the first frame. */
+int bx_ocsort_set_frame_size(bx_ocsort *e, int seq, double w, double h, void *stream);
 int bx_ocsort_tracks_host(bx_ocsort *e, int seq, int cap, int32_t *ids, double *x, double *p,
                           int *n);
 /* Last-frame statistics over sequences [seq0, seq0+nseq) (host, synchronous): sums[3] =

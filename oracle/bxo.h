@@ -21,6 +21,13 @@ enum { BXO_KF_XYAH = 0, BXO_KF_XYWH = 1 };
 
 /* utils/iou.py:50-67  AssociationFunction.iou_batch  (a[na,4], b[nb,4] xyxy → out[na,nb]) */
 void bxo_iou_batch(const double *a, int na, const double *b, int nb, double *out);
+/* utils/iou.py:79-346  AssociationFunction registry: iou, hmiou, giou, diou, ciou, centroid
+ * (centroid normalises by the frame diagonal sqrt(w^2 + h^2)). a[na,4], b[nb,4] -> out[na,nb] */
+enum { BXO_ASSO_IOU = 0, BXO_ASSO_HMIOU = 1, BXO_ASSO_GIOU = 2, BXO_ASSO_DIOU = 3,
+       BXO_ASSO_CIOU = 4, BXO_ASSO_CENTROID = 5 };
+void bxo_asso_batch(int kind, const double *a, int na, const double *b, int nb, double w,
+                    double h, double *out);
+double bxo_atan(double x);
 /* utils/matching.py:488-555  enhanced_fuse_score, in place on cost[nr,nc] */
 void bxo_fuse_score(double *cost, int nr, int nc, const double *confs);
 /* utils/matching.py:230-316  enhanced_embedding_distance (float32 features, scipy cosine) */
@@ -77,6 +84,10 @@ bxo_ocsort *bxo_ocsort_new(double min_conf, double det_thresh, int max_age, int 
                            double asso_threshold, int delta_t, double inertia, int use_byte,
                            double q_xy_scaling, double q_s_scaling);
 void bxo_ocsort_free(bxo_ocsort *o);
+/* asso_func (BXO_ASSO_*) and the frame size its centroid mode normalises by */
+void bxo_ocsort_set_asso(bxo_ocsort *o, int kind, double w, double h);
+/* one pair of AssociationFunction.<kind>_batch */
+double bxo_pair_cost(int kind, const double *a, const double *b, double w, double h);
 int bxo_ocsort_id_count(bxo_ocsort *o);
 /* track list in list order: ids [cap], XYSR means x [cap][7], covariances P [cap][49] */
 int bxo_ocsort_tracks(bxo_ocsort *o, int cap, int *ids, double *x, double *P);

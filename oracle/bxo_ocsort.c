@@ -323,6 +323,8 @@ struct bxo_ocsort {
     int max_age, min_hits, delta_t, use_byte;
     kf_params kp;
     int frame_count, id_count;
+    int asso_kind;       /* BXO_ASSO_* (BaseTracker asso_func, basetracker.py:140-147) */
+    double fw, fh;       /* frame size latched from the first image (centroid) */
     ocs_track *tr;
     int ntr, cap;
 };
@@ -473,7 +475,8 @@ static int legacy_lap(const double *cost, int nr, int nc, int *pairs) {
 /* enhanced_associate (patched, association.py:377-536): dets[nd][5], trks[nt][5],
  * velocities[nt][2], prev_obs[nt][5].  Outputs matches (det, trk) and the two unmatched lists
  * in the reference's order. */
-static void associate(const double *dets, int nd, const double *trks, int nt, double thr,
+static void associate(int kind, double fw, double fh, const double *dets, int nd,
+                      const double *trks, int nt, double thr,
                       const double *vel, const double *prev, double vdc_weight, int *matches,
                       int *nm, int *ud, int *nud, int *ut, int *nut) {
     *nm = *nud = *nut = 0;
@@ -486,13 +489,8 @@ static void associate(const double *dets, int nd, const double *trks, int nt, do
     for (int d = 0; d < nd; d++)
         for (int t = 0; t < nt; t++) {
             const double *a = dets + 5 * d, *b = trks + 5 * t;
-            /* iou_batch (utils/iou.py:50-67) */
-            const double xx1 = fmax(a[0], b[0]), yy1 = fmax(a[1], b[1]);
-            const double xx2 = fmin(a[2], b[2]), yy2 = fmin(a[3], b[3]);
-            const double w = fmax(0.0, xx2 - xx1), h = fmax(0.0, yy2 - yy1);
-            const double wh = w * h;
-            const double o = wh / ((a[2] - a[0]) * (a[3] - a[1]) + (b[2] - b[0]) * (b[3] - b[1]) - wh);
-            iou[(size_t)d * nt + t] = o;
+            /* self.asso_func (utils/iou.py:50-307; iou by default) */
+            iou[(size_t)d * nt + t] = bxo_pair_cost(kind, a, b, fw, fh);
             /* speed_direction_batch (association.py:10-20) with the track's k-previous obs */
             const double *p = prev + 5 * t;
             const double cx1 = (a[0] + a[2]) / 2.0, cy1 = (a[1] + a[3]) / 2.0;
@@ -507,7 +505,7 @@ static void associate(const double *dets, int nd, const double *trks, int nt, do
             ang = (M_PI / 2.0 - fabs(ang)) / M_PI;
             const double valid = p[4] < 0 ? 0.0 : 1.0;
             const double mc = (valid * ang) * vdc_weight;
-            total[(size_t)d * nt + t] = o + mc;
+            total[(size_t)d * nt + t] = iou[(size_t)d * nt + t] + mc;
         }
     int *mi = (int *)malloc(sizeof(int) * 2 * (size_t)(nd < nt ? (nd ? nd : 1) : nt));
     int nmi = 0;
@@ -582,19 +580,13 @@ static int setdiff1d(int *a, int na, const int *b, int nb) {
     return n;
 }
 
-/* iou_batch of two small sets (rows a, cols b), [na][nb] */
-static void iou_small(const double *a, int sa, int na, const double *b, int sb, int nb,
-                      double *out) {
+/* self.asso_func of two small sets (rows a, cols b), [na][nb] */
+static void iou_small(const bxo_ocsort *o, const double *a, int sa, int na, const double *b,
+                      int sb, int nb, double *out) {
     for (int i = 0; i < na; i++)
-        for (int j = 0; j < nb; j++) {
-            const double *p = a + (size_t)sa * i, *q = b + (size_t)sb * j;
-            const double xx1 = fmax(p[0], q[0]), yy1 = fmax(p[1], q[1]);
-            const double xx2 = fmin(p[2], q[2]), yy2 = fmin(p[3], q[3]);
-            const double w = fmax(0.0, xx2 - xx1), h = fmax(0.0, yy2 - yy1);
-            const double wh = w * h;
+        for (int j = 0; j < nb; j++)
             out[(size_t)i * nb + j] =
-                wh / ((p[2] - p[0]) * (p[3] - p[1]) + (q[2] - q[0]) * (q[3] - q[1]) - wh);
-        }
+                bxo_pair_cost(o->asso_kind, a + (size_t)sa * i, b + (size_t)sb * j, o->fw, o->fh);
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -618,6 +610,13 @@ bxo_ocsort *bxo_ocsort_new(double min_conf, double det_thresh, int max_age, int 
     o->cap = 64;
     o->tr = (ocs_track *)malloc(sizeof(ocs_track) * o->cap);
     return o;
+}
+
+/* BaseTracker: asso_func chosen by name, h/w latched from the first image (basetracker.py:140-147) */
+void bxo_ocsort_set_asso(bxo_ocsort *o, int kind, double w, double h) {
+    o->asso_kind = kind;
+    o->fw = w;
+    o->fh = h;
 }
 
 void bxo_ocsort_free(bxo_ocsort *o) {
@@ -688,7 +687,7 @@ int bxo_ocsort_update(bxo_ocsort *o, const double *dets_in, int n, double *out, 
     int *matches = (int *)malloc(sizeof(int) * 2 * big), *ud = (int *)malloc(sizeof(int) * 2 * big);
     int *ut = (int *)malloc(sizeof(int) * 2 * big);
     int nm, nud, nut;
-    associate(hd5, nh, trks, nt, o->asso_threshold, vel, kobs, o->inertia, matches, &nm, ud, &nud,
+    associate(o->asso_kind, o->fw, o->fh, hd5, nh, trks, nt, o->asso_threshold, vel, kobs, o->inertia, matches, &nm, ud, &nud,
               ut, &nut);
     for (int q = 0; q < nm; q++) {
         const double *r = hi + 7 * matches[2 * q];
@@ -699,7 +698,7 @@ int bxo_ocsort_update(bxo_ocsort *o, const double *dets_in, int n, double *out, 
         double *ul = (double *)malloc(sizeof(double) * (size_t)nl * nut);
         double *utb = (double *)malloc(sizeof(double) * 5 * nut);
         for (int k = 0; k < nut; k++) memcpy(utb + 5 * k, trks + 5 * ut[k], sizeof(double) * 5);
-        iou_small(lo, 7, nl, utb, 5, nut, ul);
+        iou_small(o, lo, 7, nl, utb, 5, nut, ul);
         double mx = -INFINITY;
         for (int q = 0; q < nl * nut; q++) mx = ul[q] > mx ? ul[q] : mx;
         if (mx > o->asso_threshold) {
@@ -731,7 +730,7 @@ int bxo_ocsort_update(bxo_ocsort *o, const double *dets_in, int n, double *out, 
         for (int k = 0; k < nud; k++) memcpy(ld + 5 * k, hi + 7 * ud[k], sizeof(double) * 5);
         for (int k = 0; k < nut; k++) memcpy(lt + 5 * k, lastb + 5 * ut[k], sizeof(double) * 5);
         double *il = (double *)malloc(sizeof(double) * (size_t)nud * nut);
-        iou_small(ld, 5, nud, lt, 5, nut, il);
+        iou_small(o, ld, 5, nud, lt, 5, nut, il);
         double mx = -INFINITY;
         for (int q = 0; q < nud * nut; q++) mx = il[q] > mx ? il[q] : mx;
         if (mx > o->asso_threshold) {

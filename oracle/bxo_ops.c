@@ -15,6 +15,8 @@
 #include "bxo.h"
 #include "bxo_internal.h"
 
+#include <stdint.h>
+
 /* ------------------------------------------------------------------------------------------ */
 /* utils/ops.py:10-150 box conversions (numpy op order)                                        */
 
@@ -565,4 +567,133 @@ int bxo_nn_cosine_distance(const double *samples, const int *off, int T, const d
     free(sh);
     free(dh);
     return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* AssociationFunction variants (utils/iou.py:79-307), one pair per call; numpy op order.      */
+/* fdlibm s_atan.c (public-domain algorithm) for np.arctan in ciou. */
+static const double at_hi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,
+                                9.82793723247329054082e-01, 1.57079632679489655800e+00};
+static const double at_lo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17,
+                                1.39033110312309984516e-17, 6.12323399573676603587e-17};
+static const double aT[11] = {3.33333333333329318027e-01, -1.99999999998764832476e-01,
+                              1.42857142725034663711e-01, -1.11111104054623557880e-01,
+                              9.09088713343650656196e-02, -7.69187620504482999495e-02,
+                              6.66107313738753120669e-02, -5.83357013379057348645e-02,
+                              4.97687799461593236017e-02, -3.65315727442169155270e-02,
+                              1.62858201153657823623e-02};
+
+double bxo_atan(double x) {
+    uint64_t bits;
+    memcpy(&bits, &x, 8);
+    const int32_t hx = (int32_t)(bits >> 32);
+    const int32_t ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x44100000) {
+        if (ix > 0x7ff00000 || (ix == 0x7ff00000 && (uint32_t)bits != 0)) return x + x;
+        return hx > 0 ? at_hi[3] + at_lo[3] : -at_hi[3] - at_lo[3];
+    }
+    if (ix < 0x3fdc0000) {
+        if (ix < 0x3e200000) return x;
+        id = -1;
+    } else {
+        x = fabs(x);
+        if (ix < 0x3ff30000) {
+            if (ix < 0x3fe60000) {
+                id = 0;
+                x = (2.0 * x - 1.0) / (2.0 + x);
+            } else {
+                id = 1;
+                x = (x - 1.0) / (x + 1.0);
+            }
+        } else {
+            if (ix < 0x40038000) {
+                id = 2;
+                x = (x - 1.5) / (1.0 + 1.5 * x);
+            } else {
+                id = 3;
+                x = -1.0 / x;
+            }
+        }
+    }
+    const double z = x * x, w = z * z;
+    const double s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const double s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    const double r = at_hi[id] - ((x * (s1 + s2) - at_lo[id]) - x);
+    return hx < 0 ? -r : r;
+}
+
+static double npmax(double a, double b) { return (a != a || b != b) ? NAN : (a > b ? a : b); }
+static double npmin(double a, double b) { return (a != a || b != b) ? NAN : (a < b ? a : b); }
+
+double bxo_pair_cost(int kind, const double *a, const double *b, double w, double h) {
+    const double xx1 = npmax(a[0], b[0]), yy1 = npmax(a[1], b[1]);
+    const double xx2 = npmin(a[2], b[2]), yy2 = npmin(a[3], b[3]);
+    const double iw = npmax(0.0, xx2 - xx1), ih = npmax(0.0, yy2 - yy1);
+    const double wh = iw * ih;
+    const double area1 = (a[2] - a[0]) * (a[3] - a[1]), area2 = (b[2] - b[0]) * (b[3] - b[1]);
+    switch (kind) {
+    case BXO_ASSO_IOU: /* :50-67 */
+        return wh / (area1 + area2 - wh);
+    case BXO_ASSO_HMIOU: { /* :79-127 */
+        const double uh = npmax(1e-10, npmax(a[3], b[3]) - npmin(a[1], b[1]));
+        const double o = ih / uh;
+        const double iou = wh / ((area1 + area2 - wh) + 1e-10);
+        return iou * o;
+    }
+    case BXO_ASSO_GIOU: { /* :129-169 */
+        const double uni = area1 + area2 - wh;
+        const double iou = wh / uni;
+        const double wc = npmax(a[2], b[2]) - npmin(a[0], b[0]);
+        const double hc = npmax(a[3], b[3]) - npmin(a[1], b[1]);
+        const double enc = wc * hc;
+        const double g = iou - (enc - uni) / enc;
+        return (g + 1.0) / 2.0;
+    }
+    case BXO_ASSO_DIOU: { /* :266-307 */
+        const double iou = wh / (area1 + area2 - wh);
+        const double cx1 = (a[0] + a[2]) / 2.0, cy1 = (a[1] + a[3]) / 2.0;
+        const double cx2 = (b[0] + b[2]) / 2.0, cy2 = (b[1] + b[3]) / 2.0;
+        const double inner = (cx1 - cx2) * (cx1 - cx2) + (cy1 - cy2) * (cy1 - cy2);
+        const double ow = npmax(a[2], b[2]) - npmin(a[0], b[0]);
+        const double oh = npmax(a[3], b[3]) - npmin(a[1], b[1]);
+        const double outer = ow * ow + oh * oh;
+        return ((iou - inner / outer) + 1) / 2.0;
+    }
+    case BXO_ASSO_CIOU: { /* :199-264 */
+        const double eps = 1e-7;
+        const double iou = wh / (((area1 + area2) - wh) + eps);
+        const double cx1 = (a[0] + a[2]) / 2.0, cy1 = (a[1] + a[3]) / 2.0;
+        const double cx2 = (b[0] + b[2]) / 2.0, cy2 = (b[1] + b[3]) / 2.0;
+        const double inner = (cx1 - cx2) * (cx1 - cx2) + (cy1 - cy2) * (cy1 - cy2);
+        const double ow = npmax(a[2], b[2]) - npmin(a[0], b[0]);
+        const double oh = npmax(a[3], b[3]) - npmin(a[1], b[1]);
+        const double outer = (ow * ow + oh * oh) + eps;
+        const double w1 = a[2] - a[0], h1 = (a[3] - a[1]) + eps;
+        const double w2 = b[2] - b[0], h2 = (b[3] - b[1]) + eps;
+        const double d = bxo_atan(w2 / h2) - bxo_atan(w1 / h1);
+        const double pi = 3.141592653589793;
+        const double v = (4 / (pi * pi)) * (d * d);
+        const double S = 1 - iou;
+        const double alpha = v / ((S + v) + eps);
+        const double c = (iou - (inner / outer)) + (alpha * v);
+        return (c + 1) / 2.0;
+    }
+    case BXO_ASSO_CENTROID: { /* :171-184 */
+        const double cx1 = (a[0] + a[2]) / 2, cy1 = (a[1] + a[3]) / 2;
+        const double cx2 = (b[0] + b[2]) / 2, cy2 = (b[1] + b[3]) / 2;
+        const double dx = cx1 - cx2, dy = cy1 - cy2;
+        const double dist = sqrt(dx * dx + dy * dy);
+        const double nf = sqrt(w * w + h * h);
+        return 1 - dist / nf;
+    }
+    }
+    return NAN;
+}
+
+void bxo_asso_batch(int kind, const double *a, int na, const double *b, int nb, double w,
+                    double h, double *out) {
+    for (int i = 0; i < na; i++)
+        for (int j = 0; j < nb; j++) out[(size_t)i * nb + j] = bxo_pair_cost(kind, a + 4 * i, b + 4 * j, w, h);
 }

@@ -128,6 +128,7 @@ def lib():
                                      C.c_int, C.c_double, C.c_int, C.c_double, C.c_double]
         L.bxo_ocsort_new.restype = C.c_void_p
         L.bxo_ocsort_free.argtypes = [C.c_void_p]
+        L.bxo_ocsort_set_asso.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double]
         L.bxo_ocsort_id_count.argtypes = [C.c_void_p]
         L.bxo_ocsort_update.argtypes = [C.c_void_p, _dp, C.c_int, _dp, C.c_int]
         L.bxo_ocsort_tracks.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -153,6 +154,10 @@ def lib():
         L.bxo_ss_update.argtypes = [C.c_void_p, _dp, C.c_int, C.c_void_p, C.c_int, _dp, _dp,
                                     C.c_int]
         L.bxo_lsap.argtypes = [_dp, C.c_int, C.c_int, _ip, _ip]
+        L.bxo_asso_batch.argtypes = [C.c_int, _dp, C.c_int, _dp, C.c_int, C.c_double,
+                                     C.c_double, _dp]
+        L.bxo_atan.argtypes = [C.c_double]
+        L.bxo_atan.restype = C.c_double
         L.bxo_exp.argtypes = [C.c_double]
         L.bxo_exp.restype = C.c_double
         L.bxo_pow15.argtypes = [C.c_double]
@@ -170,6 +175,19 @@ def iou_batch(a, b):
     b = np.ascontiguousarray(b, np.float64).reshape(-1, 4)
     out = np.zeros((a.shape[0], b.shape[0]))
     lib().bxo_iou_batch(_d(a), a.shape[0], _d(b), b.shape[0], _d(out))
+    return out
+
+
+ASSO_KIND = {"iou": 0, "hmiou": 1, "giou": 2, "diou": 3, "ciou": 4, "centroid": 5}
+
+
+def asso_batch(kind, a, b, w=1920, h=1080):
+    """AssociationFunction.<kind>_batch (utils/iou.py) restated."""
+    a = np.ascontiguousarray(a, np.float64).reshape(-1, 4)
+    b = np.ascontiguousarray(b, np.float64).reshape(-1, 4)
+    out = np.zeros((a.shape[0], b.shape[0]))
+    lib().bxo_asso_batch(ASSO_KIND[kind], _d(a), a.shape[0], _d(b), b.shape[0], float(w),
+                         float(h), _d(out))
     return out
 
 
@@ -273,8 +291,10 @@ class OracleTracker:
                 int(p.get("min_hits", 3)), p.get("asso_threshold", 0.3), int(p.get("delta_t", 3)),
                 p.get("inertia", 0.1), int(bool(p.get("use_byte", False))),
                 p.get("Q_xy_scaling", 0.01), p.get("Q_s_scaling", 0.0001))
-            if p.get("asso_func", "iou") != "iou":
-                raise NotImplementedError("oracle OCSort: asso_func 'iou' only")
+            # asso_func (utils/iou.py registry); centroid normalises by the fixtures' 1920x1080
+            # frame (make_golden.run_tracker's image), overridable with frame_w / frame_h
+            L.bxo_ocsort_set_asso(self.h, ASSO_KIND[p.get("asso_func", "iou")],
+                                  float(p.get("frame_w", 1920)), float(p.get("frame_h", 1080)))
         elif kind == "boosttrack":
             self._bp = boost_params(**p)
             self.h = L.bxo_boost_new(C.byref(self._bp))

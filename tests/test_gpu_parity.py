@@ -50,6 +50,39 @@ def host(t):
 
 
 # ------------------------------------------------------------------------------- op level
+@pytest.mark.parametrize("mode", ["iou", "hmiou", "giou", "diou", "ciou", "centroid"])
+def test_pairwise_cost_registry(torch_cuda, mode):
+    """bx_pairwise_cost vs the reference's vectors (utils/iou.py:79-307) and, bit for bit, vs
+    the oracle — on the golden boxes, on strided rows (lda 6 / ldb 9: dets carry conf/cls)
+    and at C4 size 1024 x 512."""
+    torch = torch_cuda
+    from boxmot_amd.iou import AssociationFunction, pairwise_cost
+
+    g = np.load(GOLDEN / "asso_funcs.npz")
+    af = AssociationFunction(int(g["w"]), int(g["h"]), mode)
+    for which in ("rand", "edge"):
+        a, b = g[f"{which}_a"], g[f"{which}_b"]
+        got = af.asso_func(a, b)
+        np.testing.assert_array_equal(got, po.asso_batch(mode, a, b, int(g["w"]), int(g["h"])))
+        ref = g[f"{mode}_{which}"]
+        if mode == "ciou":  # np.arctan vs fdlibm atan: <= 1 ulp
+            np.testing.assert_allclose(got, ref, rtol=0, atol=4e-16)
+        else:
+            np.testing.assert_array_equal(got, ref)
+    rng = np.random.default_rng(11)
+    c = rng.uniform(0, 1900, (1024, 2))
+    sz = rng.uniform(8, 200, (1024, 2))
+    A = np.concatenate([c - sz / 2, c + sz / 2, rng.uniform(0, 1, (1024, 2))], 1)
+    B = np.concatenate([A[:512, :4] + rng.normal(0, 6, (512, 4)), np.zeros((512, 5))], 1)
+    ad = torch.from_numpy(A).cuda()
+    bd = torch.from_numpy(B).cuda()
+    out = pairwise_cost(mode, ad, bd, 1920, 1080)
+    assert out.is_cuda and out.shape == (1024, 512)
+    np.testing.assert_array_equal(host(out), po.asso_batch(mode, A[:, :4], B[:, :4], 1920, 1080))
+    empty = pairwise_cost(mode, np.zeros((0, 4)), B[:, :4], 1920, 1080)
+    assert empty.shape == (0, 512)
+
+
 def test_iou_fuse_embedding_exact(torch_cuda, K):
     torch = torch_cuda
     from boxmot_amd import _native as N
@@ -398,7 +431,8 @@ OCS_ARGS = dict(min_conf=0.1, det_thresh=0.6, max_age=30, min_hits=3, asso_thres
                 delta_t=3, inertia=0.1, use_byte=False, Q_xy_scaling=0.01, Q_s_scaling=0.0001)
 
 
-@pytest.mark.parametrize("variant", ["default", "byte", "short_age"])
+@pytest.mark.parametrize("variant", ["default", "byte", "short_age", "giou", "diou_byte", "ciou",
+                                     "hmiou", "centroid"])
 def test_ocsort_batched_vs_oracle(torch_cuda, variant):
     """Several sequences per launch (grid / crowded layouts, low-confidence detections, missed
     detections -> ORU re-updates, deaths) against the oracle, outputs and KF state bitwise."""
@@ -409,6 +443,12 @@ def test_ocsort_batched_vs_oracle(torch_cuda, variant):
         args.update(use_byte=True, det_thresh=0.5)
     if variant == "short_age":
         args.update(max_age=5, min_hits=1, delta_t=1, inertia=0.3)
+    if variant in ("giou", "ciou", "hmiou"):
+        args.update(asso_func=variant)
+    if variant == "diou_byte":
+        args.update(asso_func="diou", use_byte=True, det_thresh=0.5)
+    if variant == "centroid":  # 1 - distance / frame diagonal: a threshold near 1
+        args.update(asso_func="centroid", asso_threshold=0.95, frame_w=1280, frame_h=720)
     scenes = [SyntheticScene(n_obj=12 + 9 * s, seed=300 + s,
                              layout="crowded" if s % 2 else "grid", p_det=0.35 + 0.1 * (s % 3),
                              conf_lo=0.2 if s % 3 == 0 else 0.55) for s in range(6)]

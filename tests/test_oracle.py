@@ -187,3 +187,42 @@ def test_nn_cosine_distance_vs_reference(case):
     np.testing.assert_allclose(got, ref, rtol=0, atol=1e-13)
     empty = np.diff(off) == 0
     assert empty.any() and np.all(got[empty] == 1e5) and np.all(ref[empty] == 1e5)
+
+
+# ----------------------------------------------------------- AssociationFunction registry
+ASSO_MODES = ("iou", "hmiou", "giou", "diou", "ciou", "centroid")
+
+
+@pytest.mark.parametrize("mode", ASSO_MODES)
+@pytest.mark.parametrize("which", ["rand", "edge"])
+def test_asso_funcs_match_reference(mode, which):
+    """utils/iou.py:79-307 restated: bit-exact except ciou, whose np.arctan (libm) and the
+    restated fdlibm atan may differ by 1 ulp (tolerance 4e-16 absolute on a [0,1] score)."""
+    g = np.load(GOLDEN / "asso_funcs.npz")
+    got = po.asso_batch(mode, g[f"{which}_a"], g[f"{which}_b"], int(g["w"]), int(g["h"]))
+    ref = g[f"{mode}_{which}"]
+    if mode == "ciou":
+        np.testing.assert_allclose(got, ref, rtol=0, atol=4e-16)
+    else:
+        np.testing.assert_array_equal(got, ref)
+
+
+def test_asso_unknown_mode_raises():
+    from boxmot_amd.iou import AssociationFunction
+
+    assert int(np.load(GOLDEN / "asso_funcs.npz")["unknown_raises"]) == 1
+    with pytest.raises(ValueError):
+        AssociationFunction(1920, 1080, "nope")
+    with pytest.raises(NotImplementedError):
+        AssociationFunction(1920, 1080, "iou_obb")
+    af = AssociationFunction(1920, 1080, "centroid")
+    assert af.asso_func == af.centroid_batch
+
+
+def test_atan_restatement_within_one_ulp():
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([rng.uniform(-4, 4, 4000), rng.uniform(-300, 300, 2000),
+                         [0.0, 1.0, -1.0, 0.4375, 1.1875, 2.4375, 1e-30, 1e30, -1e30]])
+    got = np.array([po.lib().bxo_atan(float(x)) for x in xs])
+    ref = np.arctan(xs)
+    assert np.all(np.abs(got - ref) <= np.spacing(np.abs(ref)))
