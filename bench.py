@@ -136,7 +136,13 @@ def ss_stage_bytes(stage, u, F):
         # the feature row of each lost track and the detection rows
         "recovery": u["dets"] * F * 8,
         # track records (mean, cov, histories: ~1.2 kB) read + written, detection rows
-        "frame": u["tracks"] * 2 * 1200 + u["dets"] * 64 + u["outputs"] * 80,
+        "match": u["tracks"] * 2 * 1200 + u["dets"] * 64,
+        # per match: the detection's normalised row and the last feature read, the new vector
+        # written (then read back twice for its norms), the track record read + written
+        "update": u["matches"] * (5 * F * 8 + 2 * 1200),
+        "post": u["tracks"] * 1200 + u["outputs"] * 80,
+        # per listed track: its gallery entries (<= budget + 10 of 16 B) read + written
+        "fit": u["tracks"] * 2 * 160 * 16,
     }[stage]
 
 

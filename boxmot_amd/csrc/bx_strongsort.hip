@@ -7,7 +7,7 @@
 // NearestNeighborDistanceMetric), sort/iou_matching.py:10-87, utils/occlusion_handler.py:45-87,
 // 464-490 (detect_crowd_situations).  With P6 and handle_occlusions=False.
 //
-// Per frame, four launches on the caller's stream:
+// Per frame, seven launches on the caller's stream:
 //   ss_prep_kernel   wave per detection: the feature's wave-order norm (quality; BLAS order of
 //                    the reference unpinned), its numpy pairwise norm, the NN-normalised row
 //                    feat/(‖·‖₂+1e-8) and the track-feature row feat/(‖·‖_wave+1e-8) with its
@@ -17,12 +17,15 @@
 //                    contraction on the fp64 matrix cores (v_mfma_f64_16x16x4f64, ascending-k
 //                    chain = the oracle's fma chain), max over rows by wave shuffles
 //   ss_rec_kernel    wave per (lost track, detection): ID-recovery cosine similarity
-//   ss_frame_kernel  one wave per sequence: crowd mode, CMC warp, detection quality + stable
+//   ss_match_kernel  one wave per sequence: crowd mode, CMC warp, detection quality + stable
 //                    sort, Kalman predict, the matching cascade (gating, motion/quality cost
 //                    shaping lane per track row, scipy's linear_sum_assignment restated
-//                    wave-parallel), the IoU stage, Kalman + feature updates (feature vectors
-//                    built wave-cooperatively), misses, ID recovery, births, lost buffer,
-//                    partial_fit budget pruning (lane per track), outputs
+//                    wave-parallel), the IoU stage, misses
+//   ss_update_kernel wave per match: Kalman update, feature EMA vector + norms, track scalars
+//   ss_post_kernel   one wave per sequence: ID recovery, births (lane per birth), lost buffer,
+//                    output rows
+//   ss_fit_kernel    wave per listed / lost track: partial_fit (append + budget truncation by
+//                    rank in LDS), pool bookkeeping, the next frame's gallery queries
 // Every floating-point expression restates oracle/bxo_strongsort.c operation for operation.
 //
 // Track state lives in HBM: SsTrk slots, each with a private pool of `vec_cap` feature vectors
@@ -57,7 +60,10 @@ struct SsTrk {
   double confh[MAXC];
   int id, state, hits, age, tsu, max_age, n_init;
   int nvel, npos, nconf, nfeat, missed, confirmed_det, low_streak, high_streak, lost_frame;
-  int gal_n, gal_sp;          // gallery length, its sorted prefix (partial_fit's last sort)
+  int gal_n;                 // gallery length (entries in no particular order, see ss_fit_kernel)
+  int gal_clock;             // partial_fit append counter: the entries' insertion times
+  int born_dk;               // input detection of this frame's birth (first vector copied by
+                             // ss_fit_kernel), else -1
   int feat[MAXF];
   unsigned long long vmask;  // pool entries in use (features or gallery)
   unsigned long long gmask;  // pool entries referenced by the gallery
@@ -65,7 +71,9 @@ struct SsTrk {
 
 enum {
   Q_FRAME = 0, Q_NEXTID, Q_NTR, Q_NLOST, Q_CROWD, Q_ORIG, Q_OMAXAGE, Q_OBUDGET, Q_MAXAGE,
-  Q_BUDGET, Q_HIST, Q_NNL, Q_NK, Q_NT0, Q_NOUT, Q_ROWS, Q_ROWSL, SQS
+  Q_BUDGET, Q_HIST, Q_NNL, Q_NK, Q_NT0, Q_NOUT, Q_ROWS, Q_ROWSL,
+  Q_NM, Q_NAUD, Q_FID, Q_ANYF, Q_NFUT, Q_NDUP,  // handed from ss_match_kernel / ss_post_kernel to the next launch
+  SQS
 };
 
 struct SsDev {
@@ -75,6 +83,7 @@ struct SsDev {
   SsTrk* trk;     // [S][T]
   int* gal_v;     // [S][T][GB] pool index
   double* gal_q;  // [S][T][GB] sample quality (wave norm)
+  int* gal_t;     // [S][T][GB] insertion time (the reference list's order among equal qualities)
   double* vec;    // [S][T][VP][F]
   double* vden;   // [S][T][VP] numpy pairwise norm + 1e-8 (NN sample normalisation)
   double* vwn;    // [S][T][VP] wave-order norm
@@ -89,13 +98,46 @@ struct SsDev {
   double* nf;     // [S][D][F] feat / (wave norm + 1e-8)
   double* recsim; // [S][LOSTN][D]
   double* cost;   // [S][2T*D] scratch cost matrices
-  int* gcnt;      // [S][T][VP] gallery references per pool entry
+  double* fdt;    // [S][D][DTW] this frame's detection table (kept across the frame's launches)
+  int* fdord;     // [S][D] detections in quality order
+  int* faud;      // [S][D] unmatched detections after the three stages
+  int* fmt;       // [S][4(D+2)] matches (track list position, sorted detection)
+  int* ffut;      // [S][3T] unmatched track positions (duplicates kept: mark_missed per entry)
   int* wsi;       // [S][WSI] int scratch
   double* wsd;    // [S][WSD] double scratch
   int wsi_n, wsd_n;
   int ws_lds;     // 1: the frame kernel's workspace lives in LDS
   int* status;
+  unsigned long long* dbg;  // [S][SS_DBG] phase stamps (diagnostic builds only, else null)
 };
+
+// Diagnostic phase stamps and counters (build with -DBX_PHASE_TIMING; never shipped): per
+// sequence, cycles accumulated per phase [0, 16), sub-phase cycles / counters [16, 32).
+constexpr int SS_DBG = 32;
+#ifdef BX_PHASE_TIMING
+#define SSTAMP(k)                                                                    \
+  do {                                                                               \
+    __syncthreads();                                                                 \
+    if (threadIdx.x == 0 && g.dbg) {                                                 \
+      const unsigned long long _now = __builtin_amdgcn_s_memtime();                  \
+      g.dbg[(size_t)seq * SS_DBG + (k)] += _now - t_last;                            \
+      t_last = _now;                                                                 \
+    }                                                                                \
+  } while (0)
+#define SCOUNT(k, v)                                                                 \
+  do {                                                                               \
+    if (threadIdx.x == 0 && g.dbg) g.dbg[(size_t)seq * SS_DBG + 16 + (k)] += (v);    \
+  } while (0)
+#define SS_NOW() __builtin_amdgcn_s_memtime()
+#else
+#define SSTAMP(k) \
+  do {            \
+  } while (0)
+#define SCOUNT(k, v) \
+  do {               \
+  } while (0)
+#define SS_NOW() 0ull
+#endif
 
 __device__ __forceinline__ double* vecp(const SsDev& g, int seq, int slot, int v) {
   return g.vec + ((((size_t)seq * g.T + slot) * g.VP + v) * (size_t)g.F);
@@ -406,20 +448,29 @@ __device__ int pool_alloc(SsTrk& t, int VP) {
 struct SsWs {
   // ints
   int *lst, *conf_t, *unconf_t, *aut, *cand, *ut3, *fut, *hi, *med, *lo, *aud, *rd, *ud, *ud2;
-  int *lvl, *ages, *mt, *tmp, *rows, *cols, *flag, *ti2, *dord;
+  int *lvl, *ages, *mt, *tmp, *rows, *cols, *flag, *ti2, *dord;  // mt, dord, aud: HBM (fmt..)
   int *path, *col4row, *row4col, *rem, *SR, *SC, *pwlo, *pwln, *sc;
   // doubles
   double *dt, *u, *v, *spc, *meas, *key, *pwleaf, *sd;
 };
 
 int ws_ints(int T, int D, int N) {
-  return T /*lst*/ + T + T + T + 2 * T /*cand*/ + 2 * T /*ut3*/ + 3 * T /*fut*/ + 3 * D + D /*aud*/ +
-         D /*rd*/ + 2 * (D + 2 * T) /*ud ud2*/ + T /*lvl*/ + T /*ages*/ + 4 * (D + 2) /*mt*/ +
+  return T /*lst*/ + T + T + T + 2 * T /*cand*/ + 2 * T /*ut3*/ + 3 * D +
+         D /*rd*/ + 2 * (D + 2 * T) /*ud ud2*/ + T /*lvl*/ + T /*ages*/ +
          2 * (T + D) /*tmp*/ + 2 * N /*rows cols*/ + 2 * T /*flag*/ + 2 * T /*ti2*/ +
-         6 * N + 2 * PW_MAXLEAF + 32 + D /*dord*/;
+         6 * N + 2 * PW_MAXLEAF + 32;
 }
 int ws_doubles(int T, int D, int N) {
-  return D * DTW + 3 * N + 4 * D + 2 * T + PW_MAXLEAF + 8;
+  return 3 * N + 4 * D + 2 * T + PW_MAXLEAF + 8;
+}
+
+// the per-frame tables that outlive one launch (match -> update -> post) live in HBM
+__device__ void ws_frame(const SsDev& g, int seq, SsWs& w) {
+  w.dt = g.fdt + (size_t)seq * g.D * DTW;
+  w.dord = g.fdord + (size_t)seq * g.D;
+  w.aud = g.faud + (size_t)seq * g.D;
+  w.mt = g.fmt + (size_t)seq * 4 * (g.D + 2);
+  w.fut = g.ffut + (size_t)seq * 3 * g.T;
 }
 
 __device__ void ws_carve(const SsDev& g, int seq, SsWs& w, char* lds) {
@@ -433,12 +484,13 @@ __device__ void ws_carve(const SsDev& g, int seq, SsWs& w, char* lds) {
   auto I = [&](int n) { int* p = pi; pi += n; return p; };
   auto Dd = [&](int n) { double* p = pd; pd += n; return p; };
   w.lst = I(T); w.conf_t = I(T); w.unconf_t = I(T); w.aut = I(T); w.cand = I(2 * T);
-  w.ut3 = I(2 * T); w.fut = I(3 * T); w.hi = I(D); w.med = I(D); w.lo = I(D); w.aud = I(D);
+  w.ut3 = I(2 * T); w.hi = I(D); w.med = I(D); w.lo = I(D);
   w.rd = I(D); w.ud = I(D + 2 * T); w.ud2 = I(D + 2 * T); w.lvl = I(T); w.ages = I(T);
-  w.mt = I(4 * (D + 2)); w.tmp = I(2 * (T + D)); w.rows = I(N); w.cols = I(N); w.flag = I(2 * T);
+  w.tmp = I(2 * (T + D)); w.rows = I(N); w.cols = I(N); w.flag = I(2 * T);
   w.ti2 = I(2 * T); w.path = I(N); w.col4row = I(N); w.row4col = I(N); w.rem = I(N); w.SR = I(N);
-  w.SC = I(N); w.pwlo = I(PW_MAXLEAF); w.pwln = I(PW_MAXLEAF); w.sc = I(32); w.dord = I(D);
-  w.dt = Dd(D * DTW); w.u = Dd(N); w.v = Dd(N); w.spc = Dd(N); w.meas = Dd(4 * D);
+  w.SC = I(N); w.pwlo = I(PW_MAXLEAF); w.pwln = I(PW_MAXLEAF); w.sc = I(32);
+  ws_frame(g, seq, w);
+  w.u = Dd(N); w.v = Dd(N); w.spc = Dd(N); w.meas = Dd(4 * D);
   w.key = Dd(2 * T); w.pwleaf = Dd(PW_MAXLEAF); w.sd = Dd(8);
 }
 
@@ -697,6 +749,9 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int nr, int nc) {
       }
       nrem--;
       __syncthreads();
+#ifdef BX_PHASE_TIMING
+      if (threadIdx.x == 0 && x.g.dbg) x.g.dbg[(size_t)x.seq * SS_DBG + 16 + 5] += 1;
+#endif
     }
     for (int q = lane; q < R; q += 64)
       if (q == cur)
@@ -759,6 +814,11 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
     return;
   }
   double* C = g.cost + (size_t)x.seq * 2 * g.T * g.D;
+#ifdef BX_PHASE_TIMING
+  const int seq = x.seq;
+  __syncthreads();
+  unsigned long long t0 = SS_NOW();
+#endif
   if (kind == M_GATED) {
     for (int c = lane; c < nd; c += 64) det_xyah(x.det(di[c]), w.meas + 4 * c);
     __syncthreads();
@@ -850,7 +910,18 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
     }
   }
   __syncthreads();
+#ifdef BX_PHASE_TIMING
+  unsigned long long t1 = SS_NOW();
+  SCOUNT(0, t1 - t0);
+  SCOUNT(2, 1);
+  SCOUNT(3, nt);
+  SCOUNT(4, nd);
+#endif
   const int np_ = lsap_wave(x, C, nt, nd);
+#ifdef BX_PHASE_TIMING
+  __syncthreads();
+  SCOUNT(1, SS_NOW() - t1);
+#endif
   // assigned flags (w.SR rows, w.SC columns), unmatched in index order, then the rejected pairs
   for (int r = lane; r < nt; r += 64) w.SR[r] = 0;
   for (int c = lane; c < nd; c += 64) w.SC[c] = 0;
@@ -999,89 +1070,63 @@ __device__ void track_update(SsCtx& x, int slot, int di) {
   __syncthreads();
 }
 
-// Track.__init__ (track.py:76-131) into a free slot; the detection's feature, normalised as the
-// reference normalises it in place, is the first feature vector.
-__device__ void track_birth(SsCtx& x, int slot, int di) {
+// Track.__init__ (track.py:76-131) into a free slot, by one lane (births run lane-parallel).
+// The detection's feature, normalised as the reference normalises it in place, becomes pool
+// entry 0; ss_fit_kernel copies the vector (born_dk), nothing reads it earlier in the frame.
+__device__ void track_birth(SsCtx& x, int slot, int di, int id) {
   const SsDev& g = x.g;
-  const int lane = x.lane, F = g.F;
   SsTrk& t = x.trk[slot];
   const double* d = x.det(di);
   const int dk = x.det_in(di);
-  if (lane == 0) {
-    double bb[4];
-    det_xyah(d, bb);
-    t.id = x.sq[Q_NEXTID]++;
-    t.conf = d[4], t.cls = d[5], t.det_ind = d[6];
-    t.hits = 1, t.age = 1, t.tsu = 0;
-    t.base_alpha = g.ema_alpha;
-    t.state = g.born ? 2 : 1;
-    t.confh[0] = d[4];
-    t.nconf = 1;
-    t.n_init = g.n_init;
-    t.max_age = x.sq[Q_MAXAGE];
-    t.quality = d[7];
-    t.stability = 0.0;
-    t.app_cons = 1.0;
-    t.motion_cons = 1.0;
-    t.nvel = t.npos = 0;
-    t.missed = 0;
-    t.confirmed_det = 1;
-    t.low_streak = 0;
-    t.high_streak = d[4] > 0.7 ? 1 : 0;
-    t.lost_frame = 0;
-    t.gal_n = 0;
-    t.gal_sp = 0;
-    t.gmask = 0ull;
-    t.nfeat = 0;
-    t.vmask = 1ull;  // pool entry 0 holds the first feature
-    kf_initiate(KIND_BYTE, bb, t.mean, t.cov);
-    push2(t.pos, t.npos, bb);
-    t.feat[0] = 0;
-    t.nfeat = 1;
-    const size_t vi = vidx(g, x.seq, slot, 0);
-    const double* pr = g.dprep + ((size_t)x.seq * g.D + dk) * 4;
-    g.vwn[vi] = pr[2];
-    g.vden[vi] = pr[3];
-  }
-  const double* nf = g.nf + ((size_t)x.seq * g.D + dk) * F;
-  double* dst = vecp(g, x.seq, slot, 0);
-  for (int q = lane; q < F; q += 64) dst[q] = nf[q];
-  for (int q = lane; q < g.VP; q += 64) g.gcnt[vidx(g, x.seq, slot, q)] = 0;
-  __syncthreads();
+  double bb[4];
+  det_xyah(d, bb);
+  t.id = id;
+  t.conf = d[4], t.cls = d[5], t.det_ind = d[6];
+  t.hits = 1, t.age = 1, t.tsu = 0;
+  t.base_alpha = g.ema_alpha;
+  t.state = g.born ? 2 : 1;
+  t.confh[0] = d[4];
+  t.nconf = 1;
+  t.n_init = g.n_init;
+  t.max_age = x.sq[Q_MAXAGE];
+  t.quality = d[7];
+  t.stability = 0.0;
+  t.app_cons = 1.0;
+  t.motion_cons = 1.0;
+  t.nvel = t.npos = 0;
+  t.missed = 0;
+  t.confirmed_det = 1;
+  t.low_streak = 0;
+  t.high_streak = d[4] > 0.7 ? 1 : 0;
+  t.lost_frame = 0;
+  t.gal_n = 0;
+  t.gal_clock = 0;
+  t.gmask = 0ull;
+  t.vmask = 1ull;  // pool entry 0 holds the first feature
+  t.born_dk = dk;
+  kf_initiate(KIND_BYTE, bb, t.mean, t.cov);
+  push2(t.pos, t.npos, bb);
+  t.feat[0] = 0;
+  t.nfeat = 1;
+  const size_t vi = vidx(g, x.seq, slot, 0);
+  const double* pr = g.dprep + ((size_t)x.seq * g.D + dk) * 4;
+  g.vwn[vi] = pr[2];
+  g.vden[vi] = pr[3];
 }
 
-// partial_fit's budget prune for one gallery (one lane): samples_with_quality.sort(reverse=True)
-// [:keep] — a stable sort by quality descending, done as an insertion sort over the unsorted
-// tail [sp, n) (the prefix is sorted since the last prune), then truncation; gallery reference
-// counts and the gallery mask follow the dropped entries.
-__device__ void gal_prune(SsTrk& t, int* gv, double* gq, int* cnt, int keep) {
-  const int n = t.gal_n;
-  for (int i = t.gal_sp > 1 ? t.gal_sp : 1; i < n; i++) {
-    const int v = gv[i];
-    const double q = gq[i];
-    int j = i - 1;
-    while (j >= 0 && gq[j] < q) {
-      gv[j + 1] = gv[j];
-      gq[j + 1] = gq[j];
-      j--;
-    }
-    gv[j + 1] = v;
-    gq[j + 1] = q;
-  }
-  for (int k = keep; k < n; k++)
-    if (--cnt[gv[k]] == 0) t.gmask &= ~(1ull << gv[k]);
-  t.gal_n = n > keep ? keep : n;
-  t.gal_sp = t.gal_n;
-}
-
+// ss_match_kernel (one wave per sequence): detections, crowd mode, CMC warp, quality + stable
+// sort, Kalman predict, the three matching stages and the misses.  Hands the matches (fmt), the
+// unmatched detections (faud) and the frame's detection table (fdt) to the next launches.
 __global__ void __launch_bounds__(64)
-    ss_frame_kernel(SsDev g, int seq0, const double* __restrict__ dets,
-                    const int* __restrict__ det_off, const double* __restrict__ warps,
-                    double* __restrict__ out, int* __restrict__ out_count) {
+    ss_match_kernel(SsDev g, int seq0, const double* __restrict__ dets,
+                    const int* __restrict__ det_off, const double* __restrict__ warps) {
   extern __shared__ __align__(16) char ss_lds[];
   const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
   SsWs w;
   ws_carve(g, seq, w, ss_lds);
+#ifdef BX_PHASE_TIMING
+  unsigned long long t_last = SS_NOW();
+#endif
   SsCtx x{g, w, seq, lane, g.trk + (size_t)seq * g.T, g.sq + (size_t)seq * SQS,
           g.sqd + (size_t)seq * 2, g.lost + (size_t)seq * LOSTN, 0, 0, 0, 0};
   int* sq = x.sq;
@@ -1112,6 +1157,7 @@ __global__ void __launch_bounds__(64)
         w.dord[p] = p;
       });
   int fid = frame;
+  SSTAMP(0);
   if (x.nk == 0) {
     for (int p = lane; p < x.ntr; p += 64) track_predict(x.trk[w.lst[p]]);
     __syncthreads();
@@ -1159,6 +1205,7 @@ __global__ void __launch_bounds__(64)
       }
       __syncthreads();
     }
+    SSTAMP(1);
     if (x.ntr >= 1) {
       double wm[6] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0};
       if (warps)
@@ -1185,6 +1232,7 @@ __global__ void __launch_bounds__(64)
     __syncthreads();
   }
   if (!fid) fid = sq[Q_HIST];
+  SSTAMP(2);
 
   // ---- Tracker._enhanced_match (tracker.py:183-281, P6) --------------------------------------
   x.nm = 0;
@@ -1204,12 +1252,14 @@ __global__ void __launch_bounds__(64)
   for (int k = lane; k < x.nk; k += 64) w.aud[k] = k;
   __syncthreads();
   const double thr = x.sqd[0];
+  SSTAMP(3);
   if (nhi && ncf) {  // stage 1: high-confidence detections, confirmed tracks
     const int m0 = x.nm;
     matching_cascade(x, thr * 0.8, w.conf_t, ncf, w.hi, nhi);
     naut = filter_matched(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp);
     naud = filter_matched(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp);
   }
+  SSTAMP(4);
   {  // stage 2: medium-confidence detections, remaining confirmed tracks
     const int nrt = wave_compact(naut, [&](int k) { return in_list(w.conf_t, ncf, w.aut[k]); },
                                  [&](int k, int q) { w.ti2[q] = w.aut[k]; });
@@ -1222,6 +1272,7 @@ __global__ void __launch_bounds__(64)
       naud = filter_matched(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp);
     }
   }
+  SSTAMP(5);
   // stage 3: IoU on unconfirmed (= non-tentative) + unmatched with time_since_update == 1
   int ncand = nun;
   for (int k = lane; k < nun; k += 64) w.cand[k] = w.unconf_t[k];
@@ -1243,11 +1294,115 @@ __global__ void __launch_bounds__(64)
   for (int k = lane; k < nut3; k += 64) w.fut[nfut + k] = w.ut3[k];
   nfut += nut3;
   __syncthreads();
+  SSTAMP(6);
 
-  // ---- updates, misses (tracker.py:139-145) ---------------------------------------------------
-  for (int q = 0; q < x.nm; q++) track_update(x, w.lst[w.mt[2 * q]], w.mt[2 * q + 1]);
-  for (int k = lane; k < nfut; k += 64) track_missed(x.trk[w.lst[w.fut[k]]]);
+  // the matched tracks' updates are ss_update_kernel's, the misses follow them (ss_post_kernel):
+  // a track listed twice among stage 3's candidates can be both matched and missed, and
+  // mark_missed must see the updated time_since_update (tracker.py:139-145)
+  // a track listed twice among stage 3's candidates can also be matched twice: the reference
+  // updates it twice, in match order.  Later occurrences are flagged (negative position) and
+  // listed after the matches; ss_update_kernel does the first ones, ss_post_kernel these in order.
+  int* dupl = w.mt + 2 * (g.D + 2);
+  const int ndup = wave_compact(
+      x.nm,
+      [&](int q) {
+        for (int j = 0; j < q; j++)
+          if (w.mt[2 * j] == w.mt[2 * q]) return true;
+        return false;
+      },
+      [&](int q, int p) { dupl[p] = q; });
+  for (int k = lane; k < ndup; k += 64) w.mt[2 * dupl[k]] = -1 - w.mt[2 * dupl[k]];
+  if (lane == 0) {
+    sq[Q_NDUP] = ndup;
+    sq[Q_NFUT] = nfut;
+    sq[Q_NM] = x.nm;
+    sq[Q_NAUD] = naud;
+    sq[Q_FID] = fid;
+    sq[Q_NK] = x.nk;
+  }
+  SCOUNT(6, x.nm);
+  SSTAMP(7);
+}
+
+// Track.update for every match of the three stages (tracker.py:139-141): wave per match.
+__global__ void __launch_bounds__(64) ss_update_kernel(SsDev g, int seq0) {
+  __shared__ int lo[PW_MAXLEAF], ln[PW_MAXLEAF];
+  __shared__ double leaf[PW_MAXLEAF];
+  const int b = blockIdx.y, seq = seq0 + b, q = blockIdx.x;
+  int* sq = g.sq + (size_t)seq * SQS;
+  if (q >= sq[Q_NM]) return;
+  SsWs w{};
+  ws_frame(g, seq, w);
+  if (w.mt[2 * q] < 0) return;  // a repeated track: ss_post_kernel
+  w.pwlo = lo;
+  w.pwln = ln;
+  w.pwleaf = leaf;
+  SsCtx x{g, w, seq, (int)threadIdx.x, g.trk + (size_t)seq * g.T, sq, g.sqd + (size_t)seq * 2,
+          g.lost + (size_t)seq * LOSTN, 0, 0, 0, 0};
+  track_update(x, g.order[(size_t)seq * g.T + w.mt[2 * q]], w.mt[2 * q + 1]);
+}
+
+// ss_post_kernel (one wave per sequence): ID recovery, births, the lost buffer, the output rows.
+__global__ void __launch_bounds__(64)
+    ss_post_kernel(SsDev g, int seq0, const int* __restrict__ det_off, double* __restrict__ out,
+                   int* __restrict__ out_count) {
+  extern __shared__ __align__(16) char ss_lds[];
+  const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
+  SsWs w;
+  ws_carve(g, seq, w, ss_lds);
+#ifdef BX_PHASE_TIMING
+  unsigned long long t_last = SS_NOW();
+#endif
+  SsCtx x{g, w, seq, lane, g.trk + (size_t)seq * g.T, g.sq + (size_t)seq * SQS,
+          g.sqd + (size_t)seq * 2, g.lost + (size_t)seq * LOSTN, 0, 0, 0, 0};
+  int* sq = x.sq;
+  int* order = g.order + (size_t)seq * g.T;
+  const int r0 = det_off[b];
+  int n = det_off[b + 1] - r0;
+  if (n > g.D) n = g.D;
+  const int frame = sq[Q_FRAME] + 1;
+  const int fid = sq[Q_FID];
+  int naud = sq[Q_NAUD];
+  x.ntr = sq[Q_NTR];
+  x.nlost = sq[Q_NLOST];
+  x.nk = sq[Q_NK];
+  const int nt0 = x.ntr;
+  for (int p = lane; p < x.ntr; p += 64) w.lst[p] = order[p];
   __syncthreads();
+  // repeated matches of one track, in match order (see ss_match_kernel)
+  {
+    const int ndup = sq[Q_NDUP];
+    const int* dupl = w.mt + 2 * (g.D + 2);
+    for (int k = 0; k < ndup; k++) {
+      const int q = dupl[k];
+      track_update(x, w.lst[-1 - w.mt[2 * q]], w.mt[2 * q + 1]);
+    }
+  }
+  // ---- misses (tracker.py:142-145), after the updates ------------------------------------------
+  {
+    const int nfut = sq[Q_NFUT];
+    for (int k = 0; k < nfut; k += 64) {
+      // a position may be listed twice: serialise duplicates by processing one wave-slice at a
+      // time in list order, lanes of one slice never share a track (checked below)
+      const int kk = k + lane;
+      int pos = kk < nfut ? w.fut[kk] : -1;
+      bool dup_before = false;
+      for (int j = 0; j < 64; j++) {
+        const int pj = __shfl(pos, j);
+        if (j < lane && pj == pos) dup_before = true;
+      }
+      if (pos >= 0 && !dup_before) track_missed(x.trk[w.lst[pos]]);
+      // duplicates inside this slice: apply them one by one
+      for (int j = 0; j < 64; j++) {
+        const int pj = __shfl(pos, j);
+        const bool dj = __shfl((int)dup_before, j) != 0;
+        if (dj && pj >= 0 && lane == 0) track_missed(x.trk[w.lst[pj]]);
+        __syncthreads();
+      }
+      __syncthreads();
+    }
+  }
+  SSTAMP(7);
 
   // ---- _attempt_id_recovery (tracker.py:300-344) ----------------------------------------------
   if (x.nlost && naud) {
@@ -1288,6 +1443,7 @@ __global__ void __launch_bounds__(64)
     }
   }
 
+  SSTAMP(8);
   // ---- births (_initiate_track), free slots ascending ----------------------------------------
   if (naud) {
     for (int s2 = lane; s2 < g.T; s2 += 64) w.flag[s2] = 0;
@@ -1302,15 +1458,17 @@ __global__ void __launch_bounds__(64)
       if (lane == 0) atomicExch(g.status, (int)BX_ERR_TRACK_OVERFLOW);
       nnew = nfree;
     }
-    for (int k = 0; k < nnew; k++) {
-      const int slot = w.tmp[k];
-      track_birth(x, slot, w.aud[k]);
-      if (lane == 0) w.lst[x.ntr] = slot;
-      x.ntr++;
+    const int id0 = sq[Q_NEXTID];
+    for (int k = lane; k < nnew; k += 64) {
+      track_birth(x, w.tmp[k], w.aud[k], id0 + k);
+      w.lst[x.ntr + k] = w.tmp[k];
     }
+    x.ntr += nnew;
     __syncthreads();
+    if (lane == 0) sq[Q_NEXTID] = id0 + nnew;
   }
 
+  SSTAMP(9);
   // ---- deleted tracks -> lost buffer (tracker.py:152-164) -------------------------------------
   if (lane == 0) {
     const int max_age = sq[Q_MAXAGE];
@@ -1339,57 +1497,14 @@ __global__ void __launch_bounds__(64)
   x.nlost = w.sc[1];
   __syncthreads();
 
-  // ---- metric.partial_fit (tracker.py:166-178; linear_assignment.py:521-593) -----------------
+  SSTAMP(10);
+  // metric.partial_fit runs (ss_fit_kernel) iff a confirmed track has features (tracker.py:166-178)
   int anyf = 0;
   for (int p = lane; p < x.ntr; p += 64) {
     const SsTrk& t = x.trk[w.lst[p]];
     anyf |= t.state == 2 && t.nfeat > 0;
   }
   anyf = __any(anyf);
-  if (anyf) {
-    const int budget = sq[Q_BUDGET];
-    const int keep = budget > 0 ? (budget / 4 < 5 ? budget / 4 : 5) : 5;
-    for (int p = lane; p < x.ntr; p += 64) {
-      const int s2 = w.lst[p];
-      SsTrk& t = x.trk[s2];
-      int* gv = g.gal_v + ((size_t)seq * g.T + s2) * g.GB;
-      double* gq = g.gal_q + ((size_t)seq * g.T + s2) * g.GB;
-      int* cnt = g.gcnt + vidx(g, seq, s2, 0);
-      if (t.state == 2) {
-        for (int q = 0; q < t.nfeat; q++) {
-          const int v = t.feat[q];
-          gv[t.gal_n] = v;
-          gq[t.gal_n] = g.vwn[vidx(g, seq, s2, v)];
-          t.gal_n++;
-          cnt[v]++;
-          t.gmask |= 1ull << v;
-          if (budget > 0 && t.gal_n > budget) gal_prune(t, gv, gq, cnt, budget);
-        }
-      } else if (t.gal_n > keep) {
-        gal_prune(t, gv, gq, cnt, keep);
-      }
-    }
-    for (int k = lane; k < x.nlost; k += 64) {
-      const int s2 = x.lost[k];
-      SsTrk& t = x.trk[s2];
-      if (t.gal_n > keep)
-        gal_prune(t, g.gal_v + ((size_t)seq * g.T + s2) * g.GB,
-                  g.gal_q + ((size_t)seq * g.T + s2) * g.GB, g.gcnt + vidx(g, seq, s2, 0), keep);
-    }
-    __syncthreads();
-  }
-  // pool entries still referenced by a features list or a gallery
-  for (int p = lane; p < x.ntr + x.nlost; p += 64) {
-    const int s2 = p < x.ntr ? w.lst[p] : x.lost[p - x.ntr];
-    SsTrk& t = x.trk[s2];
-    unsigned long long m = t.gmask;
-    for (int q = 0; q < t.nfeat; q++) m |= 1ull << t.feat[q];
-    t.vmask = m;
-  }
-  // the next frame's gallery queries: confirmed tracks with samples
-  const int nnl = wave_compact(
-      x.ntr, [&](int p) { const SsTrk& t = x.trk[w.lst[p]]; return t.state == 2 && t.gal_n > 0; },
-      [&](int p, int q) { g.nnl[(size_t)seq * g.T + q] = w.lst[p]; });
 
   // ---- outputs (strongsort.py:313-345) ---------------------------------------------------------
   double* orow = out + (size_t)r0 * 10;
@@ -1413,10 +1528,99 @@ __global__ void __launch_bounds__(64)
     sq[Q_NTR] = x.ntr;
     sq[Q_NLOST] = x.nlost;
     sq[Q_HIST] = sq[Q_HIST] < 100 ? sq[Q_HIST] + 1 : 100;
-    sq[Q_NNL] = nnl;
-    sq[Q_NK] = x.nk;
+    sq[Q_NNL] = 0;  // ss_fit_kernel lists the next frame's gallery queries
+    sq[Q_ANYF] = anyf;
     sq[Q_NT0] = nt0;
     sq[Q_NOUT] = nout;
+  }
+  SSTAMP(12);
+}
+
+// metric.partial_fit (linear_assignment.py:539-593) for one track of the list or the lost buffer
+// (wave per track), then its pool bookkeeping and the next frame's query list.
+//
+// The gallery is kept as a multiset of (pool vector, quality, insertion time): the reference
+// appends, and whenever a list grows past the budget stable-sorts it by quality descending and
+// truncates.  Inductively its list is ordered by (quality desc, insertion time asc) from its first
+// sort on, and a stable sort of appended entries keeps that order, so appending k features one by
+// one with a truncation after each equals appending all k and keeping the `budget` best under
+// (quality desc, time asc) — what this kernel does (rank by comparison in LDS, compaction).
+constexpr int GB_MAX = 320;
+__global__ void __launch_bounds__(64) ss_fit_kernel(SsDev g, int seq0) {
+  __shared__ double q_s[GB_MAX];
+  __shared__ int t_s[GB_MAX], v_s[GB_MAX];
+  const int b = blockIdx.y, seq = seq0 + b, k = blockIdx.x, lane = threadIdx.x;
+  int* sq = g.sq + (size_t)seq * SQS;
+  const int ntr = sq[Q_NTR], nlost = sq[Q_NLOST];
+  if (k >= ntr + nlost) return;
+  const int slot = k < ntr ? g.order[(size_t)seq * g.T + k] : g.lost[(size_t)seq * LOSTN + k - ntr];
+  SsTrk& t = g.trk[(size_t)seq * g.T + slot];
+  const int F = g.F;
+  const int bdk = t.born_dk;
+  if (bdk >= 0) {  // a track born this frame: its first feature vector
+    const double* nf = g.nf + ((size_t)seq * g.D + bdk) * F;
+    double* dst = vecp(g, seq, slot, 0);
+    for (int q = lane; q < F; q += 64) dst[q] = nf[q];
+  }
+  int* gv = g.gal_v + ((size_t)seq * g.T + slot) * g.GB;
+  double* gq = g.gal_q + ((size_t)seq * g.T + slot) * g.GB;
+  int* gt = g.gal_t + ((size_t)seq * g.T + slot) * g.GB;
+  int n = t.gal_n;
+  if (sq[Q_ANYF]) {
+    const int budget = sq[Q_BUDGET];
+    const int keep = budget / 4 < 5 ? budget / 4 : 5;
+    int lim = -1;
+    if (k < ntr && t.state == 2) {  // active target: its features appended in list order
+      const int nf = t.nfeat, c0 = t.gal_clock;
+      for (int q = lane; q < nf; q += 64) {
+        const int v = t.feat[q];
+        gv[n + q] = v;
+        gq[n + q] = g.vwn[vidx(g, seq, slot, v)];
+        gt[n + q] = c0 + q;
+      }
+      n += nf;
+      if (budget > 0 && n > budget) lim = budget;
+      if (lane == 0) t.gal_clock = c0 + nf;
+    } else if (n > keep) {  // inactive target: trimmed to min(budget // 4, 5)
+      lim = keep;
+    }
+    __syncthreads();
+    if (lim >= 0) {
+      for (int i = lane; i < n; i += 64) {
+        q_s[i] = gq[i];
+        t_s[i] = gt[i];
+        v_s[i] = gv[i];
+      }
+      __syncthreads();
+      const int kept = wave_compact(
+          n,
+          [&](int i) {
+            const double qi = q_s[i];
+            const int ti = t_s[i];
+            int r = 0;
+            for (int j = 0; j < n; j++) r += (q_s[j] > qi) || (q_s[j] == qi && t_s[j] < ti);
+            return r < lim;
+          },
+          [&](int i, int p) {
+            gv[p] = v_s[i];
+            gq[p] = q_s[i];
+            gt[p] = t_s[i];
+          });
+      n = kept;
+    }
+    if (lane == 0) t.gal_n = n;
+  }
+  __syncthreads();
+  // pool entries referenced by the gallery, then by the features list too
+  unsigned long long m = 0ull;
+  for (int i = lane; i < n; i += 64) m |= 1ull << gv[i];
+  for (int o = 32; o >= 1; o >>= 1) m |= __shfl_xor(m, o);
+  if (lane == 0) {
+    t.gmask = m;
+    for (int q = 0; q < t.nfeat; q++) m |= 1ull << t.feat[q];
+    t.vmask = m;
+    t.born_dk = -1;
+    if (k < ntr && t.state == 2 && n > 0) g.nnl[(size_t)seq * g.T + atomicAdd(sq + Q_NNL, 1)] = slot;
   }
 }
 
@@ -1492,12 +1696,24 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   hipLaunchKernelGGL(ss_rec_kernel, dim3(LOSTN, nseq), dim3(256), 0, st, d, seq0, off, embs);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 2, st))) return rc;
-  if ((rc = ss_probe_begin(e, 3, st))) return rc;
   const size_t lds = d.ws_lds ? (size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4 : 0;
-  hipLaunchKernelGGL(ss_frame_kernel, dim3(nseq), dim3(64), lds, st, d, seq0, dets, off, warps,
-                     out, cnt);
+  if ((rc = ss_probe_begin(e, 3, st))) return rc;
+  hipLaunchKernelGGL(ss_match_kernel, dim3(nseq), dim3(64), lds, st, d, seq0, dets, off, warps);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 3, st))) return rc;
+  if ((rc = ss_probe_begin(e, 4, st))) return rc;
+  hipLaunchKernelGGL(ss_update_kernel, dim3(d.T < d.D ? d.T : d.D, nseq), dim3(64), 0, st, d,
+                     seq0);
+  SCHK(hipGetLastError());
+  if ((rc = ss_probe_end(e, 4, st))) return rc;
+  if ((rc = ss_probe_begin(e, 5, st))) return rc;
+  hipLaunchKernelGGL(ss_post_kernel, dim3(nseq), dim3(64), lds, st, d, seq0, off, out, cnt);
+  SCHK(hipGetLastError());
+  if ((rc = ss_probe_end(e, 5, st))) return rc;
+  if ((rc = ss_probe_begin(e, 6, st))) return rc;
+  hipLaunchKernelGGL(ss_fit_kernel, dim3(d.T + LOSTN, nseq), dim3(64), 0, st, d, seq0);
+  SCHK(hipGetLastError());
+  if ((rc = ss_probe_end(e, 6, st))) return rc;
   return BX_OK;
 }
 
@@ -1522,7 +1738,12 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   d.F = c->emb_dim;
   d.VP = vp;
   const int crowd_budget = c->nn_budget * 2 < 300 ? c->nn_budget * 2 : 300;
-  d.GB = (c->nn_budget > crowd_budget ? c->nn_budget : crowd_budget) + 1;
+  // partial_fit appends a track's <= MAXF features before truncating to the budget
+  d.GB = (c->nn_budget > crowd_budget ? c->nn_budget : crowd_budget) + MAXF;
+  if (d.GB > GB_MAX) {
+    delete e;
+    return bx_record_error(BX_ERR_INVALID, "nn_budget too large (gallery > 320 entries)");
+  }
   d.N = 2 * d.T > d.D ? 2 * d.T : d.D;
   d.min_conf = c->min_conf;
   d.max_iou = c->max_iou_dist;
@@ -1545,6 +1766,7 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   const size_t o_trk = cb(S * T * sizeof(SsTrk));
   const size_t o_gv = cb(S * T * GB * sizeof(int));
   const size_t o_gq = cb(S * T * GB * sizeof(double));
+  const size_t o_gt = cb(S * T * GB * sizeof(int));
   const size_t o_vec = cb(S * T * VP * F * sizeof(double));
   const size_t o_vden = cb(S * T * VP * sizeof(double));
   const size_t o_vwn = cb(S * T * VP * sizeof(double));
@@ -1559,10 +1781,17 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   const size_t o_nf = cb(S * D * F * sizeof(double));
   const size_t o_rec = cb(S * LOSTN * D * sizeof(double));
   const size_t o_cost = cb(S * 2 * T * D * sizeof(double));
-  const size_t o_gcnt = cb(S * T * VP * sizeof(int));
+  const size_t o_fdt = cb(S * D * DTW * sizeof(double));
+  const size_t o_fdord = cb(S * D * sizeof(int));
+  const size_t o_faud = cb(S * D * sizeof(int));
+  const size_t o_fmt = cb(S * 4 * (D + 2) * sizeof(int));
+  const size_t o_ffut = cb(S * 3 * T * sizeof(int));
   const size_t o_wsi = cb(S * (size_t)d.wsi_n * sizeof(int));
   const size_t o_wsd = cb(S * (size_t)d.wsd_n * sizeof(double));
   const size_t o_st = cb(sizeof(int) * 4);
+#ifdef BX_PHASE_TIMING
+  const size_t o_dbg = cb(S * SS_DBG * sizeof(unsigned long long));
+#endif
   if (hipMalloc(&e->arena, off) != hipSuccess) {
     delete e;
     return bx_record_error(BX_ERR_HIP, "hipMalloc of the StrongSort arena failed");
@@ -1572,6 +1801,7 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   d.trk = (SsTrk*)(base + o_trk);
   d.gal_v = (int*)(base + o_gv);
   d.gal_q = (double*)(base + o_gq);
+  d.gal_t = (int*)(base + o_gt);
   d.vec = (double*)(base + o_vec);
   d.vden = (double*)(base + o_vden);
   d.vwn = (double*)(base + o_vwn);
@@ -1586,10 +1816,19 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   d.nf = (double*)(base + o_nf);
   d.recsim = (double*)(base + o_rec);
   d.cost = (double*)(base + o_cost);
-  d.gcnt = (int*)(base + o_gcnt);
+  d.fdt = (double*)(base + o_fdt);
+  d.fdord = (int*)(base + o_fdord);
+  d.faud = (int*)(base + o_faud);
+  d.fmt = (int*)(base + o_fmt);
+  d.ffut = (int*)(base + o_ffut);
   d.wsi = (int*)(base + o_wsi);
   d.wsd = (double*)(base + o_wsd);
   d.status = (int*)(base + o_st);
+#ifdef BX_PHASE_TIMING
+  d.dbg = (unsigned long long*)(base + o_dbg);
+#else
+  d.dbg = nullptr;
+#endif
   // per-sequence defaults (row S holds them for bx_ss_reset): max_age, budget, threshold
   std::vector<int> q((S + 1) * SQS, 0);
   std::vector<double> qd((S + 1) * 2, c->max_cos_dist);
@@ -1602,10 +1841,13 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   q[S * SQS + 1] = c->nn_budget;
   SCHK(hipMemcpy(d.sq, q.data(), q.size() * sizeof(int), hipMemcpyHostToDevice));
   SCHK(hipMemcpy(d.sqd, qd.data(), qd.size() * sizeof(double), hipMemcpyHostToDevice));
-  if (d.ws_lds)
-    SCHK(hipFuncSetAttribute((const void*)ss_frame_kernel,
-                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)((size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4)));
+  if (d.ws_lds) {
+    const int lds = (int)((size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4);
+    SCHK(hipFuncSetAttribute((const void*)ss_match_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    SCHK(hipFuncSetAttribute((const void*)ss_post_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  }
   SCHK(hipMalloc(&e->h_dets, sizeof(double) * 6 * D));
   SCHK(hipMalloc(&e->h_off, sizeof(int) * 2));
   SCHK(hipMalloc(&e->h_embs, sizeof(double) * D * F));
@@ -1731,7 +1973,7 @@ int bx_ss_frame_stats_host(bx_ss* e, int seq0, int nseq, int64_t* sums) {
   if (nseq)
     SCHK(hipMemcpy(s.data(), e->dev.sq + (size_t)seq0 * SQS, sizeof(int) * s.size(),
                    hipMemcpyDeviceToHost));
-  int64_t a[6] = {0, 0, 0, 0, 0, 0};
+  int64_t a[7] = {0, 0, 0, 0, 0, 0, 0};
   for (int k = 0; k < nseq; k++) {
     const int* q = s.data() + (size_t)k * SQS;
     a[0] += q[Q_NK];
@@ -1740,8 +1982,9 @@ int bx_ss_frame_stats_host(bx_ss* e, int seq0, int nseq, int64_t* sums) {
     a[3] += q[Q_ROWSL];
     a[4] += q[Q_NOUT];
     a[5] = q[Q_FRAME] > a[5] ? q[Q_FRAME] : a[5];
+    a[6] += q[Q_NM];
   }
-  for (int k = 0; k < 6; k++) sums[k] = a[k];
+  for (int k = 0; k < 7; k++) sums[k] = a[k];
   return BX_OK;
 }
 
@@ -1749,6 +1992,15 @@ int bx_ss_probe(bx_ss* e, int stage) {
   if (!e) return bx_record_error(BX_ERR_INVALID, "null engine");
   e->probe_stage = stage;
   e->ev_used = 0;
+  return BX_OK;
+}
+
+// Diagnostic (timing builds only; not in the public header): copies [S][32] phase counters.
+int bx_ss_debug_host(bx_ss* e, unsigned long long* out) {
+  if (!e || !out || !e->dev.dbg) return bx_record_error(BX_ERR_INVALID, "not a timing build");
+  SCHK(hipDeviceSynchronize());
+  SCHK(hipMemcpy(out, e->dev.dbg, sizeof(unsigned long long) * SS_DBG * e->dev.S,
+                 hipMemcpyDeviceToHost));
   return BX_OK;
 }
 

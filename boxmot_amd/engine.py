@@ -478,7 +478,7 @@ class SsEngine:
     per frame the detection-feature kernel, the NN-gallery distance (fp64 MFMA), the recovery
     similarities and the frame kernel (one wave per sequence)."""
 
-    STAGES = ["prep", "nn", "recovery", "frame"]
+    STAGES = ["prep", "nn", "recovery", "match", "update", "post", "fit"]
 
     def __init__(self, n_seq: int = 1, track_cap: int = 256, det_cap: int = 256,
                  emb_dim: int = 512, vec_cap: int = 32, params: SsParams | None = None):
@@ -569,9 +569,9 @@ class SsEngine:
 
     def frame_stats(self, seq0: int = 0, nseq: int | None = None) -> dict:
         nseq = self.n_seq - seq0 if nseq is None else nseq
-        a = (C.c_int64 * 6)()
+        a = (C.c_int64 * 7)()
         N.check(self._L.bx_ss_frame_stats_host(self._h, seq0, nseq, a), "frame_stats")
-        return dict(zip(["dets", "tracks", "queried", "rows", "outputs", "frame"],
+        return dict(zip(["dets", "tracks", "queried", "rows", "outputs", "frame", "matches"],
                         [int(x) for x in a]))
 
     def probe(self, stage) -> None:

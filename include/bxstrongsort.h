@@ -9,8 +9,10 @@
  * Kalman/feature updates, misses, ID recovery from the lost-track buffer, births, deaths, the
  * gallery's partial_fit budget pruning and the output rows — runs on the GPU behind these entry
  * points: per frame a detection-feature kernel (wave per detection), the gallery distance
- * (fp64 MFMA, wave per confirmed track and detection block), the recovery similarities and the
- * frame kernel (one wave per sequence).
+ * (fp64 MFMA, wave per confirmed track and detection block), the recovery similarities, the
+ * matching kernel (one wave per sequence), the track updates (wave per match), the post-match
+ * kernel (recovery, births, lost buffer, outputs; wave per sequence) and partial_fit (wave per
+ * track).
  *
  * Reference interfaces replaced (file:line in muntherr/boxmot @ /root/reference):
  *   bx_ss_create/step/update_host  StrongSort.__init__ / StrongSort.update
@@ -49,7 +51,8 @@ typedef struct {
     int32_t det_cap;    /* max detections per frame per sequence (<= 1024) */
     int32_t emb_dim;    /* embedding dimension F (float64 embeddings, required) */
     int32_t vec_cap;    /* feature vectors kept per track slot (its features + gallery
-                           samples; <= 64, default 32) */
+                           samples; <= 64, default 32).  max(nn_budget, crowd budget) + 10
+                           <= 320 (gallery entries per track) */
     double min_conf, max_cos_dist, max_iou_dist;
     int32_t max_age, n_init, nn_budget;
     double mc_lambda, ema_alpha, conf_thresh_high, conf_thresh_low, id_preservation_weight;
@@ -86,12 +89,13 @@ int bx_ss_counters_host(bx_ss *e, int seq, int *frame_count, int *next_id, int *
 /* Track list in list order (host): ids, states (1 tentative, 2 confirmed), means [8], covs [64]. */
 int bx_ss_tracks_host(bx_ss *e, int seq, int cap, int32_t *ids, int32_t *state, double *mean,
                       double *cov, int *n);
-/* Last-frame statistics over sequences [seq0, seq0+nseq) (host): sums[6] = {detections kept,
- * tracks entering the frame, confirmed tracks queried, gallery sample rows compared, output rows,
- * max frame counter} — bench.py's unit counts. */
+/* Last-frame statistics over sequences [seq0, seq0+nseq) (host): sums[7] = {detections kept,
+ * tracks entering the frame, confirmed tracks queried next frame, gallery sample rows compared,
+ * output rows, max frame counter, matches} — bench.py's unit counts. */
 int bx_ss_frame_stats_host(bx_ss *e, int seq0, int nseq, int64_t *sums);
 /* Timing probe: stage 0 = detection features, 1 = gallery distance, 2 = recovery similarities,
- * 3 = frame kernel; -1 = off (see bx_boost_probe). */
+ * 3 = matching, 4 = track updates, 5 = post-match, 6 = partial_fit; -1 = off (see
+ * bx_boost_probe). */
 int bx_ss_probe(bx_ss *e, int stage);
 int bx_ss_probe_read(bx_ss *e, double *total_ms, int *count);
 
