@@ -136,7 +136,11 @@ def ss_stage_bytes(stage, u, F):
         # the feature row of each lost track and the detection rows
         "recovery": u["dets"] * F * 8,
         # track records (mean, cov, histories: ~1.2 kB) read + written, detection rows
-        "match": u["tracks"] * 2 * 1200 + u["dets"] * 64,
+        "pre": u["tracks"] * 2 * 1200 + u["dets"] * 64,
+        # per confirmed track: its record read, one cost per detection written
+        "cost": u["queried"] * 1200 + u["queried"] * (u["dets"] // max(u["seqs"], 1)) * 8,
+        # the cost entries gathered by the cascade levels, the IoU stage's detection rows
+        "match": u["queried"] * (u["dets"] // max(u["seqs"], 1)) * 8 + u["dets"] * 64,
         # per match: the detection's normalised row and the last feature read, the new vector
         # written (then read back twice for its norms), the track record read + written
         "update": u["matches"] * (5 * F * 8 + 2 * 1200),

@@ -7,23 +7,26 @@
 // NearestNeighborDistanceMetric), sort/iou_matching.py:10-87, utils/occlusion_handler.py:45-87,
 // 464-490 (detect_crowd_situations).  With P6 and handle_occlusions=False.
 //
-// Per frame, seven launches on the caller's stream:
+// Per frame, nine launches on the caller's stream:
 //   ss_prep_kernel   wave per detection: the feature's wave-order norm (quality; BLAS order of
 //                    the reference unpinned), its numpy pairwise norm, the NN-normalised row
 //                    feat/(‖·‖₂+1e-8) and the track-feature row feat/(‖·‖_wave+1e-8) with its
 //                    norms
-//   ss_nn_kernel     wave per confirmed track: min over its distinct gallery samples of
+//   ss_nn_kernel     wave per 1-4 confirmed tracks: min over its distinct gallery samples of
 //                    1 − clip(ŝ·d̂) for every detection — the (samples × F)·(F × dets)
 //                    contraction on the fp64 matrix cores (v_mfma_f64_16x16x4f64, ascending-k
 //                    chain = the oracle's fma chain), max over rows by wave shuffles
 //   ss_rec_kernel    wave per (lost track, detection): ID-recovery cosine similarity
-//   ss_match_kernel  one wave per sequence: crowd mode, CMC warp, detection quality + stable
-//                    sort, Kalman predict, the matching cascade (gating, motion/quality cost
-//                    shaping lane per track row, scipy's linear_sum_assignment restated
-//                    wave-parallel), the IoU stage, misses
+//   ss_pre_kernel    one wave per sequence: crowd mode, CMC warp, detection quality + stable
+//                    sort, Kalman predict
+//   ss_cost_kernel   wave per confirmed track: gating + motion/quality cost shaping of the
+//                    track against every detection (lanes over detections)
+//   ss_match_kernel  one wave per sequence: the matching cascade (levels gathered from the
+//                    cost kernel's matrix, scipy's linear_sum_assignment restated
+//                    wave-parallel), the IoU stage
 //   ss_update_kernel wave per match: Kalman update, feature EMA vector + norms, track scalars
-//   ss_post_kernel   one wave per sequence: ID recovery, births (lane per birth), lost buffer,
-//                    output rows
+//   ss_post_kernel   one wave per sequence: misses, ID recovery, births (lane per birth), lost
+//                    buffer, output rows
 //   ss_fit_kernel    wave per listed / lost track: partial_fit (append + budget truncation by
 //                    rank in LDS), pool bookkeeping, the next frame's gallery queries
 // Every floating-point expression restates oracle/bxo_strongsort.c operation for operation.
@@ -85,6 +88,7 @@ struct SsDev {
   double* gal_q;  // [S][T][GB] sample quality (wave norm)
   int* gal_t;     // [S][T][GB] insertion time (the reference list's order among equal qualities)
   double* vec;    // [S][T][VP][F]
+  double* vecn;   // [S][T][VP][F] vec / vden: the sample as the NN metric normalises it
   double* vden;   // [S][T][VP] numpy pairwise norm + 1e-8 (NN sample normalisation)
   double* vwn;    // [S][T][VP] wave-order norm
   int* sq;        // [S][SQS]
@@ -98,6 +102,8 @@ struct SsDev {
   double* nf;     // [S][D][F] feat / (wave norm + 1e-8)
   double* recsim; // [S][LOSTN][D]
   double* cost;   // [S][2T*D] scratch cost matrices
+  double* cfull;  // [S][T][D] stage 1/2 cost by (track list position, sorted detection)
+  double* cfullT; // [S][D][T] the same, detection-major
   double* fdt;    // [S][D][DTW] this frame's detection table (kept across the frame's launches)
   int* fdord;     // [S][D] detections in quality order
   int* faud;      // [S][D] unmatched detections after the three stages
@@ -141,6 +147,9 @@ constexpr int SS_DBG = 32;
 
 __device__ __forceinline__ double* vecp(const SsDev& g, int seq, int slot, int v) {
   return g.vec + ((((size_t)seq * g.T + slot) * g.VP + v) * (size_t)g.F);
+}
+__device__ __forceinline__ double* vecnp(const SsDev& g, int seq, int slot, int v) {
+  return g.vecn + ((((size_t)seq * g.T + slot) * g.VP + v) * (size_t)g.F);
 }
 __device__ __forceinline__ size_t vidx(const SsDev& g, int seq, int slot, int v) {
   return ((size_t)seq * g.T + slot) * g.VP + v;
@@ -449,16 +458,19 @@ struct SsWs {
   // ints
   int *lst, *conf_t, *unconf_t, *aut, *cand, *ut3, *fut, *hi, *med, *lo, *aud, *rd, *ud, *ud2;
   int *lvl, *ages, *mt, *tmp, *rows, *cols, *flag, *ti2, *dord;  // mt, dord, aud: HBM (fmt..)
-  int *path, *col4row, *row4col, *rem, *SR, *SC, *pwlo, *pwln, *sc;
+  int *path, *col4row, *row4col, *rem, *pos, *SR, *SC, *pwlo, *pwln, *sc;
   // doubles
   double *dt, *u, *v, *spc, *meas, *key, *pwleaf, *sd;
 };
 
+// The scratch of one sequence: the LSAP state (3N doubles u v spc, 7N ints path col4row row4col
+// rem pos SR SC) and the rest.  ws_lds: 0 = all in HBM, 1 = all in LDS, 2 = the LSAP state in LDS.
+int ws_lsap_bytes(int N) { return 3 * N * 8 + 7 * N * 4; }
 int ws_ints(int T, int D, int N) {
   return T /*lst*/ + T + T + T + 2 * T /*cand*/ + 2 * T /*ut3*/ + 3 * D +
          D /*rd*/ + 2 * (D + 2 * T) /*ud ud2*/ + T /*lvl*/ + T /*ages*/ +
          2 * (T + D) /*tmp*/ + 2 * N /*rows cols*/ + 2 * T /*flag*/ + 2 * T /*ti2*/ +
-         6 * N + 2 * PW_MAXLEAF + 32;
+         7 * N + 2 * PW_MAXLEAF + 32;
 }
 int ws_doubles(int T, int D, int N) {
   return 3 * N + 4 * D + 2 * T + PW_MAXLEAF + 8;
@@ -476,7 +488,7 @@ __device__ void ws_frame(const SsDev& g, int seq, SsWs& w) {
 __device__ void ws_carve(const SsDev& g, int seq, SsWs& w, char* lds) {
   int* pi = g.wsi + (size_t)seq * g.wsi_n;
   double* pd = g.wsd + (size_t)seq * g.wsd_n;
-  if (g.ws_lds) {  // doubles first (8-byte alignment), then ints
+  if (g.ws_lds == 1) {  // doubles first (8-byte alignment), then ints
     pd = (double*)lds;
     pi = (int*)(lds + (size_t)g.wsd_n * 8);
   }
@@ -487,28 +499,37 @@ __device__ void ws_carve(const SsDev& g, int seq, SsWs& w, char* lds) {
   w.ut3 = I(2 * T); w.hi = I(D); w.med = I(D); w.lo = I(D);
   w.rd = I(D); w.ud = I(D + 2 * T); w.ud2 = I(D + 2 * T); w.lvl = I(T); w.ages = I(T);
   w.tmp = I(2 * (T + D)); w.rows = I(N); w.cols = I(N); w.flag = I(2 * T);
-  w.ti2 = I(2 * T); w.path = I(N); w.col4row = I(N); w.row4col = I(N); w.rem = I(N); w.SR = I(N);
-  w.SC = I(N); w.pwlo = I(PW_MAXLEAF); w.pwln = I(PW_MAXLEAF); w.sc = I(32);
+  w.ti2 = I(2 * T); w.pwlo = I(PW_MAXLEAF); w.pwln = I(PW_MAXLEAF); w.sc = I(32);
   ws_frame(g, seq, w);
-  w.u = Dd(N); w.v = Dd(N); w.spc = Dd(N); w.meas = Dd(4 * D);
-  w.key = Dd(2 * T); w.pwleaf = Dd(PW_MAXLEAF); w.sd = Dd(8);
+  w.meas = Dd(4 * D); w.key = Dd(2 * T); w.pwleaf = Dd(PW_MAXLEAF); w.sd = Dd(8);
+  if (g.ws_lds == 2) {  // the LSAP state alone in LDS
+    pd = (double*)lds;
+    pi = (int*)(lds + (size_t)3 * N * 8);
+  }
+  w.u = Dd(N); w.v = Dd(N); w.spc = Dd(N);
+  w.path = I(N); w.col4row = I(N); w.row4col = I(N); w.rem = I(N); w.pos = I(N); w.SR = I(N);
+  w.SC = I(N);
 }
 
 // broadcast an int from lane 0 (all lanes call)
 __device__ __forceinline__ int bcast(int v) { return __shfl(v, 0); }
 __device__ __forceinline__ double bcastd(double v) { return __shfl(v, 0); }
 
-// stable sort of idx[0..n) by key descending (ties keep order): rank placement, lane-parallel
+// stable sort of idx[0..n) by key descending (ties keep order): rank placement, lane-parallel,
+// the keys staged in ks (LDS, n entries)
 template <class K>
-__device__ void stable_sort_desc(int* idx, int n, K key, int* tmp) {
+__device__ void stable_sort_desc(int* idx, int n, K key, int* tmp, double* ks) {
   const int lane = threadIdx.x & 63;
-  for (int i = lane; i < n; i += 64) tmp[i] = idx[i];
+  for (int i = lane; i < n; i += 64) {
+    tmp[i] = idx[i];
+    ks[i] = key(idx[i]);
+  }
   __syncthreads();
   for (int i = lane; i < n; i += 64) {
-    const double ki = key(tmp[i]);
+    const double ki = ks[i];
     int r = 0;
     for (int j = 0; j < n; j++) {
-      const double kj = key(tmp[j]);
+      const double kj = ks[j];
       r += (kj > ki) || (kj == ki && j < i);
     }
     idx[r] = tmp[i];
@@ -576,70 +597,130 @@ __global__ void __launch_bounds__(64)
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// NearestNeighborDistanceMetric.distance for one confirmed track (wave per listed slot):
-// rows = its distinct gallery vectors x/den, columns = this frame's normalised detections.
+// NearestNeighborDistanceMetric.distance (linear_assignment.py:468-497, 595-618) for G listed
+// confirmed tracks per wave: rows = each track's distinct gallery vectors (pre-normalised x/den),
+// columns = this frame's normalised detections; out = 1 - clip(max over the track's rows).
+// A pass multiplies RT row tiles (16 rows each, a track's <= 64 rows are <= 4 tiles; tiles of
+// the G tracks concatenated) by up to 4 detection tiles (64 detections) on the fp64 matrix cores,
+// so every detection row loaded serves up to RT tiles and every sample row 4 detection tiles.
+// Each output's k-chain is the oracle's ascending fma chain whatever the tiling.
+template <int G, int RT>
 __global__ void __launch_bounds__(64)
     ss_nn_kernel(SsDev g, int seq0, const int* __restrict__ det_off) {
-  __shared__ int rowv[64];
-  __shared__ int nrow_s;
-  const int b = blockIdx.y, seq = seq0 + b, k = blockIdx.x;
+  __shared__ int rowv[G][64];
+  __shared__ int nrow_s[G], slot_s[G], tt[4 * G], tr0[4 * G], ntile_s;
+  const int b = blockIdx.y, seq = seq0 + b, k0 = blockIdx.x * G, lane = threadIdx.x;
   const int nl = g.sq[(size_t)seq * SQS + Q_NNL];
-  if (k >= nl) return;
+  if (k0 >= nl) return;
+  const int ng = nl - k0 < G ? nl - k0 : G;
   const int r0 = det_off[b];
   int n = det_off[b + 1] - r0;
   if (n > g.D) n = g.D;
   if (n <= 0) return;
-  const int slot = g.nnl[(size_t)seq * g.T + k], lane = threadIdx.x, F = g.F;
-  const SsTrk& t = g.trk[(size_t)seq * g.T + slot];
-  if (lane == 0) {  // distinct pool entries referenced by the gallery
-    unsigned long long m = t.gmask;
+  const int F = g.F;
+  if (lane < ng) {  // distinct pool entries referenced by each gallery
+    const int slot = g.nnl[(size_t)seq * g.T + k0 + lane];
+    unsigned long long m = g.trk[(size_t)seq * g.T + slot].gmask;
     int c = 0;
     while (m) {
-      rowv[c++] = __ffsll((long long)m) - 1;
+      rowv[lane][c++] = __ffsll((long long)m) - 1;
       m &= m - 1;
     }
-    nrow_s = c;
+    nrow_s[lane] = c;
+    slot_s[lane] = slot;
     atomicAdd(g.sq + (size_t)seq * SQS + Q_ROWS, c);
   }
   __syncthreads();
-  const int nrow = nrow_s;
-  double* out = g.nnd + ((size_t)seq * g.T + slot) * g.D;
-  const double* dnb = g.dn + (size_t)seq * g.D * F;
-  for (int d0 = 0; d0 < n; d0 += 16) {
-    double best = -INF;  // max over rows of the dot product, column d0 + (lane & 15)
-    bool any = false;
-    for (int rt = 0; rt < nrow; rt += 16) {
-      const int ra = rt + (lane & 15), col = d0 + (lane & 15);
-      const bool aok = ra < nrow, bok = col < n;
-      const double* ap = aok ? vecp(g, seq, slot, rowv[ra]) : nullptr;
-      const double den = aok ? g.vden[vidx(g, seq, slot, rowv[ra])] : 1.0;
-      const double* bp = dnb + (size_t)(bok ? col : 0) * F;
-      d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
-      for (int k0 = 0; k0 < F; k0 += 4) {
-        const int kk = k0 + (lane >> 4);
-        const double a = (aok && kk < F) ? ap[kk] / den : 0.0;
-        const double bb = (bok && kk < F) ? bp[kk] : 0.0;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+  if (lane == 0) {  // the tile list: (track, first row) per 16-row tile
+    int nt = 0;
+    for (int q = 0; q < ng; q++)
+      for (int r = 0; r < nrow_s[q]; r += 16) {
+        tt[nt] = q;
+        tr0[nt] = r;
+        nt++;
       }
-      // lane holds column (lane & 15), rows (lane >> 4) + 4 q
+    ntile_s = nt;
+  }
+  __syncthreads();
+  const int ntile = ntile_s;
+  const double* dnb = g.dn + (size_t)seq * g.D * F;
+  const int kl = lane >> 4, cl = lane & 15;
+  for (int db = 0; db < n; db += 64) {
+    const int ndt = n - db >= 64 ? 4 : (n - db + 15) / 16;  // detection tiles in this block
+    double best[G][4];
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int row = rt + (lane >> 4) + 4 * q;
-        if (row < nrow) {
-          best = any ? (acc[q] > best ? acc[q] : best) : acc[q];
-          any = true;
+    for (int q = 0; q < G; q++)
+#pragma unroll
+      for (int dt = 0; dt < 4; dt++) best[q][dt] = -INF;
+    const double* bp[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; dt++) {
+      const int col = db + 16 * dt + cl;
+      bp[dt] = dnb + (size_t)(col < n ? col : 0) * F + kl;
+    }
+    for (int p0 = 0; p0 < ntile; p0 += RT) {
+      const double* ap[RT];
+      int nrt = 0;
+#pragma unroll
+      for (int rt = 0; rt < RT; rt++) {
+        const int ti = p0 + rt < ntile ? p0 + rt : p0;
+        const int q = tt[ti], row = tr0[ti] + cl;
+        const int slot = slot_s[q];
+        ap[rt] = vecnp(g, seq, slot, rowv[q][row < nrow_s[q] ? row : 0]) + kl;
+        nrt += p0 + rt < ntile;
+      }
+      d4 acc[RT][4];
+#pragma unroll
+      for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+        for (int dt = 0; dt < 4; dt++) acc[rt][dt] = (d4){0.0, 0.0, 0.0, 0.0};
+      for (int k = 0; k < F; k += 4) {
+        const bool in = k + kl < F;
+        double a[RT], bb[4];
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++) a[rt] = in ? ap[rt][k] : 0.0;
+#pragma unroll
+        for (int dt = 0; dt < 4; dt++) bb[dt] = (in && dt < ndt) ? bp[dt][k] : 0.0;
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+          for (int dt = 0; dt < 4; dt++)
+            if (dt < ndt)
+              acc[rt][dt] =
+                  __builtin_amdgcn_mfma_f64_16x16x4f64(a[rt], bb[dt], acc[rt][dt], 0, 0, 0);
+      }
+      // lane holds column cl of each detection tile, rows kl + 4 j of each row tile
+#pragma unroll
+      for (int rt = 0; rt < RT; rt++) {
+        if (rt >= nrt) break;
+        const int ti = p0 + rt, q = tt[ti];
+        const int nr = nrow_s[q] - tr0[ti];
+#pragma unroll
+        for (int dt = 0; dt < 4; dt++) {
+          double m = -INF;
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (kl + 4 * j < nr) m = acc[rt][dt][j] > m ? acc[rt][dt][j] : m;
+          const double o1 = __shfl_xor(m, 16);
+          m = o1 > m ? o1 : m;
+          const double o2 = __shfl_xor(m, 32);
+          m = o2 > m ? o2 : m;
+#pragma unroll
+          for (int qq = 0; qq < G; qq++)
+            if (qq == q && m > best[qq][dt]) best[qq][dt] = m;
         }
       }
     }
-    // combine the four row groups holding column (lane & 15)
-    for (int o = 16; o <= 32; o <<= 1) {
-      const double ob = __shfl_xor(best, o);
-      const bool oa = __shfl_xor((int)any, o) != 0;
-      if (oa && (!any || ob > best)) best = ob;
-      any = any || oa;
+#pragma unroll
+    for (int q = 0; q < G; q++) {
+      if (q >= ng) break;
+      double* out = g.nnd + ((size_t)seq * g.T + slot_s[q]) * g.D;
+#pragma unroll
+      for (int dt = 0; dt < 4; dt++) {
+        const int col = db + 16 * dt + cl;
+        if (kl == 0 && col < n) out[col] = 1.0 - clipd(best[q][dt], -1.0, 1.0);
+      }
     }
-    const int col = d0 + (lane & 15);
-    if (lane < 16 && col < n && any) out[col] = 1.0 - clipd(best, -1.0, 1.0);
   }
 }
 
@@ -678,53 +759,59 @@ struct SsCtx {
   double* sqd;
   int* lost;
   int ntr, nlost, nk, nm;
+  double* key;  // match kernel: quality + stability by list position (LDS)
+  double* ks;   // match kernel: sort-key scratch (LDS)
   __device__ const double* det(int i) const { return w.dt + (size_t)w.dord[i] * DTW; }
   __device__ int det_in(int i) const { return (int)det(i)[6]; }
 };
 
-// scipy.optimize.linear_sum_assignment (Crouse's shortest augmenting path, rectangular) on the
-// nr x nc row-major matrix C, wave-parallel: each row's Dijkstra relaxes the remaining columns
-// lane-parallel and picks the minimum with scipy's tie rule (the last unassigned column at the
-// minimum in `remaining` order, else the first at the minimum).  Pairs sorted by row into
-// w.rows/w.cols; returns their count.
-__device__ int lsap_wave(SsCtx& x, const double* C, int nr, int nc) {
+// scipy.optimize.linear_sum_assignment (Crouse's shortest augmenting path, rectangular),
+// wave-parallel, on C given in the solver's orientation: R x CC row-major, R <= CC (`tr`: the
+// caller's matrix was transposed to get there, so the output pairs are argsorted by the original
+// row).  Each row's Dijkstra relaxes the remaining columns lane-parallel — coalesced reads of the
+// row — and picks the minimum with scipy's tie rule: the last unassigned column at the minimum in
+// `remaining` order, else the first at the minimum (pos[] tracks each column's place in scipy's
+// swap-remove `remaining` array).  Pairs sorted by row into w.rows/w.cols; returns their count.
+__device__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
   SsWs& w = x.w;
   const int lane = x.lane;
-  const bool tr = nc < nr;
-  const int R = tr ? nc : nr, CC = tr ? nr : nc;
-  auto cost = [&](int i, int j) -> double { return tr ? C[(size_t)j * nc + i] : C[(size_t)i * nc + j]; };
   for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
   for (int j = lane; j < CC; j += 64) w.v[j] = 0.0, w.path[j] = -1, w.row4col[j] = -1;
   __syncthreads();
   for (int cur = 0; cur < R; cur++) {
     double minVal = 0.0;
     int nrem = CC;
-    for (int it = lane; it < CC; it += 64) w.rem[it] = CC - it - 1;
+    for (int j = lane; j < CC; j += 64) {
+      w.rem[CC - 1 - j] = j;
+      w.pos[j] = CC - 1 - j;
+      w.SC[j] = 0;
+      w.spc[j] = INF;
+    }
     for (int i = lane; i < R; i += 64) w.SR[i] = 0;
-    for (int j = lane; j < CC; j += 64) w.SC[j] = 0, w.spc[j] = INF;
     __syncthreads();
     int sink = -1, i = cur;
     while (sink == -1) {
       if (lane == 0) w.SR[i] = 1;
       const double ui = w.u[i];
+      const double* crow = C + (size_t)i * CC;
       double m = INF;
-      for (int it = lane; it < nrem; it += 64) {
-        const int j = w.rem[it];
-        const double r = minVal + cost(i, j) - ui - w.v[j];
-        if (r < w.spc[j]) {
+      for (int j = lane; j < CC; j += 64) {
+        if (w.SC[j]) continue;
+        const double r = minVal + crow[j] - ui - w.v[j];
+        double sp = w.spc[j];
+        if (r < sp) {
           w.path[j] = i;
-          w.spc[j] = r;
+          w.spc[j] = sp = r;
         }
-        m = fmin(m, w.spc[j]);
+        m = fmin(m, sp);
       }
       m = wave_min_d(m);
-      // tie rule: the last unassigned position at the minimum, else the first at the minimum
       int last_un = -1, first_eq = 0x7fffffff;
-      for (int it = lane; it < nrem; it += 64) {
-        const int j = w.rem[it];
-        if (w.spc[j] == m) {
-          if (w.row4col[j] == -1) last_un = it > last_un ? it : last_un;
-          first_eq = it < first_eq ? it : first_eq;
+      for (int j = lane; j < CC; j += 64) {
+        if (!w.SC[j] && w.spc[j] == m) {
+          const int p = w.pos[j];
+          if (w.row4col[j] == -1) last_un = p > last_un ? p : last_un;
+          first_eq = p < first_eq ? p : first_eq;
         }
       }
       for (int o = 32; o >= 1; o >>= 1) {
@@ -738,14 +825,16 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int nr, int nc) {
       const int index = last_un >= 0 ? last_un : first_eq;
       minVal = m;
       const int j = w.rem[index];
-      __syncthreads();
       if (w.row4col[j] == -1)
         sink = j;
       else
         i = w.row4col[j];
+      __syncthreads();
       if (lane == 0) {
         w.SC[j] = 1;
-        w.rem[index] = w.rem[nrem - 1];
+        const int jl = w.rem[nrem - 1];
+        w.rem[index] = jl;
+        w.pos[jl] = index;
       }
       nrem--;
       __syncthreads();
@@ -794,6 +883,114 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int nr, int nc) {
 
 enum { M_GATED = 0, M_IOU = 1 };
 
+// _enhance_cost_matrix (linear_assignment.py:251-273) of one entry, unclamped
+__device__ __forceinline__ double enhance(const SsTrk& t, const double* d, double e) {
+  const double cq = (t.quality + d[7]) / 2.0;
+  e *= clipd(1.0 - (cq - 0.5) * 0.2, 0.8, 1.2);
+  if (t.cls == d[5]) e *= 0.9;
+  double cf = 1.0;
+  if (t.conf > 0.7 && d[4] > 0.7)
+    cf = 0.9;
+  else if (t.conf < 0.3 || d[4] < 0.3)
+    cf = 1.1;
+  return e * cf;
+}
+// ... and min_cost_matching's clamp at max_distance (linear_assignment.py:62-64)
+__device__ __forceinline__ double enhance_clamp(const SsTrk& t, const double* d, double e,
+                                                double max_d) {
+  e = enhance(t, d, e);
+  return e > max_d ? max_d + 1e-5 : e;
+}
+
+// Stage 1/2 cost of every confirmed track against every kept detection (wave per listed track,
+// lanes over detections in quality order): gated_metric's NN distance, gate_cost_matrix with the
+// motion / adaptive-lambda / track-specific shaping (linear_assignment.py:174-352), the
+// id-preservation weight (tracker.py:283-298) and _enhance_cost_matrix — everything but the
+// level's clamp.  Only depends on the predicted tracks and the detections, so the cascade levels
+// of ss_match_kernel gather from it.
+__global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
+  __shared__ double sh[32];
+  const int b = blockIdx.y, seq = seq0 + b, k = blockIdx.x, lane = threadIdx.x;
+  const int* sq = g.sq + (size_t)seq * SQS;
+  if (k >= sq[Q_NTR]) return;
+  const int nk = sq[Q_NK];
+  const int slot = g.order[(size_t)seq * g.T + k];
+  const SsTrk& t = g.trk[(size_t)seq * g.T + slot];
+  if (t.state != 2 || nk == 0) return;
+  // per-track terms, computed once (lane 0) and shared through LDS
+  if (lane == 0) {
+    double S[16], L[16], rr[4];
+    kf_meas_noise(KIND_BYTE, t.mean, 0.0, rr);
+    for (int i = 0; i < 4; i++)
+      for (int j = 0; j < 4; j++) S[4 * i + j] = t.cov[8 * i + j] + (i == j ? rr[i] : 0.0);
+    const bool ok = chol4(S, L);
+    for (int i = 0; i < 16; i++) sh[i] = L[i];
+    sh[16] = ok ? 1.0 : 0.0;
+    sh[17] = 2.0 - t.motion_cons;
+    double pp0 = 0.0, pp1 = 0.0;
+    if (t.nvel > 0) pp0 = t.mean[0] + t.vel[t.nvel - 1][0], pp1 = t.mean[1] + t.vel[t.nvel - 1][1];
+    sh[18] = pp0;
+    sh[19] = pp1;
+    const double af = pymin(t.age / 10.0, 1.0);
+    double al = g.mc_lambda + (1 - g.mc_lambda) * af * 0.1;
+    al = al * (0.8 + 0.4 * t.motion_cons);
+    if (t.app_cons < 0.5) al = pymin(al * 1.2, 0.99);
+    al = clipd(al, 0.1, 0.99);
+    sh[20] = al;
+    sh[21] = g.idw * pymin(t.hits / 10.0, 1.0);
+    for (int i = 0; i < 4; i++) sh[22 + i] = t.mean[i];
+  }
+  __syncthreads();
+  double L[16];
+  for (int i = 0; i < 16; i++) L[i] = sh[i];
+  const bool ok = sh[16] != 0.0;
+  const double mf = sh[17], pp0 = sh[18], pp1 = sh[19], al = sh[20], pb = sh[21];
+  const double m0 = sh[22], m1 = sh[23], m2 = sh[24], m3 = sh[25];
+  const bool has_vel = t.nvel > 0, has_gal = t.gal_n > 0;
+  const bool hq = t.quality > 0.8, hh = t.hits > 10 && t.tsu == 0, hs = t.high_streak > 3,
+             ls = t.low_streak > 2;
+  const double* dt = g.fdt + (size_t)seq * g.D * DTW;
+  const int* dord = g.fdord + (size_t)seq * g.D;
+  const double* nnd = g.nnd + ((size_t)seq * g.T + slot) * g.D;
+  double* out = g.cfull + ((size_t)seq * g.T + k) * g.D;
+  double* outT = g.cfullT + (size_t)seq * g.D * g.T + k;
+  for (int c = lane; c < nk; c += 64) {
+    const double* d = dt + (size_t)dord[c] * DTW;
+    double z[4];
+    det_xyah(d, z);
+    double gd;
+    if (!ok) {
+      gd = __builtin_nan("");
+    } else {
+      const double dd[4] = {z[0] - m0, z[1] - m1, z[2] - m2, z[3] - m3};
+      double y[4], s2 = 0.0;
+      for (int i = 0; i < 4; i++) {
+        double sm = dd[i];
+        for (int j = 0; j < i; j++) sm -= L[4 * i + j] * y[j];
+        y[i] = sm / L[4 * i + i];
+        s2 += y[i] * y[i];
+      }
+      gd = s2;
+    }
+    double v = has_gal ? nnd[(int)d[6]] : SS_INFTY;
+    if (gd > SS_GATE) v = SS_INFTY;
+    double m = gd * mf;
+    if (has_vel) {
+      const double ve = norm2(z[0] - pp0, z[1] - pp1);
+      m *= 1.0 + pymin(ve / 50.0, 1.0);
+    }
+    v = al * v + (1 - al) * m;
+    if (hq) v *= 0.95;
+    if (hh) v *= 0.98;
+    if (hs) v *= 0.97;
+    if (ls) v *= 1.05;
+    if (g.idw > 0) v *= (1.0 - pb);
+    const double e = enhance(t, d, v);
+    out[c] = e;
+    outT[(size_t)c * g.T] = e;
+  }
+}
+
 // min_cost_matching (linear_assignment.py:14-93) of track positions ti x sorted detections di:
 // matches appended to w.mt at x.nm; unmatched tracks to ut_out (if non-null), detections to
 // ud_out.  Cost rows lane per track (gated_metric + gate_cost_matrix + id preservation, or
@@ -813,22 +1010,46 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
     __syncthreads();
     return;
   }
-  double* C = g.cost + (size_t)x.seq * 2 * g.T * g.D;
+  // the solver's orientation: R x CC with R <= CC, transposed (tr) when detections are fewer
+  const bool tr = nd < nt;
+  double* C = g.cost + (size_t)x.seq * 4 * g.T * g.D;
+  double* C2 = C + (size_t)2 * g.T * g.D;
 #ifdef BX_PHASE_TIMING
   const int seq = x.seq;
   __syncthreads();
   unsigned long long t0 = SS_NOW();
 #endif
   if (kind == M_GATED) {
-    for (int c = lane; c < nd; c += 64) det_xyah(x.det(di[c]), w.meas + 4 * c);
-    __syncthreads();
-  }
-  const double* nnd = g.nnd + (size_t)x.seq * g.T * g.D;
-  for (int r = lane; r < nt; r += 64) {
-    const int slot = w.lst[ti[r]];
-    const SsTrk& t = x.trk[slot];
-    double* row = C + (size_t)r * nd;
-    if (kind == M_IOU) {
+    // ss_cost_kernel's gated + shaped + enhanced cost of (list position, sorted detection); the
+    // clamp at max_distance is this level's.  The lane's gather indices stay in registers.
+    constexpr int MAXJ = 32;  // 2 * track_cap / 64
+    const int nl = tr ? nt : nd, no = tr ? nd : nt;
+    const int* li = tr ? ti : di;
+    const int* oi = tr ? di : ti;
+    const double* cf = tr ? g.cfullT + (size_t)x.seq * g.D * g.T : g.cfull + (size_t)x.seq * g.T * g.D;
+    const int ld = tr ? g.T : g.D;
+    int idx[MAXJ];
+#pragma unroll
+    for (int j = 0; j < MAXJ; j++) idx[j] = lane + 64 * j < nl ? li[lane + 64 * j] : 0;
+    for (int o = 0; o < no; o++) {
+      const double* src = cf + (size_t)oi[o] * ld;
+      double* row = C + (size_t)o * nl;
+#pragma unroll
+      for (int j = 0; j < MAXJ; j++) {
+        const int c = lane + 64 * j;
+        if (c < nl) {
+          double e = src[idx[j]];
+          if (e > max_d) e = max_d + 1e-5;
+          row[c] = e;
+        }
+      }
+    }
+  } else {
+    double* Cr = tr ? C2 : C;  // row-major nt x nd, transposed below when tr
+    for (int r = lane; r < nt; r += 64) {
+      const int slot = w.lst[ti[r]];
+      const SsTrk& t = x.trk[slot];
+      double* row = Cr + (size_t)r * nd;
       if (t.tsu > 1) {
         for (int c = 0; c < nd; c++) row[c] = SS_INFTY;
       } else {
@@ -844,69 +1065,12 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
           row[c] = 1.0 - ai / ((b[2] * b[3] + q[2] * q[3]) - ai);
         }
       }
-    } else {
-      // Mahalanobis gating (base_kalman_filter.py:166-194, kf_gating_soa order)
-      double S[16], L[16], rr[4];
-      kf_meas_noise(KIND_BYTE, t.mean, 0.0, rr);
-      for (int i = 0; i < 4; i++)
-        for (int j = 0; j < 4; j++) S[4 * i + j] = t.cov[8 * i + j] + (i == j ? rr[i] : 0.0);
-      const bool ok = chol4(S, L);
-      const double mf = 2.0 - t.motion_cons;
-      double pp0 = 0.0, pp1 = 0.0;
-      if (t.nvel > 0) pp0 = t.mean[0] + t.vel[t.nvel - 1][0], pp1 = t.mean[1] + t.vel[t.nvel - 1][1];
-      const double af = pymin(t.age / 10.0, 1.0);
-      double al = g.mc_lambda + (1 - g.mc_lambda) * af * 0.1;
-      al = al * (0.8 + 0.4 * t.motion_cons);
-      if (t.app_cons < 0.5) al = pymin(al * 1.2, 0.99);
-      al = clipd(al, 0.1, 0.99);
-      const double pb = g.idw * pymin(t.hits / 10.0, 1.0);
-      for (int c = 0; c < nd; c++) {
-        const double* z = w.meas + 4 * c;
-        double gd;
-        if (!ok) {
-          gd = __builtin_nan("");
-        } else {
-          double dd[4], y[4], s2 = 0.0;
-          for (int i = 0; i < 4; i++) dd[i] = z[i] - t.mean[i];
-          for (int i = 0; i < 4; i++) {
-            double sm = dd[i];
-            for (int j = 0; j < i; j++) sm -= L[4 * i + j] * y[j];
-            y[i] = sm / L[4 * i + i];
-            s2 += y[i] * y[i];
-          }
-          gd = s2;
-        }
-        double v = t.gal_n > 0 ? nnd[(size_t)slot * g.D + x.det_in(di[c])] : SS_INFTY;
-        if (gd > SS_GATE) v = SS_INFTY;
-        double m = gd * mf;
-        if (t.nvel > 0) {
-          const double ve = norm2(z[0] - pp0, z[1] - pp1);
-          m *= 1.0 + pymin(ve / 50.0, 1.0);
-        }
-        v = al * v + (1 - al) * m;
-        if (t.quality > 0.8) v *= 0.95;
-        if (t.hits > 10 && t.tsu == 0) v *= 0.98;
-        if (t.high_streak > 3) v *= 0.97;
-        if (t.low_streak > 2) v *= 1.05;
-        if (g.idw > 0) v *= (1.0 - pb);
-        row[c] = v;
-      }
+      for (int c = 0; c < nd; c++) row[c] = enhance_clamp(t, x.det(di[c]), row[c], max_d);
     }
-    // _enhance_cost_matrix + clamp
-    for (int c = 0; c < nd; c++) {
-      const double* d = x.det(di[c]);
-      double e = row[c];
-      const double cq = (t.quality + d[7]) / 2.0;
-      e *= clipd(1.0 - (cq - 0.5) * 0.2, 0.8, 1.2);
-      if (t.cls == d[5]) e *= 0.9;
-      double cf = 1.0;
-      if (t.conf > 0.7 && d[4] > 0.7)
-        cf = 0.9;
-      else if (t.conf < 0.3 || d[4] < 0.3)
-        cf = 1.1;
-      e *= cf;
-      if (e > max_d) e = max_d + 1e-5;
-      row[c] = e;
+    if (tr) {
+      __syncthreads();
+      for (int c = 0; c < nd; c++)
+        for (int r = lane; r < nt; r += 64) C[(size_t)c * nt + r] = C2[(size_t)r * nd + c];
     }
   }
   __syncthreads();
@@ -917,7 +1081,7 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
   SCOUNT(3, nt);
   SCOUNT(4, nd);
 #endif
-  const int np_ = lsap_wave(x, C, nt, nd);
+  const int np_ = lsap_wave(x, C, tr ? nd : nt, tr ? nt : nd, tr);
 #ifdef BX_PHASE_TIMING
   __syncthreads();
   SCOUNT(1, SS_NOW() - t1);
@@ -938,7 +1102,7 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
     if (q < np_) {
       r = w.rows[q];
       c = w.cols[q];
-      rej = C[(size_t)r * nd + c] > max_d;
+      rej = (tr ? C[(size_t)c * nt + r] : C[(size_t)r * nd + c]) > max_d;
       ok = !rej;
     }
     const unsigned long long mo = __ballot(ok), mr = __ballot(rej);
@@ -991,12 +1155,7 @@ __device__ void matching_cascade(SsCtx& x, double max_d, const int* ti, int nt, 
     if (age > max_age) break;
     const int nl = wave_compact(nt, [&](int k) { return x.trk[w.lst[ti[k]]].tsu == age; },
                                 [&](int k, int p) { w.lvl[p] = ti[k]; });
-    stable_sort_desc(w.lvl, nl,
-                     [&](int pos) {
-                       const SsTrk& t = x.trk[w.lst[pos]];
-                       return t.quality + t.stability;
-                     },
-                     w.tmp);
+    stable_sort_desc(w.lvl, nl, [&](int pos) { return x.key[pos]; }, w.tmp, x.ks);
     int nut_dummy = 0, nud2 = 0;
     min_cost_matching(x, M_GATED, max_d, w.lvl, nl, w.ud, nud, nullptr, nut_dummy, w.ud2, nud2);
     for (int k = lane; k < nud2; k += 64) w.ud[k] = w.ud2[k];
@@ -1046,13 +1205,20 @@ __device__ void track_update(SsCtx& x, int slot, int di) {
       __syncthreads();
       const double wn = sqrt(wdot(dst, dst, F));
       const double pn = wpw_norm(dst, F, x.w.pwlo, x.w.pwln, x.w.pwleaf) + 1e-8;
+      double* dstn = vecnp(g, x.seq, slot, v);
+      for (int q = lane; q < F; q += 64) dstn[q] = dst[q] / pn;
       if (lane == 0) {
         t.app_cons = 0.9 * t.app_cons + 0.1 * sim;
         g.vwn[vi] = wn;
         g.vden[vi] = pn;
       }
     } else {
-      for (int q = lane; q < F; q += 64) dst[q] = nf[q];
+      double* dstn = vecnp(g, x.seq, slot, v);
+      const double pn = pr[3];
+      for (int q = lane; q < F; q += 64) {
+        dst[q] = nf[q];
+        dstn[q] = nf[q] / pn;
+      }
       if (lane == 0) {
         g.vwn[vi] = pr[2];
         g.vden[vi] = pr[3];
@@ -1114,13 +1280,14 @@ __device__ void track_birth(SsCtx& x, int slot, int di, int id) {
   g.vden[vi] = pr[3];
 }
 
-// ss_match_kernel (one wave per sequence): detections, crowd mode, CMC warp, quality + stable
-// sort, Kalman predict, the three matching stages and the misses.  Hands the matches (fmt), the
-// unmatched detections (faud) and the frame's detection table (fdt) to the next launches.
+// ss_pre_kernel (one wave per sequence): detections, crowd mode, CMC warp, quality + stable sort,
+// Kalman predict.  The detection table (fdt, fdord) and the predicted tracks are the input of
+// ss_cost_kernel and ss_match_kernel.
 __global__ void __launch_bounds__(64)
-    ss_match_kernel(SsDev g, int seq0, const double* __restrict__ dets,
-                    const int* __restrict__ det_off, const double* __restrict__ warps) {
+    ss_pre_kernel(SsDev g, int seq0, const double* __restrict__ dets,
+                  const int* __restrict__ det_off, const double* __restrict__ warps) {
   extern __shared__ __align__(16) char ss_lds[];
+  __shared__ double sbox[4 * 1024];  // crowd test: track boxes; then the detection sort keys
   const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
   SsWs w;
   ws_carve(g, seq, w, ss_lds);
@@ -1167,13 +1334,13 @@ __global__ void __launch_bounds__(64)
       int crowd = 0;
       const int nn = x.ntr;
       if (nn >= 3) {
+        for (int i = lane; i < nn; i += 64) to_tlwh(x.trk[w.lst[i]], sbox + 4 * i);
+        __syncthreads();
         long long high = 0;
         for (int i = 0; i < nn; i++) {
-          double bi[4];
-          to_tlwh(x.trk[w.lst[i]], bi);
+          const double* bi = sbox + 4 * i;
           for (int j = i + 1 + lane; j < nn; j += 64) {
-            double bj[4];
-            to_tlwh(x.trk[w.lst[j]], bj);
+            const double* bj = sbox + 4 * j;
             const double xx1 = pymax(bi[0], bj[0]), yy1 = pymax(bi[1], bj[1]);
             const double xx2 = pymin(bi[2], bj[2]), yy2 = pymin(bi[3], bj[3]);
             const double ww = pymax(0, xx2 - xx1), hh = pymax(0, yy2 - yy1);
@@ -1227,12 +1394,46 @@ __global__ void __launch_bounds__(64)
       d[7] = q;
     }
     __syncthreads();
-    stable_sort_desc(w.dord, x.nk, [&](int r) { return w.dt[(size_t)r * DTW + 7]; }, w.tmp);
+    stable_sort_desc(w.dord, x.nk, [&](int r) { return w.dt[(size_t)r * DTW + 7]; }, w.tmp, sbox);
     for (int p = lane; p < x.ntr; p += 64) track_predict(x.trk[w.lst[p]]);
     __syncthreads();
   }
   if (!fid) fid = sq[Q_HIST];
+  if (lane == 0) {
+    sq[Q_NK] = x.nk;
+    sq[Q_FID] = fid;
+  }
   SSTAMP(2);
+}
+
+// ss_match_kernel (one wave per sequence): the three matching stages of Tracker._enhanced_match
+// (stage 1/2 costs gathered from ss_cost_kernel's matrix).  Hands the matches (fmt), the unmatched
+// tracks (ffut) and detections (faud) to the next launches.
+__global__ void __launch_bounds__(64)
+    ss_match_kernel(SsDev g, int seq0) {
+  extern __shared__ __align__(16) char ss_lds[];
+  __shared__ double skey[1024], sks[1024];
+  const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
+  SsWs w;
+  ws_carve(g, seq, w, ss_lds);
+#ifdef BX_PHASE_TIMING
+  unsigned long long t_last = SS_NOW();
+#endif
+  SsCtx x{g, w, seq, lane, g.trk + (size_t)seq * g.T, g.sq + (size_t)seq * SQS,
+          g.sqd + (size_t)seq * 2, g.lost + (size_t)seq * LOSTN, 0, 0, 0, 0};
+  int* sq = x.sq;
+  const int* order = g.order + (size_t)seq * g.T;
+  x.ntr = sq[Q_NTR];
+  x.nlost = sq[Q_NLOST];
+  x.nk = sq[Q_NK];
+  for (int p = lane; p < x.ntr; p += 64) {
+    w.lst[p] = order[p];
+    const SsTrk& t = x.trk[order[p]];
+    skey[p] = t.quality + t.stability;  // the cascade levels' sort key (linear_assignment.py:276-285)
+  }
+  x.key = skey;
+  x.ks = sks;
+  __syncthreads();
 
   // ---- Tracker._enhanced_match (tracker.py:183-281, P6) --------------------------------------
   x.nm = 0;
@@ -1317,9 +1518,8 @@ __global__ void __launch_bounds__(64)
     sq[Q_NFUT] = nfut;
     sq[Q_NM] = x.nm;
     sq[Q_NAUD] = naud;
-    sq[Q_FID] = fid;
-    sq[Q_NK] = x.nk;
   }
+
   SCOUNT(6, x.nm);
   SSTAMP(7);
 }
@@ -1560,7 +1760,12 @@ __global__ void __launch_bounds__(64) ss_fit_kernel(SsDev g, int seq0) {
   if (bdk >= 0) {  // a track born this frame: its first feature vector
     const double* nf = g.nf + ((size_t)seq * g.D + bdk) * F;
     double* dst = vecp(g, seq, slot, 0);
-    for (int q = lane; q < F; q += 64) dst[q] = nf[q];
+    double* dstn = vecnp(g, seq, slot, 0);
+    const double pn = g.dprep[((size_t)seq * g.D + bdk) * 4 + 3];
+    for (int q = lane; q < F; q += 64) {
+      dst[q] = nf[q];
+      dstn[q] = nf[q] / pn;
+    }
   }
   int* gv = g.gal_v + ((size_t)seq * g.T + slot) * g.GB;
   double* gq = g.gal_q + ((size_t)seq * g.T + slot) * g.GB;
@@ -1678,6 +1883,11 @@ static int ss_probe_end(bx_ss* e, int stage, hipStream_t st) {
   return BX_OK;
 }
 
+static size_t ss_lds_bytes(const SsDev& d) {
+  return d.ws_lds == 1 ? (size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4
+                       : (d.ws_lds == 2 ? (size_t)ws_lsap_bytes(d.N) : 0);
+}
+
 static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int* off,
                      const double* embs, const double* warps, double* out, int* cnt,
                      hipStream_t st) {
@@ -1689,31 +1899,48 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 0, st))) return rc;
   if ((rc = ss_probe_begin(e, 1, st))) return rc;
-  hipLaunchKernelGGL(ss_nn_kernel, dim3(d.T, nseq), dim3(64), 0, st, d, seq0, off);
+  // tracks per wave: share detection loads among 4 when that still leaves ~8 waves per CU
+  const long qtracks = (long)d.T * nseq;
+  if (qtracks >= 4 * 2048)
+    hipLaunchKernelGGL((ss_nn_kernel<4, 4>), dim3((d.T + 3) / 4, nseq), dim3(64), 0, st, d, seq0,
+                       off);
+  else if (qtracks >= 2 * 2048)
+    hipLaunchKernelGGL((ss_nn_kernel<2, 2>), dim3((d.T + 1) / 2, nseq), dim3(64), 0, st, d, seq0,
+                       off);
+  else
+    hipLaunchKernelGGL((ss_nn_kernel<1, 1>), dim3(d.T, nseq), dim3(64), 0, st, d, seq0, off);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 1, st))) return rc;
   if ((rc = ss_probe_begin(e, 2, st))) return rc;
   hipLaunchKernelGGL(ss_rec_kernel, dim3(LOSTN, nseq), dim3(256), 0, st, d, seq0, off, embs);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 2, st))) return rc;
-  const size_t lds = d.ws_lds ? (size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4 : 0;
+  const size_t lds = ss_lds_bytes(d);
   if ((rc = ss_probe_begin(e, 3, st))) return rc;
-  hipLaunchKernelGGL(ss_match_kernel, dim3(nseq), dim3(64), lds, st, d, seq0, dets, off, warps);
+  hipLaunchKernelGGL(ss_pre_kernel, dim3(nseq), dim3(64), lds, st, d, seq0, dets, off, warps);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 3, st))) return rc;
   if ((rc = ss_probe_begin(e, 4, st))) return rc;
-  hipLaunchKernelGGL(ss_update_kernel, dim3(d.T < d.D ? d.T : d.D, nseq), dim3(64), 0, st, d,
-                     seq0);
+  hipLaunchKernelGGL(ss_cost_kernel, dim3(d.T, nseq), dim3(64), 0, st, d, seq0);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 4, st))) return rc;
   if ((rc = ss_probe_begin(e, 5, st))) return rc;
-  hipLaunchKernelGGL(ss_post_kernel, dim3(nseq), dim3(64), lds, st, d, seq0, off, out, cnt);
+  hipLaunchKernelGGL(ss_match_kernel, dim3(nseq), dim3(64), lds, st, d, seq0);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 5, st))) return rc;
   if ((rc = ss_probe_begin(e, 6, st))) return rc;
-  hipLaunchKernelGGL(ss_fit_kernel, dim3(d.T + LOSTN, nseq), dim3(64), 0, st, d, seq0);
+  hipLaunchKernelGGL(ss_update_kernel, dim3(d.T < d.D ? d.T : d.D, nseq), dim3(64), 0, st, d,
+                     seq0);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 6, st))) return rc;
+  if ((rc = ss_probe_begin(e, 7, st))) return rc;
+  hipLaunchKernelGGL(ss_post_kernel, dim3(nseq), dim3(64), lds, st, d, seq0, off, out, cnt);
+  SCHK(hipGetLastError());
+  if ((rc = ss_probe_end(e, 7, st))) return rc;
+  if ((rc = ss_probe_begin(e, 8, st))) return rc;
+  hipLaunchKernelGGL(ss_fit_kernel, dim3(d.T + LOSTN, nseq), dim3(64), 0, st, d, seq0);
+  SCHK(hipGetLastError());
+  if ((rc = ss_probe_end(e, 8, st))) return rc;
   return BX_OK;
 }
 
@@ -1759,7 +1986,9 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   d.wsd_n = ws_doubles(d.T, d.D, d.N);
   // the frame kernel's workspace in LDS when it fits beside ~3 other workgroups per CU
   const size_t ws_bytes = (size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4;
-  d.ws_lds = ws_bytes <= 48 * 1024 ? 1 : 0;
+  // all of it in LDS when it fits beside ~3 other workgroups per CU; else the LSAP state alone
+  // (the solver's inner loops) when that fits in one CU's 160 KB with room to spare
+  d.ws_lds = ws_bytes <= 48 * 1024 ? 1 : (ws_lsap_bytes(d.N) <= 120 * 1024 ? 2 : 0);
   const size_t S = d.S, T = d.T, D = d.D, F = d.F, VP = d.VP, GB = d.GB;
   size_t off = 0;
   auto cb = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
@@ -1768,6 +1997,7 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   const size_t o_gq = cb(S * T * GB * sizeof(double));
   const size_t o_gt = cb(S * T * GB * sizeof(int));
   const size_t o_vec = cb(S * T * VP * F * sizeof(double));
+  const size_t o_vecn = cb(S * T * VP * F * sizeof(double));
   const size_t o_vden = cb(S * T * VP * sizeof(double));
   const size_t o_vwn = cb(S * T * VP * sizeof(double));
   const size_t o_sq = cb((S + 1) * SQS * sizeof(int));
@@ -1780,7 +2010,9 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   const size_t o_dn = cb(S * D * F * sizeof(double));
   const size_t o_nf = cb(S * D * F * sizeof(double));
   const size_t o_rec = cb(S * LOSTN * D * sizeof(double));
-  const size_t o_cost = cb(S * 2 * T * D * sizeof(double));
+  const size_t o_cost = cb(S * 4 * T * D * sizeof(double));
+  const size_t o_cfull = cb(S * T * D * sizeof(double));
+  const size_t o_cfullT = cb(S * T * D * sizeof(double));
   const size_t o_fdt = cb(S * D * DTW * sizeof(double));
   const size_t o_fdord = cb(S * D * sizeof(int));
   const size_t o_faud = cb(S * D * sizeof(int));
@@ -1803,6 +2035,7 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   d.gal_q = (double*)(base + o_gq);
   d.gal_t = (int*)(base + o_gt);
   d.vec = (double*)(base + o_vec);
+  d.vecn = (double*)(base + o_vecn);
   d.vden = (double*)(base + o_vden);
   d.vwn = (double*)(base + o_vwn);
   d.sq = (int*)(base + o_sq);
@@ -1816,6 +2049,8 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   d.nf = (double*)(base + o_nf);
   d.recsim = (double*)(base + o_rec);
   d.cost = (double*)(base + o_cost);
+  d.cfull = (double*)(base + o_cfull);
+  d.cfullT = (double*)(base + o_cfullT);
   d.fdt = (double*)(base + o_fdt);
   d.fdord = (int*)(base + o_fdord);
   d.faud = (int*)(base + o_faud);
@@ -1842,7 +2077,9 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   SCHK(hipMemcpy(d.sq, q.data(), q.size() * sizeof(int), hipMemcpyHostToDevice));
   SCHK(hipMemcpy(d.sqd, qd.data(), qd.size() * sizeof(double), hipMemcpyHostToDevice));
   if (d.ws_lds) {
-    const int lds = (int)((size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4);
+    const int lds = (int)ss_lds_bytes(d);
+    SCHK(hipFuncSetAttribute((const void*)ss_pre_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     SCHK(hipFuncSetAttribute((const void*)ss_match_kernel,
                              hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     SCHK(hipFuncSetAttribute((const void*)ss_post_kernel,

@@ -478,7 +478,7 @@ class SsEngine:
     per frame the detection-feature kernel, the NN-gallery distance (fp64 MFMA), the recovery
     similarities and the frame kernel (one wave per sequence)."""
 
-    STAGES = ["prep", "nn", "recovery", "match", "update", "post", "fit"]
+    STAGES = ["prep", "nn", "recovery", "pre", "cost", "match", "update", "post", "fit"]
 
     def __init__(self, n_seq: int = 1, track_cap: int = 256, det_cap: int = 256,
                  emb_dim: int = 512, vec_cap: int = 32, params: SsParams | None = None):

@@ -10,6 +10,7 @@
  * gallery's partial_fit budget pruning and the output rows — runs on the GPU behind these entry
  * points: per frame a detection-feature kernel (wave per detection), the gallery distance
  * (fp64 MFMA, wave per confirmed track and detection block), the recovery similarities, the
+ * pre-match kernel (one wave per sequence), the stage 1/2 costs (wave per confirmed track), the
  * matching kernel (one wave per sequence), the track updates (wave per match), the post-match
  * kernel (recovery, births, lost buffer, outputs; wave per sequence) and partial_fit (wave per
  * track).
@@ -94,8 +95,8 @@ int bx_ss_tracks_host(bx_ss *e, int seq, int cap, int32_t *ids, int32_t *state, 
  * output rows, max frame counter, matches} — bench.py's unit counts. */
 int bx_ss_frame_stats_host(bx_ss *e, int seq0, int nseq, int64_t *sums);
 /* Timing probe: stage 0 = detection features, 1 = gallery distance, 2 = recovery similarities,
- * 3 = matching, 4 = track updates, 5 = post-match, 6 = partial_fit; -1 = off (see
- * bx_boost_probe). */
+ * 3 = pre-match (crowd, warp, quality, predict), 4 = stage 1/2 costs, 5 = matching, 6 = track
+ * updates, 7 = post-match, 8 = partial_fit; -1 = off (see bx_boost_probe). */
 int bx_ss_probe(bx_ss *e, int stage);
 int bx_ss_probe_read(bx_ss *e, double *total_ms, int *count);
 
