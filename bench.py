@@ -35,6 +35,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "association FPS (frames/sec) at N_tracks×N_dets×feat_dim, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+F64_MFMA_PEAK_TFS = 73.1  # dense v_mfma_f64_16x16x4 rate measured on the box (tools/probes/mfma_f64_peak.hip)
 
 CONFIGS = {
     # name: (tracker, n_obj, emb_dim, tracker params (YAML defaults))
@@ -343,6 +344,16 @@ def main():
             per_launch = stage_bytes(dominant, units, F)
         achieved = per_launch / (dom_ms * 1e-3) / 1e9
         traffic = load_traffic(args.config, dominant)
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
+        if sss and dominant == "nn":
+            # the gallery distance is fp64 matrix-core work: 2 x sample rows x detections x F
+            # per launch against the measured dense fp64 MFMA rate
+            flops = 2.0 * units["rows"] * (units["dets"] / max(units["seqs"], 1)) * F
+            tf = flops / (dom_ms * 1e-3) / 1e12
+            roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": F64_MFMA_PEAK_TFS,
+                    "unit": "TFLOP/s", "frac": round(tf / F64_MFMA_PEAK_TFS, 4),
+                    "traffic": traffic, "algorithmic_flops_per_launch": int(flops)}
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -355,9 +366,7 @@ def main():
                        "n_dets_mean": round(mean_d, 1), "feat_dim": F,
                        "emb_dtype": "f64" if emb_bytes == 8 else "f32",
                        "parallelism": f"seq-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": dominant,
+            "roofline": {**roof, "kernel": dominant,
                          "kernel_ms": round(dom_ms, 4),
                          "algorithmic_bytes_per_launch": int(per_launch),
                          "units_last_frame": units,

@@ -553,6 +553,20 @@ __device__ int filter_matched(int* a, int na, const int* mt, int m0, int m1, int
   return n;
 }
 
+// filter_matched with a membership table fl[0..nu) (LDS): O(na + matches) instead of O(na x m)
+__device__ int filter_matched_fl(int* a, int na, const int* mt, int m0, int m1, int col, int* tmp,
+                                 int* fl, int nu) {
+  const int lane = threadIdx.x & 63;
+  for (int k = lane; k < nu; k += 64) fl[k] = 0;
+  __syncthreads();
+  for (int q = m0 + lane; q < m1; q += 64) fl[mt[2 * q + col]] = 1;
+  __syncthreads();
+  const int n = wave_compact(na, [&](int k) { return fl[a[k]] == 0; }, [&](int k, int p) { tmp[p] = a[k]; });
+  for (int k = lane; k < n; k += 64) a[k] = tmp[k];
+  __syncthreads();
+  return n;
+}
+
 __device__ __forceinline__ bool in_list(const int* a, int n, int v) {
   for (int k = 0; k < n; k++)
     if (a[k] == v) return true;
@@ -760,6 +774,8 @@ struct SsCtx {
   int* lost;
   int ntr, nlost, nk, nm;
   double* key;  // match kernel: quality + stability by list position (LDS)
+  int* tsu;     // match kernel: time_since_update by list position (LDS)
+  int* flt;     // match kernel: scratch table (LDS, 1024 ints)
   double* ks;   // match kernel: sort-key scratch (LDS)
   __device__ const double* det(int i) const { return w.dt + (size_t)w.dord[i] * DTW; }
   __device__ int det_in(int i) const { return (int)det(i)[6]; }
@@ -793,17 +809,27 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
     while (sink == -1) {
       if (lane == 0) w.SR[i] = 1;
       const double ui = w.u[i];
-      const double* crow = C + (size_t)i * CC;
+      const double* __restrict__ crow = C + (size_t)i * CC;
       double m = INF;
-      for (int j = lane; j < CC; j += 64) {
-        if (w.SC[j]) continue;
-        const double r = minVal + crow[j] - ui - w.v[j];
-        double sp = w.spc[j];
-        if (r < sp) {
-          w.path[j] = i;
-          w.spc[j] = sp = r;
+      for (int j0 = 0; j0 < CC; j0 += 256) {  // the row's loads issued four at a time
+        double cv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int j = j0 + 64 * u + lane;
+          cv[u] = j < CC ? crow[j] : 0.0;
         }
-        m = fmin(m, sp);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int j = j0 + 64 * u + lane;
+          if (j >= CC || w.SC[j]) continue;
+          const double r = minVal + cv[u] - ui - w.v[j];
+          double sp = w.spc[j];
+          if (r < sp) {
+            w.path[j] = i;
+            w.spc[j] = sp = r;
+          }
+          m = fmin(m, sp);
+        }
       }
       m = wave_min_d(m);
       int last_un = -1, first_eq = 0x7fffffff;
@@ -1132,28 +1158,47 @@ __device__ void matching_cascade(SsCtx& x, double max_d, const int* ti, int nt, 
   const int lane = x.lane;
   int nud = nd;
   for (int k = lane; k < nd; k += 64) w.ud[k] = di[k];
-  int na = 0;
-  if (lane == 0) {
-    for (int k = 0; k < nt; k++) {
-      const int a = x.trk[w.lst[ti[k]]].tsu;
-      bool seen = false;
-      for (int q = 0; q < na && !seen; q++) seen = w.ages[q] == a;
-      if (!seen) w.ages[na++] = a;
-    }
-    for (int p = 1; p < na; p++)
-      for (int y = p; y > 0 && w.ages[y - 1] > w.ages[y]; y--) {
-        const int tmp = w.ages[y];
-        w.ages[y] = w.ages[y - 1];
-        w.ages[y - 1] = tmp;
-      }
-  }
-  na = bcast(na);
-  __syncthreads();
+  // the distinct time_since_update values, ascending (only levels <= max_age are matched)
   const int max_age = x.sq[Q_MAXAGE];
+  int* pres = x.flt;  // presence table over ages 0..max_age (LDS, 1024 entries)
+  const int amax = max_age < 1023 ? max_age : 1023;
+  for (int a = lane; a <= amax; a += 64) pres[a] = 0;
+  __syncthreads();
+  int over = 0;
+  for (int k = lane; k < nt; k += 64) {
+    const int a = x.tsu[ti[k]];
+    if (a <= amax)
+      pres[a] = 1;
+    else if (a <= max_age)
+      over = 1;
+  }
+  over = __any(over);
+  __syncthreads();
+  int na = wave_compact(amax + 1, [&](int a) { return pres[a] != 0; },
+                        [&](int a, int p) { w.ages[p] = a; });
+  if (over) {  // ages beyond the table (max_age >= 1024): the levels up to max_age, serially
+    if (lane == 0) {
+      for (int k = 0; k < nt; k++) {
+        const int a = x.tsu[ti[k]];
+        if (a <= amax || a > max_age) continue;
+        bool seen = false;
+        for (int q = 0; q < na && !seen; q++) seen = w.ages[q] == a;
+        if (!seen) w.ages[na++] = a;
+      }
+      for (int p = 1; p < na; p++)
+        for (int y = p; y > 0 && w.ages[y - 1] > w.ages[y]; y--) {
+          const int tmp = w.ages[y];
+          w.ages[y] = w.ages[y - 1];
+          w.ages[y - 1] = tmp;
+        }
+    }
+    na = bcast(na);
+  }
+  __syncthreads();
   for (int q = 0; q < na; q++) {
     const int age = w.ages[q];
     if (age > max_age) break;
-    const int nl = wave_compact(nt, [&](int k) { return x.trk[w.lst[ti[k]]].tsu == age; },
+    const int nl = wave_compact(nt, [&](int k) { return x.tsu[ti[k]] == age; },
                                 [&](int k, int p) { w.lvl[p] = ti[k]; });
     stable_sort_desc(w.lvl, nl, [&](int pos) { return x.key[pos]; }, w.tmp, x.ks);
     int nut_dummy = 0, nud2 = 0;
@@ -1413,6 +1458,8 @@ __global__ void __launch_bounds__(64)
     ss_match_kernel(SsDev g, int seq0) {
   extern __shared__ __align__(16) char ss_lds[];
   __shared__ double skey[1024], sks[1024];
+  __shared__ int flt[1024], fld[1024];  // membership tables: track positions, sorted detections
+  __shared__ int stsu[1024], sage[1024];
   const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
   SsWs w;
   ws_carve(g, seq, w, ss_lds);
@@ -1430,8 +1477,11 @@ __global__ void __launch_bounds__(64)
     w.lst[p] = order[p];
     const SsTrk& t = x.trk[order[p]];
     skey[p] = t.quality + t.stability;  // the cascade levels' sort key (linear_assignment.py:276-285)
+    stsu[p] = t.tsu;
   }
   x.key = skey;
+  x.tsu = stsu;
+  x.flt = sage;
   x.ks = sks;
   __syncthreads();
 
@@ -1454,23 +1504,29 @@ __global__ void __launch_bounds__(64)
   __syncthreads();
   const double thr = x.sqd[0];
   SSTAMP(3);
+  const int NT = x.ntr, NK = x.nk;
   if (nhi && ncf) {  // stage 1: high-confidence detections, confirmed tracks
     const int m0 = x.nm;
     matching_cascade(x, thr * 0.8, w.conf_t, ncf, w.hi, nhi);
-    naut = filter_matched(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp);
-    naud = filter_matched(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp);
+    naut = filter_matched_fl(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp, flt, NT);
+    naud = filter_matched_fl(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp, fld, NK);
   }
   SSTAMP(4);
   {  // stage 2: medium-confidence detections, remaining confirmed tracks
-    const int nrt = wave_compact(naut, [&](int k) { return in_list(w.conf_t, ncf, w.aut[k]); },
-                                 [&](int k, int q) { w.ti2[q] = w.aut[k]; });
-    const int nrm = wave_compact(nmed, [&](int k) { return in_list(w.aud, naud, w.med[k]); },
+    // the unmatched tracks are all confirmed (a subset of conf_t)
+    const int nrt = naut;
+    for (int k = lane; k < naut; k += 64) w.ti2[k] = w.aut[k];
+    for (int k = lane; k < NK; k += 64) fld[k] = 0;
+    __syncthreads();
+    for (int k = lane; k < naud; k += 64) fld[w.aud[k]] = 1;
+    __syncthreads();
+    const int nrm = wave_compact(nmed, [&](int k) { return fld[w.med[k]] != 0; },
                                  [&](int k, int q) { w.rd[q] = w.med[k]; });
     if (nrm && nrt) {
       const int m0 = x.nm;
       matching_cascade(x, thr, w.ti2, nrt, w.rd, nrm);
-      naut = filter_matched(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp);
-      naud = filter_matched(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp);
+      naut = filter_matched_fl(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp, flt, NT);
+      naud = filter_matched_fl(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp, fld, NK);
     }
   }
   SSTAMP(5);
@@ -1478,19 +1534,24 @@ __global__ void __launch_bounds__(64)
   int ncand = nun;
   for (int k = lane; k < nun; k += 64) w.cand[k] = w.unconf_t[k];
   __syncthreads();
-  ncand += wave_compact(naut, [&](int k) { return x.trk[w.lst[w.aut[k]]].tsu == 1; },
+  ncand += wave_compact(naut, [&](int k) { return stsu[w.aut[k]] == 1; },
                         [&](int k, int q) { w.cand[nun + q] = w.aut[k]; });
-  const int nrd = wave_compact(naud, [&](int k) { return !in_list(w.lo, nlo, w.aud[k]); },
+  (void)nlo;
+  const int nrd = wave_compact(naud, [&](int k) { return !(x.det(w.aud[k])[4] < g.tlo); },
                                [&](int k, int q) { w.rd[q] = w.aud[k]; });
   int nut3 = 0;
   if (nrd && ncand) {
     const int m0 = x.nm;
     int nud3 = 0;
     min_cost_matching(x, M_IOU, g.max_iou, w.cand, ncand, w.rd, nrd, w.ut3, nut3, w.ud, nud3);
-    naut = filter_matched(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp);
-    naud = filter_matched(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp);
+    naut = filter_matched_fl(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp, flt, NT);
+    naud = filter_matched_fl(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp, fld, NK);
   }
-  int nfut = wave_compact(naut, [&](int k) { return !in_list(w.cand, ncand, w.aut[k]); },
+  for (int k = lane; k < NT; k += 64) flt[k] = 0;
+  __syncthreads();
+  for (int k = lane; k < ncand; k += 64) flt[w.cand[k]] = 1;
+  __syncthreads();
+  int nfut = wave_compact(naut, [&](int k) { return flt[w.aut[k]] == 0; },
                           [&](int k, int q) { w.fut[q] = w.aut[k]; });
   for (int k = lane; k < nut3; k += 64) w.fut[nfut + k] = w.ut3[k];
   nfut += nut3;
