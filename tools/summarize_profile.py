@@ -20,7 +20,10 @@ STAGE_OF = {"det_feature_kernel": "det_features", "predict_kernel": "predict",
             "cov_predict_kernel": "cov_predict", "cov_predict_gmc_kernel": "cov_predict",
             "feature_kernel": "features", "finish_kernel": "finish",
             "ocsort_frame_kernel": "ocsort_frame", "boost_embcost_kernel": "embcost",
-            "boost_frame_kernel": "frame", "boost_feature_kernel": "feature"}
+            "boost_frame_kernel": "frame", "boost_feature_kernel": "feature",
+            "ss_prep_kernel": "prep", "ss_nn_kernel": "nn", "ss_rec_kernel": "recovery",
+            "ss_pre_kernel": "pre", "ss_cost_kernel": "cost", "ss_match_kernel": "match",
+            "ss_update_kernel": "update", "ss_post_kernel": "post", "ss_fit_kernel": "fit"}
 
 
 def kname(full):
