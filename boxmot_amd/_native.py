@@ -110,7 +110,7 @@ EXPORTS = [
     "bx_engine_reset", "bx_engine_step", "bx_engine_update_host", "bx_engine_status",
     "bx_engine_counters_host", "bx_engine_set_id_count", "bx_engine_tracks_host",
     "bx_engine_probe", "bx_engine_probe_read", "bx_engine_frame_stats_host",
-    "bx_iou_batch", "bx_pairwise_cost", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
+    "bx_iou_batch", "bx_pairwise_cost", "bx_aw_max_metric", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
     "bx_kf_multi_predict", "bx_kf_update", "bx_kf_gating_distance", "bx_linear_assignment",
     "bx_nn_cosine_distance", "bx_ocsort_create", "bx_ocsort_destroy", "bx_ocsort_reset", "bx_ocsort_step",
     "bx_ocsort_update_host", "bx_ocsort_status", "bx_ocsort_counters_host",
@@ -144,6 +144,7 @@ _SIGS = {
     "bx_iou_batch": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp], C.c_int),
     "bx_pairwise_cost": ([C.c_int, _vp, C.c_int, C.c_int, _vp, C.c_int, C.c_int, C.c_double,
                           C.c_double, _vp, _vp], C.c_int),
+    "bx_aw_max_metric": ([_vp, C.c_int, C.c_int, C.c_double, C.c_double, _vp, _vp], C.c_int),
     "bx_fuse_score": ([_vp, C.c_int, C.c_int, _vp, _vp], C.c_int),
     "bx_embedding_distance": ([_vp, C.c_int, _vp, C.c_int, C.c_int, _vp, _vp], C.c_int),
     "bx_kf_initiate": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),

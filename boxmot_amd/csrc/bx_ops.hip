@@ -40,6 +40,48 @@ __global__ void pairwise_kernel(int kind, const double* a, int na, int lda, cons
   }
 }
 
+// compute_aw_max_metric (utils/association.py:320-374): one workgroup; thread per row, then per
+// column, for the weights (LDS), then the grid of products in ((w * rw) * cw) * emb order
+constexpr int AW_MAX = 4096;
+__device__ double aw_weight(const double* v, int n, int stride, double bottom, bool* apply) {
+  double m1 = -INFINITY, m2 = -INFINITY;
+  int cnt = 0;
+  for (int k = 0; k < n; k++) {
+    const double c = v[(size_t)k * stride];
+    if (!(c > 0)) continue;
+    cnt++;
+    if (c > m1) {
+      m2 = m1;
+      m1 = c;
+    } else if (c > m2) {
+      m2 = c;
+    }
+  }
+  *apply = cnt >= 2;
+  if (cnt < 2) return 1.0;
+  if (m1 == 0) return 0.0;
+  const double ex = m2 / m1 - bottom;
+  return 1 - (ex > 0 ? ex : 0.0) / (1 - bottom);
+}
+__global__ void __launch_bounds__(1024) aw_kernel(const double* emb, int nr, int nc, double w0,
+                                                  double bottom, double* out) {
+  __shared__ double rw[AW_MAX], cw[AW_MAX];
+  __shared__ bool ra[AW_MAX], ca[AW_MAX];
+  for (int i = threadIdx.x; i < nr; i += blockDim.x)
+    rw[i] = aw_weight(emb + (size_t)i * nc, nc, 1, bottom, &ra[i]);
+  for (int j = threadIdx.x; j < nc; j += blockDim.x)
+    cw[j] = aw_weight(emb + j, nr, nc, bottom, &ca[j]);
+  __syncthreads();
+  const size_t n = (size_t)nr * nc;
+  for (size_t k = threadIdx.x; k < n; k += blockDim.x) {
+    const int i = (int)(k / nc), j = (int)(k % nc);
+    double w = w0;
+    if (ra[i]) w *= rw[i];
+    if (ca[j]) w *= cw[j];
+    out[k] = w * emb[k];
+  }
+}
+
 __global__ void fuse_kernel(double* c, int nr, int nc, const double* conf) {
   const size_t n = (size_t)nr * nc;
   for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n;
@@ -198,6 +240,17 @@ int bx_pairwise_cost(int kind, const double* a, int na, int lda, const double* b
   if (lda < 4 || ldb < 4) return op_err(BX_ERR_INVALID, "row stride below 4");
   hipLaunchKernelGGL(pairwise_kernel, dim3(grid_for((size_t)na * nb)), dim3(256), 0,
                      (hipStream_t)stream, kind, a, na, lda, b, nb, ldb, w, h, out);
+  OPCHK(hipGetLastError());
+  return BX_OK;
+}
+
+int bx_aw_max_metric(const double* emb, int nr, int nc, double w_assoc, double bottom,
+                     double* out, void* stream) {
+  if (nr < 0 || nc < 0 || nr > AW_MAX || nc > AW_MAX)
+    return op_err(BX_ERR_INVALID, "aw_max_metric: sizes out of range (0..4096)");
+  if (!nr || !nc) return BX_OK;
+  hipLaunchKernelGGL(aw_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, emb, nr, nc, w_assoc,
+                     bottom, out);
   OPCHK(hipGetLastError());
   return BX_OK;
 }

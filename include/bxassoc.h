@@ -13,6 +13,7 @@
  *                          BotSort.update            boxmot/trackers/botsort/botsort.py:94-166
  *                          (+ per-frame glue         botsort.py:168-411, botsort_utils.py:1-81)
  *   bx_iou_batch           AssociationFunction.iou_batch   boxmot/utils/iou.py:50-67
+ *   bx_aw_max_metric       compute_aw_max_metric            boxmot/utils/association.py:320-374
  *   bx_pairwise_cost       AssociationFunction.{iou,hmiou,giou,diou,ciou,centroid}_batch
  *                          boxmot/utils/iou.py:50-307, registry :320-346
  *   bx_fuse_score          matching.enhanced_fuse_score    boxmot/utils/matching.py:488-555
@@ -142,6 +143,11 @@ enum { BX_ASSO_IOU = 0, BX_ASSO_HMIOU = 1, BX_ASSO_GIOU = 2, BX_ASSO_DIOU = 3, B
 int bx_pairwise_cost(int kind, const double *a, int na, int lda, const double *b, int nb, int ldb,
                      double w, double h, double *out, void *stream);
 int bx_fuse_score(double *cost, int nr, int nc, const double *confs, void *stream);
+/* compute_aw_max_metric (utils/association.py:320-374, DeepOCSort's adaptive appearance weight):
+ * out = ((w_assoc * row_weight) * col_weight) * emb, weights from the two largest positive entries
+ * of each row / column; nr, nc <= 4096. */
+int bx_aw_max_metric(const double *emb, int nr, int nc, double w_assoc, double bottom, double *out,
+                     void *stream);
 /* float32 features, numpy float32 norms, scipy cdist-cosine summation order, clipped at 0 */
 int bx_embedding_distance(const float *trk, int nt, const float *det, int nd, int f, double *out,
                           void *stream);

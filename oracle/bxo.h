@@ -28,6 +28,9 @@ enum { BXO_ASSO_IOU = 0, BXO_ASSO_HMIOU = 1, BXO_ASSO_GIOU = 2, BXO_ASSO_DIOU = 
 void bxo_asso_batch(int kind, const double *a, int na, const double *b, int nb, double w,
                     double h, double *out);
 double bxo_atan(double x);
+/* utils/association.py:320-374 compute_aw_max_metric: out[nr,nc] */
+void bxo_aw_max_metric(const double *emb, int nr, int nc, double w_assoc, double bottom,
+                       double *out);
 /* utils/matching.py:488-555  enhanced_fuse_score, in place on cost[nr,nc] */
 void bxo_fuse_score(double *cost, int nr, int nc, const double *confs);
 /* utils/matching.py:230-316  enhanced_embedding_distance (float32 features, scipy cosine) */

@@ -697,3 +697,51 @@ void bxo_asso_batch(int kind, const double *a, int na, const double *b, int nb, 
     for (int i = 0; i < na; i++)
         for (int j = 0; j < nb; j++) out[(size_t)i * nb + j] = bxo_pair_cost(kind, a + 4 * i, b + 4 * j, w, h);
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* utils/association.py:320-374 compute_aw_max_metric (DeepOCSort's adaptive embedding weight):
+ * per row, then per column, over the strictly positive entries: weight = 1 - max(ratio - bottom,
+ * 0) / (1 - bottom) with ratio = second largest / largest (1 when fewer than two), applied as
+ * ((w * row_weight) * col_weight) * emb_cost. */
+static double aw_weight(const double *v, int n, int stride, double bottom, int *apply) {
+    double m1 = -INFINITY, m2 = -INFINITY;
+    int cnt = 0;
+    for (int k = 0; k < n; k++) {
+        const double c = v[(size_t)k * stride];
+        if (!(c > 0)) continue;
+        cnt++;
+        if (c > m1) {
+            m2 = m1;
+            m1 = c;
+        } else if (c > m2) {
+            m2 = c;
+        }
+    }
+    *apply = cnt >= 2;
+    if (cnt < 2) return 1.0;
+    if (m1 == 0) return 0.0;
+    const double ratio = m2 / m1;
+    const double ex = ratio - bottom;
+    return 1 - (ex > 0 ? ex : 0.0) / (1 - bottom);
+}
+
+void bxo_aw_max_metric(const double *emb, int nr, int nc, double w_assoc, double bottom,
+                       double *out) {
+    double *rw = (double *)malloc(sizeof(double) * (size_t)(nr ? nr : 1));
+    double *cw = (double *)malloc(sizeof(double) * (size_t)(nc ? nc : 1));
+    int *ra = (int *)malloc(sizeof(int) * (size_t)(nr ? nr : 1));
+    int *ca = (int *)malloc(sizeof(int) * (size_t)(nc ? nc : 1));
+    for (int i = 0; i < nr; i++) rw[i] = aw_weight(emb + (size_t)i * nc, nc, 1, bottom, ra + i);
+    for (int j = 0; j < nc; j++) cw[j] = aw_weight(emb + j, nr, nc, bottom, ca + j);
+    for (int i = 0; i < nr; i++)
+        for (int j = 0; j < nc; j++) {
+            double w = w_assoc;
+            if (ra[i]) w *= rw[i];
+            if (ca[j]) w *= cw[j];
+            out[(size_t)i * nc + j] = w * emb[(size_t)i * nc + j];
+        }
+    free(rw);
+    free(cw);
+    free(ra);
+    free(ca);
+}

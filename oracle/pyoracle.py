@@ -156,6 +156,7 @@ def lib():
         L.bxo_lsap.argtypes = [_dp, C.c_int, C.c_int, _ip, _ip]
         L.bxo_asso_batch.argtypes = [C.c_int, _dp, C.c_int, _dp, C.c_int, C.c_double,
                                      C.c_double, _dp]
+        L.bxo_aw_max_metric.argtypes = [_dp, C.c_int, C.c_int, C.c_double, C.c_double, _dp]
         L.bxo_atan.argtypes = [C.c_double]
         L.bxo_atan.restype = C.c_double
         L.bxo_exp.argtypes = [C.c_double]
@@ -188,6 +189,15 @@ def asso_batch(kind, a, b, w=1920, h=1080):
     out = np.zeros((a.shape[0], b.shape[0]))
     lib().bxo_asso_batch(ASSO_KIND[kind], _d(a), a.shape[0], _d(b), b.shape[0], float(w),
                          float(h), _d(out))
+    return out
+
+
+def aw_max_metric(emb_cost, w_assoc, bottom=0.5):
+    """compute_aw_max_metric (utils/association.py:320-374) restated."""
+    e = np.ascontiguousarray(emb_cost, np.float64)
+    out = np.zeros_like(e)
+    lib().bxo_aw_max_metric(_d(e), e.shape[0], e.shape[1], float(w_assoc), float(bottom),
+                            _d(out))
     return out
 
 

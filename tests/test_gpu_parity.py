@@ -83,6 +83,21 @@ def test_pairwise_cost_registry(torch_cuda, mode):
     assert empty.shape == (0, 512)
 
 
+def test_aw_max_metric_exact(torch_cuda):
+    """bx_aw_max_metric vs the reference's vectors (utils/association.py:320-374), bitwise."""
+    torch = torch_cuda
+    from boxmot_amd import _native as N
+
+    L = N.load()
+    g = np.load(GOLDEN / "asso_funcs.npz")
+    for k in range(int(g["aw_count"])):
+        e = dev(torch, g[f"aw{k}_in"])
+        out = torch.empty_like(e)
+        N.check(L.bx_aw_max_metric(e.data_ptr(), e.shape[0], e.shape[1], float(g[f"aw{k}_w"]),
+                                   0.5, out.data_ptr(), None))
+        np.testing.assert_array_equal(host(out), g[f"aw{k}_out"])
+
+
 def test_iou_fuse_embedding_exact(torch_cuda, K):
     torch = torch_cuda
     from boxmot_amd import _native as N

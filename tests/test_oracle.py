@@ -226,3 +226,11 @@ def test_atan_restatement_within_one_ulp():
     got = np.array([po.lib().bxo_atan(float(x)) for x in xs])
     ref = np.arctan(xs)
     assert np.all(np.abs(got - ref) <= np.spacing(np.abs(ref)))
+
+
+def test_aw_max_metric_matches_reference():
+    """compute_aw_max_metric (utils/association.py:320-374) restated: bit-exact."""
+    g = np.load(GOLDEN / "asso_funcs.npz")
+    for k in range(int(g["aw_count"])):
+        got = po.aw_max_metric(g[f"aw{k}_in"], float(g[f"aw{k}_w"]), 0.5)
+        np.testing.assert_array_equal(got, g[f"aw{k}_out"])

@@ -20,7 +20,8 @@ LIB = ROOT / "boxmot_amd" / "lib" / "libbxassoc_timing.so"
 PHASES = ["load", "warp+predict", "DLO", "DUO", "keep+colsum", "cost", "fastpath/LAP",
           "validate", "updates", "births", "outputs+deaths"]
 COUNTERS = ["LAP calls", "LAP n", "kept dets", "tracks", "frames", "-", "-", "-",
-            "JV free rows", "JV scans", "JV relax steps", "JV sequential scans"]
+            "JV free rows", "JV scans", "JV relax steps", "JV sequential scans",
+            "JV64 setup cyc", "JV64 scan cyc", "JV64 relax cyc", "JV64 init+path cyc"]
 
 
 def build():
