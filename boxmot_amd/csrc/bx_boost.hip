@@ -455,7 +455,65 @@ __global__ void __launch_bounds__(OW)
   BSTAMP(1);
 
   // ---- DLO confidence boost (boosttrack.py:413-456) ----------------------------------------
-  if (g.use_dlo && n > 0 && nt > 0) {
+  if (g.use_dlo && n > 0 && nt > 0 && g.rich_s && n * nt <= g.cost_lds) {
+    // the (detection, track) similarity terms lane per PAIR, staged in the (not yet used) cost
+    // matrix's LDS: E = MhDist numerator (negated where MhDist clipped, exp() > 0), then the
+    // column sums in detection order, then S = ((MhSim + shape) + soft-BIoU) / 3 in place, then
+    // each detection's max over tracks in track order (the reference's reduction order)
+    double* E = L.cost;
+    for (int p = lane; p < n * nt; p += OW) {
+      const int d = p / nt, t = p - d * nt;
+      bool m;
+      const double e = mh_num(mh_dist(L.dd + DDW * d, tb + (size_t)t * TBB), m);
+      E[p] = m ? -e : e;
+    }
+    __syncthreads();
+    for (int t = lane; t < nt; t += OW) {
+      double cs = 0.0;
+      for (int d = 0; d < n; d++) {
+        const double e = fabs(E[d * nt + t]);
+        cs = d == 0 ? e : cs + e;
+      }
+      L.colsum[t] = cs;
+    }
+    __syncthreads();
+    for (int p = lane; p < n * nt; p += OW) {
+      const int d = p / nt, t = p - d * nt;
+      const double* a = L.dd + DDW * d;
+      const double* rw = tb + (size_t)t * TBB;
+      const double ev = E[p];
+      const double mhs = ev < 0 ? 0.0 : ev / L.colsum[t];
+      const double sh = shape_sim(a, rw, g.s_sim_corr);
+      const double sb = soft_biou(a, rw, rw[4]);
+      E[p] = ((mhs + sh) + sb) / 3;
+    }
+    __syncthreads();
+    for (int d0 = 0; d0 < n; d0 += OW) {  // lane per detection
+      const int d = d0 + lane;
+      if (d < n) {
+        const double* a = L.dd + DDW * d;
+        double max_s = 0.0;
+        bool vt = false;
+        for (int t = 0; t < nt; t++) {
+          const double S = E[d * nt + t];
+          max_s = t == 0 ? S : nmax(max_s, S);
+          if (g.use_vt && !vt) vt = S > nmax(0.95 - (tb[(size_t)t * TBB + 5] - 1.0), 0.8);
+        }
+        double c = a[4];
+        if (!g.use_sb && !g.use_vt) {
+          c = nmax(c, max_s * g.dlo_coef);
+        } else {
+          if (g.use_sb) {
+            const double alpha = 0.65;
+            c = nmax(c, alpha * c + (1 - alpha) * bst_pow15(max_s));
+          }
+          if (g.use_vt && vt) c = nmax(c, det_thresh + 1e-5);
+        }
+        L.dd[DDW * d + 4] = c;
+      }
+    }
+    __syncthreads();
+  } else if (g.use_dlo && n > 0 && nt > 0) {
     if (g.rich_s) {  // MhDist_similarity column sums over all detections, lane per track
       for (int t0 = 0; t0 < nt; t0 += OW) {
         const int t = t0 + lane;
