@@ -7,7 +7,7 @@
 // NearestNeighborDistanceMetric), sort/iou_matching.py:10-87, utils/occlusion_handler.py:45-87,
 // 464-490 (detect_crowd_situations).  With P6 and handle_occlusions=False.
 //
-// Per frame, nine launches on the caller's stream:
+// Per frame, ten launches on the caller's stream:
 //   ss_prep_kernel   wave per detection: the feature's wave-order norm (quality; BLAS order of
 //                    the reference unpinned), its numpy pairwise norm, the NN-normalised row
 //                    feat/(‖·‖₂+1e-8) and the track-feature row feat/(‖·‖_wave+1e-8) with its
@@ -17,6 +17,7 @@
 //                    contraction on the fp64 matrix cores (v_mfma_f64_16x16x4f64, ascending-k
 //                    chain = the oracle's fma chain), max over rows by wave shuffles
 //   ss_rec_kernel    wave per (lost track, detection): ID-recovery cosine similarity
+//   ss_crowd_kernel  grid: detect_crowd_situations' pair test over all track pairs
 //   ss_pre_kernel    one wave per sequence: crowd mode, CMC warp, detection quality + stable
 //                    sort, Kalman predict
 //   ss_cost_kernel   wave per confirmed track: gating + motion/quality cost shaping of the
@@ -75,7 +76,8 @@ struct SsTrk {
 enum {
   Q_FRAME = 0, Q_NEXTID, Q_NTR, Q_NLOST, Q_CROWD, Q_ORIG, Q_OMAXAGE, Q_OBUDGET, Q_MAXAGE,
   Q_BUDGET, Q_HIST, Q_NNL, Q_NK, Q_NT0, Q_NOUT, Q_ROWS, Q_ROWSL,
-  Q_NM, Q_NAUD, Q_FID, Q_ANYF, Q_NFUT, Q_NDUP,  // handed from ss_match_kernel / ss_post_kernel to the next launch
+  Q_NM, Q_NAUD, Q_FID, Q_ANYF, Q_NFUT, Q_NDUP,
+  Q_CROWDN,  // high-overlap track pairs counted by ss_crowd_kernel for this frame  // handed from ss_match_kernel / ss_post_kernel to the next launch
   SQS
 };
 
@@ -794,8 +796,60 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
   for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
   for (int j = lane; j < CC; j += 64) w.v[j] = 0.0, w.path[j] = -1, w.row4col[j] = -1;
   __syncthreads();
+  constexpr int NONE = 0x7fffffff, MAXQ = 32;  // CC <= 2048
   for (int cur = 0; cur < R; cur++) {
-    double minVal = 0.0;
+    // The first Dijkstra step from row `cur` starts from scipy's fresh state (spc = INF,
+    // remaining[it] = CC-1-it), so it runs from registers: relax, minimum, tie rule.  Most rows
+    // end there on an unassigned column; only otherwise is the state written out and the search
+    // continued as below.
+    double rv[MAXQ];
+    double lmin = INF;
+    int lfirst = NONE, llast = -1;
+    {
+      const double ucur = w.u[cur];
+      const double* __restrict__ crow = C + (size_t)cur * CC;
+#pragma unroll
+      for (int q = 0; q < MAXQ; q++) {
+        const int j = lane + 64 * q;
+        rv[q] = INF;
+        if (j < CC) {
+          const double r = 0.0 + crow[j] - ucur - w.v[j];
+          const double sp = r < INF ? r : INF;
+          rv[q] = sp;
+          if (sp <= lmin) {
+            const int p = CC - 1 - j;
+            if (sp < lmin) {
+              lmin = sp;
+              lfirst = p;
+              llast = -1;
+            } else if (p < lfirst) {
+              lfirst = p;
+            }
+            if (w.row4col[j] == -1 && p > llast) llast = p;
+          }
+        }
+      }
+    }
+    const double m0 = wave_min_dpp(lmin);
+    lfirst = wave_min_i(lmin == m0 ? lfirst : NONE);
+    llast = -wave_min_i(lmin == m0 ? -llast : 1);
+    if (!(m0 < INF)) {  // infeasible (cannot happen with finite costs)
+      if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
+      return 0;
+    }
+    const int index0 = llast >= 0 ? llast : lfirst;
+    const int j0 = CC - 1 - index0;
+    if (w.row4col[j0] == -1) {  // sink reached: u[cur] += minVal, v[j0] -= 0, augment
+      __syncthreads();
+      if (lane == 0) {
+        w.u[cur] += m0;
+        w.row4col[j0] = cur;
+        w.col4row[cur] = j0;
+      }
+      __syncthreads();
+      continue;
+    }
+    double minVal = m0;
     int nrem = CC;
     for (int j = lane; j < CC; j += 64) {
       w.rem[CC - 1 - j] = j;
@@ -805,7 +859,24 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
     }
     for (int i = lane; i < R; i += 64) w.SR[i] = 0;
     __syncthreads();
-    int sink = -1, i = cur;
+#pragma unroll
+    for (int q = 0; q < MAXQ; q++) {
+      const int j = lane + 64 * q;
+      if (j < CC && rv[q] < INF) {
+        w.path[j] = cur;
+        w.spc[j] = rv[q];
+      }
+    }
+    if (lane == 0) {
+      w.SR[cur] = 1;
+      w.SC[j0] = 1;
+      const int jl = w.rem[nrem - 1];
+      w.rem[index0] = jl;
+      w.pos[jl] = index0;
+    }
+    nrem--;
+    __syncthreads();
+    int sink = -1, i = w.row4col[j0];
     while (sink == -1) {
       if (lane == 0) w.SR[i] = 1;
       const double ui = w.u[i];
@@ -831,7 +902,7 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
           m = fmin(m, sp);
         }
       }
-      m = wave_min_d(m);
+      m = wave_min_dpp(m);
       int last_un = -1, first_eq = 0x7fffffff;
       for (int j = lane; j < CC; j += 64) {
         if (!w.SC[j] && w.spc[j] == m) {
@@ -840,10 +911,8 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
           first_eq = p < first_eq ? p : first_eq;
         }
       }
-      for (int o = 32; o >= 1; o >>= 1) {
-        last_un = max(last_un, __shfl_xor(last_un, o));
-        first_eq = min(first_eq, __shfl_xor(first_eq, o));
-      }
+      last_un = -wave_min_i(-last_un);
+      first_eq = wave_min_i(first_eq);
       if (!(m < INF)) {  // infeasible (cannot happen with finite costs)
         if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
         return 0;
@@ -1325,6 +1394,40 @@ __device__ void track_birth(SsCtx& x, int slot, int di, int id) {
   g.vden[vi] = pr[3];
 }
 
+// detect_crowd_situations' pair test (utils/occlusion_handler.py:45-87; the fork passes tlwh
+// boxes that it reads as xyxy): the track pairs whose intersection exceeds 30 % of either box,
+// counted over the whole grid (block per slice of rows, threads over partners) into Q_CROWDN.
+constexpr int CROWD_BLOCKS = 16;
+__global__ void __launch_bounds__(256) ss_crowd_kernel(SsDev g, int seq0) {
+  __shared__ double box[4 * 1024];
+  const int b = blockIdx.y, seq = seq0 + b;
+  int* sq = g.sq + (size_t)seq * SQS;
+  const int nn = sq[Q_NTR];
+  if (!g.crowd || nn < 3) return;
+  const int* order = g.order + (size_t)seq * g.T;
+  const SsTrk* trk = g.trk + (size_t)seq * g.T;
+  for (int k = threadIdx.x; k < nn; k += 256) to_tlwh(trk[order[k]], box + 4 * k);
+  __syncthreads();
+  int high = 0;
+  for (int i = blockIdx.x; i < nn; i += CROWD_BLOCKS) {
+    const double* bi = box + 4 * i;
+    for (int j = i + 1 + threadIdx.x; j < nn; j += 256) {
+      const double* bj = box + 4 * j;
+      const double xx1 = pymax(bi[0], bj[0]), yy1 = pymax(bi[1], bj[1]);
+      const double xx2 = pymin(bi[2], bj[2]), yy2 = pymin(bi[3], bj[3]);
+      const double ww = pymax(0, xx2 - xx1), hh = pymax(0, yy2 - yy1);
+      const double inter = ww * hh;
+      if (inter > 0) {
+        const double ai = (bi[2] - bi[0]) * (bi[3] - bi[1]);
+        const double aj = (bj[2] - bj[0]) * (bj[3] - bj[1]);
+        if (pymax(inter / ai, inter / aj) > 0.3) high++;
+      }
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) high += __shfl_xor(high, o);
+  if ((threadIdx.x & 63) == 0 && high) atomicAdd(sq + Q_CROWDN, high);
+}
+
 // ss_pre_kernel (one wave per sequence): detections, crowd mode, CMC warp, quality + stable sort,
 // Kalman predict.  The detection table (fdt, fdord) and the predicted tracks are the input of
 // ss_cost_kernel and ss_match_kernel.
@@ -1379,25 +1482,7 @@ __global__ void __launch_bounds__(64)
       int crowd = 0;
       const int nn = x.ntr;
       if (nn >= 3) {
-        for (int i = lane; i < nn; i += 64) to_tlwh(x.trk[w.lst[i]], sbox + 4 * i);
-        __syncthreads();
-        long long high = 0;
-        for (int i = 0; i < nn; i++) {
-          const double* bi = sbox + 4 * i;
-          for (int j = i + 1 + lane; j < nn; j += 64) {
-            const double* bj = sbox + 4 * j;
-            const double xx1 = pymax(bi[0], bj[0]), yy1 = pymax(bi[1], bj[1]);
-            const double xx2 = pymin(bi[2], bj[2]), yy2 = pymin(bi[3], bj[3]);
-            const double ww = pymax(0, xx2 - xx1), hh = pymax(0, yy2 - yy1);
-            const double inter = ww * hh;
-            if (inter > 0) {
-              const double ai = (bi[2] - bi[0]) * (bi[3] - bi[1]);
-              const double aj = (bj[2] - bj[0]) * (bj[3] - bj[1]);
-              if (pymax(inter / ai, inter / aj) > 0.3) high++;
-            }
-          }
-        }
-        for (int o = 32; o >= 1; o >>= 1) high += __shfl_xor(high, o);
+        const long long high = sq[Q_CROWDN];  // ss_crowd_kernel's count
         const long long total = (long long)nn * (nn - 1) / 2;
         crowd = (double)high / (double)(total > 1 ? total : 1) > 0.3;
       }
@@ -1447,6 +1532,7 @@ __global__ void __launch_bounds__(64)
   if (lane == 0) {
     sq[Q_NK] = x.nk;
     sq[Q_FID] = fid;
+    sq[Q_CROWDN] = 0;  // the next frame's ss_crowd_kernel counts from zero
   }
   SSTAMP(2);
 }
@@ -1731,31 +1817,34 @@ __global__ void __launch_bounds__(64)
 
   SSTAMP(9);
   // ---- deleted tracks -> lost buffer (tracker.py:152-164) -------------------------------------
-  if (lane == 0) {
-    const int max_age = sq[Q_MAXAGE];
-    int wq = 0;
-    for (int p = 0; p < x.ntr; p++) {
-      const int s2 = w.lst[p];
-      SsTrk& t = x.trk[s2];
-      if (t.state == 3) {
+  // the surviving list by compaction; the deleted ones (few) through the lost buffer in order
+  const int ndel = wave_compact(
+      x.ntr, [&](int p) { return x.trk[w.lst[p]].state == 3; },
+      [&](int p, int q) { w.flag[q] = w.lst[p]; });
+  if (ndel) {
+    const int nkeep = wave_compact(
+        x.ntr, [&](int p) { return x.trk[w.lst[p]].state != 3; },
+        [&](int p, int q) { w.tmp[q] = w.lst[p]; });
+    for (int k = lane; k < nkeep; k += 64) w.lst[k] = w.tmp[k];
+    if (lane == 0) {
+      const int max_age = sq[Q_MAXAGE];
+      for (int q = 0; q < ndel; q++) {
+        const int s2 = w.flag[q];
         if (x.nlost < LOSTN) {
-          t.lost_frame = fid;
+          x.trk[s2].lost_frame = fid;
           x.lost[x.nlost++] = s2;
         }
         int lw = 0;
         for (int k = 0; k < x.nlost; k++)
           if (fid - x.trk[x.lost[k]].lost_frame < max_age) x.lost[lw++] = x.lost[k];
         x.nlost = lw;
-      } else {
-        w.lst[wq++] = s2;
       }
+      w.sc[1] = x.nlost;
     }
-    w.sc[0] = wq;
-    w.sc[1] = x.nlost;
+    __syncthreads();
+    x.ntr = nkeep;
+    x.nlost = w.sc[1];
   }
-  __syncthreads();
-  x.ntr = w.sc[0];
-  x.nlost = w.sc[1];
   __syncthreads();
 
   SSTAMP(10);
@@ -1978,6 +2067,8 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   if ((rc = ss_probe_end(e, 2, st))) return rc;
   const size_t lds = ss_lds_bytes(d);
   if ((rc = ss_probe_begin(e, 3, st))) return rc;
+  if (d.crowd)
+    hipLaunchKernelGGL(ss_crowd_kernel, dim3(CROWD_BLOCKS, nseq), dim3(256), 0, st, d, seq0);
   hipLaunchKernelGGL(ss_pre_kernel, dim3(nseq), dim3(64), lds, st, d, seq0, dets, off, warps);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 3, st))) return rc;
