@@ -104,8 +104,13 @@ struct SsDev {
   double* nf;     // [S][D][F] feat / (wave norm + 1e-8)
   double* recsim; // [S][LOSTN][D]
   double* cost;   // [S][2T*D] scratch cost matrices
-  double* cfull;  // [S][T][D] stage 1/2 cost by (track list position, sorted detection)
+  double* cfull;  // [S][T][D] stage 1/2 cost by (cascade rank, sorted detection)
   double* cfullT; // [S][D][T] the same, detection-major
+  int* crank;     // [S][T] cascade rank of a list position (confirmed tracks), else -1
+  double* ckey;   // [S][T] quality + stability by list position
+  int* ctsu;      // [S][T] time_since_update by list position (confirmed), else -1
+  int* cpos;      // [S][T] list position of a cascade rank
+  int* ncf;       // [S] confirmed tracks (ranks 0..ncf-1)
   double* fdt;    // [S][D][DTW] this frame's detection table (kept across the frame's launches)
   int* fdord;     // [S][D] detections in quality order
   int* faud;      // [S][D] unmatched detections after the three stages
@@ -777,6 +782,10 @@ struct SsCtx {
   int ntr, nlost, nk, nm;
   double* key;  // match kernel: quality + stability by list position (LDS)
   int* tsu;     // match kernel: time_since_update by list position (LDS)
+  int* rank;    // match kernel: cascade rank by list position (LDS)
+  int* gpos;    // match kernel: list position by cascade rank (LDS)
+  int* inset;   // match kernel: membership table by list position (LDS)
+  int ncf;      // confirmed tracks
   int* flt;     // match kernel: scratch table (LDS, 1024 ints)
   double* ks;   // match kernel: sort-key scratch (LDS)
   __device__ const double* det(int i) const { return w.dt + (size_t)w.dord[i] * DTW; }
@@ -796,43 +805,46 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
   for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
   for (int j = lane; j < CC; j += 64) w.v[j] = 0.0, w.path[j] = -1, w.row4col[j] = -1;
   __syncthreads();
-  constexpr int NONE = 0x7fffffff, MAXQ = 32;  // CC <= 2048
+  constexpr int NONE = 0x7fffffff;
   for (int cur = 0; cur < R; cur++) {
     // The first Dijkstra step from row `cur` starts from scipy's fresh state (spc = INF,
     // remaining[it] = CC-1-it), so it runs from registers: relax, minimum, tie rule.  Most rows
     // end there on an unassigned column; only otherwise is the state written out and the search
     // continued as below.
-    double rv[MAXQ];
+    const double ucur = w.u[cur];
+    const double* __restrict__ crow = C + (size_t)cur * CC;
     double lmin = INF;
-    int lfirst = NONE, llast = -1;
-    {
-      const double ucur = w.u[cur];
-      const double* __restrict__ crow = C + (size_t)cur * CC;
+    for (int j0 = 0; j0 < CC; j0 += 256) {
+      double cv[4];
 #pragma unroll
-      for (int q = 0; q < MAXQ; q++) {
-        const int j = lane + 64 * q;
-        rv[q] = INF;
+      for (int q = 0; q < 4; q++) {
+        const int j = j0 + 64 * q + lane;
+        cv[q] = j < CC ? crow[j] : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int j = j0 + 64 * q + lane;
         if (j < CC) {
-          const double r = 0.0 + crow[j] - ucur - w.v[j];
-          const double sp = r < INF ? r : INF;
-          rv[q] = sp;
-          if (sp <= lmin) {
-            const int p = CC - 1 - j;
-            if (sp < lmin) {
-              lmin = sp;
-              lfirst = p;
-              llast = -1;
-            } else if (p < lfirst) {
-              lfirst = p;
-            }
-            if (w.row4col[j] == -1 && p > llast) llast = p;
-          }
+          const double r = 0.0 + cv[q] - ucur - w.v[j];
+          lmin = fmin(lmin, r < INF ? r : INF);
         }
       }
     }
     const double m0 = wave_min_dpp(lmin);
-    lfirst = wave_min_i(lmin == m0 ? lfirst : NONE);
-    llast = -wave_min_i(lmin == m0 ? -llast : 1);
+    // scipy's tie rule among the columns at the minimum (fresh positions CC-1-j)
+    int lfirst = NONE, llast = -1;
+    if (lmin == m0) {
+      for (int j = lane; j < CC; j += 64) {
+        const double r = 0.0 + crow[j] - ucur - w.v[j];
+        if ((r < INF ? r : INF) == m0) {
+          const int p = CC - 1 - j;
+          lfirst = p < lfirst ? p : lfirst;
+          if (w.row4col[j] == -1 && p > llast) llast = p;
+        }
+      }
+    }
+    lfirst = wave_min_i(lfirst);
+    llast = -wave_min_i(-llast);
     if (!(m0 < INF)) {  // infeasible (cannot happen with finite costs)
       if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
       return 0;
@@ -859,12 +871,11 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
     }
     for (int i = lane; i < R; i += 64) w.SR[i] = 0;
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < MAXQ; q++) {
-      const int j = lane + 64 * q;
-      if (j < CC && rv[q] < INF) {
+    for (int j = lane; j < CC; j += 64) {  // the first step's relaxation, recomputed
+      const double r = 0.0 + crow[j] - ucur - w.v[j];
+      if (r < INF) {
         w.path[j] = cur;
-        w.spc[j] = rv[q];
+        w.spc[j] = r;
       }
     }
     if (lane == 0) {
@@ -1012,6 +1023,26 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
   const int slot = g.order[(size_t)seq * g.T + k];
   const SsTrk& t = g.trk[(size_t)seq * g.T + slot];
   if (t.state != 2 || nk == 0) return;
+  // this track's cascade rank: time_since_update ascending, -(quality + stability), list order
+  int rk = 0;
+  {
+    const int ntr = sq[Q_NTR];
+    const double* ck = g.ckey + (size_t)seq * g.T;
+    const int* ca = g.ctsu + (size_t)seq * g.T;
+    const int ai = ca[k];
+    const double ki = ck[k];
+    for (int q = lane; q < ntr; q += 64) {
+      const int aq = ca[q];
+      if (aq < 0) continue;
+      const double kq = ck[q];
+      rk += aq < ai || (aq == ai && (kq > ki || (kq == ki && q < k)));
+    }
+    for (int o = 32; o >= 1; o >>= 1) rk += __shfl_xor(rk, o);
+    if (lane == 0) {
+      g.crank[(size_t)seq * g.T + k] = rk;
+      g.cpos[(size_t)seq * g.T + rk] = k;
+    }
+  }
   // per-track terms, computed once (lane 0) and shared through LDS
   if (lane == 0) {
     double S[16], L[16], rr[4];
@@ -1047,8 +1078,8 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
   const double* dt = g.fdt + (size_t)seq * g.D * DTW;
   const int* dord = g.fdord + (size_t)seq * g.D;
   const double* nnd = g.nnd + ((size_t)seq * g.T + slot) * g.D;
-  double* out = g.cfull + ((size_t)seq * g.T + k) * g.D;
-  double* outT = g.cfullT + (size_t)seq * g.D * g.T + k;
+  double* out = g.cfull + ((size_t)seq * g.T + rk) * g.D;
+  double* outT = g.cfullT + (size_t)seq * g.D * g.T + rk;
   for (int c = lane; c < nk; c += 64) {
     const double* d = dt + (size_t)dord[c] * DTW;
     double z[4];
@@ -1117,26 +1148,25 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
   if (kind == M_GATED) {
     // ss_cost_kernel's gated + shaped + enhanced cost of (list position, sorted detection); the
     // clamp at max_distance is this level's.  The lane's gather indices stay in registers.
-    constexpr int MAXJ = 32;  // 2 * track_cap / 64
     const int nl = tr ? nt : nd, no = tr ? nd : nt;
     const int* li = tr ? ti : di;
     const int* oi = tr ? di : ti;
+    const int* rk = x.rank;  // track list position -> cascade rank (the matrix's track index)
     const double* cf = tr ? g.cfullT + (size_t)x.seq * g.D * g.T : g.cfull + (size_t)x.seq * g.T * g.D;
     const int ld = tr ? g.T : g.D;
-    int idx[MAXJ];
+    for (int c = lane; c < nl; c += 64) {  // this lane's column, then every row
+      const int v = li[c];
+      const int idx = tr ? rk[v] : v;
+      for (int o = 0; o < no; o += 4) {
+        double e[4];
 #pragma unroll
-    for (int j = 0; j < MAXJ; j++) idx[j] = lane + 64 * j < nl ? li[lane + 64 * j] : 0;
-    for (int o = 0; o < no; o++) {
-      const double* src = cf + (size_t)oi[o] * ld;
-      double* row = C + (size_t)o * nl;
-#pragma unroll
-      for (int j = 0; j < MAXJ; j++) {
-        const int c = lane + 64 * j;
-        if (c < nl) {
-          double e = src[idx[j]];
-          if (e > max_d) e = max_d + 1e-5;
-          row[c] = e;
+        for (int u = 0; u < 4; u++) {
+          const int oo = o + u < no ? o + u : o;
+          e[u] = cf[(size_t)(tr ? oi[oo] : rk[oi[oo]]) * ld + idx];
         }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (o + u < no) C[(size_t)(o + u) * nl + c] = e[u] > max_d ? max_d + 1e-5 : e[u];
       }
     }
   } else {
@@ -1264,12 +1294,18 @@ __device__ void matching_cascade(SsCtx& x, double max_d, const int* ti, int nt, 
     na = bcast(na);
   }
   __syncthreads();
+  // members of ti by list position
+  for (int p = lane; p < x.ntr; p += 64) x.inset[p] = 0;
+  __syncthreads();
+  for (int k = lane; k < nt; k += 64) x.inset[ti[k]] = 1;
+  __syncthreads();
   for (int q = 0; q < na; q++) {
     const int age = w.ages[q];
     if (age > max_age) break;
-    const int nl = wave_compact(nt, [&](int k) { return x.tsu[ti[k]] == age; },
-                                [&](int k, int p) { w.lvl[p] = ti[k]; });
-    stable_sort_desc(w.lvl, nl, [&](int pos) { return x.key[pos]; }, w.tmp, x.ks);
+    // the level's tracks in cascade order (its run of ranks, restricted to ti)
+    const int nl = wave_compact(
+        x.ncf, [&](int r) { const int p = x.gpos[r]; return x.inset[p] && x.tsu[p] == age; },
+        [&](int r, int p) { w.lvl[p] = x.gpos[r]; });
     int nut_dummy = 0, nud2 = 0;
     min_cost_matching(x, M_GATED, max_d, w.lvl, nl, w.ud, nud, nullptr, nut_dummy, w.ud2, nud2);
     for (int k = lane; k < nud2; k += 64) w.ud[k] = w.ud2[k];
@@ -1529,6 +1565,23 @@ __global__ void __launch_bounds__(64)
     __syncthreads();
   }
   if (!fid) fid = sq[Q_HIST];
+  // the cascade order of the confirmed tracks: time_since_update ascending, then -(quality +
+  // stability) with list order on ties (linear_assignment.py:96-171, 276-285) — every cascade
+  // level of stage 1 or 2 is a run of it (stage 2's a subsequence), so the cost kernel indexes
+  // its matrix by this rank and the levels gather contiguous rows
+  // (ranks: ss_cost_kernel, from these keys)
+  {
+    int nc = 0;
+    for (int p = lane; p < x.ntr; p += 64) {
+      const SsTrk& t = x.trk[w.lst[p]];
+      g.ckey[(size_t)seq * g.T + p] = t.quality + t.stability;
+      g.ctsu[(size_t)seq * g.T + p] = t.state == 2 ? t.tsu : -1;
+      g.crank[(size_t)seq * g.T + p] = -1;
+      nc += t.state == 2;
+    }
+    for (int o = 32; o >= 1; o >>= 1) nc += __shfl_xor(nc, o);
+    if (lane == 0) g.ncf[seq] = nc;
+  }
   if (lane == 0) {
     sq[Q_NK] = x.nk;
     sq[Q_FID] = fid;
@@ -1543,7 +1596,7 @@ __global__ void __launch_bounds__(64)
 __global__ void __launch_bounds__(64)
     ss_match_kernel(SsDev g, int seq0) {
   extern __shared__ __align__(16) char ss_lds[];
-  __shared__ double skey[1024], sks[1024];
+  __shared__ int srank[1024], sgpos[1024], sinset[1024];
   __shared__ int flt[1024], fld[1024];  // membership tables: track positions, sorted detections
   __shared__ int stsu[1024], sage[1024];
   const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
@@ -1561,14 +1614,17 @@ __global__ void __launch_bounds__(64)
   x.nk = sq[Q_NK];
   for (int p = lane; p < x.ntr; p += 64) {
     w.lst[p] = order[p];
-    const SsTrk& t = x.trk[order[p]];
-    skey[p] = t.quality + t.stability;  // the cascade levels' sort key (linear_assignment.py:276-285)
-    stsu[p] = t.tsu;
+    stsu[p] = x.trk[order[p]].tsu;
+    const int r = g.crank[(size_t)seq * g.T + p];
+    srank[p] = r;
+    if (r >= 0) sgpos[r] = p;
   }
-  x.key = skey;
+  x.ncf = g.ncf[seq];
   x.tsu = stsu;
   x.flt = sage;
-  x.ks = sks;
+  x.rank = srank;
+  x.gpos = sgpos;
+  x.inset = sinset;
   __syncthreads();
 
   // ---- Tracker._enhanced_match (tracker.py:183-281, P6) --------------------------------------
@@ -2165,6 +2221,11 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   const size_t o_cost = cb(S * 4 * T * D * sizeof(double));
   const size_t o_cfull = cb(S * T * D * sizeof(double));
   const size_t o_cfullT = cb(S * T * D * sizeof(double));
+  const size_t o_crank = cb(S * T * sizeof(int));
+  const size_t o_ckey = cb(S * T * sizeof(double));
+  const size_t o_ctsu = cb(S * T * sizeof(int));
+  const size_t o_cpos = cb(S * T * sizeof(int));
+  const size_t o_ncf = cb(S * sizeof(int));
   const size_t o_fdt = cb(S * D * DTW * sizeof(double));
   const size_t o_fdord = cb(S * D * sizeof(int));
   const size_t o_faud = cb(S * D * sizeof(int));
@@ -2203,6 +2264,11 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   d.cost = (double*)(base + o_cost);
   d.cfull = (double*)(base + o_cfull);
   d.cfullT = (double*)(base + o_cfullT);
+  d.crank = (int*)(base + o_crank);
+  d.ckey = (double*)(base + o_ckey);
+  d.ctsu = (int*)(base + o_ctsu);
+  d.cpos = (int*)(base + o_cpos);
+  d.ncf = (int*)(base + o_ncf);
   d.fdt = (double*)(base + o_fdt);
   d.fdord = (int*)(base + o_fdord);
   d.faud = (int*)(base + o_faud);
