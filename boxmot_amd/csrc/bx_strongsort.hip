@@ -785,6 +785,7 @@ struct SsCtx {
   int* rank;    // match kernel: cascade rank by list position (LDS)
   int* gpos;    // match kernel: list position by cascade rank (LDS)
   int* inset;   // match kernel: membership table by list position (LDS)
+  double* sdet; // match kernel: staged detection rows for the IoU stage (LDS, 256 x DTW)
   int ncf;      // confirmed tracks
   int* flt;     // match kernel: scratch table (LDS, 1024 ints)
   double* ks;   // match kernel: sort-key scratch (LDS)
@@ -1154,6 +1155,9 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
     const int* rk = x.rank;  // track list position -> cascade rank (the matrix's track index)
     const double* cf = tr ? g.cfullT + (size_t)x.seq * g.D * g.T : g.cfull + (size_t)x.seq * g.T * g.D;
     const int ld = tr ? g.T : g.D;
+    int* roff = x.flt;  // the rows' matrix indices, staged in LDS (free during the levels)
+    for (int o = lane; o < no; o += 64) roff[o] = tr ? oi[o] : rk[oi[o]];
+    __syncthreads();
     for (int c = lane; c < nl; c += 64) {  // this lane's column, then every row
       const int v = li[c];
       const int idx = tr ? rk[v] : v;
@@ -1162,7 +1166,7 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
 #pragma unroll
         for (int u = 0; u < 4; u++) {
           const int oo = o + u < no ? o + u : o;
-          e[u] = cf[(size_t)(tr ? oi[oo] : rk[oi[oo]]) * ld + idx];
+          e[u] = cf[(size_t)roff[oo] * ld + idx];
         }
 #pragma unroll
         for (int u = 0; u < 4; u++)
@@ -1171,6 +1175,16 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
     }
   } else {
     double* Cr = tr ? C2 : C;  // row-major nt x nd, transposed below when tr
+    // the detections' rows staged in LDS when they fit (x.sdet: 256 x DTW)
+    const bool staged = x.sdet && nd <= 256;
+    if (staged) {
+      for (int k = lane; k < nd * DTW; k += 64) {
+        const int c = k / DTW, f = k - c * DTW;
+        x.sdet[k] = x.det(di[c])[f];
+      }
+      __syncthreads();
+    }
+    auto dq = [&](int c) { return staged ? x.sdet + (size_t)c * DTW : x.det(di[c]); };
     for (int r = lane; r < nt; r += 64) {
       const int slot = w.lst[ti[r]];
       const SsTrk& t = x.trk[slot];
@@ -1182,7 +1196,7 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
         to_tlwh(t, b);
         const double br0 = b[0] + b[2], br1 = b[1] + b[3];
         for (int c = 0; c < nd; c++) {
-          const double* q = x.det(di[c]);
+          const double* q = dq(c);
           const double tl0 = fmax(b[0], q[0]), tl1 = fmax(b[1], q[1]);
           const double e0 = fmin(br0, q[0] + q[2]), e1 = fmin(br1, q[1] + q[3]);
           const double ww = fmax(0.0, e0 - tl0), hh = fmax(0.0, e1 - tl1);
@@ -1190,7 +1204,7 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
           row[c] = 1.0 - ai / ((b[2] * b[3] + q[2] * q[3]) - ai);
         }
       }
-      for (int c = 0; c < nd; c++) row[c] = enhance_clamp(t, x.det(di[c]), row[c], max_d);
+      for (int c = 0; c < nd; c++) row[c] = enhance_clamp(t, dq(c), row[c], max_d);
     }
     if (tr) {
       __syncthreads();
@@ -1597,6 +1611,7 @@ __global__ void __launch_bounds__(64)
     ss_match_kernel(SsDev g, int seq0) {
   extern __shared__ __align__(16) char ss_lds[];
   __shared__ int srank[1024], sgpos[1024], sinset[1024];
+  __shared__ double ssdet[256 * DTW];
   __shared__ int flt[1024], fld[1024];  // membership tables: track positions, sorted detections
   __shared__ int stsu[1024], sage[1024];
   const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
@@ -1625,6 +1640,7 @@ __global__ void __launch_bounds__(64)
   x.rank = srank;
   x.gpos = sgpos;
   x.inset = sinset;
+  x.sdet = ssdet;
   __syncthreads();
 
   // ---- Tracker._enhanced_match (tracker.py:183-281, P6) --------------------------------------
