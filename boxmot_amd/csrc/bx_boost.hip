@@ -455,6 +455,7 @@ __global__ void __launch_bounds__(OW)
   BSTAMP(1);
 
   // ---- DLO confidence boost (boosttrack.py:413-456) ----------------------------------------
+  bool have_e = false;  // L.cost holds MhDist numerators E[d][t] (sign = clipped) of all dets
   if (g.use_dlo && n > 0 && nt > 0 && g.rich_s && n * nt <= g.cost_lds) {
     // the (detection, track) similarity terms lane per PAIR, staged in the (not yet used) cost
     // matrix's LDS: E = MhDist numerator (negated where MhDist clipped, exp() > 0), then the
@@ -477,28 +478,28 @@ __global__ void __launch_bounds__(OW)
       L.colsum[t] = cs;
     }
     __syncthreads();
-    for (int p = lane; p < n * nt; p += OW) {
-      const int d = p / nt, t = p - d * nt;
+    // S = ((MhSim + shape) + soft-BIoU) / 3 row by row (lanes over tracks): each detection's
+    // max over tracks (the reference's np.max: NaN-propagating, otherwise order-free) and the
+    // VT test by wave reductions; E stays intact for the association cost
+    for (int d = 0; d < n; d++) {
       const double* a = L.dd + DDW * d;
-      const double* rw = tb + (size_t)t * TBB;
-      const double ev = E[p];
-      const double mhs = ev < 0 ? 0.0 : ev / L.colsum[t];
-      const double sh = shape_sim(a, rw, g.s_sim_corr);
-      const double sb = soft_biou(a, rw, rw[4]);
-      E[p] = ((mhs + sh) + sb) / 3;
-    }
-    __syncthreads();
-    for (int d0 = 0; d0 < n; d0 += OW) {  // lane per detection
-      const int d = d0 + lane;
-      if (d < n) {
-        const double* a = L.dd + DDW * d;
-        double max_s = 0.0;
-        bool vt = false;
-        for (int t = 0; t < nt; t++) {
-          const double S = E[d * nt + t];
-          max_s = t == 0 ? S : nmax(max_s, S);
-          if (g.use_vt && !vt) vt = S > nmax(0.95 - (tb[(size_t)t * TBB + 5] - 1.0), 0.8);
-        }
+      double mx = -INF;
+      bool nan = false, vt = false;
+      for (int t = lane; t < nt; t += OW) {
+        const double* rw = tb + (size_t)t * TBB;
+        const double ev = E[d * nt + t];
+        const double mhs = ev < 0 ? 0.0 : ev / L.colsum[t];
+        const double S = ((mhs + shape_sim(a, rw, g.s_sim_corr)) + soft_biou(a, rw, rw[4])) / 3;
+        if (S != S)
+          nan = true;
+        else
+          mx = mx > S ? mx : S;
+        if (g.use_vt && S > nmax(0.95 - (rw[5] - 1.0), 0.8)) vt = true;
+      }
+      nan = __any(nan);
+      vt = __any(vt);
+      const double max_s = nan ? __builtin_nan("") : -wave_min_dpp(-mx);
+      if (lane == 0) {
         double c = a[4];
         if (!g.use_sb && !g.use_vt) {
           c = nmax(c, max_s * g.dlo_coef);
@@ -512,6 +513,7 @@ __global__ void __launch_bounds__(OW)
         L.dd[DDW * d + 4] = c;
       }
     }
+    have_e = true;
     __syncthreads();
   } else if (g.use_dlo && n > 0 && nt > 0) {
     if (g.rich_s) {  // MhDist_similarity column sums over all detections, lane per track
@@ -629,15 +631,22 @@ __global__ void __launch_bounds__(OW)
     const double lambda_emb = (((1 + g.l_iou) + g.l_shape) + g.l_mhd) * 1.5;
     double* C = (nk * nt <= g.cost_lds) ? L.cost : costg;
     if (nk > 0) {
-      // MhDist_similarity over the kept detections: column sums, lane per track
+      // MhDist_similarity over the kept detections: column sums, lane per track (from the DLO
+      // boost's E when it staged one: the boosts change confidences, never boxes).  The cost
+      // below is written over E in place: row i <= kd[i] <= the rows still to be read.
       for (int t0 = 0; t0 < nt; t0 += OW) {
         const int t = t0 + lane;
         if (t < nt) {
           const double* rw = tb + (size_t)t * TBB;
           double cs = 0.0;
           for (int i = 0; i < nk; i++) {
-            bool m;
-            const double e = mh_num(mh_dist(L.dd + DDW * L.kd[i], rw), m);
+            double e;
+            if (have_e) {
+              e = fabs(L.cost[L.kd[i] * nt + t]);
+            } else {
+              bool m;
+              e = mh_num(mh_dist(L.dd + DDW * L.kd[i], rw), m);
+            }
             cs = i == 0 ? e : cs + e;
           }
           L.colsum[t] = cs;
@@ -662,7 +671,14 @@ __global__ void __launch_bounds__(OW)
             if (o < thr) cf = 0.0;
             cst += g.l_iou * cf * o;
             bool m;
-            const double e = mh_num(mh_dist(a, rw), m);
+            double e;
+            if (have_e) {
+              const double ev = L.cost[d * nt + t];
+              m = ev < 0;
+              e = fabs(ev);
+            } else {
+              e = mh_num(mh_dist(a, rw), m);
+            }
             cst += g.l_mhd * (m ? 0.0 : e / L.colsum[t]);
             cst += g.l_shape * cf * shape_sim(a, rw, g.s_sim_corr);
             if (ec) cst += lambda_emb * ec[(size_t)d * g.T + t];
