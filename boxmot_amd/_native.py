@@ -20,6 +20,7 @@ HEADER = REPO / "include" / "bxassoc.h"
 HEADER_OCS = REPO / "include" / "bxocsort.h"
 HEADER_BOOST = REPO / "include" / "bxboost.h"
 HEADER_SS = REPO / "include" / "bxstrongsort.h"
+HEADER_IO = REPO / "include" / "bxio.h"
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
@@ -27,7 +28,7 @@ HIPCC_FLAGS = [
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
 ]
 SOURCES = ["bx_engine.hip", "bx_ops.hip", "bx_ocsort.hip", "bx_nn.hip", "bx_boost.hip",
-           "bx_strongsort.hip"]
+           "bx_strongsort.hip", "bx_io.cpp"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -37,7 +38,7 @@ class NativeUnavailable(RuntimeError):
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the HIP extension for gfx950 in-tree (boxmot_amd/lib/libbxassoc.so)."""
     srcs = [CSRC / s for s in SOURCES] + [CSRC / "bx_device.h", CSRC / "bx_jv.h", HEADER,
-                                          HEADER_OCS, HEADER_BOOST, HEADER_SS]
+                                          HEADER_OCS, HEADER_BOOST, HEADER_SS, HEADER_IO]
     if not force and LIB_PATH.exists():
         t = LIB_PATH.stat().st_mtime
         if all(s.stat().st_mtime <= t for s in srcs):
@@ -121,6 +122,7 @@ EXPORTS = [
     "bx_boost_probe", "bx_boost_probe_read", "bx_ss_create", "bx_ss_destroy", "bx_ss_reset",
     "bx_ss_step", "bx_ss_update_host", "bx_ss_status", "bx_ss_counters_host",
     "bx_ss_tracks_host", "bx_ss_frame_stats_host", "bx_ss_probe", "bx_ss_probe_read",
+    "bx_txt_shape", "bx_txt_read", "bx_mot_format", "bx_mot_write",
 ]
 
 _vp, _ip, _dp, _fp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_float)
@@ -144,6 +146,10 @@ _SIGS = {
     "bx_iou_batch": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp], C.c_int),
     "bx_pairwise_cost": ([C.c_int, _vp, C.c_int, C.c_int, _vp, C.c_int, C.c_int, C.c_double,
                           C.c_double, _vp, _vp], C.c_int),
+    "bx_txt_shape": ([C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32)], C.c_int),
+    "bx_txt_read": ([C.c_char_p, _vp, C.c_int64, C.c_int32], C.c_int),
+    "bx_mot_format": ([_vp, C.c_int64, C.c_int32, C.c_int32, _vp], C.c_int),
+    "bx_mot_write": ([C.c_char_p, _vp, C.c_int64, C.c_int32], C.c_int),
     "bx_aw_max_metric": ([_vp, C.c_int, C.c_int, C.c_double, C.c_double, _vp, _vp], C.c_int),
     "bx_fuse_score": ([_vp, C.c_int, C.c_int, _vp, _vp], C.c_int),
     "bx_embedding_distance": ([_vp, C.c_int, _vp, C.c_int, C.c_int, _vp, _vp], C.c_int),

@@ -786,3 +786,64 @@ def test_strongsort_dropin(torch_cuda, monkeypatch):
     assert not hasattr(y, "per_class") or y.per_class is False
     with pytest.raises(AssertionError):
         y.update(d, img, base[:2])
+
+
+# ------------------------------------------------------------------- many-sequence runner
+@pytest.mark.parametrize("kind", ["bytetrack", "botsort", "ocsort", "boosttrack", "strongsort"])
+def test_run_sequences_matches_per_sequence_dropins(torch_cuda, tmp_path, kind):
+    """motio.run_sequences (one batched engine for all sequences, val.py:357-405's process pool
+    replaced) writes the same MOT files as one fresh drop-in tracker per sequence fed by
+    MOT17.py's np.loadtxt + mask selection (val.py:337-353); inputs in val.py's text format."""
+    import os
+
+    from boxmot_amd import BoostTrack, ByteTrack, motio
+    from boxmot_amd.synth import SyntheticScene
+    from boxmot_amd.tracker_zoo import create_tracker
+
+    os.environ["GITHUB_ACTIONS"] = "true"  # StrongSort born Confirmed, like its fixtures
+    os.environ.pop("GITHUB_JOB", None)
+    rng = np.random.default_rng(9)
+    F = 32
+    rows = {}
+    fx = np.load(GOLDEN / "trk_bytetrack_MOT17-02-FRCNN.npz")
+    rows["MOT17-02-FRCNN"] = fx["dets"][fx["dets"][:, 0] <= 60]
+    for s in (1, 2):
+        sc = SyntheticScene(n_obj=20 + 10 * s, seed=40 + s, layout="crowded" if s == 2 else "grid")
+        fr = []
+        for t in range(1, 50):
+            if t % 11 == 5:  # a frame without detections
+                continue
+            d = sc.frame(t)[0]
+            fr.append(np.concatenate([np.full((d.shape[0], 1), t), d], 1))
+        rows[f"SYN-{s}"] = np.concatenate(fr)
+    packed, frame_ids = {}, {}
+    for nm, r in rows.items():
+        e = rng.standard_normal((r.shape[0], F))
+        e /= np.linalg.norm(e, axis=1, keepdims=True)
+        dp, ep = tmp_path / f"{nm}.dets.txt", tmp_path / f"{nm}.embs.txt"
+        np.savetxt(dp, r, fmt="%f", header=nm)
+        np.savetxt(ep, e, fmt="%f")
+        packed[nm] = motio.pack_sequence(dp, ep, tmp_path / f"{nm}.bxmot")
+        frame_ids[nm] = list(range(1, int(r[:, 0].max()) + 2))  # image frames, some empty
+    motio.run_sequences(kind, packed, tmp_path / "batched", frame_ids=frame_ids)
+    img = np.zeros((1080, 1920, 3), np.uint8)
+    for nm in rows:
+        ByteTrack.clear_count()
+        BoostTrack._id_count = 0
+        tr = create_tracker(kind)
+        dets = np.loadtxt(tmp_path / f"{nm}.dets.txt", comments="#")
+        embs = np.loadtxt(tmp_path / f"{nm}.embs.txt", comments="#")
+        out = []
+        for fid in frame_ids[nm]:
+            mask = dets[:, 0].astype(int) == fid
+            d, e = dets[mask, 1:], embs[mask]
+            if d.size and e.size:
+                tracks = np.asarray(tr.update(d, img, e))
+                if tracks.size:
+                    out.append(motio.convert_to_mot_format(tracks, fid))
+        motio.write_mot_results(tmp_path / "single" / f"{nm}.txt",
+                                np.vstack(out) if out else np.empty((0, 0)))
+        a = (tmp_path / "batched" / f"{nm}.txt").read_bytes()
+        b = (tmp_path / "single" / f"{nm}.txt").read_bytes()
+        assert a == b, f"{kind} {nm}: batched run differs from the per-sequence drop-in"
+        assert len(a) > 0
