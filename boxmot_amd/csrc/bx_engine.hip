@@ -1341,7 +1341,10 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
 // new smooth_feat's numpy float32 norm (embedding_distance's track-side scale) is refreshed here,
 // while the row is in registers, for the next frame's K1c.  Grid (n_seq, FEAT_BLOCKS); one wave
 // per record.
-constexpr int FEAT_BLOCKS = 16;
+#ifndef BX_FEAT_BLOCKS
+#define BX_FEAT_BLOCKS 16
+#endif
+constexpr int FEAT_BLOCKS = BX_FEAT_BLOCKS;
 template <typename FT, bool NPF>
 __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
                                                      const int* __restrict__ det_off,

@@ -39,6 +39,7 @@
 #include <float.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -639,6 +640,10 @@ __global__ void __launch_bounds__(64)
   if (n > g.D) n = g.D;
   if (n <= 0) return;
   const int F = g.F;
+  if (lane < ng && blockIdx.z == 0) {  // (the statistic counted once per track)
+    unsigned long long m = g.trk[(size_t)seq * g.T + g.nnl[(size_t)seq * g.T + k0 + lane]].gmask;
+    atomicAdd(g.sq + (size_t)seq * SQS + Q_ROWS, __popcll(m));
+  }
   if (lane < ng) {  // distinct pool entries referenced by each gallery
     const int slot = g.nnl[(size_t)seq * g.T + k0 + lane];
     unsigned long long m = g.trk[(size_t)seq * g.T + slot].gmask;
@@ -649,7 +654,6 @@ __global__ void __launch_bounds__(64)
     }
     nrow_s[lane] = c;
     slot_s[lane] = slot;
-    atomicAdd(g.sq + (size_t)seq * SQS + Q_ROWS, c);
   }
   __syncthreads();
   if (lane == 0) {  // the tile list: (track, first row) per 16-row tile
@@ -666,7 +670,7 @@ __global__ void __launch_bounds__(64)
   const int ntile = ntile_s;
   const double* dnb = g.dn + (size_t)seq * g.D * F;
   const int kl = lane >> 4, cl = lane & 15;
-  for (int db = 0; db < n; db += 64) {
+  for (int db = 64 * blockIdx.z; db < n; db += 64 * gridDim.z) {  // this wave's detection blocks
     const int ndt = n - db >= 64 ? 4 : (n - db + 15) / 16;  // detection tiles in this block
     double best[G][4];
 #pragma unroll
@@ -2123,14 +2127,21 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   if ((rc = ss_probe_begin(e, 1, st))) return rc;
   // tracks per wave: share detection loads among 4 when that still leaves ~8 waves per CU
   const long qtracks = (long)d.T * nseq;
-  if (qtracks >= 4 * 2048)
-    hipLaunchKernelGGL((ss_nn_kernel<4, 4>), dim3((d.T + 3) / 4, nseq), dim3(64), 0, st, d, seq0,
-                       off);
-  else if (qtracks >= 2 * 2048)
-    hipLaunchKernelGGL((ss_nn_kernel<2, 2>), dim3((d.T + 1) / 2, nseq), dim3(64), 0, st, d, seq0,
-                       off);
+  int gsel = qtracks >= 4 * 2048 ? 4 : (qtracks >= 2 * 2048 ? 2 : 1);
+  if (const char* ev = std::getenv("BX_SS_NN_G")) gsel = std::atoi(ev);  // diagnostics
+  // detection blocks of 64 split over waves too when the tracks alone give too few waves
+  const long waves = (long)((d.T + gsel - 1) / gsel) * nseq;
+  int zb = (int)((4096 + waves - 1) / waves);
+  const int nblk = (d.D + 63) / 64;
+  zb = zb < 1 ? 1 : (zb > nblk ? nblk : zb);
+  if (gsel >= 4)
+    hipLaunchKernelGGL((ss_nn_kernel<4, 4>), dim3((d.T + 3) / 4, nseq, zb), dim3(64), 0, st, d,
+                       seq0, off);
+  else if (gsel == 2)
+    hipLaunchKernelGGL((ss_nn_kernel<2, 2>), dim3((d.T + 1) / 2, nseq, zb), dim3(64), 0, st, d,
+                       seq0, off);
   else
-    hipLaunchKernelGGL((ss_nn_kernel<1, 1>), dim3(d.T, nseq), dim3(64), 0, st, d, seq0, off);
+    hipLaunchKernelGGL((ss_nn_kernel<1, 1>), dim3(d.T, nseq, zb), dim3(64), 0, st, d, seq0, off);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 1, st))) return rc;
   if ((rc = ss_probe_begin(e, 2, st))) return rc;
