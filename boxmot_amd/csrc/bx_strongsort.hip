@@ -1332,6 +1332,49 @@ __device__ void matching_cascade(SsCtx& x, double max_d, const int* ti, int nt, 
   }
 }
 
+// kf_update_soa(KIND_BYTE, mean, cov, 1, z, conf) on eight lanes (r = 0..7 of the same wave):
+// lane r owns covariance row r and mean[r]; the innovation covariance and the gain rows travel
+// by in-group shuffles, every entry being the expression kf_update_soa evaluates (same order).
+__device__ void kf_update_octet(double* mean, double* cov, const double* z, double conf,
+                                int r) {
+  auto shfl = [](double v, int src) { return __shfl(v, src, 8); };
+  double* crow = cov + 8 * r;
+  double cr[8], mm[8];
+  for (int j = 0; j < 8; j++) cr[j] = crow[j];
+  for (int q = 0; q < 8; q++) mm[q] = mean[q];
+  double rr[4], S[16], L[16];
+  kf_meas_noise(KIND_BYTE, mm, conf, rr);
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) S[4 * i + j] = shfl(cr[j], i) + (i == j ? rr[i] : 0.0);
+  if (!chol4(S, L)) return;
+  double Kr[4], y[4];  // gain row r
+  for (int i = 0; i < 4; i++) {
+    double sv = cr[i];
+    for (int k = 0; k < i; k++) sv -= L[4 * i + k] * y[k];
+    y[i] = sv / L[4 * i + i];
+  }
+  for (int i = 3; i >= 0; i--) {
+    double sv = y[i];
+    for (int k = i + 1; k < 4; k++) sv -= L[4 * k + i] * Kr[k];
+    Kr[i] = sv / L[4 * i + i];
+  }
+  double sm = 0.0;
+  for (int k = 0; k < 4; k++) sm += (z[k] - mm[k]) * Kr[k];
+  const double mnew = mm[r] + sm;
+  double ks[4];
+  for (int j = 0; j < 4; j++) {
+    double sv = 0.0;
+    for (int k = 0; k < 4; k++) sv += Kr[k] * S[4 * k + j];
+    ks[j] = sv;
+  }
+  for (int j = 0; j < 8; j++) {
+    double sv = 0.0;
+    for (int k = 0; k < 4; k++) sv += ks[k] * shfl(Kr[k], j);
+    crow[j] = cr[j] - sv;
+  }
+  mean[r] = mnew;  // the group read mean[] above (same wave, in order)
+}
+
 // Track.update (track.py:204-277), wave-cooperative: Kalman update and scalars on lane 0, the
 // feature vectors (similarity, adaptive-EMA smoothing, norms) on all lanes.
 __device__ void track_update(SsCtx& x, int slot, int di) {
@@ -1340,12 +1383,12 @@ __device__ void track_update(SsCtx& x, int slot, int di) {
   SsTrk& t = x.trk[slot];
   const double* d = x.det(di);
   const int dk = x.det_in(di);
-  if (lane == 0) {
+  if (lane < 8) {
     double bb[4];
     det_xyah(d, bb);
-    t.conf = d[4], t.cls = d[5], t.det_ind = d[6];
-    kf_update_soa(KIND_BYTE, t.mean, t.cov, 1, bb, t.conf);
+    kf_update_octet(t.mean, t.cov, bb, d[4], lane);
   }
+  if (lane == 0) t.conf = d[4], t.cls = d[5], t.det_ind = d[6];
   __syncthreads();
   const double* nf = g.nf + ((size_t)x.seq * g.D + dk) * F;
   const double* pr = g.dprep + ((size_t)x.seq * g.D + dk) * 4;
