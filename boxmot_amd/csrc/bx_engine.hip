@@ -83,7 +83,24 @@ struct RegRow {
     if constexpr (sizeof(FT) == 4) return sqrtf((float)s);
     else return sqrt(s);
   }
+  // Div32's product form for the whole row under ONE wave-uniform test (zeros included: the
+  // product keeps x/n's signed zero); a row with a tiny/NaN quotient anywhere takes Div32.
   __device__ void div(FT n) {
+    if constexpr (sizeof(FT) == 4) {
+      const double rn = 1.0 / (double)n;
+      double p[REG_EPL];
+      bool fast = true;
+#pragma unroll
+      for (int r = 0; r < REG_EPL; r++) {
+        p[r] = (double)v[r] * rn;
+        fast &= fabs(p[r]) >= 0x1p-125 || p[r] == 0.0;
+      }
+      if (__ballot(!fast) == 0ull) {
+#pragma unroll
+        for (int r = 0; r < REG_EPL; r++) v[r] = (float)p[r];
+        return;
+      }
+    }
     const DivBy<FT> d(n);
 #pragma unroll
     for (int r = 0; r < REG_EPL; r++) v[r] = d(v[r]);
@@ -1405,12 +1422,9 @@ __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
         g.store(sm, F);
         dn = g.template np_dn<NPF>(wb, F);
       } else {
-        const DivBy<FT> n3(g.norm(F));
+        g.div(g.norm(F));
 #pragma unroll
-        for (int q = 0; q < REG_EPL; q++) {
-          FT g3 = n3(g.v[q]);
-          m.v[q] = a * m.v[q] + bb * g3;
-        }
+        for (int q = 0; q < REG_EPL; q++) m.v[q] = a * m.v[q] + bb * g.v[q];
         m.div(m.norm(F));
         m.store(sm, F);
         dn = m.template np_dn<NPF>(wb, F);
