@@ -336,9 +336,9 @@ __device__ __forceinline__ void det_measurement(const float* r, double* meas) {
 // float32 norm dn of (float)f2 that embedding_distance scales the det row by (matching.py:
 // 266-287).  Only the three norms are stored: every later use (K1c's cosine rows, K5's EMA)
 // recomputes f2 = (f / n1) / n2 elementwise from the input row, bit-identically.
-// Grid (n_seq, ceil(D/K1_DETS)); each wave walks its block's detections with stride 4, the
-// next row's load in flight while the current one is normalised.
-constexpr int K1_DETS = 8;  // detections per K1 block: 4 per wave keeps ~8 waves per SIMD busy
+// Grid (n_seq, ceil(D/K1_DETS)); each wave walks its block's detections with stride 4 (no
+// prefetch of the next row: the lower VGPR count buys more resident waves, which hide more).
+constexpr int K1_DETS = 8;  // detections per K1 block (2 per wave)
 template <typename FT, bool NPF>
 __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
                                                          const float* __restrict__ dets,
@@ -373,20 +373,14 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
   };
   if (F <= REG_F) {
     float* wb = s_w + w * REG_F;
-    int k = next(k0 + w);
-    RegRow<FT> x;
-    if (k < k1) x.load(embs + (size_t)(d0 + k) * F, F);
-    while (k < k1) {
-      const int kn = next(k + NWAVE);
-      RegRow<FT> nx;
-      if (kn < k1) nx.load(embs + (size_t)(d0 + kn) * F, F);
+    for (int k = next(k0 + w); k < k1; k = next(k + NWAVE)) {
+      RegRow<FT> x;
+      x.load(embs + (size_t)(d0 + k) * F, F);
       const FT n1 = x.norm(F);
       x.div(n1);
       const FT n2 = x.norm(F);
       x.div(n2);
       put_norms(k, n1, n2, x.template np_dn<NPF>(wb, F));
-      x = nx;
-      k = kn;
     }
     return;
   }
@@ -1394,30 +1388,18 @@ __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
     return nrec;
   };
   if (F <= REG_F) {
-    int r = next(blockIdx.y * NWAVE + wave_id());
-    RegRow<FT> g, m;
-    int2 rc = make_int2(0, 0);
-    if (r < nrec) {
-      rc = rec(r);
-      g.load(fembs + (size_t)rc.y * F, F);
-      m.load(feat + (size_t)(rc.x & 0xffff) * F, F);
-    }
-    while (r < nrec) {  // rows of the next record load while this one is computed
-      const int rn = next(r + STEP);
-      RegRow<FT> ng, nm;
-      int2 nrc = make_int2(0, 0);
-      if (rn < nrec) {
-        nrc = rec(rn);
-        ng.load(fembs + (size_t)nrc.y * F, F);
-        nm.load(feat + (size_t)(nrc.x & 0xffff) * F, F);
-      }
+    for (int r = next(blockIdx.y * NWAVE + wave_id()); r < nrec; r = next(r + STEP)) {
+      const int2 rc = rec(r);
       const int slot = rc.x & 0xffff, kind = rc.x >> 16, dk = rc.y;
+      RegRow<FT> g, m;  // no prefetch of the next record: fewer VGPRs, more waves in flight
+      g.load(fembs + (size_t)dk * F, F);
+      FT* sm = feat + (size_t)slot * F;
+      if ((kind & 3) != R_NEW) m.load(sm, F);
       const FT n1 = (FT)P.dnrm[((size_t)s * D + dk) * 4];
       const FT n2 = (FT)P.dnrm[((size_t)s * D + dk) * 4 + 1];
-      FT* sm = feat + (size_t)slot * F;
       g.div(n1);
       g.div(n2);
-      float dn;  // the new smooth_feat's numpy float32 norm, for the next frame's K1c
+      float dn;
       if ((kind & 3) == R_NEW) {
         g.store(sm, F);
         dn = g.template np_dn<NPF>(wb, F);
@@ -1430,10 +1412,6 @@ __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
         dn = m.template np_dn<NPF>(wb, F);
       }
       if (lane == 0) P.tdn[(size_t)s * T + slot] = dn;
-      r = rn;
-      rc = nrc;
-      g = ng;
-      m = nm;
     }
     return;
   }
