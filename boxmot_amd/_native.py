@@ -26,6 +26,9 @@ HIPCC_FLAGS = [
     "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
     # numpy-identical rounding: no FMA contraction, IEEE f32 division/sqrt
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
+    # MFMA accumulators in the VGPR form: the compiler otherwise copies the StrongSort NN
+    # kernel's accumulator tiles between VGPRs and AGPRs around every k-block
+    "-mllvm", "-amdgpu-mfma-vgpr-form=1",
 ]
 SOURCES = ["bx_engine.hip", "bx_ops.hip", "bx_ocsort.hip", "bx_nn.hip", "bx_boost.hip",
            "bx_strongsort.hip", "bx_io.cpp"]

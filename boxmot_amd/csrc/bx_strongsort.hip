@@ -618,6 +618,9 @@ __global__ void __launch_bounds__(64)
 }
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+#ifndef BX_NN_KU
+#define BX_NN_KU 2
+#endif
 
 // NearestNeighborDistanceMetric.distance (linear_assignment.py:468-497, 595-618) for G listed
 // confirmed tracks per wave: rows = each track's distinct gallery vectors (pre-normalised x/den),
@@ -699,20 +702,42 @@ __global__ void __launch_bounds__(64)
       for (int rt = 0; rt < RT; rt++)
 #pragma unroll
         for (int dt = 0; dt < 4; dt++) acc[rt][dt] = (d4){0.0, 0.0, 0.0, 0.0};
-      for (int k = 0; k < F; k += 4) {
+      // straight-line steps of KS (KU MFMA k-steps): every operand of the step is loaded
+      // before its MFMAs; padded tiles (rows past a track's samples, detection tiles past n)
+      // read valid rows and are discarded below, so no branch splits the accumulator chains
+      constexpr int KU = BX_NN_KU, KS = 4 * KU;  // MFMA k-steps per straight-line block
+      const int F16 = F - F % KS;
+      for (int k = 0; k < F16; k += KS) {
+        double a[KU][RT], bb[KU][4];
+#pragma unroll
+        for (int u = 0; u < KU; u++) {
+#pragma unroll
+          for (int rt = 0; rt < RT; rt++) a[u][rt] = ap[rt][k + 4 * u];
+#pragma unroll
+          for (int dt = 0; dt < 4; dt++) bb[u][dt] = bp[dt][k + 4 * u];
+        }
+#pragma unroll
+        for (int u = 0; u < KU; u++)
+#pragma unroll
+          for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int dt = 0; dt < 4; dt++)
+              acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][rt], bb[u][dt],
+                                                                 acc[rt][dt], 0, 0, 0);
+      }
+      for (int k = F16; k < F; k += 4) {  // tail: lanes past F multiply zeros (a clamped read)
         const bool in = k + kl < F;
+        const int kk = in ? k : F - 1 - kl;
         double a[RT], bb[4];
 #pragma unroll
-        for (int rt = 0; rt < RT; rt++) a[rt] = in ? ap[rt][k] : 0.0;
+        for (int rt = 0; rt < RT; rt++) { const double v = ap[rt][kk]; a[rt] = in ? v : 0.0; }
 #pragma unroll
-        for (int dt = 0; dt < 4; dt++) bb[dt] = (in && dt < ndt) ? bp[dt][k] : 0.0;
+        for (int dt = 0; dt < 4; dt++) { const double v = bp[dt][kk]; bb[dt] = in ? v : 0.0; }
 #pragma unroll
         for (int rt = 0; rt < RT; rt++)
 #pragma unroll
           for (int dt = 0; dt < 4; dt++)
-            if (dt < ndt)
-              acc[rt][dt] =
-                  __builtin_amdgcn_mfma_f64_16x16x4f64(a[rt], bb[dt], acc[rt][dt], 0, 0, 0);
+            acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[rt], bb[dt], acc[rt][dt], 0, 0, 0);
       }
       // lane holds column cl of each detection tile, rows kl + 4 j of each row tile
 #pragma unroll

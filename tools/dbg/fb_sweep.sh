@@ -1,5 +1,6 @@
 mkdir -p gpurun_out
-for v in k1np4 k1np8 k1p16 k1np16; do
-  BX_LIB_PATH=boxmot_amd/lib/libbxassoc_$v.so timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/fb_$v.log 2>&1 || exit 1
+for gg in 4 2 1; do
+  BX_SS_NN_G=$gg timeout -k 10 200 python -u bench.py --config strongsort --no-cpu-baseline > gpurun_out/fb_g$gg.log 2>&1 || exit 1
 done
-timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/fb_base.log 2>&1
+timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/fb_bot.log 2>&1
+timeout -k 10 200 python -u bench.py --config boosttrack --no-cpu-baseline > gpurun_out/fb_boost.log 2>&1
