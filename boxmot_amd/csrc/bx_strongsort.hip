@@ -622,6 +622,48 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #define BX_NN_KU 2
 #endif
 
+// The NN contraction's k loop for RT row tiles x NDT detection tiles: straight-line blocks of
+// KU MFMA k-steps, every operand of a block loaded before its MFMAs; padded rows (past a track's
+// samples) read valid rows and are discarded by the caller, so no branch splits the chains.
+template <int RT, int NDT>
+__device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT], const double* const (&bp)[4],
+                                         int F, int kl, d4 (&acc)[RT][4]) {
+  constexpr int KU = BX_NN_KU, KS = 4 * KU;
+  const int FB = F - F % KS;
+  for (int k = 0; k < FB; k += KS) {
+    double a[KU][RT], bb[KU][NDT];
+#pragma unroll
+    for (int u = 0; u < KU; u++) {
+#pragma unroll
+      for (int rt = 0; rt < RT; rt++) a[u][rt] = ap[rt][k + 4 * u];
+#pragma unroll
+      for (int dt = 0; dt < NDT; dt++) bb[u][dt] = bp[dt][k + 4 * u];
+    }
+#pragma unroll
+    for (int u = 0; u < KU; u++)
+#pragma unroll
+      for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+        for (int dt = 0; dt < NDT; dt++)
+          acc[rt][dt] =
+              __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][rt], bb[u][dt], acc[rt][dt], 0, 0, 0);
+  }
+  for (int k = FB; k < F; k += 4) {  // tail: lanes past F multiply zeros (a clamped read)
+    const bool in = k + kl < F;
+    const int kk = in ? k : F - 1 - kl;
+    double a[RT], bb[NDT];
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++) { const double v = ap[rt][kk]; a[rt] = in ? v : 0.0; }
+#pragma unroll
+    for (int dt = 0; dt < NDT; dt++) { const double v = bp[dt][kk]; bb[dt] = in ? v : 0.0; }
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+      for (int dt = 0; dt < NDT; dt++)
+        acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[rt], bb[dt], acc[rt][dt], 0, 0, 0);
+  }
+}
+
 // NearestNeighborDistanceMetric.distance (linear_assignment.py:468-497, 595-618) for G listed
 // confirmed tracks per wave: rows = each track's distinct gallery vectors (pre-normalised x/den),
 // columns = this frame's normalised detections; out = 1 - clip(max over the track's rows).
@@ -702,42 +744,11 @@ __global__ void __launch_bounds__(64)
       for (int rt = 0; rt < RT; rt++)
 #pragma unroll
         for (int dt = 0; dt < 4; dt++) acc[rt][dt] = (d4){0.0, 0.0, 0.0, 0.0};
-      // straight-line steps of KS (KU MFMA k-steps): every operand of the step is loaded
-      // before its MFMAs; padded tiles (rows past a track's samples, detection tiles past n)
-      // read valid rows and are discarded below, so no branch splits the accumulator chains
-      constexpr int KU = BX_NN_KU, KS = 4 * KU;  // MFMA k-steps per straight-line block
-      const int F16 = F - F % KS;
-      for (int k = 0; k < F16; k += KS) {
-        double a[KU][RT], bb[KU][4];
-#pragma unroll
-        for (int u = 0; u < KU; u++) {
-#pragma unroll
-          for (int rt = 0; rt < RT; rt++) a[u][rt] = ap[rt][k + 4 * u];
-#pragma unroll
-          for (int dt = 0; dt < 4; dt++) bb[u][dt] = bp[dt][k + 4 * u];
-        }
-#pragma unroll
-        for (int u = 0; u < KU; u++)
-#pragma unroll
-          for (int rt = 0; rt < RT; rt++)
-#pragma unroll
-            for (int dt = 0; dt < 4; dt++)
-              acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][rt], bb[u][dt],
-                                                                 acc[rt][dt], 0, 0, 0);
-      }
-      for (int k = F16; k < F; k += 4) {  // tail: lanes past F multiply zeros (a clamped read)
-        const bool in = k + kl < F;
-        const int kk = in ? k : F - 1 - kl;
-        double a[RT], bb[4];
-#pragma unroll
-        for (int rt = 0; rt < RT; rt++) { const double v = ap[rt][kk]; a[rt] = in ? v : 0.0; }
-#pragma unroll
-        for (int dt = 0; dt < 4; dt++) { const double v = bp[dt][kk]; bb[dt] = in ? v : 0.0; }
-#pragma unroll
-        for (int rt = 0; rt < RT; rt++)
-#pragma unroll
-          for (int dt = 0; dt < 4; dt++)
-            acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[rt], bb[dt], acc[rt][dt], 0, 0, 0);
+      switch (ndt) {  // detection tiles as a compile-time count: no MFMA on absent tiles
+        case 4: nn_kloop<RT, 4>(ap, bp, F, kl, acc); break;
+        case 3: nn_kloop<RT, 3>(ap, bp, F, kl, acc); break;
+        case 2: nn_kloop<RT, 2>(ap, bp, F, kl, acc); break;
+        default: nn_kloop<RT, 1>(ap, bp, F, kl, acc); break;
       }
       // lane holds column cl of each detection tile, rows kl + 4 j of each row tile
 #pragma unroll
