@@ -623,30 +623,48 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #endif
 
 // The NN contraction's k loop for RT row tiles x NDT detection tiles: straight-line blocks of
-// KU MFMA k-steps, every operand of a block loaded before its MFMAs; padded rows (past a track's
+// KU MFMA k-steps, the next block's operands loaded before this block's MFMAs; padded rows (past a track's
 // samples) read valid rows and are discarded by the caller, so no branch splits the chains.
 template <int RT, int NDT>
 __device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT], const double* const (&bp)[4],
                                          int F, int kl, d4 (&acc)[RT][4]) {
   constexpr int KU = BX_NN_KU, KS = 4 * KU;
   const int FB = F - F % KS;
-  for (int k = 0; k < FB; k += KS) {
+  if (FB > 0) {  // software-pipelined: block k+1's operands in flight during block k's MFMAs
     double a[KU][RT], bb[KU][NDT];
 #pragma unroll
     for (int u = 0; u < KU; u++) {
 #pragma unroll
-      for (int rt = 0; rt < RT; rt++) a[u][rt] = ap[rt][k + 4 * u];
+      for (int rt = 0; rt < RT; rt++) a[u][rt] = ap[rt][4 * u];
 #pragma unroll
-      for (int dt = 0; dt < NDT; dt++) bb[u][dt] = bp[dt][k + 4 * u];
+      for (int dt = 0; dt < NDT; dt++) bb[u][dt] = bp[dt][4 * u];
     }
+    for (int k = 0; k < FB; k += KS) {
+      const int kn = k + KS < FB ? k + KS : k;  // the last block re-reads its own operands
+      double na[KU][RT], nb[KU][NDT];
 #pragma unroll
-    for (int u = 0; u < KU; u++)
+      for (int u = 0; u < KU; u++) {
 #pragma unroll
-      for (int rt = 0; rt < RT; rt++)
+        for (int rt = 0; rt < RT; rt++) na[u][rt] = ap[rt][kn + 4 * u];
 #pragma unroll
-        for (int dt = 0; dt < NDT; dt++)
-          acc[rt][dt] =
-              __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][rt], bb[u][dt], acc[rt][dt], 0, 0, 0);
+        for (int dt = 0; dt < NDT; dt++) nb[u][dt] = bp[dt][kn + 4 * u];
+      }
+#pragma unroll
+      for (int u = 0; u < KU; u++)
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+          for (int dt = 0; dt < NDT; dt++)
+            acc[rt][dt] =
+                __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][rt], bb[u][dt], acc[rt][dt], 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < KU; u++) {
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++) a[u][rt] = na[u][rt];
+#pragma unroll
+        for (int dt = 0; dt < NDT; dt++) bb[u][dt] = nb[u][dt];
+      }
+    }
   }
   for (int k = FB; k < F; k += 4) {  // tail: lanes past F multiply zeros (a clamped read)
     const bool in = k + kl < F;
