@@ -236,6 +236,35 @@ __device__ double pw_fold(int n, const double* leaf) {
 // sqrt of numpy's pairwise sum of squares of x[0..n); lo/ln/leaf: per-wave scratch
 __device__ double wpw_norm(const double* x, int n, int* lo, int* ln, double* leaf) {
   const int lane = threadIdx.x & 63;
+  const int nlf = n >> 7;
+  if ((n & 127) == 0 && nlf > 0 && (nlf & (nlf - 1)) == 0 && nlf <= 32) {
+    // n = 128·2^j: the split tree is balanced over 128-element leaves in order, so leaf sums
+    // (8 lanes each, numpy's 8 accumulators) fold by xor shuffles across lane groups; up to 8
+    // leaves per pass, the passes' sums folded as the tree's top levels
+    const int grp = lane >> 3, k = lane & 7, np = nlf > 8 ? nlf / 8 : 1, gl = nlf < 8 ? nlf : 8;
+    double part[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      part[p] = 0.0;
+      if (p < np) {
+        double r = 0.0;
+        if (grp < gl) {
+          const double* o = x + 128 * (p * 8 + grp);
+          r = o[k] * o[k];
+          for (int i = 8 + k; i < 128; i += 8) r += o[i] * o[i];
+        }
+        r = r + __shfl_xor(r, 1);
+        r = r + __shfl_xor(r, 2);
+        r = r + __shfl_xor(r, 4);
+        for (int d = 8; d < 8 * gl; d <<= 1) r = r + __shfl_xor(r, d);
+        part[p] = r;
+      }
+    }
+    const double s = np == 1 ? part[0]
+                     : np == 2 ? part[0] + part[1]
+                               : (part[0] + part[1]) + (part[2] + part[3]);
+    return sqrt(__shfl(s, 0));
+  }
   if (lane == 0) {
     const int c = pw_leaves(n, lo, ln);
     ln[PW_MAXLEAF - 1] = c;

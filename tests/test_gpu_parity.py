@@ -765,6 +765,17 @@ def test_strongsort_large_scene_vs_oracle(torch_cuda):
     run_ss_batched(torch_cuda, [sc], 20, dict(SS_ARGS), 512, track_cap=1024)
 
 
+@pytest.mark.parametrize("emb_dim", [128, 1024, 2048, 640])
+def test_strongsort_feature_widths_vs_oracle(torch_cuda, emb_dim):
+    """Feature widths around the NN kernel's k-blocks and the pairwise norm's leaf tree: one
+    leaf (128), 8 and 16 leaves (1024, 2048: the shuffle fold), 640 (the generic split tree)."""
+    from boxmot_amd.synth import SyntheticScene
+
+    scenes = [SyntheticScene(n_obj=20 + 10 * s, seed=900 + s, emb_dim=emb_dim,
+                             emb_dtype=np.float64, conf_lo=0.15) for s in range(2)]
+    run_ss_batched(torch_cuda, scenes, 15, dict(SS_ARGS), emb_dim)
+
+
 def test_strongsort_dropin(torch_cuda, monkeypatch):
     from boxmot_amd import StrongSort, create_tracker
 
