@@ -2251,9 +2251,10 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 0, st))) return rc;
   if ((rc = ss_probe_begin(e, 1, st))) return rc;
-  // tracks per wave: share detection loads among 4 when that still leaves ~8 waves per CU
+  // tracks per wave: 4 share every detection load (the detection blocks' split over waves
+  // below restores the wave count), fewer only for a handful of tracks
   const long qtracks = (long)d.T * nseq;
-  int gsel = qtracks >= 4 * 2048 ? 4 : (qtracks >= 2 * 2048 ? 2 : 1);
+  int gsel = qtracks >= 256 ? 4 : (qtracks >= 64 ? 2 : 1);
   if (const char* ev = std::getenv("BX_SS_NN_G")) gsel = std::atoi(ev);  // diagnostics
   // detection blocks of 64 split over waves too when the tracks alone give too few waves
   const long waves = (long)((d.T + gsel - 1) / gsel) * nseq;
