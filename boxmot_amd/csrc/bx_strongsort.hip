@@ -1458,6 +1458,8 @@ __device__ void kf_update_octet(double* mean, double* cov, const double* z, doub
   mean[r] = mnew;  // the group read mean[] above (same wave, in order)
 }
 
+constexpr int UQ = 8;  // track_update keeps feature rows of up to 64·UQ elements in registers
+
 // Track.update (track.py:204-277), wave-cooperative: Kalman update and scalars on lane 0, the
 // feature vectors (similarity, adaptive-EMA smoothing, norms) on all lanes.
 __device__ void track_update(SsCtx& x, int slot, int di) {
@@ -1484,7 +1486,56 @@ __device__ void track_update(SsCtx& x, int slot, int di) {
   } else {
     double* dst = vecp(g, x.seq, slot, v);
     const size_t vi = vidx(g, x.seq, slot, v);
-    if (nfeat > 0) {
+    if (nfeat > 0 && F <= 64 * UQ) {
+      // the rows in registers (element lane + 64 r in slot r, wdot's order): the EMA vector is
+      // written once and its norms come from registers; only numpy's pairwise tree reads it back
+      const int lv = t.feat[nfeat - 1];
+      const double* last = vecp(g, x.seq, slot, lv);
+      const double wl = g.vwn[vidx(g, x.seq, slot, lv)];
+      double rn[UQ], rl[UQ];
+#pragma unroll
+      for (int r = 0; r < UQ; r++) {
+        const int q = lane + 64 * r;
+        rn[r] = q < F ? nf[q] : 0.0;
+        rl[r] = q < F ? last[q] : 0.0;
+      }
+      auto rdot = [&](const double* u, const double* v2) {
+        double sd = 0.0;
+#pragma unroll
+        for (int r = 0; r < UQ; r++)
+          if (lane + 64 * r < F) sd += u[r] * v2[r];
+#pragma unroll
+        for (int dd = 32; dd >= 1; dd >>= 1) sd += __shfl_xor(sd, dd);
+        return sd;
+      };
+      const double sim = rdot(rn, rl) / (pr[2] * wl + 1e-8);
+      const double cf = d[4] > 0.7 ? 1.0 : (d[4] > 0.3 ? 0.5 : 0.2);
+      const double af = sim > 0.7 ? 1.0 : (sim > 0.4 ? 0.7 : 0.4);
+      const double a = clipd(t.base_alpha * cf * af, 0.1, 0.95);
+#pragma unroll
+      for (int r = 0; r < UQ; r++) rl[r] = a * rl[r] + (1 - a) * rn[r];
+      const double ns = sqrt(rdot(rl, rl)) + 1e-8;
+#pragma unroll
+      for (int r = 0; r < UQ; r++) {
+        rl[r] = rl[r] / ns;
+        const int q = lane + 64 * r;
+        if (q < F) dst[q] = rl[r];
+      }
+      const double wn = sqrt(rdot(rl, rl));
+      __syncthreads();  // dst visible to the pairwise tree's lane mapping
+      const double pn = wpw_norm(dst, F, x.w.pwlo, x.w.pwln, x.w.pwleaf) + 1e-8;
+      double* dstn = vecnp(g, x.seq, slot, v);
+#pragma unroll
+      for (int r = 0; r < UQ; r++) {
+        const int q = lane + 64 * r;
+        if (q < F) dstn[q] = rl[r] / pn;
+      }
+      if (lane == 0) {
+        t.app_cons = 0.9 * t.app_cons + 0.1 * sim;
+        g.vwn[vi] = wn;
+        g.vden[vi] = pn;
+      }
+    } else if (nfeat > 0) {
       const int lv = t.feat[nfeat - 1];
       const double* last = vecp(g, x.seq, slot, lv);
       const double wl = g.vwn[vidx(g, x.seq, slot, lv)];
