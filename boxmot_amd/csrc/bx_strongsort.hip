@@ -65,7 +65,7 @@ struct SsTrk {
   double confh[MAXC];
   int id, state, hits, age, tsu, max_age, n_init;
   int nvel, npos, nconf, nfeat, missed, confirmed_det, low_streak, high_streak, lost_frame;
-  int gal_n;                 // gallery length (entries in no particular order, see ss_fit_kernel)
+  int gal_n;                 // gallery length (entries sorted by quality desc, time asc)
   int gal_clock;             // partial_fit append counter: the entries' insertion times
   int born_dk;               // input detection of this frame's birth (first vector copied by
                              // ss_fit_kernel), else -1
@@ -2147,7 +2147,8 @@ __global__ void __launch_bounds__(64)
 // truncates.  Inductively its list is ordered by (quality desc, insertion time asc) from its first
 // sort on, and a stable sort of appended entries keeps that order, so appending k features one by
 // one with a truncation after each equals appending all k and keeping the `budget` best under
-// (quality desc, time asc) — what this kernel does (rank by comparison in LDS, compaction).
+// (quality desc, time asc) — what this kernel does.  The stored gallery is kept in that order,
+// so the new entries merge in by rank (O(n·k) comparisons in LDS, not a full re-rank).
 constexpr int GB_MAX = 320;
 __global__ void __launch_bounds__(64) ss_fit_kernel(SsDev g, int seq0) {
   __shared__ double q_s[GB_MAX];
@@ -2177,45 +2178,55 @@ __global__ void __launch_bounds__(64) ss_fit_kernel(SsDev g, int seq0) {
   if (sq[Q_ANYF]) {
     const int budget = sq[Q_BUDGET];
     const int keep = budget / 4 < 5 ? budget / 4 : 5;
-    int lim = -1;
     if (k < ntr && t.state == 2) {  // active target: its features appended in list order
-      const int nf = t.nfeat, c0 = t.gal_clock;
-      for (int q = lane; q < nf; q += 64) {
-        const int v = t.feat[q];
-        gv[n + q] = v;
-        gq[n + q] = g.vwn[vidx(g, seq, slot, v)];
-        gt[n + q] = c0 + q;
-      }
-      n += nf;
-      if (budget > 0 && n > budget) lim = budget;
-      if (lane == 0) t.gal_clock = c0 + nf;
-    } else if (n > keep) {  // inactive target: trimmed to min(budget // 4, 5)
-      lim = keep;
-    }
-    __syncthreads();
-    if (lim >= 0) {
-      for (int i = lane; i < n; i += 64) {
+      // The stored gallery is sorted by (quality desc, time asc) — every update below keeps it
+      // so — and the appended features are newer than all of it: an old entry's rank is its
+      // index plus the new entries of higher quality, a new entry's the old entries of at least
+      // its quality (binary search) plus the new ones ahead of it.  Entries ranked below the
+      // budget land at their rank; old ones already there are not rewritten.
+      const int nfe = t.nfeat, c0 = t.gal_clock, n0 = n, nt = n0 + nfe;
+      for (int i = lane; i < n0; i += 64) {
         q_s[i] = gq[i];
         t_s[i] = gt[i];
         v_s[i] = gv[i];
       }
+      for (int q = lane; q < nfe; q += 64) {
+        const int v = t.feat[q];
+        q_s[n0 + q] = g.vwn[vidx(g, seq, slot, v)];
+        t_s[n0 + q] = c0 + q;
+        v_s[n0 + q] = v;
+      }
       __syncthreads();
-      const int kept = wave_compact(
-          n,
-          [&](int i) {
-            const double qi = q_s[i];
-            const int ti = t_s[i];
-            int r = 0;
-            for (int j = 0; j < n; j++) r += (q_s[j] > qi) || (q_s[j] == qi && t_s[j] < ti);
-            return r < lim;
-          },
-          [&](int i, int p) {
-            gv[p] = v_s[i];
-            gq[p] = q_s[i];
-            gt[p] = t_s[i];
-          });
-      n = kept;
+      const int lim = (budget > 0 && nt > budget) ? budget : nt;
+      for (int i = lane; i < nt; i += 64) {
+        const double qi = q_s[i];
+        int r;
+        if (i < n0) {
+          r = i;
+          for (int j = n0; j < nt; j++) r += q_s[j] > qi;
+        } else {
+          int lo = 0, hi = n0;  // first old entry of lower quality
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (q_s[mid] >= qi) lo = mid + 1;
+            else hi = mid;
+          }
+          r = lo;
+          for (int j = n0; j < i; j++) r += q_s[j] >= qi;
+          for (int j = i + 1; j < nt; j++) r += q_s[j] > qi;
+        }
+        if (r < lim && (i >= n0 || r != i)) {
+          gv[r] = v_s[i];
+          gq[r] = qi;
+          gt[r] = t_s[i];
+        }
+      }
+      n = lim;
+      if (lane == 0) t.gal_clock = c0 + nfe;
+    } else if (n > keep) {  // inactive target: trimmed to its min(budget // 4, 5) best
+      n = keep;
     }
+    __syncthreads();
     if (lane == 0) t.gal_n = n;
   }
   __syncthreads();
