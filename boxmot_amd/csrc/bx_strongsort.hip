@@ -654,9 +654,10 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // The NN contraction's k loop for RT row tiles x NDT detection tiles: straight-line blocks of
 // KU MFMA k-steps, the next block's operands loaded before this block's MFMAs; padded rows (past a track's
 // samples) read valid rows and are discarded by the caller, so no branch splits the chains.
-template <int RT, int NDT>
-__device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT], const double* const (&bp)[4],
-                                         int F, int kl, d4 (&acc)[RT][4]) {
+template <int RT, int NDT, int NA>
+__device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT],
+                                         const double* const (&bp)[NA], int F, int kl,
+                                         d4 (&acc)[RT][NA]) {
   constexpr int KU = BX_NN_KU, KS = 4 * KU;
   const int FB = F - F % KS;
   if (FB > 0) {  // software-pipelined: block k+1's operands in flight during block k's MFMAs
@@ -718,7 +719,7 @@ __device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT], const do
 // the G tracks concatenated) by up to 4 detection tiles (64 detections) on the fp64 matrix cores,
 // so every detection row loaded serves up to RT tiles and every sample row 4 detection tiles.
 // Each output's k-chain is the oracle's ascending fma chain whatever the tiling.
-template <int G, int RT>
+template <int G, int RT, int NDT>
 __global__ void __launch_bounds__(64)
     ss_nn_kernel(SsDev g, int seq0, const int* __restrict__ det_off) {
   __shared__ int rowv[G][64];
@@ -762,16 +763,17 @@ __global__ void __launch_bounds__(64)
   const int ntile = ntile_s;
   const double* dnb = g.dn + (size_t)seq * g.D * F;
   const int kl = lane >> 4, cl = lane & 15;
-  for (int db = 64 * blockIdx.z; db < n; db += 64 * gridDim.z) {  // this wave's detection blocks
-    const int ndt = n - db >= 64 ? 4 : (n - db + 15) / 16;  // detection tiles in this block
-    double best[G][4];
+  constexpr int DB = 16 * NDT;  // detections per block: NDT tiles of 16
+  for (int db = DB * blockIdx.z; db < n; db += DB * gridDim.z) {  // this wave's detection blocks
+    const int ndt = n - db >= DB ? NDT : (n - db + 15) / 16;  // detection tiles in this block
+    double best[G][NDT];
 #pragma unroll
     for (int q = 0; q < G; q++)
 #pragma unroll
-      for (int dt = 0; dt < 4; dt++) best[q][dt] = -INF;
-    const double* bp[4];
+      for (int dt = 0; dt < NDT; dt++) best[q][dt] = -INF;
+    const double* bp[NDT];
 #pragma unroll
-    for (int dt = 0; dt < 4; dt++) {
+    for (int dt = 0; dt < NDT; dt++) {
       const int col = db + 16 * dt + cl;
       bp[dt] = dnb + (size_t)(col < n ? col : 0) * F + kl;
     }
@@ -786,16 +788,20 @@ __global__ void __launch_bounds__(64)
         ap[rt] = vecnp(g, seq, slot, rowv[q][row < nrow_s[q] ? row : 0]) + kl;
         nrt += p0 + rt < ntile;
       }
-      d4 acc[RT][4];
+      d4 acc[RT][NDT];
 #pragma unroll
       for (int rt = 0; rt < RT; rt++)
 #pragma unroll
-        for (int dt = 0; dt < 4; dt++) acc[rt][dt] = (d4){0.0, 0.0, 0.0, 0.0};
-      switch (ndt) {  // detection tiles as a compile-time count: no MFMA on absent tiles
-        case 4: nn_kloop<RT, 4>(ap, bp, F, kl, acc); break;
-        case 3: nn_kloop<RT, 3>(ap, bp, F, kl, acc); break;
-        case 2: nn_kloop<RT, 2>(ap, bp, F, kl, acc); break;
-        default: nn_kloop<RT, 1>(ap, bp, F, kl, acc); break;
+        for (int dt = 0; dt < NDT; dt++) acc[rt][dt] = (d4){0.0, 0.0, 0.0, 0.0};
+      // detection tiles as a compile-time count: no MFMA on absent tiles
+      if constexpr (NDT == 4) {
+        if (ndt == 4) nn_kloop<RT, 4, NDT>(ap, bp, F, kl, acc);
+        else if (ndt == 3) nn_kloop<RT, 3, NDT>(ap, bp, F, kl, acc);
+        else if (ndt == 2) nn_kloop<RT, 2, NDT>(ap, bp, F, kl, acc);
+        else nn_kloop<RT, 1, NDT>(ap, bp, F, kl, acc);
+      } else {
+        if (ndt == 2) nn_kloop<RT, 2, NDT>(ap, bp, F, kl, acc);
+        else nn_kloop<RT, 1, NDT>(ap, bp, F, kl, acc);
       }
       // lane holds column cl of each detection tile, rows kl + 4 j of each row tile
 #pragma unroll
@@ -804,7 +810,7 @@ __global__ void __launch_bounds__(64)
         const int ti = p0 + rt, q = tt[ti];
         const int nr = nrow_s[q] - tr0[ti];
 #pragma unroll
-        for (int dt = 0; dt < 4; dt++) {
+        for (int dt = 0; dt < NDT; dt++) {
           double m = -INF;
 #pragma unroll
           for (int j = 0; j < 4; j++)
@@ -824,7 +830,7 @@ __global__ void __launch_bounds__(64)
       if (q >= ng) break;
       double* out = g.nnd + ((size_t)seq * g.T + slot_s[q]) * g.D;
 #pragma unroll
-      for (int dt = 0; dt < 4; dt++) {
+      for (int dt = 0; dt < NDT; dt++) {
         const int col = db + 16 * dt + cl;
         if (kl == 0 && col < n) out[col] = 1.0 - clipd(best[q][dt], -1.0, 1.0);
       }
@@ -2302,6 +2308,16 @@ static size_t ss_lds_bytes(const SsDev& d) {
                        : (d.ws_lds == 2 ? (size_t)ws_lsap_bytes(d.N) : 0);
 }
 
+template <int G>
+static void launch_nn(const SsDev& d, int seq0, int nseq, int zb, int ndt, const int* off,
+                      hipStream_t st) {
+  const dim3 grid((d.T + G - 1) / G, nseq, zb);
+  if (ndt == 2)
+    hipLaunchKernelGGL((ss_nn_kernel<G, G, 2>), grid, dim3(64), 0, st, d, seq0, off);
+  else
+    hipLaunchKernelGGL((ss_nn_kernel<G, G, 4>), grid, dim3(64), 0, st, d, seq0, off);
+}
+
 static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int* off,
                      const double* embs, const double* warps, double* out, int* cnt,
                      hipStream_t st) {
@@ -2318,19 +2334,21 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   const long qtracks = (long)d.T * nseq;
   int gsel = qtracks >= 256 ? 4 : (qtracks >= 64 ? 2 : 1);
   if (const char* ev = std::getenv("BX_SS_NN_G")) gsel = std::atoi(ev);  // diagnostics
-  // detection blocks of 64 split over waves too when the tracks alone give too few waves
+  // detection blocks of 16·ndt (ndt = 2 tiles when the detection capacity is <= 64: half the
+  // accumulators, more resident waves), split over waves too when the tracks alone give too few
+  int ndtsel = d.D <= 64 ? 2 : 4;
+  if (const char* ev = std::getenv("BX_SS_NN_NDT")) ndtsel = std::atoi(ev) <= 2 ? 2 : 4;
   const long waves = (long)((d.T + gsel - 1) / gsel) * nseq;
   int zb = (int)((4096 + waves - 1) / waves);
-  const int nblk = (d.D + 63) / 64;
+  const int nblk = (d.D + 16 * ndtsel - 1) / (16 * ndtsel);
   zb = zb < 1 ? 1 : (zb > nblk ? nblk : zb);
+
   if (gsel >= 4)
-    hipLaunchKernelGGL((ss_nn_kernel<4, 4>), dim3((d.T + 3) / 4, nseq, zb), dim3(64), 0, st, d,
-                       seq0, off);
+    launch_nn<4>(d, seq0, nseq, zb, ndtsel, off, st);
   else if (gsel == 2)
-    hipLaunchKernelGGL((ss_nn_kernel<2, 2>), dim3((d.T + 1) / 2, nseq, zb), dim3(64), 0, st, d,
-                       seq0, off);
+    launch_nn<2>(d, seq0, nseq, zb, ndtsel, off, st);
   else
-    hipLaunchKernelGGL((ss_nn_kernel<1, 1>), dim3(d.T, nseq, zb), dim3(64), 0, st, d, seq0, off);
+    launch_nn<1>(d, seq0, nseq, zb, ndtsel, off, st);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 1, st))) return rc;
   if ((rc = ss_probe_begin(e, 2, st))) return rc;
