@@ -627,6 +627,42 @@ __global__ void __launch_bounds__(64)
   const double* x = embs + (size_t)(r0 + k) * F;
   double* dn = g.dn + ((size_t)seq * g.D + k) * F;
   double* nf = g.nf + ((size_t)seq * g.D + k) * F;
+  constexpr int PQ = 8;
+  if (F <= 64 * PQ) {  // the row in registers (element lane + 64 r, wdot's order)
+    double rx[PQ];
+#pragma unroll
+    for (int r = 0; r < PQ; r++) rx[r] = lane + 64 * r < F ? x[lane + 64 * r] : 0.0;
+    auto rdot = [&]() {
+      double sd = 0.0;
+#pragma unroll
+      for (int r = 0; r < PQ; r++)
+        if (lane + 64 * r < F) sd += rx[r] * rx[r];
+#pragma unroll
+      for (int dd = 32; dd >= 1; dd >>= 1) sd += __shfl_xor(sd, dd);
+      return sd;
+    };
+    const double fn = sqrt(rdot());
+    const double pwn = wpw_norm(x, F, lo, ln, leaf);
+    const double dd = pwn + 1e-8, dw = fn + 1e-8;
+#pragma unroll
+    for (int r = 0; r < PQ; r++) {
+      const int q = lane + 64 * r;
+      if (q < F) dn[q] = rx[r] / dd;
+      rx[r] = rx[r] / dw;
+      if (q < F) nf[q] = rx[r];
+    }
+    const double wn = sqrt(rdot());
+    __syncthreads();  // nf visible to the pairwise tree's lane mapping
+    const double pn = wpw_norm(nf, F, lo, ln, leaf) + 1e-8;
+    if (lane == 0) {
+      double* p = g.dprep + ((size_t)seq * g.D + k) * 4;
+      p[0] = fn;
+      p[1] = pwn;
+      p[2] = wn;
+      p[3] = pn;
+    }
+    return;
+  }
   const double fn = sqrt(wdot(x, x, F));
   const double pwn = wpw_norm(x, F, lo, ln, leaf);
   const double dd = pwn + 1e-8, dw = fn + 1e-8;
