@@ -460,6 +460,31 @@ __device__ inline float np_sumsq_wave_fast(const XT* x, int n) {  // requires np
                           : (part[0] + part[1]) + (part[2] + part[3]);
   return __shfl(res, 0);
 }
+// np_sumsq_wave_fast over a float row stored with 8 pad floats after every 128 elements (the
+// accumulator reads of one instruction then fall in distinct LDS banks)
+__device__ inline float np_sumsq_wave_fast_padded(const float* x, int n) {
+  const int lane = threadIdx.x & 63;
+  const int nacc = (n >> 7) * 8;
+  const int regs = nacc > 64 ? nacc / 64 : 1;
+  float part[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    part[r] = 0.0f;
+    const int a = lane + 64 * r;
+    if (r < regs && a < nacc) {
+      const float* p = x + 136 * (a >> 3) + (a & 7);
+      float acc = p[0] * p[0];
+      for (int i = 1; i < 16; i++) { float v = p[8 * i]; acc += v * v; }
+      part[r] = acc;
+    }
+    const int width = nacc < 64 ? nacc : 64;
+    for (int d = 1; d < width; d <<= 1) part[r] += __shfl_xor(part[r], d);
+  }
+  float res = regs == 1 ? part[0]
+              : regs == 2 ? part[0] + part[1]
+                          : (part[0] + part[1]) + (part[2] + part[3]);
+  return __shfl(res, 0);
+}
 // NPF: the caller knows np_wave_exact(n) (compile-time split keeps the sequential fallback and
 // its register footprint out of the fast kernels)
 template <bool NPF, typename XT>

@@ -39,6 +39,7 @@ constexpr int CLS_HIST = 8;  // BoT-SORT per-track class-history entries (update
 constexpr int ELDS_DEFAULT = 1024;  // LAP edges kept in LDS; the rest spill to global scratch
 constexpr int REG_F = 512;   // feature rows up to this width live in registers: 8 per lane
 constexpr int REG_EPL = REG_F / 64;
+constexpr int REG_FP = REG_F + REG_F / 16;  // LDS row stride: 8 pad floats per 128 (np_dn)
 constexpr int NWAVE = WG / WAVE;
 // doubles per slot: mean[8], covariance[64], then the pre-predict mean[2], mean[3] the pending
 // covariance predict's process noise is computed from (see K2)
@@ -109,6 +110,19 @@ struct RegRow {
   // through this wave's LDS row so lanes can read numpy's accumulator layout
   template <bool NPF>
   __device__ float np_dn(float* wbuf, int F) const {
+    if constexpr (NPF) {  // padded layout (element e at e + 8·(e/128)): conflict-free LDS reads
+      const int lane = threadIdx.x & 63;
+#pragma unroll
+      for (int r = 0; r < REG_EPL; r++) {
+        const int q = lane + 64 * r;
+        if (q < F) wbuf[q + 8 * (q >> 7)] = (float)v[r];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      float dn = sqrtf(np_sumsq_wave_fast_padded(wbuf, F)) + 1e-8f;
+      __builtin_amdgcn_wave_barrier();
+      return dn;
+    }
     store(wbuf, F);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -344,7 +358,7 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
                                                          const float* __restrict__ dets,
                                                          const int* __restrict__ det_off,
                                                          const FT* __restrict__ embs) {
-  __shared__ __align__(16) float s_w[NWAVE * REG_F];
+  __shared__ __align__(16) float s_w[NWAVE * REG_FP];
   const int b = blockIdx.x, s = seq0 + b, w = wave_id(), lane = lane_id();
   const int F = P.F, D = P.D;
   const int d0 = det_off[b], N = min(det_off[b + 1] - d0, D);
@@ -372,7 +386,7 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
     }
   };
   if (F <= REG_F) {
-    float* wb = s_w + w * REG_F;
+    float* wb = s_w + w * REG_FP;
     for (int k = next(k0 + w); k < k1; k = next(k + NWAVE)) {
       RegRow<FT> x;
       x.load(embs + (size_t)(d0 + k) * F, F);
@@ -1360,11 +1374,11 @@ template <typename FT, bool NPF>
 __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
                                                      const int* __restrict__ det_off,
                                                      const FT* __restrict__ embs) {
-  __shared__ __align__(16) float s_w[NWAVE * REG_F];
+  __shared__ __align__(16) float s_w[NWAVE * REG_FP];
   const int b = blockIdx.x, s = seq0 + b, F = P.F, D = P.D, T = P.T, lane = lane_id();
   const int nrec = P.seq[(size_t)s * SQ_STRIDE + SQ_NREC];
   const FT a = (FT)0.9, bb = (FT)(1.0 - 0.9);
-  float* wb = s_w + wave_id() * REG_F;
+  float* wb = s_w + wave_id() * REG_FP;
   const FT* fembs = embs + (size_t)det_off[b] * F;
   FT* feat = (FT*)P.feat + (size_t)s * T * F;
   constexpr int STEP = FEAT_BLOCKS * NWAVE;
