@@ -983,6 +983,26 @@ __global__ void __launch_bounds__(256)
     return;
   }
   const double om = 1 - alpha;
+  constexpr int EQ = 8;
+  if (F <= 64 * EQ) {  // the row in registers: one read of each input, one write of the result
+    double v[EQ];
+    double s = 0.0;
+#pragma unroll
+    for (int r = 0; r < EQ; r++) {
+      const int q = lane + 64 * r;
+      v[r] = q < F ? alpha * e[q] + om * x[q] : 0.0;
+      if (q < F) s += v[r] * v[r];
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+    const double nrm = sqrt(s);
+#pragma unroll
+    for (int r = 0; r < EQ; r++) {
+      const int q = lane + 64 * r;
+      if (q < F) e[q] = v[r] / nrm;
+    }
+    return;
+  }
   double s = 0.0;
   for (int q = lane; q < F; q += 64) {
     const double v = alpha * e[q] + om * x[q];
