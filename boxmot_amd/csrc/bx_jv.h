@@ -1,13 +1,16 @@
 // bx_jv.h — wave-cooperative building blocks shared by the one-wave-per-sequence trackers
-// (OCSort, BoostTrack): lapx's dense Jonker-Volgenant with the oracle's tie order, and a
+// (OCSort, BoostTrack) and the op-level bx_lapjv: lapx's dense lapjv with lapx's own tie order
+// (oracle/bxo_ops.c bxo_lapjv: _ccrrt_dense, up to two _carr_dense passes, _ca_dense), and a
 // wave-order-preserving compaction.  Include inside a translation unit's anonymous namespace
 // after bx_device.h (uses bx::INF); a workgroup is exactly one wave64.
 #pragma once
 
-constexpr int OW = 64;  // threads per workgroup: one wave per sequence
+constexpr int OW = 64;                    // threads per workgroup: one wave per sequence
+constexpr double LAPX_LARGE = 1000000.0;  // lapx's LARGE sentinel (lapjv.h)
+constexpr int JV_IMAX = 0x7fffffff;
 
-// Wave-cooperative lapx lapjv (oracle/bxo_ops.c bxo_lapjv) on the zero-padded square
-// max(nr, nc) of a row-major nr x nc matrix (legacy linear_assignment, association.py:105-114).
+// Wave-cooperative lapx lapjv on the zero-padded square max(nr, nc) of a row-major nr x nc
+// matrix (legacy linear_assignment, association.py:105-114; boosttrack/assoc.py:106-114).
 struct JvLds {
   double *v, *d;
   int *x, *y, *matches, *freer, *pred, *col;
@@ -25,74 +28,181 @@ __device__ double wave_min_d(double a) {
   return a;
 }
 
+// (value, index) argmin across the wave: the smallest value, the smallest index among equal
+// values — what a sequential ascending `<` scan keeps.  No NaNs.
+__device__ __forceinline__ void wave_argmin(double& m, int& j) {
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double om = __shfl_xor(m, o);
+    const int oj = __shfl_xor(j, o);
+    if (om < m || (om == m && oj < j)) {
+      m = om;
+      j = oj;
+    }
+  }
+}
+
+// Wave-order-preserving compaction: emit(k, pos) for k < n with pred(k); returns the count.
+template <class P, class E>
+__device__ int wave_compact(int n, P pred, E emit) {
+  const int lane = threadIdx.x;
+  int base = 0;
+  for (int c = 0; c < n; c += OW) {
+    const int k = c + lane;
+    const bool f = k < n && pred(k);
+    const unsigned long long m = __ballot(f);
+    if (f) emit(k, base + __popcll(m & ((1ull << lane) - 1ull)));
+    base += __popcll(m);
+  }
+  __syncthreads();
+  return base;
+}
+
 constexpr int JV_CH = 8;  // 64-position chunks of one relaxation (assignment sizes <= 512)
 
+// ------------------------------------------------------------------------------------------
+// Any n <= 64 * JV_CH, state in LDS.
 __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
   const int n = nr > nc ? nr : nc;
   const int lane = threadIdx.x;
-  // column reduction: minima (first row index on ties) lane-parallel ...
+  // ---- _ccrrt_dense.  Column minima from LARGE, first row on ties (lane per column) ...
   for (int j = lane; j < n; j += OW) {
-    double mn = cget(C, nr, nc, 0, j);
-    int imin = 0;
-    for (int i = 1; i < n; i++) {
+    double mn = LAPX_LARGE;
+    int im = 0;
+    for (int i = 0; i < n; i++) {
       const double c = cget(C, nr, nc, i, j);
-      if (c < mn) mn = c, imin = i;
+      if (c < mn) mn = c, im = i;
     }
-    w.d[j] = mn;
-    w.pred[j] = imin;
+    w.v[j] = mn;
+    w.y[j] = im;
     w.x[j] = -1;
     w.matches[j] = 0;
   }
   __syncthreads();
-  // ... and the sweep j = n-1..0 that settles them in the oracle's order
-  if (lane == 0) {
-    for (int j = n - 1; j >= 0; j--) {
-      const int imin = w.pred[j];
-      w.v[j] = w.d[j];
-      if (++w.matches[imin] == 1) {
-        w.x[imin] = j;
-        w.y[j] = imin;
-      } else if (w.v[j] < w.v[w.x[imin]]) {
-        const int j1 = w.x[imin];
-        w.x[imin] = j;
-        w.y[j] = imin;
-        w.y[j1] = -1;
-      } else {
-        w.y[j] = -1;
-      }
-    }
+  // ... the sweep j = n-1..0 leaves each row the LARGEST column whose minimum it holds and
+  // releases the others; `matches` counts them (lapx's unique[] is a count of one)
+  for (int j = lane; j < n; j += OW) {
+    atomicMax(&w.x[w.y[j]], j);
+    atomicAdd(&w.matches[w.y[j]], 1);
   }
   __syncthreads();
-  // reduction transfer (rows in order: each changes v[x[i]], read by the rows after it)
-  int nfree = 0;
+  for (int j = lane; j < n; j += OW)
+    if (w.x[w.y[j]] != j) w.y[j] = -1;
+  int nfree = wave_compact(
+      n, [&](int i) { return w.x[i] < 0; }, [&](int i, int p) { w.freer[p] = i; });
+  // reduction transfer, uniquely-assigned rows in order (each lowers v[x[i]], which the rows
+  // after it read)
   for (int i = 0; i < n; i++) {
-    const int m = w.matches[i];
-    if (m == 0) {
-      if (lane == 0) w.freer[nfree] = i;
-      nfree++;
-    } else if (m == 1) {
-      const int j1 = w.x[i];
-      double mn = DBL_MAX;
+    const int j1 = w.x[i];
+    if (j1 < 0 || w.matches[i] != 1) continue;
+    double mn = LAPX_LARGE;
+    for (int j = lane; j < n; j += OW) {
+      const double h = cget(C, nr, nc, i, j) - w.v[j];
+      if (j != j1 && h < mn) mn = h;
+    }
+    mn = wave_min_d(mn);
+    __syncthreads();
+    if (lane == 0) w.v[j1] = w.v[j1] - mn;
+    __syncthreads();
+  }
+  // ---- _carr_dense, at most two passes over the free rows (lapjv_internal)
+  for (int pass = 0; pass < 2 && nfree > 0; pass++) {
+    unsigned current = 0, rr_cnt = 0;
+    int nnew = 0;
+    while (current < (unsigned)nfree) {
+      rr_cnt++;
+      const int fi = w.freer[current++];
+      // the cheapest column j1 (first on ties) and the cheapest other one j2 (first on ties):
+      // exactly lapx's running pair whenever every reduced cost is below LARGE
+      double m1 = INF;
+      int k1 = JV_IMAX;
+      bool odd = false;
       for (int j = lane; j < n; j += OW) {
-        const double h = cget(C, nr, nc, i, j) - w.v[j];
-        if (j != j1 && h < mn) mn = h;
+        const double h = cget(C, nr, nc, fi, j) - w.v[j];
+        odd |= !(h < LAPX_LARGE);
+        if (h < m1) m1 = h, k1 = j;
       }
-      mn = wave_min_d(mn);
+      int j1, j2;
+      double v1, v2;
+      if (!__any(odd)) {
+        wave_argmin(m1, k1);
+        j1 = k1;
+        double m2 = INF;
+        int k2 = JV_IMAX;
+        for (int j = lane; j < n; j += OW) {
+          const double h = cget(C, nr, nc, fi, j) - w.v[j];
+          if (j != j1 && h < m2) m2 = h, k2 = j;
+        }
+        wave_argmin(m2, k2);
+        v1 = cget(C, nr, nc, fi, j1) - w.v[j1];
+        if (n >= 2) {
+          j2 = k2;
+          v2 = cget(C, nr, nc, fi, j2) - w.v[j2];
+        } else {
+          j2 = -1;
+          v2 = LAPX_LARGE;
+        }
+      } else {  // NaN or huge reduced costs: lapx's scan as written
+        j1 = 0;
+        j2 = -1;
+        v1 = cget(C, nr, nc, fi, 0) - w.v[0];
+        v2 = LAPX_LARGE;
+        for (int j = 1; j < n; j++) {
+          const double h = cget(C, nr, nc, fi, j) - w.v[j];
+          if (h < v2) {
+            if (h >= v1) {
+              v2 = h;
+              j2 = j;
+            } else {
+              v2 = v1;
+              v1 = h;
+              j2 = j1;
+              j1 = j;
+            }
+          }
+        }
+      }
+      int i0 = w.y[j1];
+      const double vj1 = w.v[j1];
+      const double v1_new = vj1 - (v2 - v1);
+      const bool lowers = v1_new < vj1;
+      if (rr_cnt < current * (unsigned)n) {
+        if (lowers) {
+          if (lane == 0) w.v[j1] = v1_new;
+        } else if (i0 >= 0 && j2 >= 0) {
+          j1 = j2;
+          i0 = w.y[j2];
+        }
+        if (i0 >= 0) {
+          if (lowers) {
+            --current;
+            if (lane == 0) w.freer[current] = i0;
+          } else {
+            if (lane == 0) w.freer[nnew] = i0;
+            nnew++;
+          }
+        }
+      } else if (i0 >= 0) {
+        if (lane == 0) w.freer[nnew] = i0;
+        nnew++;
+      }
       __syncthreads();
-      if (lane == 0 && mn < DBL_MAX) w.v[j1] = w.v[j1] - mn;
+      if (lane == 0) {
+        w.x[fi] = j1;
+        w.y[j1] = fi;
+      }
       __syncthreads();
     }
+    nfree = nnew;
   }
-  __syncthreads();
 #ifdef BX_PHASE_TIMING
   if (lane == 0 && w.dc) w.dc[0] += nfree;
 #endif
-  // augmentation
+  // ---- _ca_dense: one shortest augmenting path per remaining free row
   for (int f = 0; f < nfree; f++) {
-    const int fr = w.freer[f];
+    const int start = w.freer[f];
     for (int j = lane; j < n; j += OW) {
-      w.d[j] = cget(C, nr, nc, fr, j) - w.v[j];
-      w.pred[j] = fr;
+      w.d[j] = cget(C, nr, nc, start, j) - w.v[j];
+      w.pred[j] = start;
       w.col[j] = j;
     }
     __syncthreads();
@@ -103,11 +213,11 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
       if (lane == 0 && w.dc) w.dc[up == low ? 1 : 2] += 1;
 #endif
       if (up == low) {
-        // Minimum scan.  The oracle's sequential scan gathers, in position order, every column
-        // at the minimum distance into col[low..up) and takes the first unassigned one as the
-        // path end.  When one exists the search ends here and the rest of the permutation it
-        // built is never read again (col is rebuilt for the next free row), so the lane-parallel
-        // path finds it directly; otherwise (or with NaN distances) the scan runs as written.
+        // _find_dense.  It gathers, in position order, every TODO column at the minimum into
+        // col[low..up) and the path ends at the LAST unassigned one.  When one exists the search
+        // ends here and the rest of the permutation is never read again (col is rebuilt for the
+        // next free row), so the lane-parallel path finds it directly; otherwise (or with NaN
+        // distances) the scan runs as written.
         double m = INF;
         bool bad = false;
         for (int k = low + lane; k < n; k += OW) {
@@ -119,7 +229,7 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
         bad = __any(bad) || !(m < INF);
         int kg = -1, ke = -1;
         if (!bad) {
-          for (int base = low; base < n && ke < 0; base += OW) {
+          for (int base = low; base < n; base += OW) {
             const int k = base + lane;
             bool G = false, E = false;
             if (k < n) {
@@ -129,7 +239,7 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
             }
             const unsigned long long gm = __ballot(G), em = __ballot(E);
             if (kg < 0 && gm) kg = base + __ffsll((long long)gm) - 1;
-            if (em) ke = base + __ffsll((long long)em) - 1;
+            if (em) ke = base + 63 - __clzll((long long)em);
           }
         }
 #ifdef BX_PHASE_TIMING
@@ -137,7 +247,7 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
 #endif
         if (ke >= 0) {
           last = low - 1;
-          mn = w.d[w.col[kg]];  // the first minimum, exactly as the sequential scan keeps it
+          mn = w.d[w.col[kg]];  // d[cols[lo]] after the scan: the first column at the minimum
           endofpath = w.col[ke];
           found = 1;
         } else {
@@ -160,7 +270,6 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
               if (w.y[w.col[k]] < 0) {
                 endofpath = w.col[k];
                 found = 1;
-                break;
               }
             w.sc[0] = last;
             w.sc[1] = up;
@@ -178,14 +287,15 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
         }
       }
       if (!found) {
+        // _scan_dense from SCAN column j1 = col[low]: relax the TODO columns col[up..n) in
+        // chunks of 64 positions; the first column lowered to the minimum that is unassigned
+        // ends the path.  Every operand of every chunk is loaded up front: a swap writes only
+        // positions up to the chunk in flight, and each column appears once, so later chunks
+        // read what the sequential loop would.
         const int j1 = w.col[low++];
         const int i = w.y[j1];
-        const double h = cget(C, nr, nc, i, j1) - w.v[j1] - mn;
-        // relaxation from row i over col[up..n) in chunks of 64 positions; the first column
-        // reached at distance mn that is unassigned ends the path (the oracle's break).  Every
-        // operand of every chunk is loaded up front: a swap writes only positions up to the
-        // chunk in flight, and each column appears once, so later chunks read what the
-        // sequential loop would.
+        const double mind = w.d[j1];
+        const double h = cget(C, nr, nc, i, j1) - w.v[j1] - mind;
         const int up0 = up;
         int jc[JV_CH];
         double v2c[JV_CH], dc[JV_CH];
@@ -211,17 +321,16 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
           bool A = false, B = false, E = false;
           if (j >= 0) {
             A = v2 < dc[c];
-            B = A && v2 == mn;
+            B = A && v2 == mind;
             E = B && yc[c];
           }
           const unsigned long long em = __ballot(E);
           int kE = OW;
           if (em) kE = __ffsll((long long)em) - 1;
-          if (A && lane < kE) {
+          if (A && lane <= kE) {
             w.pred[j] = i;
             w.d[j] = v2;
           }
-          if (em && lane == kE) w.pred[j] = i;
           unsigned long long hm = __ballot(B && !E && lane < kE);
           if (hm) {
             while (hm) {  // the swaps, in position order (lane 0 owns col)
@@ -256,19 +365,20 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
         const int j1 = endofpath;
         endofpath = w.x[i];
         w.x[i] = j1;
-      } while (i != fr);
+      } while (i != start);
     }
     __syncthreads();
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// The same lapjv for n <= 64, register-resident.  Setup (column reduction, reduction transfer):
-// lane j owns column j and row j.  Augmentation: lane k holds the column at POSITION k of the
-// oracle's `col` permutation with its v, d, y and pred, so position-ordered choices (first column
-// at the minimum, first unassigned, the oracle's break) are single ballots and the swaps
-// col[k] <-> col[up] exchange two lanes' registers (readlane); rows keep x in lane i.  Every
-// comparison, arithmetic operation and tie is the oracle's.
+// The same lapjv for n <= 64, register-resident.  Setup (_ccrrt_dense, _carr_dense): lane j owns
+// column j (v, y) and row j (x, the free-row list entry j).  Augmentation: lane k holds the
+// column at POSITION k of lapx's `cols` permutation with its v, d, y and pred, so
+// position-ordered choices (the first / last column at the minimum, the first unassigned one the
+// scan lowers) are single ballots and the swaps cols[k] <-> cols[hi] exchange two lanes'
+// registers (readlane); rows keep x in lane i.  Every comparison, arithmetic operation and tie
+// is lapx's.
 // DPP inclusive min-scan across the wave (row_shr 1/2/4/8 within rows of 16, then row_bcast 15
 // and 31 — the gfx9 wave64 scan sequence); lanes whose source is outside the row keep the
 // identity.  Lane 63 holds the wave minimum.
@@ -315,6 +425,10 @@ __device__ __forceinline__ int first_lane(bool p) {
   const unsigned long long m = __ballot(p);
   return m ? __ffsll((long long)m) - 1 : -1;
 }
+__device__ __forceinline__ int last_lane(bool p) {
+  const unsigned long long m = __ballot(p);
+  return m ? 63 - __clzll((long long)m) : -1;
+}
 // send each lane's value to lane `dst` (a permutation)
 __device__ __forceinline__ int perm_i(int v, int dst) {
   return __builtin_amdgcn_ds_permute(dst << 2, v);
@@ -347,58 +461,133 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
   do {            \
   } while (0)
 #endif
-  double v = 0.0, d = 0.0;
-  int y = -1, pred = 0, col = lane, xr = -1, matches = 0;
-  // column reduction: the column minima (first row on ties) ...
-  int imin = 0;
+  // ---- _ccrrt_dense.  Column minima from LARGE (first row on ties) ...
+  double v = LAPX_LARGE, d = 0.0;
+  int y = 0, pred = 0, col = lane, xr = -1;
   if (own) {
-    double mn = cget(C, nr, nc, 0, lane);
-    for (int i = 1; i < n; i++) {
+    for (int i = 0; i < n; i++) {
       const double c = cget(C, nr, nc, i, lane);
-      if (c < mn) mn = c, imin = i;
+      if (c < v) v = c, y = i;
     }
-    v = mn;
+    w.x[lane] = -1;
+    w.matches[lane] = 0;
   }
-  // ... settled j = n-1..0 as the oracle does
-  for (int j = n - 1; j >= 0; j--) {
-    const int im = rl_i(imin, j);
-    const double vj = rl_d(v, j);
-    const int mc = rl_i(matches, im);
-    const int xi = rl_i(xr, im);
-    const double vx = rl_d(v, xi < 0 ? 0 : xi);
-    if (mc == 0 || vj < vx) {
-      if (lane == im) xr = j;
-      if (lane == j) y = im;
-      if (mc != 0 && lane == xi) y = -1;
-    } else if (lane == j) {
-      y = -1;
-    }
-    if (lane == im) matches++;
+  __syncthreads();
+  // ... each row keeps the largest column whose minimum it holds (the j = n-1..0 sweep's first)
+  if (own) {
+    atomicMax(&w.x[y], lane);
+    atomicAdd(&w.matches[y], 1);
   }
-  // reduction transfer, rows in order
-  int nfree = 0;
-  for (int i = 0; i < n; i++) {
-    const int m = rl_i(matches, i);
-    if (m == 0) {
-      if (lane == 0) w.freer[nfree] = i;
-      nfree++;
-    } else if (m == 1) {
+  __syncthreads();
+  bool uniq = false;
+  if (own) {
+    xr = w.x[lane];
+    uniq = w.matches[lane] == 1;
+    if (w.x[y] != lane) y = -1;
+  }
+  // reduction transfer, uniquely-assigned rows in order
+  {
+    unsigned long long rt = __ballot(own && xr >= 0 && uniq);
+    while (rt) {
+      const int i = __ffsll((long long)rt) - 1;
+      rt &= rt - 1;
       const int j1 = rl_i(xr, i);
-      double h = DBL_MAX;
+      double h = LAPX_LARGE;
       if (own && lane != j1) {
         const double t = cget(C, nr, nc, i, lane) - v;
         if (t < h) h = t;
       }
       h = wave_min_dpp(h);
-      if (h < DBL_MAX && lane == j1) v = v - h;
+      if (lane == j1) v = v - h;
     }
   }
-  __syncthreads();
+  // free rows in row order: lane k holds the k-th
+  int fr = -1, nfree;
+  {
+    const unsigned long long fm = __ballot(own && xr < 0);
+    nfree = __popcll(fm);
+    if (own && xr < 0) w.freer[__popcll(fm & ((1ull << lane) - 1ull))] = lane;
+    __syncthreads();
+    if (lane < nfree) fr = w.freer[lane];
+  }
+  // ---- _carr_dense, at most two passes
+  for (int pass = 0; pass < 2 && nfree > 0; pass++) {
+    unsigned current = 0, rr_cnt = 0;
+    int nnew = 0;
+    while (current < (unsigned)nfree) {
+      rr_cnt++;
+      const int fi = rl_i(fr, (int)current);
+      current++;
+      const double h = own ? cget(C, nr, nc, fi, lane) - v : INF;
+      int j1, j2;
+      double v1, v2;
+      if (!__any(own && !(h < LAPX_LARGE))) {
+        const double m1 = wave_min_dpp(own ? h : INF);
+        j1 = first_lane(own && h == m1);
+        v1 = rl_d(h, j1);
+        if (n >= 2) {
+          const bool o2 = own && lane != j1;
+          const double m2 = wave_min_dpp(o2 ? h : INF);
+          j2 = first_lane(o2 && h == m2);
+          v2 = rl_d(h, j2);
+        } else {
+          j2 = -1;
+          v2 = LAPX_LARGE;
+        }
+      } else {  // NaN or huge reduced costs: lapx's scan as written
+        j1 = 0;
+        j2 = -1;
+        v1 = rl_d(h, 0);
+        v2 = LAPX_LARGE;
+        for (int j = 1; j < n; j++) {
+          const double t = rl_d(h, j);
+          if (t < v2) {
+            if (t >= v1) {
+              v2 = t;
+              j2 = j;
+            } else {
+              v2 = v1;
+              v1 = t;
+              j2 = j1;
+              j1 = j;
+            }
+          }
+        }
+      }
+      int i0 = rl_i(y, j1);
+      const double vj1 = rl_d(v, j1);
+      const double v1_new = vj1 - (v2 - v1);
+      const bool lowers = v1_new < vj1;
+      if (rr_cnt < current * (unsigned)n) {
+        if (lowers) {
+          if (lane == j1) v = v1_new;
+        } else if (i0 >= 0 && j2 >= 0) {
+          j1 = j2;
+          i0 = rl_i(y, j2);
+        }
+        if (i0 >= 0) {
+          if (lowers) {
+            --current;
+            if (lane == (int)current) fr = i0;
+          } else {
+            if (lane == nnew) fr = i0;
+            nnew++;
+          }
+        }
+      } else if (i0 >= 0) {
+        if (lane == nnew) fr = i0;
+        nnew++;
+      }
+      if (lane == fi) xr = j1;
+      if (lane == j1) y = fi;
+    }
+    nfree = nnew;
+  }
 #ifdef BX_PHASE_TIMING
   if (lane == 0 && w.dc) w.dc[0] += nfree;
 #endif
   JVT(4);
-  // exchange the registers of positions a and b (col[a] <-> col[b])
+  // exchange the registers of positions a and b (cols[a] <-> cols[b])
   auto swap_pos = [&](int a, int b) {
     if (a == b) return;
     const int ca = rl_i(col, a), cb = rl_i(col, b);
@@ -409,18 +598,18 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
     if (lane == a) col = cb, y = yb, pred = pb, v = vb, d = db;
     if (lane == b) col = ca, y = ya, pred = pa, v = va, d = da;
   };
-  // augmentation
+  // ---- _ca_dense
   for (int f = 0; f < nfree; f++) {
-    const int fr = w.freer[f];
-    if (col != lane) {  // the oracle restarts from col[j] = j: every column back to its lane
+    const int start = rl_i(fr, f);
+    if (col != lane) {  // find_path_dense restarts from cols[j] = j: every column back to its lane
       const int c0 = col;
       v = perm_d(v, c0);
       y = perm_i(y, c0);
       col = lane;
     }
     if (own) {
-      d = cget(C, nr, nc, fr, lane) - v;
-      pred = fr;
+      d = cget(C, nr, nc, start, lane) - v;
+      pred = start;
     }
     int low = 0, up = 0, last = 0, endofpath = -1;
     bool found = false;
@@ -436,21 +625,21 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
         bool bad = __any(cand && isnan(d));
         double m = bad ? INF : wave_min_dpp(cand ? d : INF);
         bad = bad || !(m < INF);
-        const int ke = bad ? -1 : first_lane(cand && d == m && y < 0);
+        const int ke = bad ? -1 : last_lane(cand && d == m && y < 0);
         if (ke >= 0) {
-          // the columns at the minimum form the new TODO set in position order; the first
-          // unassigned one ends the path (the rest of the permutation is never read again)
-          mn = m;
+          // _find_dense's SCAN set = the TODO columns at the minimum in position order; the path
+          // ends at the LAST unassigned one (the rest of the permutation is never read again)
+          mn = rl_d(d, first_lane(cand && d == m));
           endofpath = rl_i(col, ke);
           found = true;
         } else {
 #ifdef BX_PHASE_TIMING
           if (lane == 0 && w.dc) w.dc[3] += 1;
 #endif
-          // the oracle's scan, on the position lanes: mn runs from d[col[low]], and the
-          // positions k > low whose d is <= the minimum of d over [low, k) are its events (a
-          // swap only exchanges k with a position <= k, so later positions still hold their
-          // columns) — found by a prefix minimum across the lanes, then replayed in order
+          // _find_dense on the position lanes: mind runs from d[cols[lo]], and the positions
+          // k > lo whose d is <= the minimum of d over [lo, k) are its events (a swap only
+          // exchanges k with a position <= k, so later positions still hold their columns) —
+          // found by a prefix minimum across the lanes, then replayed in order
           mn = rl_d(d, low);
           up = low + 1;
           if (!__any(own && lane >= low && isnan(d))) {
@@ -482,7 +671,7 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
               }
             }
           }
-          const int ke2 = first_lane(own && lane >= low && lane < up && y < 0);
+          const int ke2 = last_lane(own && lane >= low && lane < up && y < 0);
           if (ke2 >= 0) {
             endofpath = rl_i(col, ke2);
             found = true;
@@ -491,9 +680,11 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
       }
       JVT(5);
       if (!found) {
+        // _scan_dense from the SCAN column at position lo
         const int j1 = rl_i(col, low);
         const int i = rl_i(y, low);
-        const double h = cget(C, nr, nc, i, j1) - rl_d(v, low) - mn;
+        const double mind = rl_d(d, low);
+        const double h = cget(C, nr, nc, i, j1) - rl_d(v, low) - mind;
         low++;
         const bool R = own && lane >= up;
         double v2 = 0.0;
@@ -501,23 +692,22 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
         if (R) {
           v2 = cget(C, nr, nc, i, col) - v - h;
           A = v2 < d;
-          B = A && v2 == mn;
+          B = A && v2 == mind;
           E = B && y < 0;
         }
-        int pe = first_lane(E);  // the oracle's break
+        int pe = first_lane(E);  // _scan_dense's early return
         if (pe < 0) pe = OW;
-        const bool act = R && lane < pe;
+        const bool act = R && lane <= pe;
         if (act && A) {
           pred = i;
           d = v2;
         }
-        if (lane == pe) pred = i;
         if (pe < OW) {
           endofpath = rl_i(col, pe);
           found = true;
         }
-        // columns reaching the minimum join the TODO set, in position order (all before pe)
-        unsigned long long bits = __ballot(act && B);
+        // columns lowered to the minimum join the SCAN set, in position order (all before pe)
+        unsigned long long bits = __ballot(act && B && lane < pe);
         while (bits) {
           const int k = __ffsll((long long)bits) - 1;
           bits &= bits - 1;
@@ -536,7 +726,7 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
       const int j1 = endofpath;
       endofpath = rl_i(xr, i);
       if (lane == i) xr = j1;
-    } while (i != fr);
+    } while (i != start);
   }
   if (own) {
     w.x[lane] = xr;
@@ -550,23 +740,6 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
   if (lane == 0 && w.dc)
     for (int q = 4; q < 8; q++) w.dc[q] += jacc[q];
 #endif
-}
-
-// ------------------------------------------------------------------------------------------
-// Wave-order-preserving compaction: emit(k, pos) for k < n with pred(k); returns the count.
-template <class P, class E>
-__device__ int wave_compact(int n, P pred, E emit) {
-  const int lane = threadIdx.x;
-  int base = 0;
-  for (int c = 0; c < n; c += OW) {
-    const int k = c + lane;
-    const bool f = k < n && pred(k);
-    const unsigned long long m = __ballot(f);
-    if (f) emit(k, base + __popcll(m & ((1ull << lane) - 1ull)));
-    base += __popcll(m);
-  }
-  __syncthreads();
-  return base;
 }
 
 // legacy linear_assignment of the nr x nc matrix C: pairs (row, col) in row order into out

@@ -218,6 +218,51 @@ int grid_for(size_t n) {
   return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
 }
 
+#include "bx_jv.h"
+
+// lapx.lapjv(cost, extend_cost, cost_limit) on one dense problem, one wave: mode 0 = square,
+// 1 = extend_cost (zero padding to max(nr, nc), read through cget), 2 = cost_limit (the
+// (nr+nc)^2 extension with cost_limit / 2 off the diagonal blocks, built in E first).
+__global__ __launch_bounds__(OW) void lapjv_kernel(const double* cost, int nr, int nc, int mode,
+                                                   double lim, double* E, int32_t* x, int32_t* y) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int n = mode == 2 ? nr + nc : (nr > nc ? nr : nc);
+  const double* C = cost;
+  int cr = nr, cc = nc;
+  if (mode == 2) {
+    const double half = lim / 2.;
+    for (int k = threadIdx.x; k < n * n; k += OW) {
+      const int i = k / n, j = k % n;
+      E[k] = (i < nr && j < nc) ? cost[(size_t)i * nc + j] : (i >= nr && j >= nc) ? 0.0 : half;
+    }
+    __syncthreads();
+    C = E;
+    cr = cc = n;
+  }
+  JvLds w;
+  size_t o = 0;
+  auto takeD = [&](int k) { double* p = (double*)(smem + o); o += (size_t)k * 8; return p; };
+  auto takeI = [&](int k) { int* p = (int*)(smem + o); o += (((size_t)k * 4 + 7) / 8) * 8; return p; };
+  w.v = takeD(n);
+  w.d = takeD(n);
+  w.sd = takeD(2);
+  w.x = takeI(n);
+  w.y = takeI(n);
+  w.matches = takeI(n);
+  w.freer = takeI(n);
+  w.pred = takeI(n);
+  w.col = takeI(n);
+  w.sc = takeI(8);
+  w.dc = nullptr;
+  if (n <= OW)
+    jv_wave64(C, cr, cc, w);
+  else
+    jv_wave(C, cr, cc, w);
+  const bool cut = mode != 0;  // lapx: x >= n_cols -> -1, y >= n_rows -> -1, then [:nr] / [:nc]
+  for (int i = threadIdx.x; i < nr; i += OW) x[i] = (cut && w.x[i] >= nc) ? -1 : w.x[i];
+  for (int j = threadIdx.x; j < nc; j += OW) y[j] = (cut && w.y[j] >= nr) ? -1 : w.y[j];
+}
+
 }  // namespace
 
 extern "C" {
@@ -363,6 +408,33 @@ int bx_linear_assignment(const double* cost, int nr, int nc, double thresh, int3
                      gcol, gcost, x, y);
   OPCHK(hipGetLastError());
   OPCHK(hipFreeAsync(ws, st));
+  return BX_OK;
+}
+
+int bx_lapjv(const double* cost, int nr, int nc, int extend_cost, double cost_limit, int32_t* x,
+             int32_t* y, void* stream) {
+  const bool lim = cost_limit < INFINITY;  // NaN compares false: no limit, as lapx's `< np.inf`
+  if (nr < 0 || nc < 0) return op_err(BX_ERR_INVALID, "negative size");
+  if (!extend_cost && nr != nc)  // lapx checks this before the cost_limit extension
+    return op_err(BX_ERR_INVALID,
+                  "Square cost array expected. If cost is intentionally non-square, pass "
+                  "extend_cost=True.");
+  const int mode = lim ? 2 : (extend_cost ? 1 : 0);
+  const int n = mode == 2 ? nr + nc : (nr > nc ? nr : nc);
+  if (n > OW * JV_CH) return op_err(BX_ERR_INVALID, "lapjv: extended size above 512");
+  hipStream_t st = (hipStream_t)stream;
+  if (!nr || !nc) {
+    if (nr) OPCHK(hipMemsetAsync(x, 0xff, sizeof(int32_t) * nr, st));
+    if (nc) OPCHK(hipMemsetAsync(y, 0xff, sizeof(int32_t) * nc, st));
+    return BX_OK;
+  }
+  double* E = nullptr;
+  if (mode == 2) OPCHK(hipMallocAsync((void**)&E, sizeof(double) * (size_t)n * n, st));
+  const size_t lds = 2 * 8 * (size_t)n + 16 + 6 * (((size_t)n * 4 + 7) / 8) * 8 + 32;
+  hipLaunchKernelGGL(lapjv_kernel, dim3(1), dim3(OW), lds, st, cost, nr, nc, mode, cost_limit, E,
+                     x, y);
+  OPCHK(hipGetLastError());
+  if (E) OPCHK(hipFreeAsync(E, st));
   return BX_OK;
 }
 

@@ -25,6 +25,10 @@
  *                          boxmot/trackers/strongsort/sort/linear_assignment.py:468-618
  *   bx_linear_assignment   matching.enhanced_linear_assignment (lapx.lapjv extend_cost=True,
  *                          cost_limit=thresh)        boxmot/utils/matching.py:30-141
+ *   bx_lapjv               lapx.lapjv itself (square / extend_cost / cost_limit), lapx's own
+ *                          algorithm and tie order: association.linear_assignment
+ *                          boxmot/utils/association.py:105-114, boosttrack/assoc.py:106-114,
+ *                          matching.py:54
  *
  * Memory: unless a name ends in _host, pointer arguments are DEVICE pointers and the call is
  * asynchronous on `stream` (a hipStream_t; NULL = the default stream).  The engine owns its
@@ -172,6 +176,14 @@ int bx_nn_cosine_distance(const double *samples, int G, const int32_t *off, int 
                           const double *feats, int D, int F, int flags, double *out, void *stream);
 int bx_linear_assignment(const double *cost, int nr, int nc, double thresh, int32_t *x,
                          int32_t *y, void *stream);
+/* lapx 0.5.11 lapjv(cost, extend_cost, cost_limit) on a dense [nr][nc] float64 cost, solved by
+ * lapx's algorithm (_ccrrt_dense, two _carr_dense passes, _ca_dense) on one wave, so tied
+ * problems return lapx's optimum.  cost_limit = +inf for none (then nr == nc unless
+ * extend_cost).  x [nr] = column or -1, y [nc] = row or -1 (lapx's post-processing when
+ * extended).  The (possibly extended) size must be <= 512.  BX_ERR_INVALID carries lapx's
+ * ValueError text for a non-square cost without extend_cost. */
+int bx_lapjv(const double *cost, int nr, int nc, int extend_cost, double cost_limit, int32_t *x,
+             int32_t *y, void *stream);
 
 #ifdef __cplusplus
 }

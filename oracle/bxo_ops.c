@@ -340,117 +340,218 @@ void bxo_kf_gating_distance(int kind, const double *mean, const double *cov, con
 }
 
 /* ------------------------------------------------------------------------------------------ */
-/* Dense Jonker-Volgenant: column reduction + reduction transfer + shortest augmenting paths.  */
+/* lapx 0.5.11.post1 `lapjv` (uv.lock:1789-1795; its lapjv.cpp is the gatagat/lap dense solver),  */
+/* restated from the published algorithm: lapjv_internal = _ccrrt_dense (column reduction +      */
+/* reduction transfer), at most two _carr_dense passes (augmenting row reduction), then          */
+/* _ca_dense (one find_path_dense shortest augmenting path per remaining free row).  Every       */
+/* comparison, its strictness and every scan order below decides which optimum a tied problem    */
+/* returns, so they are kept exactly (callers: utils/association.py:105-114,                     */
+/* trackers/boosttrack/assoc.py:106-114, utils/matching.py:54).  lapx's LARGE sentinel is 1e6.   */
 
-int bxo_lapjv(int n, const double *c, int *x, int *y) {
-    if (n <= 0) return 0;
-    double *v = (double *)malloc(sizeof(double) * n), *d = (double *)malloc(sizeof(double) * n);
-    int *matches = (int *)calloc(n, sizeof(int)), *freer = (int *)malloc(sizeof(int) * n);
-    int *pred = (int *)malloc(sizeof(int) * n), *col = (int *)malloc(sizeof(int) * n);
-    for (int i = 0; i < n; i++) x[i] = -1;
-    for (int j = n - 1; j >= 0; j--) { /* column reduction */
-        double mn = c[j];
-        int imin = 0;
-        for (int i = 1; i < n; i++)
-            if (c[(size_t)i * n + j] < mn) mn = c[(size_t)i * n + j], imin = i;
-        v[j] = mn;
-        if (++matches[imin] == 1) {
-            x[imin] = j;
-            y[j] = imin;
-        } else if (v[j] < v[x[imin]]) {
-            int j1 = x[imin];
-            x[imin] = j;
-            y[j] = imin;
-            y[j1] = -1;
+#define LAPX_LARGE 1000000.0
+
+/* _ccrrt_dense: v[j] = min_i c[i][j] (first row on ties, from a LARGE start), columns claimed
+ * j = n-1..0 (a row keeps the first column it is found for, later ones are released and the row
+ * marked non-unique), then for every uniquely-assigned row in row order v[x[i]] -= the row's
+ * smallest other reduced cost.  Returns the free rows (no column) in row order. */
+static int lapx_ccrrt(int n, const double *c, int *fr, int *x, int *y, double *v) {
+    unsigned char *uniq = (unsigned char *)malloc((size_t)n);
+    for (int i = 0; i < n; i++) {
+        x[i] = -1;
+        v[i] = LAPX_LARGE;
+        y[i] = 0;
+    }
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            const double h = c[(size_t)i * n + j];
+            if (h < v[j]) {
+                v[j] = h;
+                y[j] = i;
+            }
+        }
+    memset(uniq, 1, (size_t)n);
+    for (int j = n - 1; j >= 0; j--) {
+        const int i = y[j];
+        if (x[i] < 0) {
+            x[i] = j;
         } else {
+            uniq[i] = 0;
             y[j] = -1;
         }
     }
-    int nfree = 0;
-    for (int i = 0; i < n; i++) { /* reduction transfer */
-        if (matches[i] == 0) {
-            freer[nfree++] = i;
-        } else if (matches[i] == 1) {
-            int j1 = x[i];
-            double mn = DBL_MAX;
-            for (int j = 0; j < n; j++)
-                if (j != j1 && c[(size_t)i * n + j] - v[j] < mn) mn = c[(size_t)i * n + j] - v[j];
-            if (mn < DBL_MAX) v[j1] = v[j1] - mn;
+    int nf = 0;
+    for (int i = 0; i < n; i++) {
+        if (x[i] < 0) {
+            fr[nf++] = i;
+        } else if (uniq[i]) {
+            const int j = x[i];
+            double mn = LAPX_LARGE;
+            for (int j2 = 0; j2 < n; j2++) {
+                if (j2 == j) continue;
+                const double h = c[(size_t)i * n + j2] - v[j2];
+                if (h < mn) mn = h;
+            }
+            v[j] -= mn;
         }
     }
-    for (int f = 0; f < nfree; f++) { /* augmentation */
-        int fr = freer[f], low = 0, up = 0, last = 0, endofpath = -1, found = 0;
-        double mn = 0.0;
-        for (int j = 0; j < n; j++) {
-            d[j] = c[(size_t)fr * n + j] - v[j];
-            pred[j] = fr;
-            col[j] = j;
-        }
-        do {
-            if (up == low) {
-                last = low - 1;
-                mn = d[col[up++]];
-                for (int k = up; k < n; k++) {
-                    int j = col[k];
-                    double h = d[j];
-                    if (h <= mn) {
-                        if (h < mn) {
-                            up = low;
-                            mn = h;
-                        }
-                        col[k] = col[up];
-                        col[up++] = j;
-                    }
+    free(uniq);
+    return nf;
+}
+
+/* _carr_dense: one augmenting-row-reduction pass over fr[0..nfree).  A free row takes its
+ * cheapest column j1 (first index on ties; v2 = its second-cheapest reduced cost, first index
+ * != j1, from a LARGE start) and lowers v[j1] by v2 - v1; the displaced owner is processed next
+ * when v[j1] strictly dropped, else it (or, on a tie, the owner of j2 after switching to j2) is
+ * queued for the next pass.  The rr_cnt < current*n guard bounds the pass.  Returns the number of
+ * rows queued (they are written back into fr from the front). */
+static int lapx_carr(int n, const double *c, int nfree, int *fr, int *x, int *y, double *v) {
+    unsigned current = 0, rr_cnt = 0;
+    int nnew = 0;
+    while (current < (unsigned)nfree) {
+        rr_cnt++;
+        const int fi = fr[current++];
+        int j1 = 0, j2 = -1;
+        double v1 = c[(size_t)fi * n] - v[0], v2 = LAPX_LARGE;
+        for (int j = 1; j < n; j++) {
+            const double h = c[(size_t)fi * n + j] - v[j];
+            if (h < v2) {
+                if (h >= v1) {
+                    v2 = h;
+                    j2 = j;
+                } else {
+                    v2 = v1;
+                    v1 = h;
+                    j2 = j1;
+                    j1 = j;
                 }
-                for (int k = low; k < up; k++)
-                    if (y[col[k]] < 0) {
-                        endofpath = col[k];
-                        found = 1;
-                        break;
-                    }
             }
-            if (!found) {
-                int j1 = col[low++];
-                int i = y[j1];
-                double h = c[(size_t)i * n + j1] - v[j1] - mn;
-                for (int k = up; k < n; k++) {
-                    int j = col[k];
-                    double v2 = c[(size_t)i * n + j] - v[j] - h;
-                    if (v2 < d[j]) {
+        }
+        int i0 = y[j1];
+        const double v1_new = v[j1] - (v2 - v1);
+        const int lowers = v1_new < v[j1];
+        if (rr_cnt < current * (unsigned)n) {
+            if (lowers) {
+                v[j1] = v1_new;
+            } else if (i0 >= 0 && j2 >= 0) {
+                j1 = j2;
+                i0 = y[j2];
+            }
+            if (i0 >= 0) {
+                if (lowers)
+                    fr[--current] = i0;
+                else
+                    fr[nnew++] = i0;
+            }
+        } else if (i0 >= 0) {
+            fr[nnew++] = i0;
+        }
+        x[fi] = j1;
+        y[j1] = fi;
+    }
+    return nnew;
+}
+
+/* find_path_dense (with _find_dense / _scan_dense): Dijkstra from free row `start` over reduced
+ * costs.  `cols` is a position permutation: [0, lo) scanned ("ready"), [lo, hi) the SCAN set at
+ * the current minimum, [hi, n) TODO.  _find_dense moves every TODO column at the new minimum to
+ * the SCAN set in position order and the path ends at the LAST unassigned one of them;
+ * _scan_dense relaxes TODO columns from each SCAN column and ends at the FIRST column it lowers to
+ * the minimum that is unassigned.  Ready columns' v are then raised by d - min. */
+static int lapx_find_path(int n, const double *c, int start, const int *y, double *v, int *pred,
+                          int *cols, double *d) {
+    int lo = 0, hi = 0, final_j = -1, n_ready = 0;
+    for (int j = 0; j < n; j++) {
+        cols[j] = j;
+        pred[j] = start;
+        d[j] = c[(size_t)start * n + j] - v[j];
+    }
+    while (final_j == -1) {
+        if (lo == hi) { /* _find_dense */
+            n_ready = lo;
+            hi = lo + 1;
+            double mind = d[cols[lo]];
+            for (int k = hi; k < n; k++) {
+                const int j = cols[k];
+                if (d[j] <= mind) {
+                    if (d[j] < mind) {
+                        hi = lo;
+                        mind = d[j];
+                    }
+                    cols[k] = cols[hi];
+                    cols[hi++] = j;
+                }
+            }
+            for (int k = lo; k < hi; k++)
+                if (y[cols[k]] < 0) final_j = cols[k];
+        }
+        if (final_j == -1) { /* _scan_dense: lo/hi are only written back when it exhausts SCAN */
+            int l = lo, h = hi;
+            while (l != h && final_j == -1) {
+                int j = cols[l++];
+                const int i = y[j];
+                const double mind = d[j];
+                const double hh = c[(size_t)i * n + j] - v[j] - mind;
+                for (int k = h; k < n; k++) {
+                    j = cols[k];
+                    const double cred = c[(size_t)i * n + j] - v[j] - hh;
+                    if (cred < d[j]) {
+                        d[j] = cred;
                         pred[j] = i;
-                        if (v2 == mn) {
+                        if (cred == mind) {
                             if (y[j] < 0) {
-                                endofpath = j;
-                                found = 1;
+                                final_j = j;
                                 break;
                             }
-                            col[k] = col[up];
-                            col[up++] = j;
+                            cols[k] = cols[h];
+                            cols[h++] = j;
                         }
-                        d[j] = v2;
                     }
                 }
             }
-        } while (!found);
-        for (int k = 0; k <= last; k++) {
-            int j1 = col[k];
-            v[j1] = v[j1] + d[j1] - mn;
+            if (final_j == -1) {
+                lo = l;
+                hi = h;
+            }
         }
-        int i;
-        do {
-            i = pred[endofpath];
-            y[endofpath] = i;
-            int j1 = endofpath;
-            endofpath = x[i];
-            x[i] = j1;
-        } while (i != fr);
     }
-    free(v);
-    free(d);
-    free(matches);
-    free(freer);
+    const double mind = d[cols[lo]];
+    for (int k = 0; k < n_ready; k++) {
+        const int j = cols[k];
+        v[j] += d[j] - mind;
+    }
+    return final_j;
+}
+
+/* _ca_dense: augment along pred from each remaining free row, in list order. */
+static void lapx_ca(int n, const double *c, int nfree, const int *fr, int *x, int *y, double *v) {
+    int *pred = (int *)malloc(sizeof(int) * n), *cols = (int *)malloc(sizeof(int) * n);
+    double *d = (double *)malloc(sizeof(double) * n);
+    for (int f = 0; f < nfree; f++) {
+        const int start = fr[f];
+        int j = lapx_find_path(n, c, start, y, v, pred, cols, d), i = -1;
+        while (i != start) {
+            i = pred[j];
+            y[j] = i;
+            const int t = x[i];
+            x[i] = j;
+            j = t;
+        }
+    }
     free(pred);
-    free(col);
+    free(cols);
+    free(d);
+}
+
+/* lapjv_internal on a dense n x n row-major matrix: x[row] = column, y[column] = row. */
+int bxo_lapjv(int n, const double *c, int *x, int *y) {
+    if (n <= 0) return 0;
+    int *fr = (int *)malloc(sizeof(int) * n);
+    double *v = (double *)malloc(sizeof(double) * n);
+    int nf = lapx_ccrrt(n, c, fr, x, y, v);
+    for (int pass = 0; nf > 0 && pass < 2; pass++) nf = lapx_carr(n, c, nf, fr, x, y, v);
+    if (nf > 0) lapx_ca(n, c, nf, fr, x, y, v);
+    free(fr);
+    free(v);
     return 0;
 }
 

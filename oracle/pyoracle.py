@@ -78,6 +78,37 @@ def lsap(cost):
     return r[:max(n, 0)], cc[:max(n, 0)]
 
 
+def lapjv(cost, extend_cost=False, cost_limit=np.inf):
+    """lapx.lapjv (0.5.11 _lapjv.pyx wrapper rules) around the restated lapjv_internal
+    (bxo_lapjv): returns (x [nr], y [nc]) int32 with -1 for unmatched when extended."""
+    c = np.ascontiguousarray(cost, np.float64)
+    nr, nc = c.shape
+    if nr != nc and not extend_cost:
+        raise ValueError("Square cost array expected. If cost is intentionally non-square, "
+                         "pass extend_cost=True.")
+    if cost_limit < np.inf:
+        n = nr + nc
+        E = np.full((n, n), cost_limit / 2.0)
+        E[nr:, nc:] = 0
+        E[:nr, :nc] = c
+    elif extend_cost:
+        n = max(nr, nc)
+        E = np.zeros((n, n))
+        E[:nr, :nc] = c
+    else:
+        n, E = nr, c
+    x = np.zeros(n, np.int32)
+    y = np.zeros(n, np.int32)
+    if n:
+        lib().bxo_lapjv(n, _d(np.ascontiguousarray(E)), x.ctypes.data_as(_ip),
+                        y.ctypes.data_as(_ip))
+    if cost_limit < np.inf or extend_cost:
+        x[x >= nc] = -1
+        y[y >= nr] = -1
+        x, y = x[:nr], y[:nc]
+    return x, y
+
+
 # BoostTrack.__init__ defaults (boosttrack.py:154-181)
 BOOST_DEFAULTS = dict(max_age=60, min_hits=3, det_thresh=0.6, iou_threshold=0.3, use_ecc=True,
                       min_box_area=10, aspect_ratio_thresh=1.6, lambda_iou=0.5, lambda_mhd=0.25,

@@ -226,6 +226,56 @@ def test_linear_assignment_sparse_components_vs_oracle(torch_cuda, shape, densit
         np.testing.assert_array_equal(gub, oub)
 
 
+def gpu_lapjv(torch, cost, extend_cost=False, cost_limit=float("inf")):
+    from boxmot_amd import _native as N
+
+    c = dev(torch, np.ascontiguousarray(cost, np.float64))
+    nr, nc = cost.shape
+    x = torch.empty(max(nr, 1), dtype=torch.int32, device="cuda")
+    y = torch.empty(max(nc, 1), dtype=torch.int32, device="cuda")
+    N.check(N.load().bx_lapjv(c.data_ptr(), nr, nc, int(extend_cost), float(cost_limit),
+                              x.data_ptr(), y.data_ptr(), None), "bx_lapjv")
+    torch.cuda.synchronize()
+    return host(x)[:nr], host(y)[:nc]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["square", "extend", "limit"])
+def test_lapjv_ties_vs_oracle(torch_cuda, mode):
+    """lapx's own algorithm on the GPU (register wave for n <= 64, LDS wave above) returns the
+    oracle's x / y bit for bit on tie-heavy problems: small-integer costs, zero padding
+    (association.py:105-114 / boosttrack/assoc.py:106-114) and cost_limit extensions."""
+    rng = np.random.default_rng({"square": 1, "extend": 2, "limit": 3}[mode])
+    sizes = [(1, 1), (2, 2), (3, 5), (7, 4), (17, 30), (40, 63), (64, 64), (50, 65), (65, 40),
+             (100, 120), (200, 130), (333, 178), (512, 300)]
+    for t, (nr, nc) in enumerate(sizes * 3):
+        if mode == "square":
+            nc = nr
+        if mode == "limit" and nr + nc > 512:
+            nr, nc = nr // 2, nc // 2
+        hi = 2 + t % 5
+        c = rng.integers(0, hi, (nr, nc)).astype(np.float64)
+        if t % 3 == 1:
+            c = -c  # maximisation form, as assoc.match's lapjv(-cost)
+        if t % 3 == 2:
+            c = np.round(rng.uniform(-1, 1, (nr, nc)), 1)
+        kw = dict(extend_cost=mode != "square")
+        if mode == "limit":
+            kw["cost_limit"] = float(hi) / 2
+        ox, oy = po.lapjv(c, **kw)
+        gx, gy = gpu_lapjv(torch_cuda, c, **kw)
+        np.testing.assert_array_equal(gx, ox, err_msg=f"x {mode} {nr}x{nc} t={t}")
+        np.testing.assert_array_equal(gy, oy, err_msg=f"y {mode} {nr}x{nc} t={t}")
+
+
+@pytest.mark.gpu
+def test_lapjv_errors(torch_cuda):
+    with pytest.raises(ValueError, match="Square cost array expected"):
+        gpu_lapjv(torch_cuda, np.zeros((2, 3)))
+    x, y = gpu_lapjv(torch_cuda, np.zeros((0, 3)), extend_cost=True)
+    assert x.size == 0 and list(y) == [-1, -1, -1]
+
+
 def test_linear_assignment_empty(torch_cuda):
     for shape in [(0, 4), (4, 0)]:
         m, ua, ub = gpu_linear_assignment(torch_cuda, np.zeros(shape), 0.5)

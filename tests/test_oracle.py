@@ -86,6 +86,56 @@ def test_lapjv_random_vs_scipy():
             np.testing.assert_array_equal(y[x], np.arange(n))
 
 
+def test_lapx_lapjv_ties_optimal():
+    """The lapx restatement (column reduction + reduction transfer, two augmenting row
+    reductions, shortest augmenting paths) returns an optimal permutation on tie-heavy
+    problems of every wrapper mode; hand-traced known answers pin its tie order."""
+    from scipy.optimize import linear_sum_assignment
+
+    # all-zero 3x3: every column's minimum is row 0; the j = n-1..0 sweep gives row 0 column 2
+    # and frees rows 1, 2.  ARR: row 1 takes its first minimum, column 0 (unowned); row 2's first
+    # minimum is row 1's column 0 and v does not drop (a tie), so it takes column j2 = 1.
+    x, y = po.lapjv(np.zeros((3, 3)))
+    assert list(x) == [2, 0, 1] and list(y) == [1, 2, 0]
+    rng = np.random.default_rng(11)
+    for trial in range(600):
+        nr, nc = (int(v) for v in rng.integers(1, 40, 2))
+        mode = trial % 3
+        c = rng.integers(0, 3 + trial % 4, (nr, nc)).astype(np.float64)
+        if trial % 5 == 0:
+            c = -c
+        if mode == 0:
+            nc = nr
+            c = c[:, :1].repeat(nr, 1) if trial % 7 == 0 else rng.integers(0, 3, (nr, nr)) * 1.0
+            x, y = po.lapjv(c)
+            E = c
+        elif mode == 1:
+            x, y = po.lapjv(c, extend_cost=True)
+            n = max(nr, nc)
+            E = np.zeros((n, n))
+            E[:nr, :nc] = c
+        else:
+            lim = float(rng.integers(1, 4))
+            x, y = po.lapjv(c, extend_cost=True, cost_limit=lim)
+            n = nr + nc
+            E = np.full((n, n), lim / 2)
+            E[nr:, nc:] = 0
+            E[:nr, :nc] = c
+        r, k = linear_sum_assignment(E)
+        best = E[r, k].sum()
+        m = x >= 0
+        assert len(set(x[m].tolist())) == int(m.sum())
+        for i in np.nonzero(m)[0]:
+            assert y[x[i]] == i
+        if mode == 0:
+            assert E[np.arange(nr), x].sum() == best
+        else:  # objective of the extended problem from the real pairs
+            got = c[np.nonzero(m)[0], x[m]].sum()
+            if mode == 2:
+                got += (nr - m.sum() + nc - m.sum()) * (lim / 2)
+            assert got == best, (trial, got, best)
+
+
 def test_linear_assignment_empty():
     m, ua, ub = po.linear_assignment(np.zeros((0, 3)), 0.5)
     assert m.shape == (0, 2) and ua.size == 0 and list(ub) == [0, 1, 2]
