@@ -61,18 +61,28 @@ CONFIGS = {
         lambda_shape=0.25, use_dlo_boost=True, use_duo_boost=True, dlo_boost_coef=0.65,
         s_sim_corr=False, use_rich_s=True, use_sb=True, use_vt=True, with_reid=True)),
     # StrongSort (configs[3]'s tracker, constructor defaults, born Confirmed): many MOT-sized
-    # sequences with 512-d ReID, and the C4 geometry (1000 tracks x ~500 dets x 2048-d) as one
+    # sequences with 512-d ReID, and configs[3] itself (1024 tracks x ~512 dets x 2048-d) as one
     # sequence
     "strongsort": ("strongsort", 48, 512, dict(
         min_conf=0.1, max_cos_dist=0.15, max_iou_dist=0.7, max_age=50, n_init=2, nn_budget=150,
         mc_lambda=0.995, ema_alpha=0.9, conf_thresh_high=0.7, conf_thresh_low=0.3,
         id_preservation_weight=0.1, crowd_detection=True, born_confirmed=True)),
-    "strongsort_c4": ("strongsort", 1000, 2048, dict(
+    "strongsort_c4": ("strongsort", 1024, 2048, dict(
         min_conf=0.1, max_cos_dist=0.15, max_iou_dist=0.7, max_age=50, n_init=2, nn_budget=150,
         mc_lambda=0.995, ema_alpha=0.9, conf_thresh_high=0.7, conf_thresh_low=0.3,
         id_preservation_weight=0.1, crowd_detection=True, born_confirmed=True)),
 }
 DEFAULT_SEQS = {"strongsort": 256, "strongsort_c4": 1}
+# StrongSort engine capacities (track slots, detections per frame, pool vectors per slot); the C4
+# ones are shared with tests/test_gpu_parity.py::test_strongsort_c4_size_vs_oracle
+SS_C4_CAPS = dict(track_cap=1024, det_cap=1024, vec_cap=64)
+
+
+def ss_caps(config, n_obj):
+    if config == "strongsort_c4":
+        return dict(SS_C4_CAPS)
+    return dict(track_cap=min(1024, max(96, 2 * n_obj)), det_cap=min(1024, max(64, n_obj)),
+                vec_cap=64)
 OCS_CONF_LO = 0.3  # OCSort / BoostTrack scenes: confidences U(0.3, 1) -> ~40% below det_thresh
 
 # OCSort per-launch algorithmic bytes: per live track the XYSR state (x[7], P[49] f64) read and
@@ -234,9 +244,8 @@ def main():
     bst = kind == "boosttrack"
     sss = kind == "strongsort"
     if sss:
-        eng = SsEngine(n_seq=S, track_cap=min(1024, max(96, 2 * n_obj)),
-                       det_cap=min(1024, max(64, n_obj)), emb_dim=F, vec_cap=64,
-                       params=SsParams(**params))
+        eng = SsEngine(n_seq=S, emb_dim=F, params=SsParams(**params),
+                       **ss_caps(args.config, n_obj))
         stages = list(SsEngine.STAGES)
     elif bst:
         eng = BoostEngine(n_seq=S, track_cap=128, det_cap=max(64, n_obj), emb_dim=F,

@@ -21,7 +21,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-__all__ = ["SyntheticScene", "load_mot_dets"]
+__all__ = ["SyntheticScene", "SyntheticCMC", "TorchSceneBatch", "load_mot_dets", "synth_warp"]
 
 
 @dataclass
@@ -92,6 +92,34 @@ class SyntheticScene:
             e /= np.linalg.norm(e, axis=1, keepdims=True)
             embs = e.astype(self.emb_dtype)
         return dets, embs, ids
+
+
+def synth_warp(seed: int, t: int, rot: float = 0.003, scale: float = 0.002,
+               shift: float = 2.0) -> np.ndarray:
+    """Seeded 2x3 camera warp of frame ``t`` — a small similarity (rotation about the image
+    origin, isotropic scale, shift in px) standing in for an ECC estimate (``motion/cmc/ecc.py``
+    returns the same 2x3 affine form).  Drawn from ``default_rng([seed, t, 0xC3C])``."""
+    rng = np.random.default_rng([int(seed), int(t), 0xC3C])
+    a = rng.uniform(-rot, rot)
+    s = 1.0 + rng.uniform(-scale, scale)
+    tx, ty = rng.uniform(-shift, shift, 2)
+    return np.array([[s * math.cos(a), -s * math.sin(a), tx],
+                     [s * math.sin(a), s * math.cos(a), ty]], np.float64)
+
+
+class SyntheticCMC:
+    """A CMC object for the trackers' ``cmc`` slot (``apply(img, dets) -> 2x3``) that returns a
+    per-frame warp from a table keyed by frame number: the caller sets ``t`` before each
+    ``update``, so the warp a frame sees does not depend on which frames call ``apply``
+    (StrongSort skips it when there are no tracks, ``strongsort.py:168-172``)."""
+
+    def __init__(self, warps):
+        self.warps = warps  # {frame: (2,3)} or a callable t -> (2,3)
+        self.t = 0
+
+    def apply(self, img, dets=None):
+        w = self.warps(self.t) if callable(self.warps) else self.warps[self.t]
+        return np.array(w, np.float64).reshape(2, 3)
 
 
 class TorchSceneBatch:

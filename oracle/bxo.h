@@ -17,6 +17,10 @@
 extern "C" {
 #endif
 
+/* Worker threads of the few parallel oracle loops (StrongSort NN rows); 1 = single thread.
+ * Results do not depend on it. */
+void bxo_set_threads(int n);
+
 enum { BXO_KF_XYAH = 0, BXO_KF_XYWH = 1 };
 
 /* utils/iou.py:50-67  AssociationFunction.iou_batch  (a[na,4], b[nb,4] xyxy → out[na,nb]) */

@@ -12,6 +12,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <omp.h>
+
 #include "bxo.h"
 #include "bxo_internal.h"
 
@@ -846,3 +848,5 @@ void bxo_aw_max_metric(const double *emb, int nr, int nc, double w_assoc, double
     free(ra);
     free(ca);
 }
+
+void bxo_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }

@@ -130,8 +130,11 @@ typedef struct ss_track {
 
 typedef struct {
     int id, n, cap;
-    double **vec;
+    double **vec; /* samples pre-normalised: x / (np_row_norm(x) + 1e-8), the divisions
+                     _nn_cosine_distance performs (linear_assignment.py:468-497) — done once at
+                     insertion, bit-identical to doing them per query */
     double *q;
+    uint64_t *h;  /* content hash of the raw sample (duplicate samples give identical rows) */
 } ss_gallery;
 
 struct bxo_ss {
@@ -153,6 +156,13 @@ static double *vdup(const double *x, int F) {
     double *y = (double *)malloc(sizeof(double) * F);
     memcpy(y, x, sizeof(double) * F);
     return y;
+}
+
+static uint64_t fnv64(const double *x, int F) {
+    const unsigned char *b = (const unsigned char *)x;
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(double) * (size_t)F; i++) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
 }
 
 static void track_free(ss_track *t) {
@@ -182,6 +192,7 @@ void bxo_ss_free(bxo_ss *s) {
         for (int k = 0; k < s->gal[g].n; k++) free(s->gal[g].vec[k]);
         free(s->gal[g].vec);
         free(s->gal[g].q);
+        free(s->gal[g].h);
     }
     free(s->gal);
     free(s->trk);
@@ -409,14 +420,17 @@ static void gal_prune(ss_gallery *g, int keep) {
     for (int i = 1; i < g->n; i++) { /* stable insertion sort, descending */
         double *v = g->vec[i];
         const double q = g->q[i];
+        const uint64_t h = g->h[i];
         int j = i - 1;
         while (j >= 0 && g->q[j] < q) {
             g->vec[j + 1] = g->vec[j];
             g->q[j + 1] = g->q[j];
+            g->h[j + 1] = g->h[j];
             j--;
         }
         g->vec[j + 1] = v;
         g->q[j + 1] = q;
+        g->h[j + 1] = h;
     }
     for (int k = keep; k < g->n; k++) free(g->vec[k]);
     if (g->n > keep) g->n = keep;
@@ -431,9 +445,14 @@ static void partial_fit(bxo_ss *s, double **feats, const int *tgt, int n, const 
             g->cap = g->cap ? 2 * g->cap : 16;
             g->vec = (double **)realloc(g->vec, sizeof(double *) * g->cap);
             g->q = (double *)realloc(g->q, sizeof(double) * g->cap);
+            g->h = (uint64_t *)realloc(g->h, sizeof(uint64_t) * g->cap);
         }
-        g->vec[g->n] = vdup(feats[k], F);
+        double *v = vdup(feats[k], F);
+        const double den = np_row_norm(feats[k], F) + 1e-8;
+        for (int q = 0; q < F; q++) v[q] = feats[k][q] / den;
+        g->vec[g->n] = v;
         g->q[g->n] = wave_norm(feats[k], F);
+        g->h[g->n] = fnv64(feats[k], F);
         g->n++;
         if (s->budget > 0 && g->n > s->budget) gal_prune(g, s->budget);
     }
@@ -447,20 +466,39 @@ static void partial_fit(bxo_ss *s, double **feats, const int *tgt, int n, const 
     }
 }
 
-/* distance(): min over the target's samples of 1 - clip(s^.d^, -1, 1); no samples -> 1e5 */
-static double nn_dist(bxo_ss *s, int id, const double *dn) {
+/* distance(): min over the target's samples of 1 - clip(s^.d^, -1, 1); no samples -> 1e5.
+ * One target against nd detections.  A sample equal to an earlier one (the tracker re-appends
+ * the same smoothed features every frame, tracker.py:166-178) gives the same distances, so only
+ * distinct samples are evaluated — the minimum is unchanged. */
+static void nn_dist_row(bxo_ss *s, int id, double *const *dn, const int *di, int nd,
+                        double *row) {
     ss_gallery *g = gal_find(s, id, 0);
-    if (!g || g->n == 0) return SS_INFTY;
-    const int F = s->F;
-    double best = 0.0;
-    for (int k = 0; k < g->n; k++) {
-        const double den = np_row_norm(g->vec[k], F) + 1e-8;
-        double acc = 0.0;
-        for (int q = 0; q < F; q++) acc = fma(g->vec[k][q] / den, dn[q], acc);
-        const double d = 1.0 - clip(acc, -1.0, 1.0);
-        if (k == 0 || d < best) best = d;
+    if (!g || g->n == 0) {
+        for (int c = 0; c < nd; c++) row[c] = SS_INFTY;
+        return;
     }
-    return best;
+    const int F = s->F;
+    int *uniq = (int *)malloc(sizeof(int) * g->n);
+    int nu = 0;
+    for (int k = 0; k < g->n; k++) {
+        int dup = 0;
+        for (int u = 0; u < nu && !dup; u++)
+            dup = g->h[uniq[u]] == g->h[k] && !memcmp(g->vec[uniq[u]], g->vec[k], sizeof(double) * F);
+        if (!dup) uniq[nu++] = k;
+    }
+    for (int c = 0; c < nd; c++) {
+        const double *x = dn[di[c]];
+        double best = 0.0;
+        for (int u = 0; u < nu; u++) {
+            const double *v = g->vec[uniq[u]];
+            double acc = 0.0;
+            for (int q = 0; q < F; q++) acc = fma(v[q], x[q], acc);
+            const double d = 1.0 - clip(acc, -1.0, 1.0);
+            if (u == 0 || d < best) best = d;
+        }
+        row[c] = best;
+    }
+    free(uniq);
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -599,10 +637,12 @@ static void metric_cost(bxo_ss *s, ss_frame *fr, int kind, const int *ti, int nt
     double (*meas)[4] = (double(*)[4])malloc(sizeof(double) * 4 * (nd ? nd : 1));
     for (int c = 0; c < nd; c++) det_xyah(&fr->d[di[c]], meas[c]);
     double *gd = (double *)malloc(sizeof(double) * (nd ? nd : 1));
+    /* the NN block is independent per target: rows in parallel (OpenMP; bxo_set_threads) */
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int r = 0; r < nt; r++) nn_dist_row(s, s->trk[ti[r]]->id, fr->dn, di, nd, cost + r * nd);
     for (int r = 0; r < nt; r++) {
         const ss_track *t = s->trk[ti[r]];
         double *row = cost + r * nd;
-        for (int c = 0; c < nd; c++) row[c] = nn_dist(s, t->id, fr->dn[di[c]]);
         bxo_kf_gating_distance(BXO_KF_XYAH, t->mean, t->cov, &meas[0][0], nd, gd);
         for (int c = 0; c < nd; c++)
             if (gd[c] > SS_GATE) row[c] = SS_INFTY;

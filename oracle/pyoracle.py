@@ -128,11 +128,17 @@ def boost_params(**p):
 _lib = None
 
 
+def set_threads(n: int) -> None:
+    """Threads for the oracle's parallel loops (StrongSort NN rows); results do not depend on it."""
+    lib().bxo_set_threads(int(n))
+
+
 def lib():
     global _lib
     if _lib is None:
         build()
         L = C.CDLL(str(LIB_PATH))
+        L.bxo_set_threads.argtypes = [C.c_int]
         L.bxo_iou_batch.argtypes = [_dp, C.c_int, _dp, C.c_int, _dp]
         L.bxo_fuse_score.argtypes = [_dp, C.c_int, C.c_int, _dp]
         L.bxo_embedding_distance.argtypes = [_fp, C.c_int, _fp, C.c_int, C.c_int, _dp]

@@ -19,6 +19,13 @@ def fixture_frames(fx):
             yield t, d, e
 
 
+def fixture_warp(fx, f):
+    """The 2x3 CMC warp a fixture's frame ``f`` was captured with (None = identity CMC)."""
+    if "warps" not in fx.files:
+        return None
+    return np.asarray(fx["warps"][int(f) - 1], np.float64)
+
+
 def fixture_tracker_args(fx):
     return str(fx["kind"]), ast.literal_eval(str(fx["tracker_args"]))
 

@@ -11,7 +11,8 @@ import numpy as np
 import pytest
 
 from oracle import pyoracle as po
-from tests.golden_util import compare_outputs, fixture_frames, fixture_tracker_args
+from tests.golden_util import (compare_outputs, fixture_frames, fixture_tracker_args,
+                               fixture_warp)
 
 pytestmark = pytest.mark.gpu
 
@@ -309,26 +310,39 @@ def make_dropin(kind, args):
 def test_tracker_fixture_parity(torch_cuda, path):
     fx = np.load(path)
     kind, args = fixture_tracker_args(fx)
+    large = "large" in fx.files  # C4 size: drop-in capacities for 1024 objects; no oracle replay
+    if large:
+        import bench
+
+        args = dict(args, **bench.SS_C4_CAPS)
     tr = make_dropin(kind, args)
-    orc = po.OracleTracker(kind, **(dict(args, born_confirmed=True) if kind == "strongsort"
-                                    else args))
+    orc = None if large else po.OracleTracker(
+        kind, **(dict(args, born_confirmed=True) if kind == "strongsort" else args))
+    cmc = None
+    if "warps" in fx.files:
+        from boxmot_amd.synth import SyntheticCMC
+
+        cmc = SyntheticCMC(lambda t: fixture_warp(fx, t))
+        tr.cmc = cmc
     img = np.zeros((1080, 1920, 3), np.uint8)
     rows = []
     ncol = 10 if kind == "strongsort" else 8
-    if kind == "strongsort":
-        args = dict(args, born_confirmed=True)
     for f, d, e in fixture_frames(fx):
+        if cmc is not None:
+            cmc.t = f
         o = tr.update(d, img, e) if e is not None else tr.update(d, img)
         o = np.asarray(o, np.float64).reshape(-1, ncol)
-        oo = orc.update(d, e).reshape(-1, ncol)
-        np.testing.assert_array_equal(o, oo, err_msg=f"frame {f}: GPU != oracle")
+        if orc is not None:
+            oo = orc.update(d, e, fixture_warp(fx, f)).reshape(-1, ncol)
+            np.testing.assert_array_equal(o, oo, err_msg=f"frame {f}: GPU != oracle")
         rows.append(np.concatenate([np.full((o.shape[0], 1), f), o], 1))
     compare_outputs(np.concatenate(rows, 0), fx["outputs"], box_atol=1e-9,
                     conf_atol=1e-9 if kind == "boosttrack" else None)
 
 
-def run_batched(torch, kind, scenes, n_frames, args, emb_dim=0, seq_frames=None):
-    """Drive an Engine with len(scenes) sequences in one launch per frame."""
+def run_batched(torch, kind, scenes, n_frames, args, emb_dim=0, seq_frames=None, warps=None):
+    """Drive an Engine with len(scenes) sequences in one launch per frame (``warps(s, t)``: the
+    2x3 CMC warp of sequence s at frame t, BoT-SORT's multi_gmc)."""
     from boxmot_amd.engine import Engine, EngineParams
 
     S = len(scenes)
@@ -345,7 +359,9 @@ def run_batched(torch, kind, scenes, n_frames, args, emb_dim=0, seq_frames=None)
         de = dev(torch, np.concatenate([f[1] for f in frames], 0)) if emb_dim else None
         out = torch.empty((max(int(off[-1]), 1), 8), dtype=torch.float64, device="cuda")
         cnt = torch.empty(S, dtype=torch.int32, device="cuda")
-        eng.step(dd, do, de, None, out, cnt)
+        w = None if warps is None else dev(torch, np.stack([warps(s, t).reshape(6)
+                                                            for s in range(S)]))
+        eng.step(dd, do, de, w, out, cnt)
         o, c = host(out), host(cnt)
         for s in range(S):
             outs[s].append(o[off[s]: off[s] + c[s]])
@@ -370,6 +386,24 @@ def test_batched_sequences_vs_oracle(torch_cuda, kind):
         for t in range(1, 61):
             d, e, _ = sc.frame(t)
             np.testing.assert_array_equal(outs[s][t - 1], orc.update(d, e),
+                                          err_msg=f"seq {s} frame {t}")
+
+
+def test_botsort_batched_warps_vs_oracle(torch_cuda):
+    """multi_gmc (botsort_track.py:91-104) on per-sequence non-identity warps, several sequences
+    per launch, against the oracle (itself pinned by the trk_botsort_warp_* fixtures)."""
+    from boxmot_amd.synth import SyntheticScene, synth_warp
+
+    scenes = [SyntheticScene(n_obj=24 + 9 * s, seed=140 + s, emb_dim=64,
+                             layout="crowded" if s % 2 else "grid") for s in range(4)]
+    args = dict(track_high_thresh=0.6, new_track_thresh=0.7, match_thresh=0.8)
+    warps = lambda s, t: synth_warp(140 + s, t, rot=0.004 * (s + 1))  # noqa: E731
+    outs = run_batched(torch_cuda, "botsort", scenes, 50, args, 64, warps=warps)
+    for s, sc in enumerate(scenes):
+        orc = po.OracleTracker("botsort", **args)
+        for t in range(1, 51):
+            d, e, _ = sc.frame(t)
+            np.testing.assert_array_equal(outs[s][t - 1], orc.update(d, e, warps(s, t)),
                                           err_msg=f"seq {s} frame {t}")
 
 
@@ -737,14 +771,14 @@ SS_ARGS = dict(min_conf=0.1, max_cos_dist=0.15, max_iou_dist=0.7, max_age=50, n_
 
 
 def run_ss_batched(torch, scenes, n_frames, args, emb_dim, track_cap=256, det_cap=256,
-                   warps=None):
+                   warps=None, vec_cap=32):
     """SsEngine with len(scenes) sequences per launch vs one oracle per sequence: outputs and
     Kalman state bitwise."""
     from boxmot_amd.engine import SsEngine, SsParams
 
     S = len(scenes)
     eng = SsEngine(n_seq=S, track_cap=track_cap, det_cap=det_cap, emb_dim=emb_dim,
-                   params=SsParams(**args))
+                   vec_cap=vec_cap, params=SsParams(**args))
     orcs = [po.OracleTracker("strongsort", **args) for _ in range(S)]
     for t in range(1, n_frames + 1):
         frames = [sc.frame(t) for sc in scenes]
@@ -813,6 +847,36 @@ def test_strongsort_large_scene_vs_oracle(torch_cuda):
 
     sc = SyntheticScene(n_obj=128, seed=31, emb_dim=512, emb_dtype=np.float64, conf_lo=0.15)
     run_ss_batched(torch_cuda, [sc], 20, dict(SS_ARGS), 512, track_cap=1024)
+
+
+def test_strongsort_batched_warps_vs_oracle(torch_cuda):
+    """Track.camera_update (sort/track.py:173-189) on per-sequence non-identity warps, against
+    the oracle (pinned by the trk_strongsort_warp_* fixtures); outputs and Kalman state."""
+    from boxmot_amd.synth import SyntheticScene, synth_warp
+
+    scenes = [SyntheticScene(n_obj=20 + 8 * s, seed=860 + s, emb_dim=48, emb_dtype=np.float64,
+                             conf_lo=0.15, layout="crowded" if s % 2 else "grid")
+              for s in range(3)]
+    run_ss_batched(torch_cuda, scenes, 40, dict(SS_ARGS), 48,
+                   warps=lambda s, t: synth_warp(860 + s, t, rot=0.004 * (s + 1)).reshape(6))
+
+
+def test_strongsort_c4_size_vs_oracle(torch_cuda):
+    """configs[3] at its stated size: one sequence of 1024 objects (~512 detections a frame) with
+    2048-d ReID and budget 150, at the bench's capacities (bench.py strongsort_c4) — the frames
+    take the LDS-overflow paths of the match / pre kernels and the 4-track NN tiles; outputs
+    every frame and the final Kalman state bitwise against the oracle (sort/tracker.py:183-281)."""
+    from boxmot_amd.synth import SyntheticScene
+
+    import bench
+
+    _, n_obj, F, params = bench.CONFIGS["strongsort_c4"]
+    caps = bench.SS_C4_CAPS
+    sc = SyntheticScene(n_obj=n_obj, seed=41, emb_dim=F, emb_dtype=np.float64, conf_lo=0.3)
+    eng = run_ss_batched(torch_cuda, [sc], 16, dict(params), F, track_cap=caps["track_cap"],
+                         det_cap=caps["det_cap"], vec_cap=caps["vec_cap"])
+    st = eng.frame_stats()
+    assert st["dets"] > 450 and st["tracks"] > 900, st  # the C4 geometry was really exercised
 
 
 @pytest.mark.parametrize("emb_dim", [128, 1024, 2048, 640])

@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 
 from oracle import pyoracle as po
-from tests.golden_util import compare_outputs, fixture_frames, fixture_tracker_args
+from tests.golden_util import (compare_outputs, fixture_frames, fixture_tracker_args,
+                               fixture_warp)
 
 GOLDEN = __import__("pathlib").Path(__file__).parent / "golden"
 
@@ -159,7 +160,7 @@ def test_tracker_fixture(path):
     tr = po.OracleTracker(kind, **args)
     rows = []
     for f, d, e in fixture_frames(fx):
-        o = tr.update(d, e)
+        o = tr.update(d, e, fixture_warp(fx, f))
         rows.append(np.concatenate([np.full((o.shape[0], 1), f), o], 1))
     got = np.concatenate(rows, 0)
     compare_outputs(got, fx["outputs"], box_atol=1e-9,
