@@ -43,6 +43,12 @@ CONFIGS = {
                                           new_track_thresh=0.7, track_buffer=30,
                                           match_thresh=0.8, proximity_thresh=0.5,
                                           appearance_thresh=0.25)),
+    # C3's tracker and sizes on the crowded layout (random centres, heavy overlap: many gated
+    # pairs per track, non-trivial LAP components) — SURVEY §8(d)'s crowded variant
+    "botsort_crowded": ("botsort", 256, 512, dict(track_high_thresh=0.6, track_low_thresh=0.1,
+                                                  new_track_thresh=0.7, track_buffer=30,
+                                                  match_thresh=0.8, proximity_thresh=0.5,
+                                                  appearance_thresh=0.25)),
     "bytetrack": ("bytetrack", 256, 0, dict(min_conf=0.1, track_thresh=0.6, match_thresh=0.9,
                                             track_buffer=30)),
     # OCSort (configs[0]'s tracker, YAML defaults): ~20 tracks/frame like MOT17-mini, and the
@@ -161,34 +167,116 @@ def ss_stage_bytes(stage, u, F):
     }[stage]
 
 
-def cpu_baseline(kind, n_obj, emb_dim, params, seconds=15.0, warm_frames=40):
-    """Time the C oracle (port of the reference semantics, 1 thread) on one sequence of the
-    same workload: frames/s over a bounded sample after `warm_frames` of warm-up."""
+# The reference's own CPU path (Python/numpy/scipy), measured during the survey on one core of an
+# Intel Xeon (8 vCPU) container — carried beside the port's numbers, with its
+# hardware; the Python reference itself never runs on the GPU box.
+REFERENCE_CPU_FPS = {
+    "botsort": (26.4, "C3 BoT-SORT 256 x 129 x 512-d"),
+    "bytetrack": (29.6, "C2 ByteTrack 256 x 129"),
+    "strongsort_c4": (0.16, "C4 StrongSort 1024 x ~512 x 2048-d"),
+    "boosttrack": (36.3, "BoostTrack 256 x 129 x 512-d (one sequence)"),
+    "ocsort": (430.0, "C1 OCSort MOT17-02 (~17 tracks)"),
+}
+
+
+def host_cpu():
+    """CPU model, logical CPUs of the machine and CPUs this process may run on."""
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return {"model": model, "logical_cpus": os.cpu_count(), "usable_cpus": usable}
+
+
+def cpu_worker(spec):
+    """One CPU-baseline worker (run in a child process: no torch, no GPU): the C oracle on one
+    sequence of the workload, `warm` untimed frames, then frames until `seconds` of busy time."""
     from boxmot_amd.synth import SyntheticScene
     from oracle import pyoracle as po
 
+    kind, n_obj, emb_dim, params = spec["kind"], spec["n_obj"], spec["emb_dim"], spec["params"]
+    po.set_threads(spec.get("threads", 1))
     extra = dict(conf_lo=OCS_CONF_LO) if kind in ("ocsort", "boosttrack", "strongsort") else {}
     if kind in ("boosttrack", "strongsort"):
         extra["emb_dtype"] = np.float64
-    sc = SyntheticScene(n_obj=n_obj, seed=12345, emb_dim=emb_dim, **extra)
+    sc = SyntheticScene(n_obj=n_obj, seed=spec["seed"], emb_dim=emb_dim,
+                        layout=spec.get("layout", "grid"), **extra)
     tr = po.OracleTracker(kind, **params)
     t = 0
-    for _ in range(warm_frames):
+    for _ in range(spec["warm"]):
         t += 1
         d, e, _ = sc.frame(t)
         tr.update(d, e)
     frames, busy = 0, 0.0
-    while busy < seconds:
+    while busy < spec["seconds"] and frames < spec.get("max_frames", 1 << 30):
         t += 1
         d, e, _ = sc.frame(t)  # generation excluded from the timed work
         t0 = time.perf_counter()
         tr.update(d, e)
         busy += time.perf_counter() - t0
         frames += 1
-    return {"value": frames / busy, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"1 sequence, {n_obj} objects (~{n_obj // 2} dets/frame)"
-                      f"{f' x {emb_dim}-d' if emb_dim else ''}, frames {warm_frames + 1}.."
-                      f"{t} ({frames} timed, {busy:.1f}s single-thread; oracle/ C fp64 port)"}
+    return {"frames": frames, "busy": busy, "first": spec["warm"] + 1, "last": t}
+
+
+def run_cpu_workers(specs):
+    """Run each spec in its own child process (subprocess: a fresh interpreter per worker, like
+    val.py:389's process pool; the parent's GPU context is never forked or exec'd over)."""
+    import subprocess
+
+    procs = [subprocess.Popen([sys.executable, str(Path(__file__).resolve()), "--cpu-worker",
+                               json.dumps(sp)], stdout=subprocess.PIPE, text=True,
+                              env=dict(os.environ, OMP_NUM_THREADS=str(sp.get("threads", 1))))
+             for sp in specs]
+    res = []
+    for p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError(f"cpu worker failed (rc {p.returncode})")
+        res.append(json.loads(out.strip().splitlines()[-1]))
+    return res
+
+
+def cpu_baseline(config, kind, n_obj, emb_dim, params, seconds=15.0):
+    """The C oracle (port of the reference semantics) on the GPU box's host cores: one sequence on
+    one thread, and one process per sequence on all usable cores (val.py:389's model; C4 is one
+    sequence, so its all-cores variant is one process whose NN rows run on all cores)."""
+    host = host_cpu()
+    P = max(1, min(16, host["usable_cpus"]))
+    c4 = config == "strongsort_c4"
+    warm = 8 if c4 else 40
+    base = dict(kind=kind, n_obj=n_obj, emb_dim=emb_dim, params=params, warm=warm,
+                layout="crowded" if config.endswith("_crowded") else "grid",
+                seconds=seconds, max_frames=6 if c4 else 1 << 30)
+    one = run_cpu_workers([dict(base, seed=12345, threads=1)])[0]
+    if c4:
+        many = run_cpu_workers([dict(base, seed=12345, threads=P)])
+    else:
+        many = run_cpu_workers([dict(base, seed=12345 + k, threads=1) for k in range(P)])
+    fps1 = one["frames"] / one["busy"]
+    fpsP = sum(r["frames"] / r["busy"] for r in many)
+    what = (f"{n_obj} objects (~{n_obj // 2} dets/frame)" + (f" x {emb_dim}-d" if emb_dim else ""))
+    ref = REFERENCE_CPU_FPS.get(config)
+    return {
+        "value": round(fpsP, 2), "unit": "frames/s", "cores": P, "kind": "port",
+        "sample": (f"{'1 sequence, NN rows on' if c4 else f'{P} sequences, one process each on'}"
+                   f" {P} cores; {what}; frames {warm + 1}..{many[0]['last']} per sequence, "
+                   f"~{seconds:.0f}s busy each; oracle/ C fp64 port"),
+        "host": host,
+        "single_thread": {"value": round(fps1, 2), "cores": 1,
+                          "sample": f"1 sequence, frames {one['first']}..{one['last']} "
+                                    f"({one['frames']} timed, {one['busy']:.1f}s)"},
+        "reference_python": None if ref is None else {
+            "value": ref[0], "unit": "frames/s", "cores": 1, "workload": ref[1],
+            "hardware": "survey container, Intel Xeon 8 vCPU, 1 core (BASELINE.md §2)"},
+    }
 
 
 def load_traffic(config, stage):
@@ -213,8 +301,12 @@ def main():
     ap.add_argument("--seqs", type=int, default=None,
                     help="sequences per GPU (default 1024; strongsort 256, strongsort_c4 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_worker:
+        print(json.dumps(cpu_worker(json.loads(args.cpu_worker))), flush=True)
+        return
 
     import torch
 
@@ -262,9 +354,14 @@ def main():
         stages = [s for s in Engine.STAGES
                   if F or s not in ("det_features", "gate", "cosine", "features")]
     # this rank's shard: global sequences [rank*S, (rank+1)*S) — weak scaling, no exchange
-    gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev,
+    layout = "crowded" if args.config.endswith("_crowded") else "grid"
+    gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev, layout=layout,
                           **(dict(conf_lo=OCS_CONF_LO) if ocs or bst or sss else {}))
-    total = args.warmup + args.steps
+    # W warm-up steps, then one untimed probe step per pipeline stage (each stage timed once
+    # whatever W is), then the K timed steps
+    n_probe = len(stages)
+    t_first = args.warmup + n_probe
+    total = t_first + args.steps
     frames = [gen.frame(t) for t in range(1, total + 1)]  # resident in HBM before timing
     if bst:  # BoostTrack consumes float64 embeddings (the dtype `boxmot eval` loads)
         frames = [(d, o, e.double()) for d, o, e in frames]
@@ -285,15 +382,14 @@ def main():
         else:
             eng.step(d, off, e, None, out, cnt, stream=stream.cuda_stream)
 
-    # warm-up; its last len(stages) steps time one stage each to find the dominant kernel
+    # warm-up, then the probe steps: each times one stage to find the dominant kernel
     stage_ms = {}
-    cyc0 = args.warmup - len(stages)
-    for k in range(args.warmup):
-        j = k - cyc0
-        if 0 <= j < len(stages):
+    for k in range(t_first):
+        j = k - args.warmup
+        if j >= 0:
             eng.probe(stages[j])
         step(k)
-        if 0 <= j < len(stages):
+        if j >= 0:
             ms, n = eng.probe_read()
             stage_ms[stages[j]] = ms / max(n, 1)
             eng.probe(None)
@@ -306,7 +402,7 @@ def main():
     # two event records per step around the dominant stage's launch (OCSort: its one kernel)
     eng.probe(True if ocs else dominant)
     t0 = time.perf_counter()
-    for k in range(args.warmup, total):
+    for k in range(t_first, total):
         step(k)
     torch.cuda.synchronize()
     if dist:
@@ -327,7 +423,7 @@ def main():
 
     # per-sequence records of this rank's shard: [global seq id, frames timed, dets timed,
     # rows of the last frame, checksum of the last frame, rank wall s, dominant-stage ms]
-    off_h = [frames[k][1].cpu().numpy() for k in range(args.warmup, total)]
+    off_h = [frames[k][1].cpu().numpy() for k in range(t_first, total)]
     dets_seq = np.sum([np.diff(o) for o in off_h], 0)
     last_off, cnt_h, out_h = off_h[-1], cnt.cpu().numpy(), out.cpu().numpy()
     recs = np.zeros((S, 7))
@@ -368,7 +464,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_max / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (GPU-generated grid scenes, resident in HBM before timing)",
+            "data": f"synthetic (GPU-generated {layout} scenes, resident in HBM before timing)",
             "config": {"workload": f"{args.config}: {S} sequences/GPU x {n_obj} tracks x "
                                    f"~{mean_d:.0f} dets" + (f" x {F}-d ReID" if F else ""),
                        "tracker": kind, "n_seq_per_gpu": S, "n_tracks": n_obj,
@@ -376,16 +472,15 @@ def main():
                        "emb_dtype": "f64" if emb_bytes == 8 else "f32",
                        "parallelism": f"seq-sharded x{world}"},
             "roofline": {**roof, "kernel": dominant,
-                         "kernel_ms": round(dom_ms, 4),
+                         "kernel_ms": round(dom_ms, 4), "probe_steps": n_probe,
                          "algorithmic_bytes_per_launch": int(per_launch),
                          "units_last_frame": units,
-                         "stage_ms_warmup": {k: round(v, 4) for k, v in stage_ms.items()}},
+                         "stage_ms_probe": {k: round(v, 4) for k, v in stage_ms.items()}},
             "cpu_baseline": None,
         }
-        # (strongsort_c4: one oracle frame of 1000 tracks x 150 samples x ~500 dets x 2048-d is
-        # minutes of single-thread CPU — no bounded sample fits; reported separately)
-        if world == 1 and not args.no_cpu_baseline and args.config != "strongsort_c4":
-            line["cpu_baseline"] = cpu_baseline(kind, n_obj, F, params, args.cpu_seconds)
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.config, kind, n_obj, F, params,
+                                                args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

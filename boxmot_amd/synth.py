@@ -123,17 +123,18 @@ class SyntheticCMC:
 
 
 class TorchSceneBatch:
-    """The ``grid`` scene process for ``n_seq`` independent sequences, generated on the GPU.
+    """The scene process for ``n_seq`` independent sequences, generated on the GPU.
 
-    Same geometry, motion, detection probability, jitter, confidence and embedding model as
-    ``SyntheticScene(layout="grid")``, but drawn with torch's device RNG so that thousands of
+    Same geometry (``grid`` or ``crowded``), motion, detection probability, jitter, confidence and
+    embedding model as ``SyntheticScene``, but drawn with torch's device RNG so that thousands of
     sequences × frames can be staged in HBM before a timed region (numbers differ from the numpy
     generator; the distribution does not).  ``frame(t)`` returns packed
     ``(dets[sum N,6] f32, det_off[n_seq+1] i32, embs[sum N,F] f32 | None)`` on ``device``.
     """
 
     def __init__(self, n_seq, n_obj, emb_dim=0, seed=0, device="cuda", p_det=0.5,
-                 conf_lo=0.65, conf_hi=1.0, jitter=0.5, width=1920.0, height=1080.0):
+                 conf_lo=0.65, conf_hi=1.0, jitter=0.5, width=1920.0, height=1080.0,
+                 layout="grid"):
         import torch
 
         self.torch, self.n_seq, self.n_obj, self.emb_dim = torch, n_seq, n_obj, emb_dim
@@ -149,9 +150,17 @@ class TorchSceneBatch:
         cx = ((idx % cols) + 0.5) * cw
         cy = torch.div(idx, cols, rounding_mode="floor").add(0.5) * ch
         u = lambda *s: torch.rand(*s, generator=g, device=device, dtype=torch.float64)  # noqa
-        w = 0.45 * cw * (0.8 + 0.4 * u(n_seq, n_obj))
-        h = 0.80 * ch * (0.8 + 0.4 * u(n_seq, n_obj))
-        self.c0 = torch.stack([cx.expand(n_seq, n_obj), cy.expand(n_seq, n_obj)], -1)
+        if layout == "grid":
+            w = 0.45 * cw * (0.8 + 0.4 * u(n_seq, n_obj))
+            h = 0.80 * ch * (0.8 + 0.4 * u(n_seq, n_obj))
+            self.c0 = torch.stack([cx.expand(n_seq, n_obj), cy.expand(n_seq, n_obj)], -1)
+        elif layout == "crowded":  # SyntheticScene's crowded process: random centres, overlap
+            self.c0 = torch.stack([(0.1 + 0.8 * u(n_seq, n_obj)) * width,
+                                   (0.1 + 0.8 * u(n_seq, n_obj)) * height], -1)
+            w = 30.0 + 60.0 * u(n_seq, n_obj)
+            h = w * (1.5 + 1.5 * u(n_seq, n_obj))
+        else:
+            raise ValueError(f"unknown layout {layout!r}")
         self.half = torch.stack([w, h], -1) * 0.5
         self.vel = u(n_seq, n_obj, 2) - 0.5
         if emb_dim:
