@@ -328,6 +328,7 @@ __device__ inline void kf_gating_soa(int kind, const double* mean, const double*
 struct Div32 {
   float n;
   double r;
+  Div32() = default;
   __device__ explicit Div32(float n_) : n(n_), r(1.0 / (double)n_) {}
   __device__ __forceinline__ float operator()(float x) const {
     const double p = (double)x * r;
@@ -337,6 +338,7 @@ struct Div32 {
 // same interface for fp64 rows: plain division
 struct Div64 {
   double n;
+  Div64() = default;
   __device__ explicit Div64(double n_) : n(n_) {}
   __device__ __forceinline__ double operator()(double x) const { return x / n; }
 };

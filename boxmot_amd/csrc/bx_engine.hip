@@ -467,12 +467,20 @@ __global__ __launch_bounds__(WG) void gate_kernel(Dev P, int seq0, const float* 
 // A = (float)smooth_feat / dn_t (dn_t kept per track by K5), B = (float)f2 / dn_d with f2 =
 // (f / n1) / n2 rebuilt from the input row (K1's norms); scipy cdist cosine with its own
 // two-accumulator dots for A.B, |A|, |B|; /2; > appearance_thresh → 1.  Stored in the dense
-// per-sequence [T][D] table K3 reads.  The dots are sequential per pair (scipy's order), so a
-// lane owns a pair; a wave's 64 pairs stream through LDS in 16-element chunks loaded coalesced
-// (4 lanes per row, 16 B each), the elementwise divisions done by the loading lane.
+// per-sequence [T][D] table K3 reads.
+// scipy's two accumulators are independent chains (even elements into one, odd into the other,
+// summed at the end), so a pair's dots run on TWO lanes — lane 2p the even chain, lane 2p+1 the
+// odd one — and a wave owns COS_P pairs: COS_P = 16 gives ~8 waves per SIMD at C3 (the kernel is
+// load-latency bound; the old 64-pairs-per-wave layout left 2).  Rows stream through LDS in
+// COS_CH = 32-element chunks (one whole 128-B line of each row per chunk: 8 lanes x 16 B), the
+// elementwise divisions done by the loading lane, the next chunk's loads in flight meanwhile.
 // Grid (n_seq, COS_BLOCKS).
-constexpr int COS_BLOCKS = 1;
-constexpr int COS_CH = 16;
+constexpr int COS_BLOCKS = 2;
+constexpr int COS_CH = 32;
+#ifndef BX_COS_P
+#define BX_COS_P 16
+#endif
+constexpr int COS_P = BX_COS_P;  // 8 or 16 (a multiple of 8: 8 lanes load a row's chunk)
 __device__ inline void cos_finish(Dev& P, int s, int slot, int dk, double ab, double aa,
                                   double bb) {
   double c = ab / (sqrt(aa) * sqrt(bb));
@@ -496,48 +504,46 @@ __device__ __forceinline__ void load4(const FT* p, FT* v) {
 template <typename FT>
 __global__ __launch_bounds__(WG) void cosine_kernel(Dev P, int seq0, const int* __restrict__ det_off,
                                                     const FT* __restrict__ embs) {
-  __shared__ float s_a[NWAVE][WAVE][COS_CH + 1], s_b[NWAVE][WAVE][COS_CH + 1];
+  constexpr int KR = COS_P / 8;  // row pieces per lane on each side (A: tracks, B: detections)
+  // row stride COS_CH + 2: the 32 chain lanes (pair p, parity) read banks 2p + parity
+  __shared__ float s_a[NWAVE][COS_P][COS_CH + 2], s_b[NWAVE][COS_P][COS_CH + 2];
   const int b = blockIdx.x, s = seq0 + b, T = P.T, D = P.D, F = P.F, w = wave_id(),
             lane = lane_id();
   const int np = P.npair[s], d0 = det_off[b];
   const uint32_t* pairs = P.pairs + (size_t)s * T * D;
-  for (int p0 = (blockIdx.y * NWAVE + w) * WAVE; p0 < np; p0 += COS_BLOCKS * NWAVE * WAVE) {
-    // this lane loads 4-element pieces of rows k*16 + lane/4 (k < 4) of the wave's 64 pairs
-    const FT* arow[4];
-    const FT* brow[4];
-    float adn[4], bdn[4];
-    FT bn1[4], bn2[4];
+  const int col = (lane & 7) * 4;  // this lane's 4 elements of every chunk
+  const int cp = lane >> 1, par = lane & 1;  // chain lanes: pair cp, even/odd elements
+  for (int p0 = (blockIdx.y * NWAVE + w) * COS_P; p0 < np; p0 += COS_BLOCKS * NWAVE * COS_P) {
+    // row pieces: pairs (lane >> 3) + 8k, k < KR
+    const FT* arow[KR];
+    const FT* brow[KR];
+    Div32 da[KR], db[KR];
+    DivBy<FT> d1[KR], d2[KR];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int pp = p0 + k * 16 + (lane >> 2);
+    for (int k = 0; k < KR; k++) {
+      const int pp = p0 + (lane >> 3) + 8 * k;
       const uint32_t pr = pp < np ? pairs[pp] : pairs[p0];
       const int slot = pr >> 16, dk = pr & 0xffff;
-      arow[k] = (const FT*)P.feat + ((size_t)s * T + slot) * F + (lane & 3) * 4;
-      brow[k] = embs + (size_t)(d0 + dk) * F + (lane & 3) * 4;
-      adn[k] = P.tdn[(size_t)s * T + slot];
+      arow[k] = (const FT*)P.feat + ((size_t)s * T + slot) * F + col;
+      brow[k] = embs + (size_t)(d0 + dk) * F + col;
+      da[k] = Div32(P.tdn[(size_t)s * T + slot]);
       const double* nr = P.dnrm + ((size_t)s * D + dk) * 4;
-      bn1[k] = (FT)nr[0];
-      bn2[k] = (FT)nr[1];
-      bdn[k] = (float)nr[2];
+      d1[k] = DivBy<FT>((FT)nr[0]);
+      d2[k] = DivBy<FT>((FT)nr[1]);
+      db[k] = Div32((float)nr[2]);
     }
-    const Div32 da[4] = {Div32(adn[0]), Div32(adn[1]), Div32(adn[2]), Div32(adn[3])};
-    const Div32 db[4] = {Div32(bdn[0]), Div32(bdn[1]), Div32(bdn[2]), Div32(bdn[3])};
-    const DivBy<FT> d1[4] = {DivBy<FT>(bn1[0]), DivBy<FT>(bn1[1]), DivBy<FT>(bn1[2]),
-                             DivBy<FT>(bn1[3])};
-    const DivBy<FT> d2[4] = {DivBy<FT>(bn2[0]), DivBy<FT>(bn2[1]), DivBy<FT>(bn2[2]),
-                             DivBy<FT>(bn2[3])};
-    double ab0 = 0.0, ab1 = 0.0, aa0 = 0.0, aa1 = 0.0, bb0 = 0.0, bb1 = 0.0;
-    FT av[4][4], bv[4][4];  // raw elements of the current chunk; the next chunk's are in flight
+    double ab = 0.0, aa = 0.0, bb = 0.0;  // this lane's chain (even or odd elements)
+    FT av[KR][4], bv[KR][4];  // raw elements of the current chunk; the next chunk's in flight
 #pragma unroll
-    for (int k = 0; k < 4; k++) { load4(arow[k], av[k]); load4(brow[k], bv[k]); }
+    for (int k = 0; k < KR; k++) { load4(arow[k], av[k]); load4(brow[k], bv[k]); }
     for (int c0 = 0; c0 < F; c0 += COS_CH) {
-      FT nav[4][4], nbv[4][4];
+      FT nav[KR][4], nbv[KR][4];
       const int cn = c0 + COS_CH < F ? c0 + COS_CH : c0;
 #pragma unroll
-      for (int k = 0; k < 4; k++) { load4(arow[k] + cn, nav[k]); load4(brow[k] + cn, nbv[k]); }
+      for (int k = 0; k < KR; k++) { load4(arow[k] + cn, nav[k]); load4(brow[k] + cn, nbv[k]); }
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int row = k * 16 + (lane >> 2), col = (lane & 3) * 4;
+      for (int k = 0; k < KR; k++) {
+        const int row = (lane >> 3) + 8 * k;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
           s_a[w][row][col + q] = da[k]((float)av[k][q]);
@@ -546,25 +552,28 @@ __global__ __launch_bounds__(WG) void cosine_kernel(Dev P, int seq0, const int* 
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
+      if (lane < 2 * COS_P) {
 #pragma unroll
-      for (int q = 0; q < COS_CH; q += 2) {
-        // products of two floats are exact in fp64: fma rounds identically to acc + x*y
-        const double x0 = (double)s_a[w][lane][q], x1 = (double)s_a[w][lane][q + 1];
-        const double y0 = (double)s_b[w][lane][q], y1 = (double)s_b[w][lane][q + 1];
-        ab0 = __builtin_fma(x0, y0, ab0); ab1 = __builtin_fma(x1, y1, ab1);
-        aa0 = __builtin_fma(x0, x0, aa0); aa1 = __builtin_fma(x1, x1, aa1);
-        bb0 = __builtin_fma(y0, y0, bb0); bb1 = __builtin_fma(y1, y1, bb1);
+        for (int q = par; q < COS_CH; q += 2) {
+          // products of two floats are exact in fp64: fma rounds identically to acc + x*y
+          const double x = (double)s_a[w][cp][q], y = (double)s_b[w][cp][q];
+          ab = __builtin_fma(x, y, ab);
+          aa = __builtin_fma(x, x, aa);
+          bb = __builtin_fma(y, y, bb);
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int k = 0; k < 4; k++)
+      for (int k = 0; k < KR; k++)
 #pragma unroll
         for (int q = 0; q < 4; q++) { av[k][q] = nav[k][q]; bv[k][q] = nbv[k][q]; }
     }
-    if (p0 + lane < np) {
-      const uint32_t pr = pairs[p0 + lane];
-      cos_finish(P, s, pr >> 16, pr & 0xffff, ab0 + ab1, aa0 + aa1, bb0 + bb1);
+    // even chain + odd chain, as scipy adds its two accumulators
+    const double ab1 = __shfl_xor(ab, 1), aa1 = __shfl_xor(aa, 1), bb1 = __shfl_xor(bb, 1);
+    if (lane < 2 * COS_P && par == 0 && p0 + cp < np) {
+      const uint32_t pr = pairs[p0 + cp];
+      cos_finish(P, s, pr >> 16, pr & 0xffff, ab + ab1, aa + aa1, bb + bb1);
     }
   }
 }
@@ -1589,6 +1598,10 @@ struct bx_engine {
   double* h_out;
   int* h_cnt;
   double* h_warp;
+  // side stream of the frame's fork-join (launch_frame): the ReID feature kernels K1 and K5 run
+  // there beside the Kalman/list kernels they share no data with
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
   std::mutex mu;
 };
 
@@ -1622,7 +1635,29 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
                  hipStream_t st) {
   const Dev& d = e->dev;
   const bool reid = KIND == KIND_BOT && d.with_reid;
-  auto probe_begin = [&](int stage) -> int {
+  // Fork-join: K1 (detection norms) only feeds K1c, and K5 (feature EMA) only reads K3's records
+  // and K1's norms and writes smooth_feat / tdn, which nothing else in the frame touches — so K1
+  // runs on the side stream beside K2/K1b, and K5 beside K4/K4b/K6.  Both joins land on `st`
+  // before the frame returns (the next frame's K1 rewrites the norms K5 reads).
+  if (reid && !e->side) {
+    HIPCHK(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+    for (int k = 0; k < 2; k++) {
+      HIPCHK(hipEventCreateWithFlags(&e->ev_fork[k], hipEventDisableTiming | hipEventDisableSystemFence));
+      HIPCHK(hipEventCreateWithFlags(&e->ev_join[k], hipEventDisableTiming | hipEventDisableSystemFence));
+    }
+  }
+  hipStream_t side = e->side;
+  auto fork = [&](int k) -> int {
+    HIPCHK(hipEventRecord(e->ev_fork[k], st));
+    HIPCHK(hipStreamWaitEvent(side, e->ev_fork[k], 0));
+    return BX_OK;
+  };
+  auto join = [&](int k) -> int {
+    HIPCHK(hipEventRecord(e->ev_join[k], side));
+    HIPCHK(hipStreamWaitEvent(st, e->ev_join[k], 0));
+    return BX_OK;
+  };
+  auto probe_begin = [&](int stage, hipStream_t st) -> int {
     if (stage != e->probe_stage) return BX_OK;
     if (e->probe_used == e->probe_ev.size()) {
       hipEvent_t a, b;
@@ -1635,23 +1670,27 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
     HIPCHK(hipEventRecord(e->probe_ev[e->probe_used].first, st));
     return BX_OK;
   };
-  auto probe_end = [&](int stage) -> int {
+  auto probe_end = [&](int stage, hipStream_t st) -> int {
     if (stage != e->probe_stage) return BX_OK;
     HIPCHK(hipEventRecord(e->probe_ev[e->probe_used++].second, st));
     return BX_OK;
   };
-#define BX_PROBED(stage, launch)                           \
-  do {                                                     \
-    if (int rc_ = probe_begin(stage)) return rc_;          \
-    launch;                                                \
-    HIPCHK(hipGetLastError());                             \
-    if (int rc_ = probe_end(stage)) return rc_;            \
+  // a probed stage is timed by events on the stream it is launched on
+#define BX_PROBED_ON(stage, sstream, ...)                     \
+  do {                                                        \
+    if (int rc_ = probe_begin(stage, sstream)) return rc_;    \
+    __VA_ARGS__;                                              \
+    HIPCHK(hipGetLastError());                                \
+    if (int rc_ = probe_end(stage, sstream)) return rc_;      \
   } while (0)
+#define BX_PROBED(stage, ...) BX_PROBED_ON(stage, st, __VA_ARGS__)
   const int gy_det64 = (d.D + K1_DETS - 1) / K1_DETS, gy_slot = (d.T + WG - 1) / WG;
-  if (reid)
-    BX_PROBED(BX_STAGE_DET_FEATURES,
-              hipLaunchKernelGGL((det_feature_kernel<FT, NPF>), dim3(nseq, gy_det64), dim3(WG), 0,
-                                 st, d, seq0, dets, det_off, (const FT*)embs));
+  if (reid) {
+    if (int rc = fork(0)) return rc;
+    BX_PROBED_ON(BX_STAGE_DET_FEATURES, side,
+                 hipLaunchKernelGGL((det_feature_kernel<FT, NPF>), dim3(nseq, gy_det64), dim3(WG),
+                                    0, side, d, seq0, dets, det_off, (const FT*)embs));
+  }
   const bool gmc = KIND == KIND_BOT && warps;
   if (gmc)
     BX_PROBED(BX_STAGE_PREDICT,
@@ -1666,6 +1705,7 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
               hipLaunchKernelGGL(gate_kernel<KIND>, dim3(nseq, GATE_BLOCKS), dim3(WG),
                                  (sizeof(double) * 4 + sizeof(float4)) * d.D, st, d, seq0, dets,
                                  det_off));
+    if (int rc = join(0)) return rc;
     if (d.F % COS_CH == 0)
       BX_PROBED(BX_STAGE_COSINE,
                 hipLaunchKernelGGL(cosine_kernel<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st, d,
@@ -1679,6 +1719,12 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
   if (int rc = lds_attr((const void*)assoc, e->lds_assoc)) return rc;
   BX_PROBED(BX_STAGE_ASSOC, hipLaunchKernelGGL(assoc, dim3(nseq), dim3(WG), e->lds_assoc, st, d,
                                                seq0, dets, det_off));
+  if (reid) {
+    if (int rc = fork(1)) return rc;
+    BX_PROBED_ON(BX_STAGE_FEATURES, side,
+                 hipLaunchKernelGGL((feature_kernel<FT, NPF>), dim3(nseq, FEAT_BLOCKS), dim3(WG),
+                                    0, side, d, seq0, det_off, (const FT*)embs));
+  }
   BX_PROBED(BX_STAGE_UPDATE,
             hipLaunchKernelGGL(update_kernel<KIND>,
                                dim3(nseq, (d.D + UPD_PER_BLOCK - 1) / UPD_PER_BLOCK), dim3(WG), 0,
@@ -1691,15 +1737,14 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
     BX_PROBED(BX_STAGE_COV_PREDICT,
               hipLaunchKernelGGL(cov_predict_kernel<KIND>, dim3(nseq, (d.T + 15) / 16), dim3(WG),
                                  0, st, d, seq0));
-  if (reid)
-    BX_PROBED(BX_STAGE_FEATURES,
-              hipLaunchKernelGGL((feature_kernel<FT, NPF>), dim3(nseq, FEAT_BLOCKS), dim3(WG), 0,
-                                 st, d, seq0, det_off, (const FT*)embs));
   if (int rc = lds_attr((const void*)finish_kernel<KIND>, e->lds_finish)) return rc;
   BX_PROBED(BX_STAGE_FINISH,
             hipLaunchKernelGGL(finish_kernel<KIND>, dim3(nseq), dim3(WG), e->lds_finish, st, d,
                                seq0, det_off, out, out_count));
+  if (reid)
+    if (int rc = join(1)) return rc;
 #undef BX_PROBED
+#undef BX_PROBED_ON
   return BX_OK;
 }
 
@@ -1822,6 +1867,14 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
 
 int bx_engine_destroy(bx_engine* e) {
   if (!e) return BX_OK;
+  if (e->side) {
+    (void)hipStreamSynchronize(e->side);
+    (void)hipStreamDestroy(e->side);
+    for (int k = 0; k < 2; k++) {
+      (void)hipEventDestroy(e->ev_fork[k]);
+      (void)hipEventDestroy(e->ev_join[k]);
+    }
+  }
   for (auto& ev : e->probe_ev) {
     (void)hipEventDestroy(ev.first);
     (void)hipEventDestroy(ev.second);
