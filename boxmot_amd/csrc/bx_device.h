@@ -23,12 +23,17 @@ enum : uint32_t { ST_NEW = 0, ST_TRACKED = 1, ST_LOST = 2, ST_REMOVED = 3 };
 // (lets the slot-parallel kernels select joint(tracked, lost) without walking the lists)
 // F_PRED / F_GMC / F_REC are frame-transient: mean predicted (covariance predict pending), CMC
 // warp applied to the mean (covariance warp pending), slot has an update record this frame.
+// F_PEND (bits 16-23, persistent): covariance predicts applied to the mean but not yet to the
+// covariance — a track without an update keeps them pending until it is updated again (or its
+// state is read), see bx_engine.hip K2/K4.
 enum : uint32_t {
   F_STATE = 0x7u, F_ACT = 0x8u, F_INREM = 0x10u, F_INUSE = 0x20u, F_INACT = 0x40u,
-  F_INLOST = 0x80u, F_PRED = 0x100u, F_GMC = 0x200u, F_REC = 0x400u, F_TRANSIENT = 0x700u
+  F_INLOST = 0x80u, F_PRED = 0x100u, F_GMC = 0x200u, F_REC = 0x400u, F_TRANSIENT = 0x700u,
+  F_PEND1 = 0x10000u, F_PEND_MASK = 0xFF0000u
 };
 
 __device__ __forceinline__ uint32_t st_of(uint32_t f) { return f & F_STATE; }
+__device__ __forceinline__ int pend_of(uint32_t f) { return (int)((f & F_PEND_MASK) >> 16); }
 
 // ------------------------------------------------------------------------------------------
 // utils/ops.py box conversions (numpy op order)
@@ -409,6 +414,70 @@ __device__ inline double dot2(const A& a, const B& b, int n) {
   return s;
 }
 
+// ------------------------------------------------------------------------------------------
+// Xor butterflies without LDS round trips.  `s += __shfl_xor(s, d)` is a ds_bpermute (an LDS
+// pipe op, ~100+ cycles) per 32-bit word; these use DPP (a VALU operand modifier) within 16-lane
+// rows and gfx950's v_permlane{16,32}_swap across rows.  Every step adds the same two values as
+// the xor butterfly (IEEE addition is commutative, so a pair's two lanes get identical bits):
+// a DPP rotate or mirror reads a lane whose value EQUALS lane l^d's once the earlier steps have
+// made the values periodic (descending d = 32..1: rotate by d; ascending d = 1..: quad perms,
+// then half-mirror / mirror).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+// v[l] + v[l ^ 16] and v[l] + v[l ^ 32] (either operand order: same bits)
+__device__ __forceinline__ float xsum16_f32(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32_f32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ double xsum16_f64(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+}
+__device__ __forceinline__ double xsum32_f64(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+}
+constexpr int DPP_ROR = 0x120, DPP_QP_X1 = 0xB1, DPP_QP_X2 = 0x4E, DPP_HALF_MIRROR = 0x141,
+              DPP_MIRROR = 0x140;
+// the full descending butterfly d = 32, 16, ..., 1 of an fp64 value (all lanes end equal)
+__device__ __forceinline__ double wave_bfly_desc_f64(double s) {
+  s = xsum32_f64(s);
+  s = xsum16_f64(s);
+  s += dpp_f64<DPP_ROR + 8>(s);
+  s += dpp_f64<DPP_ROR + 4>(s);
+  s += dpp_f64<DPP_ROR + 2>(s);
+  s += dpp_f64<DPP_ROR + 1>(s);
+  return s;
+}
+// the ascending butterfly d = 1, 2, ..., < width (width a power of two <= 64) of a float
+__device__ __forceinline__ float wave_bfly_asc_f32(float s, int width) {
+  if (width > 1) s += dpp_f32<DPP_QP_X1>(s);
+  if (width > 2) s += dpp_f32<DPP_QP_X2>(s);
+  if (width > 4) s += dpp_f32<DPP_HALF_MIRROR>(s);
+  if (width > 8) s += dpp_f32<DPP_MIRROR>(s);
+  if (width > 16) s = xsum16_f32(s);
+  if (width > 32) s = xsum32_f32(s);
+  return s;
+}
+
 // np.linalg.norm of a 1-D feature is a BLAS dot with an unpinned order; the engine fixes the
 // "wave order" (restated in oracle/bxo_track.c vnorm): lane l accumulates x[l], x[l+64], ...
 // sequentially in fp64, then an xor butterfly d = 32..1 (commutative: every lane ends with the
@@ -418,9 +487,7 @@ __device__ inline double wave_sumsq(const FT* x, int n) {
   const int lane = threadIdx.x & 63;
   double s = 0.0;
   for (int k = lane; k < n; k += 64) { double v = (double)x[k]; s += v * v; }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
-  return s;
+  return wave_bfly_desc_f64(s);
 }
 template <typename FT>
 __device__ inline FT wave_norm(const FT* x, int n) {
@@ -453,8 +520,7 @@ __device__ inline float np_sumsq_wave_fast(const XT* x, int n) {  // requires np
       for (int i = 1; i < 16; i++) { float v = (float)p[8 * i]; acc += v * v; }
       part[r] = acc;
     }
-    const int width = nacc < 64 ? nacc : 64;
-    for (int d = 1; d < width; d <<= 1) part[r] += __shfl_xor(part[r], d);
+    part[r] = wave_bfly_asc_f32(part[r], nacc < 64 ? nacc : 64);
   }
   // registers hold consecutive blocks of 8 leaves; combine them as a balanced tree
   float res = regs == 1 ? part[0]
@@ -479,8 +545,7 @@ __device__ inline float np_sumsq_wave_fast_padded(const float* x, int n) {
       for (int i = 1; i < 16; i++) { float v = p[8 * i]; acc += v * v; }
       part[r] = acc;
     }
-    const int width = nacc < 64 ? nacc : 64;
-    for (int d = 1; d < width; d <<= 1) part[r] += __shfl_xor(part[r], d);
+    part[r] = wave_bfly_asc_f32(part[r], nacc < 64 ? nacc : 64);
   }
   float res = regs == 1 ? part[0]
               : regs == 2 ? part[0] + part[1]

@@ -41,10 +41,12 @@ constexpr int REG_F = 512;   // feature rows up to this width live in registers:
 constexpr int REG_EPL = REG_F / 64;
 constexpr int REG_FP = REG_F + REG_F / 16;  // LDS row stride: 8 pad floats per 128 (np_dn)
 constexpr int NWAVE = WG / WAVE;
-// doubles per slot: mean[8], covariance[64], then the pre-predict mean[2], mean[3] the pending
-// covariance predict's process noise is computed from (see K2)
-constexpr int KF_STRIDE = 74;
+// doubles per slot: mean[8], covariance[64], then the pre-predict mean[2], mean[3] of the first
+// pending covariance predict and of the later ones (their process noise is computed from them;
+// see K2)
+constexpr int KF_STRIDE = 76;
 constexpr int KF_QM = 72;
+constexpr int KF_QM2 = 74;
 
 // A feature row held by one wave, element q = lane + 64 r in v[r] (F <= REG_F).
 template <typename FT>
@@ -79,8 +81,7 @@ struct RegRow {
         if constexpr (sizeof(FT) == 4) s = __builtin_fma(d, d, s);
         else s += d * d;
       }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+    s = wave_bfly_desc_f64(s);
     if constexpr (sizeof(FT) == 4) return sqrtf((float)s);
     else return sqrt(s);
   }
@@ -195,7 +196,7 @@ struct Dev {
   int* detind;        // [S][T]
   double* conf;       // [S][T]
   double* cls;        // [S][T]
-  double* kf;         // [S][T][KF_STRIDE] Kalman state per slot: mean[8] then cov[64] (576 B)
+  double* kf;         // [S][T][KF_STRIDE] Kalman state per slot: mean[8], cov[64], qm[2], qm2[2]
   void* feat;         // [S][T][F] smooth_feat
   double* clsh;       // [S][T][CLS_HIST][2]
   int* ncls;          // [S][T]
@@ -638,6 +639,10 @@ __device__ __forceinline__ void kf_predict_cov(int kind, const double* qm, doubl
   for (int i = 0; i < 4; i++)
     for (int j = 0; j < 4; j++) kf_predict_quad(kind, qm, c, i, j);
 }
+// n pending covariance predicts of slot state m (K2): the first with qm, the rest with qm2
+__device__ inline void kf_materialize(int kind, double* m, int n) {
+  for (int k = 0; k < n; k++) kf_predict_cov(kind, m + (k ? KF_QM2 : KF_QM), m + 8);
+}
 // multi_gmc covariance part: cov = R8·cov·R8ᵀ, R8 = kron(I4, R) (botsort.py:192-195)
 __device__ inline void gmc_cov(const double* H, double* c) {
   double RP[64];
@@ -680,9 +685,20 @@ __global__ __launch_bounds__(WG) void predict_kernel(Dev P, int seq0,
       if (KIND == KIND_BOT) mm[6] = 0.0;
       mm[7] = 0.0;
     }
-    m2[KF_QM / 2] = make_double2(mm[2], mm[3]);
+    // the covariance predict is deferred (pending count + the process-noise operands).  All
+    // pending predicts after the first see the same (w, h) | h: a track without an update is
+    // Lost from its next predict on, which zeroes the size velocities (v_w, v_h | v_h) first —
+    // so two operand pairs describe any number of pending predicts exactly.
+    if (pend_of(f) == 0) m2[KF_QM / 2] = make_double2(mm[2], mm[3]);
+    else m2[KF_QM2 / 2] = make_double2(mm[2], mm[3]);
     for (int k = 0; k < 4; k++) mm[k] = mm[k] + mm[k + 4];
     nf |= F_PRED;
+    if (pend_of(f) < 255) nf += F_PEND1;
+    else {  // never reached (tracks are removed after max_time_lost frames); kept exact anyway
+      kf_materialize(KIND, m, pend_of(f));
+      m2[KF_QM / 2] = make_double2(mm[2] - mm[6], mm[3] - mm[7]);
+      nf = (nf & ~F_PEND_MASK) | F_PEND1;
+    }
   }
   if (GMC) {  // mean = R8·mean + t
     const double* H = warps + 6 * (size_t)b;
@@ -700,31 +716,38 @@ __global__ __launch_bounds__(WG) void predict_kernel(Dev P, int seq0,
   *fp = nf;
 }
 
-// K4b: the deferred covariance predict (+ CMC warp) of pool tracks that got no update record
-// (matched tracks have theirs done inside K4).  Without a warp: one thread per quad, 16 threads
-// per slot, so a wave touches 4 slots' contiguous state.  Grid (n_seq, ceil(T/16)).
-template <int KIND>
-__global__ __launch_bounds__(WG) void cov_predict_kernel(Dev P, int seq0) {
-  const int s = seq0 + blockIdx.x, T = P.T;
-  const int slot = blockIdx.y * (WG / 16) + (threadIdx.x >> 4), qd = threadIdx.x & 15;
-  if (slot >= T) return;
-  const uint32_t f = P.flags[(size_t)s * T + slot];
-  if ((f & (F_PRED | F_REC)) != F_PRED) return;
-  double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
-  kf_predict_quad(KIND, m + KF_QM, m + 8, qd >> 2, qd & 3);
-}
-// with a CMC warp: thread per slot, predict then warp (and warp-only for unconfirmed tracks)
+// Without a CMC warp there is no K4b: a pool track without an update keeps its covariance
+// predicts pending (a Lost track's covariance is only read again when it is re-found, K4, or
+// when the host reads the state, materialize_kernel), so each frame touches the covariance of
+// updated tracks only.  The pending predicts are applied in their original order with their
+// original operands, so the result is bit-identical to predicting every frame.
+// K4b (CMC warp frames): the pending predicts then the warp of pool tracks that got no update
+// record, and the warp alone for unconfirmed tracks (multi_gmc, botsort.py:192-195): the warp
+// does not commute with later predicts, so nothing stays pending across it.  Thread per slot.
 template <int KIND>
 __global__ __launch_bounds__(WG) void cov_predict_gmc_kernel(Dev P, int seq0,
                                                              const double* __restrict__ warps) {
   const int b = blockIdx.x, s = seq0 + b, T = P.T;
   const int slot = blockIdx.y * WG + threadIdx.x;
   if (slot >= T) return;
-  const uint32_t f = P.flags[(size_t)s * T + slot];
+  uint32_t* fp = P.flags + (size_t)s * T + slot;
+  const uint32_t f = *fp;
   if ((f & F_REC) || !(f & (F_PRED | F_GMC))) return;
   double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
-  if (f & F_PRED) kf_predict_cov(KIND, m + KF_QM, m + 8);
+  kf_materialize(KIND, m, pend_of(f));
   if (f & F_GMC) gmc_cov(warps + 6 * (size_t)b, m + 8);
+  *fp = f & ~F_PEND_MASK;
+}
+// the host reads covariances (bx_engine_tracks_host): apply every pending predict first
+template <int KIND>
+__global__ __launch_bounds__(WG) void materialize_kernel(Dev P, int s) {
+  const int T = P.T, slot = blockIdx.x * WG + threadIdx.x;
+  if (slot >= T) return;
+  uint32_t* fp = P.flags + (size_t)s * T + slot;
+  const uint32_t f = *fp;
+  if (!pend_of(f)) return;
+  kf_materialize(KIND, P.kf + ((size_t)s * T + slot) * KF_STRIDE, pend_of(f));
+  *fp = f & ~F_PEND_MASK;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1270,10 +1293,13 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
   const uint32_t fl = P.flags[sT + slot];
   double cr[8];
   for (int q = 0; q < 4; q++) { const double2 t = crow[q]; cr[2 * q] = t.x; cr[2 * q + 1] = t.y; }
-  if (fl & F_PRED) {  // K2's deferred half: rows i < 4 need row i + 4
+  const int npend = pend_of(fl);
+  if (r == 0 && npend) P.flags[sT + slot] = fl & ~F_PEND_MASK;
+  for (int k = 0; k < npend; k++) {  // K2's pending predicts: rows i < 4 need row i + 4
     double o[8];
     for (int j = 0; j < 8; j++) o[j] = shfl(cr[j], (r + 4) & 7);
-    double mv[4] = {0.0, 0.0, m[KF_QM], m[KF_QM + 1]}, q[8];
+    const int qi = k ? KF_QM2 : KF_QM;
+    double mv[4] = {0.0, 0.0, m[qi], m[qi + 1]}, q[8];
     kf_process_noise(KIND, mv, q);
     double nr[8];
     if (r < 4) {
@@ -1729,14 +1755,10 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
             hipLaunchKernelGGL(update_kernel<KIND>,
                                dim3(nseq, (d.D + UPD_PER_BLOCK - 1) / UPD_PER_BLOCK), dim3(WG), 0,
                                st, d, seq0, dets, det_off, warps));
-  if (gmc)
+  if (gmc)  // (without a warp the covariance predicts of tracks without an update stay pending)
     BX_PROBED(BX_STAGE_COV_PREDICT,
               hipLaunchKernelGGL(cov_predict_gmc_kernel<KIND>, dim3(nseq, gy_slot), dim3(WG), 0,
                                  st, d, seq0, warps));
-  else
-    BX_PROBED(BX_STAGE_COV_PREDICT,
-              hipLaunchKernelGGL(cov_predict_kernel<KIND>, dim3(nseq, (d.T + 15) / 16), dim3(WG),
-                                 0, st, d, seq0));
   if (int rc = lds_attr((const void*)finish_kernel<KIND>, e->lds_finish)) return rc;
   BX_PROBED(BX_STAGE_FINISH,
             hipLaunchKernelGGL(finish_kernel<KIND>, dim3(nseq), dim3(WG), e->lds_finish, st, d,
@@ -2042,6 +2064,16 @@ int bx_engine_tracks_host(bx_engine* e, int seq, int cap, int32_t* ids, int32_t*
   if (n_active) *n_active = na;
   if (n_lost) *n_lost = nl;
   if (na + nl > cap) return set_err(BX_ERR_CAPACITY, "cap too small for the live tracks");
+  if (cov) {  // the covariance of tracks without an update since their last predicts
+    if (e->cfg.kind == BX_BYTETRACK)
+      hipLaunchKernelGGL(materialize_kernel<KIND_BYTE>, dim3((T + WG - 1) / WG), dim3(WG), 0, 0,
+                         e->dev, seq);
+    else
+      hipLaunchKernelGGL(materialize_kernel<KIND_BOT>, dim3((T + WG - 1) / WG), dim3(WG), 0, 0,
+                         e->dev, seq);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+  }
   std::vector<uint16_t> act(T), lost(T);
   std::vector<uint32_t> fl(T);
   std::vector<int> id(T), fid(T), st(T);

@@ -136,6 +136,8 @@ typedef struct bxo_ss bxo_ss;
 bxo_ss *bxo_ss_new(const bxo_ss_params *p);
 void bxo_ss_free(bxo_ss *s);
 int bxo_ss_next_id(const bxo_ss *s);
+/* ByteTrack / BoT-SORT: tracked then lost list — ids, states, mean [8], covariance [8x8] */
+int bxo_tracks(const bxo_tracker *T, int cap, int *ids, int *state, double *mean, double *cov);
 int bxo_ss_tracks(const bxo_ss *s, int cap, int *ids, int *state, double *mean, double *cov);
 /* dets[n,6] float64; embs [n][F] float64 (required when a detection passes min_conf); warp[6]
  * 2x3 CMC affine (NULL = identity).  out [M][10] (x1,y1,x2,y2,id,conf,cls,det_ind,quality,

@@ -335,6 +335,20 @@ bxo_tracker *bxo_botsort_new(double track_high_thresh, double track_low_thresh,
     return T;
 }
 
+/* tracked_stracks then lost_stracks (list order): ids, states, Kalman mean/covariance.  Returns
+ * the count; fills at most cap entries (NULL arrays skipped). */
+int bxo_tracks(const bxo_tracker *T, int cap, int *ids, int *state, double *mean, double *cov) {
+    const int n = T->active.n + T->lost.n;
+    for (int k = 0; k < n && k < cap; k++) {
+        const Trk *t = k < T->active.n ? T->active.v[k] : T->lost.v[k - T->active.n];
+        if (ids) ids[k] = t->id;
+        if (state) state[k] = t->state;
+        if (mean) memcpy(mean + 8 * k, t->mean, sizeof t->mean);
+        if (cov) memcpy(cov + 64 * k, t->cov, sizeof t->cov);
+    }
+    return n;
+}
+
 int bxo_id_count(const bxo_tracker *T) { return T->id_count; }
 int bxo_frame_count(const bxo_tracker *T) { return T->frame_count; }
 

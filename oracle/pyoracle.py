@@ -168,6 +168,8 @@ def lib():
         L.bxo_ocsort_set_asso.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double]
         L.bxo_ocsort_id_count.argtypes = [C.c_void_p]
         L.bxo_ocsort_update.argtypes = [C.c_void_p, _dp, C.c_int, _dp, C.c_int]
+        L.bxo_tracks.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_void_p]
         L.bxo_ocsort_tracks.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.bxo_nn_cosine_distance.argtypes = [_dp, _ip, C.c_int, _dp, C.c_int, C.c_int, _dp]
         L.bxo_np_norm_f64.argtypes = [_dp, C.c_int]
@@ -418,6 +420,18 @@ class OracleTracker:
         if self.kind == "strongsort":
             return lib().bxo_ss_next_id(self.h) - 1
         return lib().bxo_id_count(self.h)
+
+    def tracks(self):
+        """ByteTrack / BoT-SORT: tracked then lost list — ids, states, means [n,8], covs [n,8,8]."""
+        L = lib()
+        n = L.bxo_tracks(self.h, 0, None, None, None, None)
+        ids = np.zeros(max(n, 1), np.int32)
+        st = np.zeros(max(n, 1), np.int32)
+        mean = np.zeros((max(n, 1), 8))
+        cov = np.zeros((max(n, 1), 8, 8))
+        L.bxo_tracks(self.h, n, ids.ctypes.data, st.ctypes.data, mean.ctypes.data,
+                     cov.ctypes.data)
+        return {"id": ids[:n], "state": st[:n], "mean": mean[:n], "covariance": cov[:n]}
 
     def ocsort_tracks(self):
         """OCSort track list (list order): ids, XYSR means [n,7], covariances [n,7,7]."""

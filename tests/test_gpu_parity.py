@@ -366,7 +366,17 @@ def run_batched(torch, kind, scenes, n_frames, args, emb_dim=0, seq_frames=None,
         for s in range(S):
             outs[s].append(o[off[s]: off[s] + c[s]])
     assert eng.status() == 0
+    run_batched.engine = eng  # the last run's engine (Kalman-state checks)
     return outs
+
+
+def assert_kalman_state_equal(eng, s, orc):
+    """Track lists and Kalman state (covariances with their pending predicts applied) bitwise."""
+    g, r = eng.tracks(s), orc.tracks()
+    np.testing.assert_array_equal(g["id"], r["id"])
+    np.testing.assert_array_equal(g["state"], r["state"])
+    np.testing.assert_array_equal(g["mean"], r["mean"])
+    np.testing.assert_array_equal(g["covariance"], r["covariance"])
 
 
 @pytest.mark.parametrize("kind", ["bytetrack", "botsort"])
@@ -381,12 +391,14 @@ def test_batched_sequences_vs_oracle(torch_cuda, kind):
         if kind == "bytetrack" else dict(track_high_thresh=0.6, new_track_thresh=0.7,
                                          match_thresh=0.8)
     outs = run_batched(torch_cuda, kind, scenes, 60, args, emb)
+    eng = run_batched.engine
     for s, sc in enumerate(scenes):
         orc = po.OracleTracker(kind, **args)
         for t in range(1, 61):
             d, e, _ = sc.frame(t)
             np.testing.assert_array_equal(outs[s][t - 1], orc.update(d, e),
                                           err_msg=f"seq {s} frame {t}")
+        assert_kalman_state_equal(eng, s, orc)
 
 
 def test_botsort_batched_warps_vs_oracle(torch_cuda):
@@ -399,12 +411,50 @@ def test_botsort_batched_warps_vs_oracle(torch_cuda):
     args = dict(track_high_thresh=0.6, new_track_thresh=0.7, match_thresh=0.8)
     warps = lambda s, t: synth_warp(140 + s, t, rot=0.004 * (s + 1))  # noqa: E731
     outs = run_batched(torch_cuda, "botsort", scenes, 50, args, 64, warps=warps)
+    eng = run_batched.engine
     for s, sc in enumerate(scenes):
         orc = po.OracleTracker("botsort", **args)
         for t in range(1, 51):
             d, e, _ = sc.frame(t)
             np.testing.assert_array_equal(outs[s][t - 1], orc.update(d, e, warps(s, t)),
                                           err_msg=f"seq {s} frame {t}")
+        assert_kalman_state_equal(eng, s, orc)
+
+
+def test_pending_covariance_predicts_mixed_warps(torch_cuda):
+    """Lost tracks keep covariance predicts pending across identity-CMC frames (no per-frame
+    covariance pass); warp frames and state reads apply them.  Warps on some frames only, Kalman
+    state read mid-sequence and at the end — all bitwise against the oracle."""
+    from boxmot_amd.synth import SyntheticScene, synth_warp
+
+    scenes = [SyntheticScene(n_obj=30 + 10 * s, seed=150 + s, emb_dim=64, p_det=0.35,
+                             layout="crowded" if s else "grid") for s in range(3)]
+    args = dict(track_high_thresh=0.6, new_track_thresh=0.7, match_thresh=0.8)
+    warps = lambda s, t: synth_warp(150 + s, t) if t % 7 == 0 else None  # noqa: E731
+    from boxmot_amd.engine import Engine, EngineParams
+
+    eng = Engine("botsort", n_seq=3, track_cap=512, det_cap=256, emb_dim=64,
+                 params=EngineParams(**args))
+    orcs = [po.OracleTracker("botsort", **args) for _ in scenes]
+    for t in range(1, 46):
+        fr = [sc.frame(t) for sc in scenes]
+        off = np.zeros(4, np.int32)
+        off[1:] = np.cumsum([f[0].shape[0] for f in fr])
+        w = [warps(s, t) for s in range(3)]
+        wd = None if w[0] is None else dev(torch_cuda, np.stack([x.reshape(6) for x in w]))
+        out = torch_cuda.empty((max(int(off[-1]), 1), 8), dtype=torch_cuda.float64, device="cuda")
+        cnt = torch_cuda.empty(3, dtype=torch_cuda.int32, device="cuda")
+        eng.step(dev(torch_cuda, np.concatenate([f[0] for f in fr]).astype(np.float32)),
+                 dev(torch_cuda, off), dev(torch_cuda, np.concatenate([f[1] for f in fr])), wd,
+                 out, cnt)
+        o, c = host(out), host(cnt)
+        for s in range(3):
+            np.testing.assert_array_equal(o[off[s]: off[s] + c[s]],
+                                          orcs[s].update(fr[s][0], fr[s][1], w[s]),
+                                          err_msg=f"seq {s} frame {t}")
+            if t in (12, 30, 45):
+                assert_kalman_state_equal(eng, s, orcs[s])
+    assert eng.status() == 0
 
 
 def test_botsort_c3_scale_vs_oracle(torch_cuda):
