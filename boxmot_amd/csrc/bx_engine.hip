@@ -418,6 +418,8 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
 // fp64 cost K3 uses, so K3 finds each gated edge's embedding distance precomputed.
 // Grid (n_seq, GATE_BLOCKS); detection boxes staged in LDS (fp64 + outward-rounded fp32 for a
 // conservative reject); one thread per track, detections walked in order from LDS (broadcast).
+// (Fusing K2's predict into this kernel and overlapping it with K1 measured slower: the two
+// VALU-bound kernels slowed each other down.)
 constexpr int GATE_BLOCKS = 2;
 template <int KIND>
 __global__ __launch_bounds__(WG) void gate_kernel(Dev P, int seq0, const float* __restrict__ dets,
@@ -664,18 +666,14 @@ __device__ inline void gmc_cov(const double* H, double* c) {
 // 205-207, botsort.py:188-189) and, for BoT-SORT with a CMC warp, multi_gmc's mean part over the
 // pool and the unconfirmed tracks (botsort.py:192-195).  Sets F_PRED / F_GMC for K4.
 // Grid (n_seq, ceil(T/256)); thread per slot.
+// The per-slot body is shared with the fused gating kernel (K1b predicts its listed tracks).
 template <int KIND, bool GMC>
-__global__ __launch_bounds__(WG) void predict_kernel(Dev P, int seq0,
-                                                     const double* __restrict__ warps) {
-  const int b = blockIdx.x, s = seq0 + b, T = P.T;
-  const int slot = blockIdx.y * WG + threadIdx.x;
-  if (slot >= T) return;
-  uint32_t* fp = P.flags + (size_t)s * T + slot;
-  const uint32_t f = *fp;
+__device__ __forceinline__ void predict_slot(Dev& P, int s, int slot, uint32_t f,
+                                             const double* __restrict__ H) {
   const bool pool = ((f & F_INACT) && (f & F_ACT)) || (f & F_INLOST);
   const bool unconf = (f & F_INACT) && !(f & F_ACT);
   if (!pool && !(GMC && unconf)) return;
-  double* m = P.kf + ((size_t)s * T + slot) * KF_STRIDE;
+  double* m = P.kf + ((size_t)s * P.T + slot) * KF_STRIDE;
   double2* m2 = (double2*)m;
   double mm[8];
   for (int q = 0; q < 4; q++) { const double2 t = m2[q]; mm[2 * q] = t.x; mm[2 * q + 1] = t.y; }
@@ -689,19 +687,18 @@ __global__ __launch_bounds__(WG) void predict_kernel(Dev P, int seq0,
     // pending predicts after the first see the same (w, h) | h: a track without an update is
     // Lost from its next predict on, which zeroes the size velocities (v_w, v_h | v_h) first —
     // so two operand pairs describe any number of pending predicts exactly.
-    if (pend_of(f) == 0) m2[KF_QM / 2] = make_double2(mm[2], mm[3]);
+    int pend = pend_of(f);
+    if (pend == 255) {  // never reached (tracks are removed after max_time_lost frames)
+      kf_materialize(KIND, m, pend);
+      pend = 0;
+      nf &= ~F_PEND_MASK;
+    }
+    if (pend == 0) m2[KF_QM / 2] = make_double2(mm[2], mm[3]);
     else m2[KF_QM2 / 2] = make_double2(mm[2], mm[3]);
     for (int k = 0; k < 4; k++) mm[k] = mm[k] + mm[k + 4];
-    nf |= F_PRED;
-    if (pend_of(f) < 255) nf += F_PEND1;
-    else {  // never reached (tracks are removed after max_time_lost frames); kept exact anyway
-      kf_materialize(KIND, m, pend_of(f));
-      m2[KF_QM / 2] = make_double2(mm[2] - mm[6], mm[3] - mm[7]);
-      nf = (nf & ~F_PEND_MASK) | F_PEND1;
-    }
+    nf = (nf | F_PRED) + F_PEND1;
   }
   if (GMC) {  // mean = R8·mean + t
-    const double* H = warps + 6 * (size_t)b;
     for (int q = 0; q < 4; q++) {
       double a0 = H[0] * mm[2 * q] + H[1] * mm[2 * q + 1];
       double a1 = H[3] * mm[2 * q] + H[4] * mm[2 * q + 1];
@@ -713,7 +710,16 @@ __global__ __launch_bounds__(WG) void predict_kernel(Dev P, int seq0,
     nf |= F_GMC;
   }
   for (int q = 0; q < 4; q++) m2[q] = make_double2(mm[2 * q], mm[2 * q + 1]);
-  *fp = nf;
+  P.flags[(size_t)s * P.T + slot] = nf;
+}
+template <int KIND, bool GMC>
+__global__ __launch_bounds__(WG) void predict_kernel(Dev P, int seq0,
+                                                     const double* __restrict__ warps) {
+  const int b = blockIdx.x, s = seq0 + b, T = P.T;
+  const int slot = blockIdx.y * WG + threadIdx.x;
+  if (slot >= T) return;
+  predict_slot<KIND, GMC>(P, s, slot, P.flags[(size_t)s * T + slot],
+                          GMC ? warps + 6 * (size_t)b : nullptr);
 }
 
 // Without a CMC warp there is no K4b: a pool track without an update keeps its covariance
@@ -1711,13 +1717,15 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
   } while (0)
 #define BX_PROBED(stage, ...) BX_PROBED_ON(stage, st, __VA_ARGS__)
   const int gy_det64 = (d.D + K1_DETS - 1) / K1_DETS, gy_slot = (d.T + WG - 1) / WG;
-  if (reid) {
+  if (reid)
     if (int rc = fork(0)) return rc;
+  const bool gmc = KIND == KIND_BOT && warps;
+  // K1 on the side stream, submitted first (measured: 0.644 ms/step; submitted after K2/K1b
+  // 0.647; serial on the main stream 0.661)
+  if (reid)
     BX_PROBED_ON(BX_STAGE_DET_FEATURES, side,
                  hipLaunchKernelGGL((det_feature_kernel<FT, NPF>), dim3(nseq, gy_det64), dim3(WG),
                                     0, side, d, seq0, dets, det_off, (const FT*)embs));
-  }
-  const bool gmc = KIND == KIND_BOT && warps;
   if (gmc)
     BX_PROBED(BX_STAGE_PREDICT,
               hipLaunchKernelGGL((predict_kernel<KIND, true>), dim3(nseq, gy_slot), dim3(WG), 0,
@@ -1727,10 +1735,10 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
               hipLaunchKernelGGL((predict_kernel<KIND, false>), dim3(nseq, gy_slot), dim3(WG), 0,
                                  st, d, seq0, warps));
   if (reid) {
+    const size_t glds = (sizeof(double) * 4 + sizeof(float4)) * d.D;  // det boxes in LDS
     BX_PROBED(BX_STAGE_GATE,
-              hipLaunchKernelGGL(gate_kernel<KIND>, dim3(nseq, GATE_BLOCKS), dim3(WG),
-                                 (sizeof(double) * 4 + sizeof(float4)) * d.D, st, d, seq0, dets,
-                                 det_off));
+              hipLaunchKernelGGL(gate_kernel<KIND>, dim3(nseq, GATE_BLOCKS), dim3(WG), glds, st,
+                                 d, seq0, dets, det_off));
     if (int rc = join(0)) return rc;
     if (d.F % COS_CH == 0)
       BX_PROBED(BX_STAGE_COSINE,
