@@ -113,6 +113,8 @@ EXPORTS = [
     "bx_last_error", "bx_device_count", "bx_engine_create", "bx_engine_destroy",
     "bx_engine_reset", "bx_engine_step", "bx_engine_update_host", "bx_engine_status",
     "bx_engine_counters_host", "bx_engine_set_id_count", "bx_engine_tracks_host",
+    "bx_engine_state_set_host", "bx_ocsort_state_set_host", "bx_boost_state_set_host",
+    "bx_ss_state_set_host",
     "bx_engine_probe", "bx_engine_probe_read", "bx_engine_frame_stats_host",
     "bx_iou_batch", "bx_pairwise_cost", "bx_aw_max_metric", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
     "bx_kf_multi_predict", "bx_kf_update", "bx_kf_gating_distance", "bx_linear_assignment", "bx_lapjv",
@@ -197,6 +199,10 @@ _SIGS = {
     "bx_ss_status": ([_vp, _ip], C.c_int),
     "bx_ss_counters_host": ([_vp, C.c_int, _ip, _ip, _ip, _ip], C.c_int),
     "bx_ss_tracks_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _ip], C.c_int),
+    "bx_engine_state_set_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
+    "bx_ocsort_state_set_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
+    "bx_boost_state_set_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
+    "bx_ss_state_set_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
     "bx_ss_frame_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_ss_probe": ([_vp, C.c_int], C.c_int),
     "bx_ss_probe_read": ([_vp, _dp, _ip], C.c_int),

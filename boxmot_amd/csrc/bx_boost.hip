@@ -1318,6 +1318,34 @@ int bx_boost_tracks_host(bx_boost* e, int seq, int cap, int32_t* ids, double* x,
   return BX_OK;
 }
 
+int bx_boost_state_set_host(bx_boost* e, int seq, int n, const int32_t* ids, const double* x,
+                            const double* p) {
+  if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && !ids))
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_boost_state_set_host");
+  BCHK(hipDeviceSynchronize());
+  int s[SQB];
+  BCHK(hipMemcpy(s, e->dev.seqst + (size_t)seq * SQB, sizeof(s), hipMemcpyDeviceToHost));
+  const int nt = s[SB_NTR];
+  std::vector<int> ord(nt);
+  if (nt)
+    BCHK(hipMemcpy(ord.data(), e->dev.order + (size_t)seq * e->dev.T, sizeof(int) * nt,
+                   hipMemcpyDeviceToHost));
+  for (int j = 0; j < n; j++) {
+    BstTrk* dt = nullptr;
+    BstTrk t;
+    for (int k = 0; k < nt && !dt; k++) {
+      BstTrk* cand = e->dev.trk + (size_t)seq * e->dev.T + ord[k];
+      BCHK(hipMemcpy(&t, cand, sizeof(BstTrk), hipMemcpyDeviceToHost));
+      if (t.id == ids[j]) dt = cand;
+    }
+    if (!dt) return bx_record_error(BX_ERR_INVALID, "state_set: no live track with that id");
+    if (x) memcpy(t.x, x + 8 * j, sizeof(t.x));
+    if (p) memcpy(t.P, p + 64 * j, sizeof(t.P));
+    BCHK(hipMemcpy(dt, &t, sizeof(BstTrk), hipMemcpyHostToDevice));
+  }
+  return BX_OK;
+}
+
 int bx_boost_frame_stats_host(bx_boost* e, int seq0, int nseq, int64_t* sums) {
   if (!e || !sums || seq0 < 0 || nseq < 0 || seq0 + nseq > e->dev.S)
     return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_boost_frame_stats_host");

@@ -33,7 +33,7 @@ enum : uint32_t {
 };
 
 __device__ __forceinline__ uint32_t st_of(uint32_t f) { return f & F_STATE; }
-__device__ __forceinline__ int pend_of(uint32_t f) { return (int)((f & F_PEND_MASK) >> 16); }
+__host__ __device__ __forceinline__ int pend_of(uint32_t f) { return (int)((f & F_PEND_MASK) >> 16); }
 
 // ------------------------------------------------------------------------------------------
 // utils/ops.py box conversions (numpy op order)

@@ -2108,4 +2108,50 @@ int bx_engine_tracks_host(bx_engine* e, int seq, int cap, int32_t* ids, int32_t*
   return BX_OK;
 }
 
+int bx_engine_state_set_host(bx_engine* e, int seq, int n, const int32_t* ids, const double* mean,
+                             const double* cov) {
+  if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && !ids))
+    return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_state_set_host");
+  HIPCHK(hipDeviceSynchronize());
+  const int T = e->dev.T;
+  const size_t sT = (size_t)seq * T;
+  int v[SQ_STRIDE];
+  HIPCHK(hipMemcpy(v, e->dev.seq + (size_t)seq * SQ_STRIDE, sizeof(v), hipMemcpyDeviceToHost));
+  const int na = v[SQ_NA], nl = v[SQ_NL];
+  std::vector<uint16_t> act(T), lost(T);
+  std::vector<int> id(T);
+  HIPCHK(hipMemcpy(act.data(), e->dev.act + sT, 2 * T, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(lost.data(), e->dev.lost + sT, 2 * T, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(id.data(), e->dev.id + sT, 4 * T, hipMemcpyDeviceToHost));
+  for (int j = 0; j < n; j++) {
+    int slot = -1;
+    for (int k = 0; k < na + nl && slot < 0; k++) {
+      const int sl = k < na ? act[k] : lost[k - na];
+      if (id[sl] == ids[j]) slot = sl;
+    }
+    if (slot < 0) return set_err(BX_ERR_INVALID, "state_set: no live track with that id");
+    double* kf = e->dev.kf + (sT + slot) * KF_STRIDE;
+    uint32_t f;
+    HIPCHK(hipMemcpy(&f, e->dev.flags + sT + slot, 4, hipMemcpyDeviceToHost));
+    if (cov && pend_of(f)) {  // the set covariance is current: its pending predicts are void
+      f &= ~F_PEND_MASK;
+      HIPCHK(hipMemcpy(e->dev.flags + sT + slot, &f, 4, hipMemcpyHostToDevice));
+    } else if (pend_of(f)) {  // keep the covariance: apply its pending predicts (with the
+      // operands of the mean they were made from) before the mean changes
+      if (e->cfg.kind == BX_BYTETRACK)
+        hipLaunchKernelGGL(materialize_kernel<KIND_BYTE>, dim3((T + WG - 1) / WG), dim3(WG), 0,
+                           0, e->dev, seq);
+      else
+        hipLaunchKernelGGL(materialize_kernel<KIND_BOT>, dim3((T + WG - 1) / WG), dim3(WG), 0,
+                           0, e->dev, seq);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipDeviceSynchronize());
+    }
+    if (mean) HIPCHK(hipMemcpy(kf, mean + 8 * j, 8 * 8, hipMemcpyHostToDevice));
+    if (cov) HIPCHK(hipMemcpy(kf + 8, cov + 64 * j, 64 * 8, hipMemcpyHostToDevice));
+  }
+  HIPCHK(hipDeviceSynchronize());
+  return BX_OK;
+}
+
 }  // extern "C"

@@ -1179,6 +1179,34 @@ int bx_ocsort_tracks_host(bx_ocsort* e, int seq, int cap, int32_t* ids, double* 
   return BX_OK;
 }
 
+int bx_ocsort_state_set_host(bx_ocsort* e, int seq, int n, const int32_t* ids, const double* x,
+                             const double* p) {
+  if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && !ids))
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ocsort_state_set_host");
+  OCHK(hipDeviceSynchronize());
+  int s[SQO];
+  OCHK(hipMemcpy(s, e->dev.seqst + (size_t)seq * SQO, sizeof(s), hipMemcpyDeviceToHost));
+  const int nt = s[SO_NTR];
+  std::vector<int> ord(nt);
+  if (nt)
+    OCHK(hipMemcpy(ord.data(), e->dev.order + (size_t)seq * e->dev.T, sizeof(int) * nt,
+                   hipMemcpyDeviceToHost));
+  for (int j = 0; j < n; j++) {
+    OcsTrk* dt = nullptr;
+    OcsTrk t;
+    for (int k = 0; k < nt && !dt; k++) {
+      OcsTrk* cand = e->dev.trk + (size_t)seq * e->dev.T + ord[k];
+      OCHK(hipMemcpy(&t, cand, sizeof(OcsTrk), hipMemcpyDeviceToHost));
+      if (t.id == ids[j]) dt = cand;
+    }
+    if (!dt) return bx_record_error(BX_ERR_INVALID, "state_set: no live track with that id");
+    if (x) memcpy(t.x, x + 7 * j, sizeof(t.x));
+    if (p) memcpy(t.P, p + 49 * j, sizeof(t.P));
+    OCHK(hipMemcpy(dt, &t, sizeof(OcsTrk), hipMemcpyHostToDevice));
+  }
+  return BX_OK;
+}
+
 int bx_ocsort_frame_stats_host(bx_ocsort* e, int seq0, int nseq, int64_t* sums) {
   if (!e || !sums || seq0 < 0 || nseq < 0 || seq0 + nseq > e->dev.S)
     return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ocsort_frame_stats_host");

@@ -2690,6 +2690,34 @@ int bx_ss_tracks_host(bx_ss* e, int seq, int cap, int32_t* ids, int32_t* state, 
   return BX_OK;
 }
 
+int bx_ss_state_set_host(bx_ss* e, int seq, int n, const int32_t* ids, const double* mean,
+                         const double* cov) {
+  if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && !ids))
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_state_set_host");
+  SCHK(hipDeviceSynchronize());
+  int s[SQS];
+  SCHK(hipMemcpy(s, e->dev.sq + (size_t)seq * SQS, sizeof(s), hipMemcpyDeviceToHost));
+  const int nt = s[Q_NTR];
+  std::vector<int> ord(nt);
+  if (nt)
+    SCHK(hipMemcpy(ord.data(), e->dev.order + (size_t)seq * e->dev.T, sizeof(int) * nt,
+                   hipMemcpyDeviceToHost));
+  for (int j = 0; j < n; j++) {
+    SsTrk* dt = nullptr;
+    SsTrk t;
+    for (int k = 0; k < nt && !dt; k++) {
+      SsTrk* cand = e->dev.trk + (size_t)seq * e->dev.T + ord[k];
+      SCHK(hipMemcpy(&t, cand, sizeof(SsTrk), hipMemcpyDeviceToHost));
+      if (t.id == ids[j]) dt = cand;
+    }
+    if (!dt) return bx_record_error(BX_ERR_INVALID, "state_set: no live track with that id");
+    if (mean) memcpy(t.mean, mean + 8 * j, sizeof(t.mean));
+    if (cov) memcpy(t.cov, cov + 64 * j, sizeof(t.cov));
+    SCHK(hipMemcpy(dt, &t, sizeof(SsTrk), hipMemcpyHostToDevice));
+  }
+  return BX_OK;
+}
+
 int bx_ss_frame_stats_host(bx_ss* e, int seq0, int nseq, int64_t* sums) {
   if (!e || !sums || seq0 < 0 || nseq < 0 || seq0 + nseq > e->dev.S)
     return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_frame_stats_host");

@@ -174,6 +174,25 @@ class Engine:
                 "is_activated": act[:n].astype(bool), "frame_id": fid[:n],
                 "start_frame": sf[:n], "mean": mean[:n], "covariance": cov[:n]}
 
+    def state_set(self, seq: int, ids, mean=None, covariance=None) -> None:
+        """Write the Kalman mean [n,8] / covariance [n,8,8] of live tracks by id (host code
+        editing STrack.mean / .covariance in the reference)."""
+        n, ids, m, c = _state_arrays(ids, mean, covariance, 8, 64)
+        N.check(self._L.bx_engine_state_set_host(self._h, seq, n, ids.ctypes.data, _p(m), _p(c)),
+                "state_set")
+
+
+
+def _state_arrays(ids, a, b, na, nb):
+    ids = np.ascontiguousarray(ids, np.int32).reshape(-1)
+    n = ids.size
+    a = None if a is None else np.ascontiguousarray(a, np.float64).reshape(n, na)
+    b = None if b is None else np.ascontiguousarray(b, np.float64).reshape(n, nb)
+    return n, ids, a, b
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
 
 def _asso_kind(name: str) -> int:
     from .iou import KINDS
@@ -285,6 +304,12 @@ class OcsortEngine:
                                               P.ctypes.data, C.byref(n)), "tracks")
         k = min(n.value, cap)
         return {"id": ids[:k], "x": x[:k], "P": P[:k]}
+
+    def state_set(self, seq: int, ids, x=None, P=None) -> None:
+        """Write KalmanBoxTracker.kf.x [n,7] / .kf.P [n,7,7] of live tracks by id."""
+        n, ids, a, b = _state_arrays(ids, x, P, 7, 49)
+        N.check(self._L.bx_ocsort_state_set_host(self._h, seq, n, ids.ctypes.data, _p(a), _p(b)),
+                "state_set")
 
     def frame_stats(self, seq0: int = 0, nseq: int | None = None) -> dict:
         """Last frame over sequences [seq0, seq0+nseq): live tracks, output rows, frame."""
@@ -433,6 +458,12 @@ class BoostEngine:
             snap["emb"] = E[:k]
         return snap
 
+    def state_set(self, seq: int, ids, x=None, P=None) -> None:
+        """Write KalmanBoxTracker.kf.x [n,8] / .kf.covariance [n,8,8] of live tracks by id."""
+        n, ids, a, b = _state_arrays(ids, x, P, 8, 64)
+        N.check(self._L.bx_boost_state_set_host(self._h, seq, n, ids.ctypes.data, _p(a), _p(b)),
+                "state_set")
+
     def frame_stats(self, seq0: int = 0, nseq: int | None = None) -> dict:
         nseq = self.n_seq - seq0 if nseq is None else nseq
         a = (C.c_int64 * 7)()
@@ -566,6 +597,12 @@ class SsEngine:
                 "tracks")
         k = min(n.value, cap)
         return {"id": ids[:k], "state": st[:k], "mean": mean[:k], "covariance": cov[:k]}
+
+    def state_set(self, seq: int, ids, mean=None, covariance=None) -> None:
+        """Write Track.mean [n,8] / Track.covariance [n,8,8] of live tracks by id."""
+        n, ids, m, c = _state_arrays(ids, mean, covariance, 8, 64)
+        N.check(self._L.bx_ss_state_set_host(self._h, seq, n, ids.ctypes.data, _p(m), _p(c)),
+                "state_set")
 
     def frame_stats(self, seq0: int = 0, nseq: int | None = None) -> dict:
         nseq = self.n_seq - seq0 if nseq is None else nseq

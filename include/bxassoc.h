@@ -134,6 +134,13 @@ int bx_engine_set_id_count(bx_engine *e, int seq, int id_count, void *stream);
 int bx_engine_tracks_host(bx_engine *e, int seq, int cap, int32_t *ids, int32_t *state,
                           int32_t *is_activated, int32_t *frame_id, int32_t *start_frame,
                           double *mean, double *cov, int *n_active, int *n_lost);
+/* Write the Kalman state of live tracks (host, synchronous), addressed by track id: mean [n][8],
+ * cov [n][64] (either may be NULL).  What host code does to `STrack.mean` / `.covariance` in
+ * the reference (the objects are plain attributes: bytetrack.py:40-53 / botsort_track.py:75-104
+ * read them back on the next predict); the occlusion handler's edit is the model
+ * (utils/occlusion_handler.py:380-398).  BX_ERR_INVALID if an id is not live. */
+int bx_engine_state_set_host(bx_engine *e, int seq, int n, const int32_t *ids, const double *mean,
+                             const double *cov);
 
 /* ---------------------------- op-level kernels (device pointers) ---------------------------- */
 int bx_iou_batch(const double *a, int na, const double *b, int nb, double *out, void *stream);

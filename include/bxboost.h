@@ -84,6 +84,11 @@ int bx_boost_set_id_count(bx_boost *e, int seq, int id_count, void *stream);
  * covariances P [cap][64], embeddings emb [cap][emb_dim] (any may be NULL); *n = tracks. */
 int bx_boost_tracks_host(bx_boost *e, int seq, int cap, int32_t *ids, double *x, double *p,
                          double *emb, int *n);
+/* Write KalmanBoxTracker.kf.x [n][8] / .kf.covariance [n][64] of live tracks by id (host,
+ * synchronous; either may be NULL) — trackers/boosttrack/boosttrack.py:45-121 /
+ * kalmanfilter.py:8-157 state attributes.  BX_ERR_INVALID for an unknown id. */
+int bx_boost_state_set_host(bx_boost *e, int seq, int n, const int32_t *ids, const double *x,
+                            const double *p);
 /* Last-frame statistics over sequences [seq0, seq0+nseq) (host, synchronous): sums[7] =
  * {detections, detections kept after the boosts, tracks entering the frame, output rows,
  * embedding-update records, max frame counter, sum of detections x tracks (the ReID

@@ -79,6 +79,11 @@ int bx_ocsort_set_id_count(bx_ocsort *e, int seq, int id_count, void *stream);
 int bx_ocsort_set_frame_size(bx_ocsort *e, int seq, double w, double h, void *stream);
 int bx_ocsort_tracks_host(bx_ocsort *e, int seq, int cap, int32_t *ids, double *x, double *p,
                           int *n);
+/* Write KalmanBoxTracker.kf.x [n][7] / .kf.P [n][49] of live tracks by id (host, synchronous;
+ * either may be NULL) — host code editing `trk.kf.x` / `trk.kf.P` (ocsort.py:56-192,
+ * motion/kalman_filters/aabb/xysr_kf.py state attributes).  BX_ERR_INVALID for an unknown id. */
+int bx_ocsort_state_set_host(bx_ocsort *e, int seq, int n, const int32_t *ids, const double *x,
+                             const double *p);
 /* Last-frame statistics over sequences [seq0, seq0+nseq) (host, synchronous): sums[3] =
  * {tracks alive after the frame, output rows, max frame counter} — bench.py's unit counts. */
 int bx_ocsort_frame_stats_host(bx_ocsort *e, int seq0, int nseq, int64_t *sums);

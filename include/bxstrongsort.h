@@ -90,6 +90,12 @@ int bx_ss_counters_host(bx_ss *e, int seq, int *frame_count, int *next_id, int *
 /* Track list in list order (host): ids, states (1 tentative, 2 confirmed), means [8], covs [64]. */
 int bx_ss_tracks_host(bx_ss *e, int seq, int cap, int32_t *ids, int32_t *state, double *mean,
                       double *cov, int *n);
+/* Write Track.mean [n][8] / Track.covariance [n][64] of live tracks by id (host, synchronous;
+ * either may be NULL): the state edit OcclusionAwareTracker._update_track_with_predicted_position
+ * makes (utils/occlusion_handler.py:380-398; sort/track.py:76-400 attributes).
+ * BX_ERR_INVALID for an unknown id. */
+int bx_ss_state_set_host(bx_ss *e, int seq, int n, const int32_t *ids, const double *mean,
+                         const double *cov);
 /* Last-frame statistics over sequences [seq0, seq0+nseq) (host): sums[7] = {detections kept,
  * tracks entering the frame, confirmed tracks queried next frame, gallery sample rows compared,
  * output rows, max frame counter, matches} — bench.py's unit counts. */

@@ -136,6 +136,12 @@ typedef struct bxo_ss bxo_ss;
 bxo_ss *bxo_ss_new(const bxo_ss_params *p);
 void bxo_ss_free(bxo_ss *s);
 int bxo_ss_next_id(const bxo_ss *s);
+/* host edits of the Kalman state by track id (mirrors of the engines' bx_*_state_set_host);
+ * each returns the number of ids found */
+int bxo_state_set(bxo_tracker *T, int n, const int *ids, const double *mean, const double *cov);
+int bxo_ocsort_state_set(bxo_ocsort *o, int n, const int *ids, const double *x, const double *P);
+int bxo_boost_state_set(bxo_boost *b, int n, const int *ids, const double *x, const double *P);
+int bxo_ss_state_set(bxo_ss *s, int n, const int *ids, const double *mean, const double *cov);
 /* ByteTrack / BoT-SORT: tracked then lost list — ids, states, mean [8], covariance [8x8] */
 int bxo_tracks(const bxo_tracker *T, int cap, int *ids, int *state, double *mean, double *cov);
 int bxo_ss_tracks(const bxo_ss *s, int cap, int *ids, int *state, double *mean, double *cov);

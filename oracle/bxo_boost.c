@@ -312,6 +312,20 @@ void bxo_boost_free(bxo_boost *b) {
 }
 
 int bxo_boost_id_count(const bxo_boost *b) { return b->id_count; }
+
+/* host edit of trk.kf.x / trk.kf.covariance by id; returns the number of ids found */
+int bxo_boost_state_set(bxo_boost *b, int n, const int *ids, const double *x, const double *P) {
+    int found = 0;
+    for (int j = 0; j < n; j++)
+        for (int i = 0; i < b->n; i++)
+            if (b->trk[i].id == ids[j]) {
+                if (x) memcpy(b->trk[i].kf.x, x + 8 * j, sizeof(double) * 8);
+                if (P) memcpy(b->trk[i].kf.P, P + 64 * j, sizeof(double) * 64);
+                found++;
+                break;
+            }
+    return found;
+}
 void bxo_boost_set_id_count(bxo_boost *b, int c) { b->id_count = c; }
 
 int bxo_boost_tracks(const bxo_boost *b, int cap, int *ids, double *x, double *P) {

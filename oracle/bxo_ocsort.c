@@ -627,6 +627,20 @@ void bxo_ocsort_free(bxo_ocsort *o) {
 
 int bxo_ocsort_id_count(bxo_ocsort *o) { return o->id_count; }
 
+/* host edit of trk.kf.x / trk.kf.P by id; returns the number of ids found */
+int bxo_ocsort_state_set(bxo_ocsort *o, int n, const int *ids, const double *x, const double *P) {
+    int found = 0;
+    for (int j = 0; j < n; j++)
+        for (int k = 0; k < o->ntr; k++)
+            if (o->tr[k].id == ids[j]) {
+                if (x) memcpy(o->tr[k].kf.s.x, x + 7 * j, sizeof(double) * 7);
+                if (P) memcpy(o->tr[k].kf.s.P, P + 49 * j, sizeof(double) * 49);
+                found++;
+                break;
+            }
+    return found;
+}
+
 int bxo_ocsort_tracks(bxo_ocsort *o, int cap, int *ids, double *x, double *P) {
     for (int k = 0; k < o->ntr && k < cap; k++) {
         if (ids) ids[k] = o->tr[k].id;

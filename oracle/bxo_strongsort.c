@@ -202,6 +202,20 @@ void bxo_ss_free(bxo_ss *s) {
 
 int bxo_ss_next_id(const bxo_ss *s) { return s->next_id; }
 
+/* host edit of Track.mean / Track.covariance by id; returns the number of ids found */
+int bxo_ss_state_set(bxo_ss *s, int n, const int *ids, const double *mean, const double *cov) {
+    int found = 0;
+    for (int j = 0; j < n; j++)
+        for (int i = 0; i < s->ntrk; i++)
+            if (s->trk[i]->id == ids[j]) {
+                if (mean) memcpy(s->trk[i]->mean, mean + 8 * j, sizeof(double) * 8);
+                if (cov) memcpy(s->trk[i]->cov, cov + 64 * j, sizeof(double) * 64);
+                found++;
+                break;
+            }
+    return found;
+}
+
 int bxo_ss_tracks(const bxo_ss *s, int cap, int *ids, int *state, double *mean, double *cov) {
     for (int i = 0; i < s->ntrk && i < cap; i++) {
         if (ids) ids[i] = s->trk[i]->id;

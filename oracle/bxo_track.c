@@ -349,6 +349,21 @@ int bxo_tracks(const bxo_tracker *T, int cap, int *ids, int *state, double *mean
     return n;
 }
 
+/* host edit of STrack.mean / .covariance by id; returns the number of ids found */
+int bxo_state_set(bxo_tracker *T, int n, const int *ids, const double *mean, const double *cov) {
+    int found = 0;
+    for (int j = 0; j < n; j++)
+        for (int k = 0; k < T->active.n + T->lost.n; k++) {
+            Trk *t = k < T->active.n ? T->active.v[k] : T->lost.v[k - T->active.n];
+            if (t->id != ids[j]) continue;
+            if (mean) memcpy(t->mean, mean + 8 * j, sizeof t->mean);
+            if (cov) memcpy(t->cov, cov + 64 * j, sizeof t->cov);
+            found++;
+            break;
+        }
+    return found;
+}
+
 int bxo_id_count(const bxo_tracker *T) { return T->id_count; }
 int bxo_frame_count(const bxo_tracker *T) { return T->frame_count; }
 

@@ -170,6 +170,9 @@ def lib():
         L.bxo_ocsort_update.argtypes = [C.c_void_p, _dp, C.c_int, _dp, C.c_int]
         L.bxo_tracks.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_void_p]
+        for fn in ("bxo_state_set", "bxo_ocsort_state_set", "bxo_boost_state_set",
+                   "bxo_ss_state_set"):
+            getattr(L, fn).argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.bxo_ocsort_tracks.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.bxo_nn_cosine_distance.argtypes = [_dp, _ip, C.c_int, _dp, C.c_int, C.c_int, _dp]
         L.bxo_np_norm_f64.argtypes = [_dp, C.c_int]
@@ -420,6 +423,20 @@ class OracleTracker:
         if self.kind == "strongsort":
             return lib().bxo_ss_next_id(self.h) - 1
         return lib().bxo_id_count(self.h)
+
+    def state_set(self, ids, a=None, b=None):
+        """Kalman state edit by track id, as the engines' state_set (ByteTrack/BoT-SORT/StrongSort:
+        mean, covariance; OCSort: x [7], P [49]; BoostTrack: x [8], P [64])."""
+        ids = np.ascontiguousarray(ids, np.int32).reshape(-1)
+        fn = {"bytetrack": "bxo_state_set", "botsort": "bxo_state_set",
+              "ocsort": "bxo_ocsort_state_set", "boosttrack": "bxo_boost_state_set",
+              "strongsort": "bxo_ss_state_set"}[self.kind]
+        a = None if a is None else np.ascontiguousarray(a, np.float64)
+        b = None if b is None else np.ascontiguousarray(b, np.float64)
+        found = getattr(lib(), fn)(self.h, ids.size, ids.ctypes.data,
+                                   None if a is None else a.ctypes.data,
+                                   None if b is None else b.ctypes.data)
+        assert found == ids.size, "state_set: unknown track id"
 
     def tracks(self):
         """ByteTrack / BoT-SORT: tracked then lost list — ids, states, means [n,8], covs [n,8,8]."""

@@ -1022,3 +1022,48 @@ def test_run_sequences_matches_per_sequence_dropins(torch_cuda, tmp_path, kind):
         b = (tmp_path / "single" / f"{nm}.txt").read_bytes()
         assert a == b, f"{kind} {nm}: batched run differs from the per-sequence drop-in"
         assert len(a) > 0
+
+
+# ------------------------------------------------------------------ host state write-back
+@pytest.mark.parametrize("kind", ["bytetrack", "botsort", "ocsort", "boosttrack", "strongsort"])
+def test_state_set_vs_oracle(torch_cuda, kind):
+    """bx_*_state_set_host: host code edits the Kalman mean / covariance of some live tracks
+    between frames (what the reference's occlusion handler does to Track.mean / .covariance,
+    utils/occlusion_handler.py:380-398); the same edit on the oracle, outputs bitwise after."""
+    from boxmot_amd.synth import SyntheticScene
+
+    emb = {"botsort": 32, "boosttrack": 32, "strongsort": 32}.get(kind, 0)
+    args = {"bytetrack": dict(min_conf=0.1, track_thresh=0.6, match_thresh=0.9, track_buffer=30),
+            "botsort": dict(track_high_thresh=0.6, new_track_thresh=0.7, match_thresh=0.8),
+            "ocsort": dict(OCS_ARGS), "boosttrack": dict(BOOST_ARGS),
+            "strongsort": dict(SS_ARGS)}[kind]
+    tr = make_dropin(kind, {k: v for k, v in args.items() if k != "born_confirmed"})
+    orc = po.OracleTracker(kind, **args)
+    sc = SyntheticScene(n_obj=36, seed=77, emb_dim=emb, layout="crowded",
+                        emb_dtype=np.float64 if kind in ("boosttrack", "strongsort") else np.float32,
+                        conf_lo=0.3 if kind in ("ocsort", "boosttrack", "strongsort") else 0.65)
+    img = np.zeros((1080, 1920, 3), np.uint8)
+    ncol = 10 if kind == "strongsort" else 8
+    edits = 0
+    for t in range(1, 36):
+        d, e, _ = sc.frame(t)
+        o = tr.update(d, img, e) if emb else tr.update(d, img)
+        o = np.asarray(o, np.float64).reshape(-1, ncol)
+        np.testing.assert_array_equal(o, orc.update(d, e).reshape(-1, ncol), err_msg=f"frame {t}")
+        if t in (10, 18, 25):
+            g = tr.engine.tracks(0)
+            a, b = (g["x"], g["P"]) if kind in ("ocsort", "boosttrack") else (g["mean"],
+                                                                                g["covariance"])
+            sel = np.arange(0, len(g["id"]), 3)
+            ids, a, b = g["id"][sel], a[sel].copy(), b[sel].copy()
+            a[:, 0] += 3.25
+            a[:, 1] -= 1.5
+            b[:, :4, :4] *= 1.5
+            if t == 18:  # mean only: the covariance (and its pending predicts) stay
+                b = None
+            tr.engine.state_set(0, ids, a, b)
+            orc.state_set(ids, a, b)
+            edits += len(ids)
+    assert edits > 0
+    with pytest.raises(ValueError):
+        tr.engine.state_set(0, [10 ** 6], np.zeros((1, 7 if kind == "ocsort" else 8)))
