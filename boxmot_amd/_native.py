@@ -128,6 +128,8 @@ EXPORTS = [
     "bx_ss_step", "bx_ss_update_host", "bx_ss_status", "bx_ss_counters_host",
     "bx_ss_tracks_host", "bx_ss_frame_stats_host", "bx_ss_probe", "bx_ss_probe_read",
     "bx_txt_shape", "bx_txt_read", "bx_mot_format", "bx_mot_write",
+    "bx_engine_update_classes_host", "bx_ocsort_update_classes_host",
+    "bx_boost_update_classes_host",
 ]
 
 _vp, _ip, _dp, _fp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_float)
@@ -206,6 +208,12 @@ _SIGS = {
     "bx_ss_frame_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_ss_probe": ([_vp, C.c_int], C.c_int),
     "bx_ss_probe_read": ([_vp, _dp, _ip], C.c_int),
+    "bx_engine_update_classes_host": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp, C.c_int, _vp, _ip,
+                                       _vp], C.c_int),
+    "bx_ocsort_update_classes_host": ([_vp, C.c_int, C.c_int, _vp, C.c_int, _ip, _vp, _ip, _vp],
+                                      C.c_int),
+    "bx_boost_update_classes_host": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp, C.c_int, _vp, _ip,
+                                      _vp], C.c_int),
 }
 
 _lib = None

@@ -1022,6 +1022,14 @@ __global__ void boost_reset_kernel(BstDev g, int seq0, int nseq) {
 
 }  // namespace
 
+// per_class: the frame counter is held across a frame's class calls (basetracker.py:177,186:
+// `self.frame_count = frame_count` before every class's update) — saved by the first call
+__global__ void boost_hold_frame_kernel(int* seqst, int s, int* hold, int first) {
+  int* f = seqst + (size_t)s * SQB + SB_FRAME;
+  if (first) hold[0] = *f;
+  *f = hold[0];
+}
+
 struct bx_boost {
   BstDev dev;
   bx_boost_config cfg;
@@ -1034,6 +1042,12 @@ struct bx_boost {
   double* h_warp = nullptr;
   double* h_out = nullptr;
   int* h_cnt = nullptr;
+  // per_class host path (bx_boost_update_classes_host): class offsets [C][2], counts [C], the
+  // held frame counter
+  int n_classes = 0;
+  int* h_coff = nullptr;
+  int* h_ccnt = nullptr;
+  int* h_hold = nullptr;
   // timing probe
   int probe_stage = -1;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -1212,6 +1226,9 @@ int bx_boost_destroy(bx_boost* e) {
   (void)hipFree(e->h_warp);
   (void)hipFree(e->h_out);
   (void)hipFree(e->h_cnt);
+  (void)hipFree(e->h_coff);
+  (void)hipFree(e->h_ccnt);
+  (void)hipFree(e->h_hold);
   delete e;
   return BX_OK;
 }
@@ -1257,6 +1274,83 @@ int bx_boost_update_host(bx_boost* e, int seq, const float* dets, int n, const d
   BCHK(hipStreamSynchronize(st));
   if (cnt) BCHK(hipMemcpy(out, e->h_out, sizeof(double) * 8 * cnt, hipMemcpyDeviceToHost));
   *n_out = cnt;
+  int status = 0;
+  BCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
+  if (status)
+    return bx_record_error(status, status == BX_ERR_CAPACITY ? "detections exceed det_cap"
+                                                             : "a sequence ran out of track slots (raise track_cap)");
+  return BX_OK;
+}
+
+// per_class=True (basetracker.py:155-201) for one sequence: BoostTrack keeps its `trackers`
+// list outside active_tracks, so the decorator's swap does not isolate the classes:
+// every class call predicts, associates and ages ALL tracks against that class's detections.
+// Restated as one engine sequence stepped once per class id 0..C-1 with the frame counter held;
+// rows stacked in class order, det_ind indexing the class's subset.  One sync at the end.
+int bx_boost_update_classes_host(bx_boost* e, int seq, const float* dets, int n,
+                                 const double* embs, const double* warp, int n_classes,
+                                 double* out, int* n_out, void* stream) {
+  if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && !dets) || !n_out || n_classes <= 0 ||
+      n_classes > 4096)
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_boost_update_classes_host");
+  if (n > e->dev.D) return bx_record_error(BX_ERR_CAPACITY, "detections exceed det_cap");
+  const bool reid = e->dev.reid;
+  if (reid && n && !embs) return bx_record_error(BX_ERR_SHAPE, "with_reid BoostTrack needs embeddings");
+  hipStream_t st = (hipStream_t)stream;
+  const int C = n_classes, F = e->dev.F;
+  if (e->n_classes && e->n_classes != C)
+    return bx_record_error(BX_ERR_INVALID, "n_classes differs from the engine's first per-class call");
+  if (!e->n_classes) {
+    e->n_classes = C;
+    BCHK(hipMalloc(&e->h_coff, sizeof(int) * 2 * C));
+    BCHK(hipMalloc(&e->h_ccnt, sizeof(int) * C));
+    BCHK(hipMalloc(&e->h_hold, sizeof(int)));
+  }
+  auto cls_of = [&](int i) -> int {
+    const float v = dets[6 * i + 5];
+    return (v >= 0.f && v < (float)C && v == (float)(int)v) ? (int)v : -1;
+  };
+  std::vector<int> cnt(C + 1, 0);
+  for (int i = 0; i < n; i++)
+    if (cls_of(i) >= 0) cnt[cls_of(i) + 1]++;
+  for (int c = 0; c < C; c++) cnt[c + 1] += cnt[c];
+  const int m = cnt[C];
+  std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+  std::vector<float> hd((size_t)6 * (m ? m : 1));
+  std::vector<double> he(reid ? (size_t)(m ? m : 1) * F : 1);
+  for (int i = 0; i < n; i++) {
+    const int c = cls_of(i);
+    if (c < 0) continue;
+    const int k = fill[c]++;
+    memcpy(&hd[6 * (size_t)k], dets + 6 * (size_t)i, 6 * sizeof(float));
+    if (reid) memcpy(&he[(size_t)F * k], embs + (size_t)F * i, sizeof(double) * F);
+  }
+  std::vector<int> hoff(2 * C);
+  for (int c = 0; c < C; c++) { hoff[2 * c] = 0; hoff[2 * c + 1] = cnt[c + 1] - cnt[c]; }
+  if (m) BCHK(hipMemcpyAsync(e->h_dets, hd.data(), sizeof(float) * 6 * m, hipMemcpyHostToDevice, st));
+  if (m && reid)
+    BCHK(hipMemcpyAsync(e->h_embs, he.data(), sizeof(double) * (size_t)m * F, hipMemcpyHostToDevice, st));
+  BCHK(hipMemcpyAsync(e->h_coff, hoff.data(), sizeof(int) * 2 * C, hipMemcpyHostToDevice, st));
+  if (warp) BCHK(hipMemcpyAsync(e->h_warp, warp, sizeof(double) * 6, hipMemcpyHostToDevice, st));
+  for (int c = 0; c < C; c++) {
+    hipLaunchKernelGGL(boost_hold_frame_kernel, dim3(1), dim3(1), 0, st, e->dev.seqst, seq,
+                       e->h_hold, c == 0 ? 1 : 0);
+    BCHK(hipGetLastError());
+    int rc = launch(e, seq, 1, e->h_dets + 6 * (size_t)cnt[c], e->h_coff + 2 * c,
+                    reid ? e->h_embs + (size_t)F * cnt[c] : nullptr, warp ? e->h_warp : nullptr,
+                    e->h_out + 8 * (size_t)cnt[c], e->h_ccnt + c, st);
+    if (rc) return rc;
+  }
+  std::vector<int> oc(C);
+  std::vector<double> ho((size_t)8 * (m ? m : 1));
+  BCHK(hipMemcpyAsync(oc.data(), e->h_ccnt, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  if (m) BCHK(hipMemcpyAsync(ho.data(), e->h_out, sizeof(double) * 8 * m, hipMemcpyDeviceToHost, st));
+  BCHK(hipStreamSynchronize(st));
+  int k = 0;
+  for (int c = 0; c < C; c++)
+    for (int j = 0; j < oc[c]; j++, k++)
+      if (out) memcpy(out + 8 * (size_t)k, &ho[8 * ((size_t)cnt[c] + j)], 8 * sizeof(double));
+  *n_out = k;
   int status = 0;
   BCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
   if (status)

@@ -29,6 +29,7 @@ enum : uint32_t { ST_NEW = 0, ST_TRACKED = 1, ST_LOST = 2, ST_REMOVED = 3 };
 enum : uint32_t {
   F_STATE = 0x7u, F_ACT = 0x8u, F_INREM = 0x10u, F_INUSE = 0x20u, F_INACT = 0x40u,
   F_INLOST = 0x80u, F_PRED = 0x100u, F_GMC = 0x200u, F_REC = 0x400u, F_TRANSIENT = 0x700u,
+  F_PARKED = 0x800u,  // per_class mode: on another class's (parked) active list — kept alive
   F_PEND1 = 0x10000u, F_PEND_MASK = 0xFF0000u
 };
 

@@ -1588,7 +1588,8 @@ __global__ __launch_bounds__(WG) void finish_kernel(Dev P, int seq0, const int* 
     const uint32_t f = g_flags[k];
     const uint8_t kp = s_keep[k];
     const uint32_t nf =
-        kp ? ((f & ~(F_INACT | F_INLOST | F_TRANSIENT)) | (kp == 1 ? F_INACT : F_INLOST)) : 0u;
+        kp ? ((f & ~(F_INACT | F_INLOST | F_TRANSIENT)) | (kp == 1 ? F_INACT : F_INLOST))
+           : (f & F_PARKED) ? f : 0u;
     if (nf != f) g_flags[k] = nf;
   }
   if (tid == 0) {
@@ -1609,6 +1610,47 @@ __global__ void reset_kernel(int* seq, uint32_t* flags, int T, int seq0, int nse
 }
 
 __global__ void set_id_kernel(int* seq, int s, int v) { seq[(size_t)s * SQ_STRIDE + SQ_IDC] = v; }
+
+// per_class mode (BaseTracker.per_class_decorator, basetracker.py:181-192): before class
+// `next`'s update the active list of the class that ran last (`cur`) is parked and `next`'s
+// comes back — `self.active_tracks = self.per_class_active_tracks[cls_id]`.  Only the active list
+// is swapped: the lost list, the removed flags and the id counter stay shared, as in the
+// reference (ByteTrack / BoT-SORT keep lost_stracks / removed_stracks on the tracker).  Parked
+// slots leave the pool (no F_INACT: K2 does not predict them) but stay allocated (F_PARKED).
+// The frame counter is held across a frame's class calls (`self.frame_count = frame_count`):
+// the first class call of a frame saves it, every class call starts from it.  One workgroup.
+__global__ __launch_bounds__(WG) void class_swap_kernel(Dev P, int s, uint16_t* park, int* npark,
+                                                        int C, int cur, int next, int first) {
+  const int T = P.T, tid = threadIdx.x;
+  const size_t sT = (size_t)s * T;
+  int* seq = P.seq + (size_t)s * SQ_STRIDE;
+  uint16_t* act = P.act + sT;
+  uint32_t* fl = P.flags + sT;
+  if (cur != next) {
+    const int na = seq[SQ_NA];
+    for (int k = tid; k < na; k += WG) {
+      const int sl = act[k];
+      park[(size_t)cur * T + k] = (uint16_t)sl;
+      fl[sl] = (fl[sl] & ~F_INACT) | F_PARKED;
+    }
+    __syncthreads();
+    const int nn = npark[next];
+    for (int k = tid; k < nn; k += WG) {
+      const int sl = park[(size_t)next * T + k];
+      act[k] = (uint16_t)sl;
+      fl[sl] = (fl[sl] & ~F_PARKED) | F_INACT;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      npark[cur] = na;
+      seq[SQ_NA] = nn;
+    }
+  }
+  if (tid == 0) {
+    if (first) npark[C] = seq[SQ_FC];
+    seq[SQ_FC] = npark[C];
+  }
+}
 
 }  // namespace
 
@@ -1635,6 +1677,14 @@ struct bx_engine {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
   std::mutex mu;
+  // per_class mode (bx_engine_update_classes_host), allocated on first use: per sequence the
+  // parked active lists [C][T] + their lengths [C] + the held frame counter, the class that ran
+  // last; host-path class offsets [C][2] and output counts [C]
+  int n_classes = 0;
+  std::vector<char*> park;
+  std::vector<int> cur_cls;
+  int* h_coff = nullptr;
+  int* h_ccnt = nullptr;
 };
 
 namespace {
@@ -1658,6 +1708,11 @@ int lds_attr(const void* kern, size_t bytes) {
   HIPCHK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
   done.emplace_back(kern, bytes);
   return BX_OK;
+}
+
+// per_class state of one sequence: parked lists [C][T] uint16, then npark [C] + held fc
+size_t park_npark_off(const bx_engine* e) {
+  return ((size_t)e->n_classes * e->dev.T * sizeof(uint16_t) + 255) & ~size_t(255);
 }
 
 // One frame of sequences [seq0, seq0+nseq): the K1..K6 pipeline on stream st.
@@ -1916,6 +1971,9 @@ int bx_engine_destroy(bx_engine* e) {
   (void)hipFree(e->h_out);
   (void)hipFree(e->h_cnt);
   (void)hipFree(e->h_warp);
+  for (char* p : e->park) (void)hipFree(p);
+  (void)hipFree(e->h_coff);
+  (void)hipFree(e->h_ccnt);
   delete e;
   return BX_OK;
 }
@@ -1926,6 +1984,12 @@ int bx_engine_reset(bx_engine* e, int seq0, int nseq, void* stream) {
   hipLaunchKernelGGL(reset_kernel, dim3(nseq), dim3(256), 0, (hipStream_t)stream, e->dev.seq,
                      e->dev.flags, e->dev.T, seq0, nseq);
   HIPCHK(hipGetLastError());
+  for (int s = seq0; s < seq0 + nseq && e->n_classes; s++)
+    if (e->park[s]) {  // parked class lists are gone with the tracks
+      HIPCHK(hipMemsetAsync(e->park[s] + park_npark_off(e), 0, sizeof(int) * (e->n_classes + 1),
+                            (hipStream_t)stream));
+      e->cur_cls[s] = 0;
+    }
   return BX_OK;
 }
 
@@ -1976,6 +2040,100 @@ int bx_engine_update_host(bx_engine* e, int seq, const float* dets, int n, const
   if (cnt && out)
     HIPCHK(hipMemcpy(out, e->h_out, sizeof(double) * 8 * cnt, hipMemcpyDeviceToHost));
   *n_out = cnt;
+  int status = 0;
+  HIPCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
+  if (status & (1 << BX_ERR_TRACK_OVERFLOW))
+    return set_err(BX_ERR_TRACK_OVERFLOW, "a sequence ran out of track slots (raise track_cap)");
+  return BX_OK;
+}
+
+// per_class=True (BaseTracker.per_class_decorator, basetracker.py:155-201) for one sequence:
+// the update runs once per class id 0..C-1 on that class's detections (`dets[:, 5] == cls_id` on
+// the float32 array; rows keep their input order; det_ind indexes the class's subset), with the
+// class's active list swapped in (class_swap_kernel) and the frame counter held; outputs are
+// stacked in class order.  All C class calls are enqueued back to back on `stream` (no host sync
+// between them); one synchronisation at the end.
+int bx_engine_update_classes_host(bx_engine* e, int seq, const float* dets, int n,
+                                  const void* embs, const double* warp, int n_classes,
+                                  double* out, int* n_out, void* stream) {
+  if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && !dets) || !n_out || n_classes <= 0 ||
+      n_classes > 4096)
+    return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_update_classes_host");
+  if (n > e->dev.D) return set_err(BX_ERR_CAPACITY, "detections exceed det_cap");
+  const bool reid = e->dev.with_reid;
+  if (reid && n > 0 && !embs) return set_err(BX_ERR_SHAPE, "BoT-SORT with_reid needs embs");
+  std::lock_guard<std::mutex> lk(e->mu);
+  hipStream_t st = (hipStream_t)stream;
+  const int C = n_classes, F = e->dev.F;
+  if (e->n_classes && e->n_classes != C)
+    return set_err(BX_ERR_INVALID, "n_classes differs from the engine's first per-class call");
+  if (!e->n_classes) {
+    e->n_classes = C;
+    e->park.assign(e->dev.S, nullptr);
+    e->cur_cls.assign(e->dev.S, 0);
+    HIPCHK(hipMalloc(&e->h_coff, sizeof(int) * 2 * C));
+    HIPCHK(hipMalloc(&e->h_ccnt, sizeof(int) * C));
+  }
+  if (!e->park[seq]) {
+    const size_t bytes = park_npark_off(e) + sizeof(int) * (C + 1);
+    HIPCHK(hipMalloc(&e->park[seq], bytes));
+    HIPCHK(hipMemset(e->park[seq], 0, bytes));
+  }
+  uint16_t* park = (uint16_t*)e->park[seq];
+  int* npark = (int*)(e->park[seq] + park_npark_off(e));
+  // class split, stable within a class
+  std::vector<int> cnt(C + 1, 0), order;
+  order.reserve(n);
+  auto cls_of = [&](int i) -> int {
+    const float v = dets[6 * i + 5];
+    return (v >= 0.f && v < (float)C && v == (float)(int)v) ? (int)v : -1;
+  };
+  for (int i = 0; i < n; i++) {
+    const int c = cls_of(i);
+    if (c >= 0) cnt[c + 1]++;
+  }
+  for (int c = 0; c < C; c++) cnt[c + 1] += cnt[c];
+  std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+  order.assign(cnt[C], 0);
+  for (int i = 0; i < n; i++) {
+    const int c = cls_of(i);
+    if (c >= 0) order[fill[c]++] = i;
+  }
+  const int m = cnt[C];
+  const size_t fs = e->cfg.emb_f64 ? 8 : 4;
+  std::vector<float> hd((size_t)6 * (m ? m : 1));
+  std::vector<char> he(reid ? fs * (size_t)(m ? m : 1) * F : 1);
+  for (int k = 0; k < m; k++) {
+    memcpy(&hd[6 * (size_t)k], dets + 6 * (size_t)order[k], 6 * sizeof(float));
+    if (reid) memcpy(&he[fs * F * (size_t)k], (const char*)embs + fs * F * (size_t)order[k], fs * F);
+  }
+  std::vector<int> hoff(2 * C);
+  for (int c = 0; c < C; c++) { hoff[2 * c] = 0; hoff[2 * c + 1] = cnt[c + 1] - cnt[c]; }
+  if (m) HIPCHK(hipMemcpyAsync(e->h_dets, hd.data(), sizeof(float) * 6 * m, hipMemcpyHostToDevice, st));
+  if (m && reid) HIPCHK(hipMemcpyAsync(e->h_embs, he.data(), fs * (size_t)m * F, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(e->h_coff, hoff.data(), sizeof(int) * 2 * C, hipMemcpyHostToDevice, st));
+  if (warp) HIPCHK(hipMemcpyAsync(e->h_warp, warp, sizeof(double) * 6, hipMemcpyHostToDevice, st));
+  for (int c = 0; c < C; c++) {
+    hipLaunchKernelGGL(class_swap_kernel, dim3(1), dim3(WG), 0, st, e->dev, seq, park, npark, C,
+                       e->cur_cls[seq], c, c == 0 ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    e->cur_cls[seq] = c;
+    const char* ep = reid ? (const char*)e->h_embs + fs * F * (size_t)cnt[c] : nullptr;
+    int rc = bx_engine_step(e, seq, 1, e->h_dets + 6 * (size_t)cnt[c], e->h_coff + 2 * c, ep,
+                            warp ? e->h_warp : nullptr, e->h_out + 8 * (size_t)cnt[c],
+                            e->h_ccnt + c, stream);
+    if (rc) return rc;
+  }
+  std::vector<int> oc(C);
+  HIPCHK(hipMemcpyAsync(oc.data(), e->h_ccnt, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  std::vector<double> ho((size_t)8 * (m ? m : 1));
+  if (m) HIPCHK(hipMemcpyAsync(ho.data(), e->h_out, sizeof(double) * 8 * m, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  int k = 0;
+  for (int c = 0; c < C; c++)
+    for (int j = 0; j < oc[c]; j++, k++)
+      if (out) memcpy(out + 8 * (size_t)k, &ho[8 * ((size_t)cnt[c] + j)], 8 * sizeof(double));
+  *n_out = k;
   int status = 0;
   HIPCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
   if (status & (1 << BX_ERR_TRACK_OVERFLOW))

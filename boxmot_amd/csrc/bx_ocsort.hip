@@ -935,6 +935,13 @@ struct bx_ocsort {
   int* h_off = nullptr;
   double* h_out = nullptr;
   int* h_cnt = nullptr;
+  // per_class host path (bx_ocsort_update_classes_host): per sequence the local -> class-global
+  // track id map and the local id counter the map covers; class offsets [C+1], counts [C]
+  std::vector<std::vector<int>> gid;
+  std::vector<int> lids;
+  int* h_coff = nullptr;
+  int* h_ccnt = nullptr;
+  int ncls_alloc = 0;
   // timing probe
   bool probe_on = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -1076,6 +1083,8 @@ int bx_ocsort_destroy(bx_ocsort* e) {
   (void)hipFree(e->h_off);
   (void)hipFree(e->h_out);
   (void)hipFree(e->h_cnt);
+  (void)hipFree(e->h_coff);
+  (void)hipFree(e->h_ccnt);
   delete e;
   return BX_OK;
 }
@@ -1087,6 +1096,10 @@ int bx_ocsort_reset(bx_ocsort* e, int seq0, int nseq, void* stream) {
   hipLaunchKernelGGL(ocsort_reset_kernel, dim3((nseq * SQO + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, e->dev, seq0, nseq);
   OCHK(hipGetLastError());
+  for (int s = seq0; s < seq0 + nseq && !e->lids.empty(); s++) {
+    e->lids[s] = 0;
+    e->gid[s].clear();
+  }
   return BX_OK;
 }
 
@@ -1117,6 +1130,82 @@ int bx_ocsort_update_host(bx_ocsort* e, int seq, const float* dets, int n, doubl
   OCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
   if (status)
     return bx_record_error(BX_ERR_TRACK_OVERFLOW, "a sequence ran out of track slots (raise track_cap)");
+  return BX_OK;
+}
+
+// per_class=True (basetracker.py:155-201): OCSort keeps all of its state in active_tracks, so
+// the decorator's per-class swap gives every class an isolated tracker — only the frame counter
+// (equal for all: each class is called once per frame) and KalmanBoxTracker.count (class-global,
+// ocsort.py:61,115-116) are shared.  Here class c is engine sequence seq0 + c and the whole frame
+// is ONE launch over the n_classes sequences; ids are then renumbered into the reference's
+// class-global order (births of class 0 first, then class 1, ...), continuing *id_count.
+int bx_ocsort_update_classes_host(bx_ocsort* e, int seq0, int n_classes, const float* dets,
+                                  int n, int* id_count, double* out, int* n_out, void* stream) {
+  if (!e || n_classes <= 0 || seq0 < 0 || seq0 + n_classes > e->dev.S || n < 0 ||
+      (n && !dets) || !n_out || !id_count)
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ocsort_update_classes_host");
+  if (n > e->dev.D) return bx_record_error(BX_ERR_CAPACITY, "detections exceed det_cap");
+  hipStream_t st = (hipStream_t)stream;
+  const int C = n_classes;
+  if (e->lids.empty()) {
+    e->lids.assign(e->dev.S, 0);
+    e->gid.assign(e->dev.S, {});
+  }
+  if (e->ncls_alloc < C) {
+    (void)hipFree(e->h_coff);
+    (void)hipFree(e->h_ccnt);
+    OCHK(hipMalloc(&e->h_coff, sizeof(int) * (C + 1)));
+    OCHK(hipMalloc(&e->h_ccnt, sizeof(int) * C));
+    e->ncls_alloc = C;
+  }
+  auto cls_of = [&](int i) -> int {
+    const float v = dets[6 * i + 5];
+    return (v >= 0.f && v < (float)C && v == (float)(int)v) ? (int)v : -1;
+  };
+  std::vector<int> cnt(C + 1, 0);
+  for (int i = 0; i < n; i++)
+    if (cls_of(i) >= 0) cnt[cls_of(i) + 1]++;
+  for (int c = 0; c < C; c++) cnt[c + 1] += cnt[c];
+  const int m = cnt[C];
+  std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+  std::vector<float> hd((size_t)6 * (m ? m : 1));
+  for (int i = 0; i < n; i++) {
+    const int c = cls_of(i);
+    if (c >= 0) memcpy(&hd[6 * (size_t)fill[c]++], dets + 6 * (size_t)i, 6 * sizeof(float));
+  }
+  if (m) OCHK(hipMemcpyAsync(e->h_dets, hd.data(), sizeof(float) * 6 * m, hipMemcpyHostToDevice, st));
+  OCHK(hipMemcpyAsync(e->h_coff, cnt.data(), sizeof(int) * (C + 1), hipMemcpyHostToDevice, st));
+  int rc = launch(e, seq0, C, e->h_dets, e->h_coff, e->h_out, e->h_ccnt, st);
+  if (rc) return rc;
+  std::vector<int> oc(C), sq((size_t)C * SQO);
+  std::vector<double> ho((size_t)8 * (m ? m : 1));
+  OCHK(hipMemcpyAsync(oc.data(), e->h_ccnt, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  if (m) OCHK(hipMemcpyAsync(ho.data(), e->h_out, sizeof(double) * 8 * m, hipMemcpyDeviceToHost, st));
+  OCHK(hipMemcpyAsync(sq.data(), e->dev.seqst + (size_t)seq0 * SQO, sizeof(int) * C * SQO,
+                      hipMemcpyDeviceToHost, st));
+  OCHK(hipStreamSynchronize(st));
+  int status = 0;
+  OCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
+  if (status)
+    return bx_record_error(BX_ERR_TRACK_OVERFLOW, "a sequence ran out of track slots (raise track_cap)");
+  int g = *id_count;
+  for (int c = 0; c < C; c++) {  // births in class order take the next class-global ids
+    std::vector<int>& map = e->gid[seq0 + c];
+    for (int l = e->lids[seq0 + c]; l < sq[(size_t)c * SQO + SO_IDS]; l++) {
+      if ((int)map.size() <= l) map.resize(l + 1, -1);
+      map[l] = g++;
+    }
+    e->lids[seq0 + c] = sq[(size_t)c * SQO + SO_IDS];
+  }
+  *id_count = g;
+  int k = 0;
+  for (int c = 0; c < C; c++)
+    for (int j = 0; j < oc[c]; j++, k++) {
+      double* o = out + 8 * (size_t)k;
+      memcpy(o, &ho[8 * ((size_t)cnt[c] + j)], 8 * sizeof(double));
+      o[4] = (double)(e->gid[seq0 + c][(int)o[4] - 1] + 1);
+    }
+  *n_out = k;
   return BX_OK;
 }
 

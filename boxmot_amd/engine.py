@@ -116,6 +116,29 @@ class Engine:
             out.ctypes.data, C.byref(m), None), "bx_engine_update_host")
         return out[: m.value].copy()
 
+    def update_classes_host(self, seq: int, dets: np.ndarray, embs: np.ndarray | None = None,
+                            warp: np.ndarray | None = None, n_classes: int = 80) -> np.ndarray:
+        """per_class=True frame of one sequence (bx_engine_update_classes_host): one update per
+        class id on that class's detections, active lists per class, lost list shared."""
+        d = np.ascontiguousarray(dets, dtype=np.float32).reshape(-1, 6)
+        n = d.shape[0]
+        e = None
+        if self.with_reid and n:
+            if embs is None:
+                raise ValueError("BoT-SORT with_reid needs embeddings (ReID inference is outside "
+                                 "the association engine)")
+            e = np.ascontiguousarray(embs, dtype=np.float64 if self.emb_f64 else np.float32)
+            if e.shape != (n, self.emb_dim):
+                raise ValueError(f"embs shape {e.shape} != ({n}, {self.emb_dim})")
+        w = None if warp is None else np.ascontiguousarray(warp, np.float64).reshape(6)
+        out = np.empty((max(n, 1), 8), np.float64)
+        m = C.c_int(0)
+        N.check(self._L.bx_engine_update_classes_host(
+            self._h, seq, d.ctypes.data if n else None, n,
+            e.ctypes.data if e is not None else None, w.ctypes.data if w is not None else None,
+            int(n_classes), out.ctypes.data, C.byref(m), None), "bx_engine_update_classes_host")
+        return out[: m.value].copy()
+
     # ---------------------------------------------------------------------------- state I/O
     def status(self) -> int:
         s = C.c_int(0)
@@ -275,6 +298,18 @@ class OcsortEngine:
                 "bx_ocsort_update_host")
         return out[: m.value].copy()
 
+    def update_classes_host(self, seq0: int, n_classes: int, dets: np.ndarray, id_count: int):
+        """per_class=True frame (bx_ocsort_update_classes_host): class c is sequence seq0 + c, one
+        launch; returns (rows with class-global ids, the advanced class-global id counter)."""
+        d = np.ascontiguousarray(dets, dtype=np.float32).reshape(-1, 6)
+        n = d.shape[0]
+        out = np.empty((max(n, 1), 8), np.float64)
+        m, g = C.c_int(0), C.c_int(int(id_count))
+        N.check(self._L.bx_ocsort_update_classes_host(
+            self._h, seq0, int(n_classes), d.ctypes.data if n else None, n, C.byref(g),
+            out.ctypes.data, C.byref(m), None), "bx_ocsort_update_classes_host")
+        return out[: m.value].copy(), g.value
+
     def status(self) -> int:
         s = C.c_int(0)
         N.check(self._L.bx_ocsort_status(self._h, C.byref(s)), "bx_ocsort_status")
@@ -424,6 +459,27 @@ class BoostEngine:
             self._h, seq, d.ctypes.data if n else None, n, None if e is None else e.ctypes.data,
             None if w is None else w.ctypes.data, out.ctypes.data, C.byref(m), None),
             "bx_boost_update_host")
+        return out[: m.value].copy()
+
+    def update_classes_host(self, seq: int, dets: np.ndarray, embs: np.ndarray | None = None,
+                            warp: np.ndarray | None = None, n_classes: int = 80) -> np.ndarray:
+        """per_class=True frame of one sequence (bx_boost_update_classes_host)."""
+        d = np.ascontiguousarray(dets, dtype=np.float32).reshape(-1, 6)
+        n = d.shape[0]
+        e = None
+        if self.emb_dim and n:
+            if embs is None:
+                raise ValueError("with_reid BoostTrack needs embeddings")
+            e = np.ascontiguousarray(embs, dtype=np.float64).reshape(n, -1)
+            if e.shape[1] != self.emb_dim:
+                raise ValueError(f"embedding dim {e.shape[1]} != engine emb_dim {self.emb_dim}")
+        w = None if warp is None else np.ascontiguousarray(warp, np.float64).reshape(6)
+        out = np.empty((max(n, 1), 8), np.float64)
+        m = C.c_int(0)
+        N.check(self._L.bx_boost_update_classes_host(
+            self._h, seq, d.ctypes.data if n else None, n, None if e is None else e.ctypes.data,
+            None if w is None else w.ctypes.data, int(n_classes), out.ctypes.data, C.byref(m),
+            None), "bx_boost_update_classes_host")
         return out[: m.value].copy()
 
     def status(self) -> int:

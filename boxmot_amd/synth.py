@@ -2,8 +2,9 @@
 
 This is the build's own scene generator (SURVEY.md §8(d) "Synthetic inputs"): ``n_obj``
 constant-velocity boxes over a 1920x1080 frame, each detected with probability ``p_det`` per
-frame, jittered box corners, confidences U(conf_lo, conf_hi), class 0, and per-identity unit
-embeddings perturbed by 0.1*N(0,1)/sqrt(F) and renormalised.
+frame, jittered box corners, confidences U(conf_lo, conf_hi), class 0 (or a fixed class per
+identity from ``classes``), and per-identity unit embeddings perturbed by 0.1*N(0,1)/sqrt(F)
+and renormalised.
 
 Every frame is generated from its own ``numpy.random.default_rng([seed, frame])`` stream, so a
 frame can be produced independently of the frames before it (bench shards, GPU-side staging and
@@ -37,6 +38,7 @@ class SyntheticScene:
     width: float = 1920.0
     height: float = 1080.0
     emb_dtype: type = np.float32
+    classes: tuple = ()  # per-identity class ids (identity k -> classes[k % len]); () = class 0
 
     def __post_init__(self):
         rng = np.random.default_rng([self.seed, 0x5CE7E])
@@ -84,6 +86,8 @@ class SyntheticScene:
         dets = np.zeros((m, 6), np.float64)
         dets[:, :4] = box
         dets[:, 4] = conf
+        if self.classes:  # per-class mode fixtures: the class is a fixed property of the identity
+            dets[:, 5] = np.asarray(self.classes, np.float64)[ids % len(self.classes)]
         embs = None
         if self.base_emb is not None:
             e = self.base_emb[ids] + 0.1 * rng.standard_normal((m, self.emb_dim)) / math.sqrt(

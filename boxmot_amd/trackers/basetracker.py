@@ -55,10 +55,6 @@ class BaseTracker:
         self._first_dets_processed = False
         if self.max_age >= self.max_obs:
             self.max_obs = self.max_age + 5
-        if per_class:
-            # The reference swaps only `active_tracks` per class while lost/removed lists stay
-            # shared (basetracker.py:154-201); that mode is not yet on the engine.
-            raise NotImplementedError("per_class tracking is not implemented by boxmot_amd yet")
 
     # -------------------------------------------------------------------- reference decorators
     @staticmethod
@@ -96,9 +92,19 @@ class BaseTracker:
 
     @staticmethod
     def per_class_decorator(update_method):
+        """basetracker.py:155-201.  With per_class=True the reference calls the update once per
+        class id 0..nr_classes-1 on that class's detections, swapping only ``active_tracks``;
+        here the whole per-class frame is one native call (``*_update_classes_host``) that
+        restates that loop on the device, so the wrapper only normalises empty input and checks
+        the detection/embedding pairing the class split asserts (basetracker.py:95-98)."""
+
         def wrapper(self, dets, img, embs=None):
             if dets is None or len(dets) == 0:
                 dets = np.empty((0, 6))
+            if self.per_class and embs is not None and dets.size:
+                assert dets.shape[0] == embs.shape[0], (
+                    "Detections and embeddings must have the same number of elements when both "
+                    "are provided")
             return update_method(self, dets=dets, img=img, embs=embs)
 
         return wrapper

@@ -110,7 +110,11 @@ class BoostTrack(BaseTracker):
                 warp = warp[:2]
             if warp.shape != (2, 3):
                 raise ValueError(f"Expected 2x3 or 3x3 matrix, got {warp.shape}")
-        out = self.engine.update_host(0, dets, embs if self.with_reid else None, warp)
+        if self.per_class:  # every class call sees every track (D10; basetracker.py:155-201)
+            out = self.engine.update_classes_host(0, dets, embs if self.with_reid else None, warp,
+                                                  n_classes=self.nr_classes)
+        else:
+            out = self.engine.update_host(0, dets, embs if self.with_reid else None, warp)
         self._engine_ids = BoostTrack._id_count = self.engine.counters(0)["id_count"]
         return out if out.shape[0] else np.empty((0, 8))
 

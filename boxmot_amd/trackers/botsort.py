@@ -78,6 +78,11 @@ class BotSort(BaseTracker):
         self.frame_count += 1
         warp = np.asarray(self.cmc.apply(img, dets), np.float64).reshape(2, 3)
         warp = None if np.array_equal(warp, np.eye(2, 3)) else warp
+        if self.per_class:  # one update per class id, lost list shared (basetracker.py:155-201)
+            # (the reference's cmc.apply runs once per class call on the frame's image; the warp
+            # object here is per frame, so every class call applies the same warp)
+            return self.engine.update_classes_host(0, dets, embs if self.with_reid else None,
+                                                   warp, n_classes=self.nr_classes)
         out = self.engine.update_host(0, dets, embs if self.with_reid else None, warp)
         return out if out.shape[0] else np.asarray([])
 

@@ -52,8 +52,13 @@ class ByteTrack(BaseTracker):
         if self._engine_ids != ByteTrack._id_count:
             self.engine.set_id_count(0, ByteTrack._id_count)
         self.frame_count += 1
-        out = self.engine.update_host(0, dets)
+        if self.per_class:  # one update per class id, lost list shared (basetracker.py:155-201)
+            out = self.engine.update_classes_host(0, dets, n_classes=self.nr_classes)
+        else:
+            out = self.engine.update_host(0, dets)
         self._engine_ids = ByteTrack._id_count = self.engine.counters(0)["id_count"]
+        if self.per_class:  # np.vstack of the classes' rows, else np.empty((0, 8))
+            return out
         # the reference returns np.asarray([]) (shape (0,)) when nothing is output
         return out if out.shape[0] else np.asarray([])
 

@@ -38,8 +38,10 @@ class OcSort(BaseTracker):
         self.Q_xy_scaling = Q_xy_scaling
         self.Q_s_scaling = Q_s_scaling
         OcSort._id_count = 0
+        # per_class: class c is engine sequence c (OCSort's state is all in the swapped
+        # active_tracks, so classes are isolated trackers; basetracker.py:155-201)
         self.engine = OcsortEngine(
-            n_seq=1, track_cap=track_cap, det_cap=det_cap,
+            n_seq=self.nr_classes if per_class else 1, track_cap=track_cap, det_cap=det_cap,
             params=OcsortParams(min_conf=min_conf, det_thresh=det_thresh, max_age=max_age,
                                 min_hits=min_hits, asso_threshold=asso_threshold,
                                 delta_t=delta_t, inertia=inertia, use_byte=use_byte,
@@ -54,11 +56,16 @@ class OcSort(BaseTracker):
         self.check_inputs(dets, img)
         if not self._frame_latched and self._first_frame_processed:
             # the engine's asso_func / centroid frame size follow BaseTracker's first-frame latch
-            self.engine.set_frame_size(0, self.w, self.h)
+            for q in range(self.engine.n_seq):
+                self.engine.set_frame_size(q, self.w, self.h)
             self._frame_latched = True
+        self.frame_count += 1
+        if self.per_class:  # one launch over the class sequences, ids renumbered class-globally
+            out, OcSort._id_count = self.engine.update_classes_host(0, self.nr_classes, dets,
+                                                                    OcSort._id_count)
+            return out
         if self._engine_ids != OcSort._id_count:
             self.engine.set_id_count(0, OcSort._id_count)
-        self.frame_count += 1
         out = self.engine.update_host(0, dets)
         self._engine_ids = OcSort._id_count = self.engine.counters(0)["id_count"]
         return out if out.shape[0] else np.array([])

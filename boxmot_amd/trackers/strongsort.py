@@ -43,7 +43,11 @@ class StrongSort:
                  handle_occlusions=False, crowd_detection=True, track_cap: int = 512,
                  det_cap: int = 256, vec_cap: int = 32):
         if per_class:
-            raise NotImplementedError("per_class tracking is not implemented by boxmot_amd yet")
+            # create_tracker pops per_class for StrongSort (tracker_zoo.py:84-85); constructed
+            # directly with per_class=True the reference fails in its first update (StrongSort
+            # never runs BaseTracker.__init__, so the decorator's nr_classes does not exist)
+            raise NotImplementedError("StrongSort has no per-class mode (the reference's "
+                                      "create_tracker drops per_class for it)")
         if handle_occlusions:
             raise NotImplementedError(
                 "handle_occlusions=True (OcclusionAwareTracker) is not on the engine: the fork's "

@@ -104,6 +104,16 @@ int bx_engine_step(bx_engine *e, int seq0, int nseq, const float *dets, const in
 int bx_engine_update_host(bx_engine *e, int seq, const float *dets, int n, const void *embs,
                           const double *warp, double *out, int *n_out, void *stream);
 
+/* per_class=True (BaseTracker.per_class_decorator, boxmot/trackers/basetracker.py:155-201) for
+ * one sequence: one update per class id 0..n_classes-1 (nr_classes = 80 in the reference) on the
+ * detections whose float32 class equals it (det_ind then indexes that subset, as in the
+ * reference), each with the class's own active list while the lost list and the id counter stay
+ * shared, and the frame counter held across the frame's class calls; rows stacked in class
+ * order.  Arguments as bx_engine_update_host; n_classes must stay the same for an engine. */
+int bx_engine_update_classes_host(bx_engine *e, int seq, const float *dets, int n,
+                                  const void *embs, const double *warp, int n_classes,
+                                  double *out, int *n_out, void *stream);
+
 /* Stage timing probe (benchmarks): while enabled, bx_engine_step records a HIP event pair
  * around every launch of pipeline stage `stage` on its stream; bx_engine_probe_read
  * synchronises, returns the summed milliseconds and the number of timed launches, and clears

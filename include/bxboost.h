@@ -75,6 +75,14 @@ int bx_boost_step(bx_boost *e, int seq0, int nseq, const float *dets, const int3
 int bx_boost_update_host(bx_boost *e, int seq, const float *dets, int n, const double *embs,
                          const double *warp, double *out, int *n_out, void *stream);
 /* Latched device status (BX_OK, BX_ERR_TRACK_OVERFLOW or BX_ERR_CAPACITY). */
+/* per_class=True (boxmot/trackers/basetracker.py:155-201) for one sequence: one update per class
+ * id 0..n_classes-1 on that class's detections with the frame counter held, rows stacked in class
+ * order (det_ind indexes the class's subset).  BoostTrack keeps its tracks outside the swapped
+ * active_tracks, so every class call sees every track.  Arguments as
+ * bx_boost_update_host. */
+int bx_boost_update_classes_host(bx_boost *e, int seq, const float *dets, int n,
+                                 const double *embs, const double *warp, int n_classes,
+                                 double *out, int *n_out, void *stream);
 int bx_boost_status(bx_boost *e, int *status);
 int bx_boost_counters_host(bx_boost *e, int seq, int *frame_count, int *id_count, int *n_tracks);
 /* KalmanBoxTracker.count is class-global in the reference (boosttrack.py:50,53-56, never reset

@@ -66,6 +66,14 @@ int bx_ocsort_step(bx_ocsort *e, int seq0, int nseq, const float *dets, const in
  * synchronises.  out must hold n rows. */
 int bx_ocsort_update_host(bx_ocsort *e, int seq, const float *dets, int n, double *out,
                           int *n_out, void *stream);
+/* per_class=True (boxmot/trackers/basetracker.py:155-201): class c (0..n_classes-1, the
+ * reference's nr_classes = 80) is engine sequence seq0 + c — OCSort's whole state lives in the
+ * active list the decorator swaps, so classes are isolated trackers — and the frame is one launch
+ * over those sequences.  Output rows are stacked in class order (det_ind indexes the class's
+ * subset) with ids renumbered in the reference's class-global birth order: *id_count is the
+ * class-global KalmanBoxTracker.count, read and advanced.  out must hold n rows. */
+int bx_ocsort_update_classes_host(bx_ocsort *e, int seq0, int n_classes, const float *dets,
+                                  int n, int *id_count, double *out, int *n_out, void *stream);
 /* Latched device status (BX_OK, BX_ERR_TRACK_OVERFLOW or BX_ERR_CAPACITY). */
 int bx_ocsort_status(bx_ocsort *e, int *status);
 int bx_ocsort_counters_host(bx_ocsort *e, int seq, int *frame_count, int *id_count,

@@ -76,6 +76,10 @@ int bxo_update(bxo_tracker *t, const double *dets, int n, const void *embs, int 
 int bxo_id_count(const bxo_tracker *t);
 int bxo_frame_count(const bxo_tracker *t);
 void bxo_free(bxo_tracker *t);
+/* per_class mode (basetracker.py:155-201): swap in class `cls`'s active list (the lost list and
+ * the id counter stay shared) and hold the frame counter across a frame's class calls */
+void bxo_select_class(bxo_tracker *t, int cls);
+void bxo_set_frame_count(bxo_tracker *t, int fc);
 
 /* ----------------------------------------------------------------------------------------- */
 /* StrongSort NearestNeighborDistanceMetric.distance, cosine (sort/linear_assignment.py:595-618):
@@ -96,6 +100,7 @@ void bxo_ocsort_set_asso(bxo_ocsort *o, int kind, double w, double h);
 /* one pair of AssociationFunction.<kind>_batch */
 double bxo_pair_cost(int kind, const double *a, const double *b, double w, double h);
 int bxo_ocsort_id_count(bxo_ocsort *o);
+void bxo_ocsort_set_id_count(bxo_ocsort *o, int c); /* KalmanBoxTracker.count is class-global */
 /* track list in list order: ids [cap], XYSR means x [cap][7], covariances P [cap][49] */
 int bxo_ocsort_tracks(bxo_ocsort *o, int cap, int *ids, double *x, double *P);
 /* dets[n,6] float64 (float32-rounded); out[M,8]; returns M or -2 if out_cap is too small */
@@ -115,6 +120,7 @@ bxo_boost *bxo_boost_new(const bxo_boost_params *p);
 void bxo_boost_free(bxo_boost *b);
 int bxo_boost_id_count(const bxo_boost *b);
 void bxo_boost_set_id_count(bxo_boost *b, int c);
+void bxo_boost_set_frame_count(bxo_boost *b, int fc); /* per_class: held across class calls */
 /* track list in list order: ids [cap], means x [cap][8], covariances P [cap][64] */
 int bxo_boost_tracks(const bxo_boost *b, int cap, int *ids, double *x, double *P);
 /* dets[n,6] float64 (float32-rounded); embs [n][emb_dim] float64 or NULL; warp[6] 2x3 CMC

@@ -327,6 +327,7 @@ int bxo_boost_state_set(bxo_boost *b, int n, const int *ids, const double *x, co
     return found;
 }
 void bxo_boost_set_id_count(bxo_boost *b, int c) { b->id_count = c; }
+void bxo_boost_set_frame_count(bxo_boost *b, int fc) { b->frame_count = fc; }
 
 int bxo_boost_tracks(const bxo_boost *b, int cap, int *ids, double *x, double *P) {
     for (int i = 0; i < b->n && i < cap; i++) {

@@ -626,6 +626,7 @@ void bxo_ocsort_free(bxo_ocsort *o) {
 }
 
 int bxo_ocsort_id_count(bxo_ocsort *o) { return o->id_count; }
+void bxo_ocsort_set_id_count(bxo_ocsort *o, int c) { o->id_count = c; }
 
 /* host edit of trk.kf.x / trk.kf.P by id; returns the number of ids found */
 int bxo_ocsort_state_set(bxo_ocsort *o, int n, const int *ids, const double *x, const double *P) {

@@ -64,6 +64,9 @@ struct bxo_tracker {
     unsigned stamp;
     List active, lost;
     int emb_dim, f64;
+    /* per_class mode: the other classes' active lists, parked while `cur_cls` runs */
+    List *parked;
+    int nparked, cur_cls;
 };
 
 /* ---- feature helpers: values held in double, rounded to float32 after every op in f32 mode - */
@@ -366,8 +369,31 @@ int bxo_state_set(bxo_tracker *T, int n, const int *ids, const double *mean, con
 
 int bxo_id_count(const bxo_tracker *T) { return T->id_count; }
 int bxo_frame_count(const bxo_tracker *T) { return T->frame_count; }
+void bxo_set_frame_count(bxo_tracker *T, int fc) { T->frame_count = fc; }
+
+/* BaseTracker.per_class_decorator (basetracker.py:181-192): `self.active_tracks =
+ * self.per_class_active_tracks[cls_id]` before the class's update, saved back after it.  Only
+ * the active list is swapped: lost_stracks, removed_stracks and the id counter stay shared. */
+void bxo_select_class(bxo_tracker *T, int cls) {
+    if (cls == T->cur_cls) return;
+    const int need = (cls > T->cur_cls ? cls : T->cur_cls) + 1;
+    if (need > T->nparked) {
+        T->parked = (List *)realloc(T->parked, sizeof(List) * need);
+        memset(T->parked + T->nparked, 0, sizeof(List) * (need - T->nparked));
+        T->nparked = need;
+    }
+    T->parked[T->cur_cls] = T->active;
+    T->active = T->parked[cls];
+    memset(&T->parked[cls], 0, sizeof(List));
+    T->cur_cls = cls;
+}
 
 void bxo_free(bxo_tracker *T) {
+    for (int c = 0; c < T->nparked; c++) { /* parked lists hold tracks of no other list */
+        for (int i = 0; i < T->parked[c].n; i++) free_trk(T->parked[c].v[i]);
+        lfree(&T->parked[c]);
+    }
+    free(T->parked);
     unsigned s = ++T->stamp;
     for (int i = 0; i < T->active.n; i++) T->active.v[i]->stamp = s;
     for (int i = 0; i < T->lost.n; i++)

@@ -160,6 +160,10 @@ def lib():
                                  _dp, C.c_int]
         L.bxo_id_count.argtypes = [C.c_void_p]
         L.bxo_frame_count.argtypes = [C.c_void_p]
+        L.bxo_select_class.argtypes = [C.c_void_p, C.c_int]
+        L.bxo_set_frame_count.argtypes = [C.c_void_p, C.c_int]
+        L.bxo_ocsort_set_id_count.argtypes = [C.c_void_p, C.c_int]
+        L.bxo_boost_set_frame_count.argtypes = [C.c_void_p, C.c_int]
         L.bxo_free.argtypes = [C.c_void_p]
         L.bxo_ocsort_new.argtypes = [C.c_double, C.c_double, C.c_int, C.c_int, C.c_double,
                                      C.c_int, C.c_double, C.c_int, C.c_double, C.c_double]
@@ -320,12 +324,26 @@ def linear_assignment(cost, thresh):
     return m[: 2 * nm.value].reshape(-1, 2), ua[: nua.value], ub[: nub.value]
 
 
+NR_CLASSES = 80  # BaseTracker(nr_classes=80) (basetracker.py:23)
+
+
 class OracleTracker:
-    """Per-sequence CPU oracle tracker with the reference ``update`` contract."""
+    """Per-sequence CPU oracle tracker with the reference ``update`` contract.
+
+    ``per_class=True`` restates BaseTracker.per_class_decorator (basetracker.py:155-201): one
+    update per class id 0..79 on that class's detections with the frame counter held; ByteTrack /
+    BoT-SORT swap only the active list (lost list and ids shared), OCSort runs one tracker per
+    class with the class-global id counter, BoostTrack calls its one tracker per class (D10)."""
 
     def __init__(self, kind: str, **p):
         L = lib()
         self.kind = kind
+        self.per_class = bool(p.pop("per_class", False))
+        if self.per_class and kind == "strongsort":
+            raise NotImplementedError("StrongSort has no per-class mode (tracker_zoo.py:85-86)")
+        self._p = dict(p)
+        self._oc = {}  # OCSort per-class trackers
+        self._frame = 0
         if kind == "bytetrack":
             self.h = L.bxo_bytetrack_new(
                 p.get("min_conf", 0.1), p.get("track_thresh", 0.45), p.get("match_thresh", 0.8),
@@ -360,6 +378,48 @@ class OracleTracker:
         self._cap = 1024
 
     def update(self, dets, embs=None, warp=None):
+        if self.per_class:
+            return self._update_per_class(dets, embs, warp)
+        return self._update_one(dets, embs, warp)
+
+    def _update_per_class(self, dets, embs, warp):
+        L = lib()
+        dets = np.asarray(dets, np.float64).reshape(-1, 6)
+        fc = self._frame
+        outs = []
+        for c in range(NR_CLASSES):
+            idx = np.flatnonzero(dets[:, 5].astype(np.float32) == c)
+            cd = dets[idx]
+            ce = None if embs is None else np.asarray(embs)[idx]
+            if self.kind == "ocsort":
+                if c not in self._oc:
+                    self._oc[c] = OracleTracker("ocsort", **self._p)
+                    self._oc[c]._frame_sync(fc)
+                t = self._oc[c]
+                L.bxo_ocsort_set_id_count(t.h, self._ids_shared())
+                o = t._update_one(cd, ce, warp)
+                self._oc_ids = L.bxo_ocsort_id_count(t.h)
+            else:
+                if self.kind == "boosttrack":
+                    L.bxo_boost_set_frame_count(self.h, fc)
+                else:
+                    L.bxo_select_class(self.h, c)
+                    L.bxo_set_frame_count(self.h, fc)
+                o = self._update_one(cd, ce, warp)
+            if o.size:
+                outs.append(o)
+        self._frame = fc + 1
+        return np.vstack(outs) if outs else np.empty((0, 8))
+
+    def _ids_shared(self):
+        return getattr(self, "_oc_ids", 0)
+
+    def _frame_sync(self, fc):
+        """A per-class OCSort tracker created at frame fc+1 has seen fc (empty) frames before."""
+        for _ in range(fc):
+            self._update_one(np.empty((0, 6)), None, None)
+
+    def _update_one(self, dets, embs=None, warp=None):
         dets = np.ascontiguousarray(np.asarray(dets, np.float64).reshape(-1, 6))
         n = dets.shape[0]
         e_ptr, f, is64 = None, 0, 0

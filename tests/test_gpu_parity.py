@@ -340,6 +340,50 @@ def test_tracker_fixture_parity(torch_cuda, path):
                     conf_atol=1e-9 if kind == "boosttrack" else None)
 
 
+PER_CLASS_CASES = [
+    ("bytetrack", dict(min_conf=0.1, track_thresh=0.6, match_thresh=0.9, track_buffer=30),
+     dict(n_obj=60, seed=31, layout="crowded", conf_lo=0.05, classes=(0, 1, 1, 3, 79, 80))),
+    ("botsort", dict(track_high_thresh=0.6, new_track_thresh=0.7, match_thresh=0.8),
+     dict(n_obj=56, seed=32, layout="crowded", emb_dim=48, conf_lo=0.05, classes=(2, 0, 5))),
+    ("ocsort", dict(det_thresh=0.6, max_age=30, min_hits=3, inertia=0.1),
+     dict(n_obj=56, seed=33, layout="crowded", conf_lo=0.2, p_det=0.85, classes=(0, 7, 3))),
+    ("boosttrack", dict(max_age=60, min_hits=3, det_thresh=0.6, use_rich_s=True, use_sb=True,
+                        use_vt=True, with_reid=True),
+     dict(n_obj=40, seed=34, layout="crowded", emb_dim=32, emb_dtype=np.float64, conf_lo=0.3,
+          p_det=0.9, classes=(1, 0))),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,args,skw", PER_CLASS_CASES, ids=[c[0] for c in PER_CLASS_CASES])
+def test_per_class_vs_oracle(torch_cuda, kind, args, skw):
+    """per_class=True (basetracker.py:155-201) through the drop-ins' native per-class paths:
+    every frame bitwise equal to the oracle's restated class loop (ByteTrack/BoT-SORT with the
+    shared lost list, OCSort isolated per class with class-global ids, BoostTrack's D10 sharing);
+    BoT-SORT also on CMC-warp frames."""
+    from boxmot_amd.synth import SyntheticCMC, SyntheticScene, synth_warp
+
+    args = dict(args, per_class=True)
+    tr = make_dropin(kind, args)
+    orc = po.OracleTracker(kind, **args)
+    sc = SyntheticScene(**skw)
+    warp = kind == "botsort"
+    if warp:
+        tr.cmc = SyntheticCMC(lambda t: synth_warp(32, t))
+    img = np.zeros((1080, 1920, 3), np.uint8)
+    rows = 0
+    for t in range(1, 51):
+        d, e, _ = sc.frame(t)
+        if warp:
+            tr.cmc.t = t
+        o = tr.update(d, img, e) if e is not None else tr.update(d, img)
+        oo = orc.update(d, e, synth_warp(32, t) if warp else None)
+        np.testing.assert_array_equal(np.asarray(o, np.float64).reshape(-1, 8), oo,
+                                      err_msg=f"{kind} frame {t}")
+        rows += oo.shape[0]
+    assert rows > 0
+
+
 def run_batched(torch, kind, scenes, n_frames, args, emb_dim=0, seq_frames=None, warps=None):
     """Drive an Engine with len(scenes) sequences in one launch per frame (``warps(s, t)``: the
     2x3 CMC warp of sequence s at frame t, BoT-SORT's multi_gmc)."""
