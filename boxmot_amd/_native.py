@@ -129,7 +129,9 @@ EXPORTS = [
     "bx_ss_tracks_host", "bx_ss_frame_stats_host", "bx_ss_probe", "bx_ss_probe_read",
     "bx_txt_shape", "bx_txt_read", "bx_mot_format", "bx_mot_write",
     "bx_engine_update_classes_host", "bx_ocsort_update_classes_host",
-    "bx_boost_update_classes_host",
+    "bx_boost_update_classes_host", "bx_kf_xysr_initiate", "bx_kf_xysr_predict",
+    "bx_kf_xysr_update", "bx_kf_boost_initiate", "bx_kf_boost_predict", "bx_kf_boost_update",
+    "bx_kf_boost_mh_dist",
 ]
 
 _vp, _ip, _dp, _fp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_float)
@@ -214,6 +216,13 @@ _SIGS = {
                                       C.c_int),
     "bx_boost_update_classes_host": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp, C.c_int, _vp, _ip,
                                       _vp], C.c_int),
+    "bx_kf_xysr_initiate": ([C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_kf_xysr_predict": ([C.c_int, _vp, _vp, C.c_double, C.c_double, _vp], C.c_int),
+    "bx_kf_xysr_update": ([C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_kf_boost_initiate": ([C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_kf_boost_predict": ([C.c_int, _vp, _vp, _vp], C.c_int),
+    "bx_kf_boost_update": ([C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_kf_boost_mh_dist": ([C.c_int, _vp, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
 }
 
 _lib = None

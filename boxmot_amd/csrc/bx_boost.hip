@@ -1020,6 +1020,53 @@ __global__ void boost_reset_kernel(BstDev g, int seq0, int nseq) {
   if (k < nseq * SQB) g.seqst[(size_t)seq0 * SQB + k] = 0;
 }
 
+// Op-level BoostTrack filter (bx_kf_boost_*) with the frame kernel's octet code: op 0 initiate
+// (kalmanfilter.py:47-73 from z = convert_bbox_to_z), 1 predict (:75-107), 2 update (:127-157).
+__global__ __launch_bounds__(256) void kf_boost_kernel(int op, int n, double* __restrict__ x,
+                                                       double* __restrict__ P,
+                                                       const double* __restrict__ z) {
+  const int gt = blockIdx.x * 256 + threadIdx.x;
+  const int k = gt >> 3, r = gt & 7;
+  if (k >= n) return;  // whole octets leave together
+  double* xk = x + 8 * (size_t)k;
+  double* Pk = P + 64 * (size_t)k;
+  if (op == 0) {
+    xk[r] = r < 4 ? z[4 * (size_t)k + r] : 0.0;
+    for (int j = 0; j < 8; j++) Pk[8 * r + j] = j == r ? (r < 4 ? 10.0 : 10000.0) : 0.0;
+    return;
+  }
+  double xr = xk[r], Pr[8];
+  for (int j = 0; j < 8; j++) Pr[j] = Pk[8 * r + j];
+  if (op == 1) {
+    okf_predict(r, xr, Pr);
+  } else {
+    const double* zk = z + 4 * (size_t)k;
+    const double zz[4] = {zk[0], zk[1], zk[2], zk[3]};
+    okf_update(r, xr, Pr, zz);
+  }
+  xk[r] = xr;
+  for (int j = 0; j < 8; j++) Pk[8 * r + j] = Pr[j];
+}
+
+// get_mh_dist_matrix (boosttrack.py:356-369): thread per (detection, track); the same sum order
+// as the frame kernel's mh_dist (numpy's in-order 4-term sum)
+__global__ __launch_bounds__(256) void kf_boost_mh_kernel(int nd, const double* __restrict__ dets,
+                                                          int nt, const double* __restrict__ x,
+                                                          const double* __restrict__ P,
+                                                          double* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)nd * nt) return;
+  const int d = (int)(i / nt), t = (int)(i % nt);
+  double z[4];
+  bbox_to_z(dets + 4 * (size_t)d, z);
+  double s = 0.0;
+  for (int q = 0; q < 4; q++) {
+    const double v = z[q] - x[8 * (size_t)t + q];
+    s += v * v * (1.0 / P[64 * (size_t)t + 9 * q]);
+  }
+  out[i] = s;
+}
+
 }  // namespace
 
 // per_class: the frame counter is held across a frame's class calls (basetracker.py:177,186:
@@ -1356,6 +1403,42 @@ int bx_boost_update_classes_host(bx_boost* e, int seq, const float* dets, int n,
   if (status)
     return bx_record_error(status, status == BX_ERR_CAPACITY ? "detections exceed det_cap"
                                                              : "a sequence ran out of track slots (raise track_cap)");
+  return BX_OK;
+}
+
+int bx_kf_boost_initiate(int n, const double* z, double* x, double* P, void* stream) {
+  if (n < 0 || (n && (!z || !x || !P))) return bx_record_error(BX_ERR_INVALID, "bad arguments");
+  if (!n) return BX_OK;
+  hipLaunchKernelGGL(kf_boost_kernel, dim3((8 * n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     0, n, x, P, z);
+  BCHK(hipGetLastError());
+  return BX_OK;
+}
+int bx_kf_boost_predict(int n, double* x, double* P, void* stream) {
+  if (n < 0 || (n && (!x || !P))) return bx_record_error(BX_ERR_INVALID, "bad arguments");
+  if (!n) return BX_OK;
+  hipLaunchKernelGGL(kf_boost_kernel, dim3((8 * n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     1, n, x, P, (const double*)nullptr);
+  BCHK(hipGetLastError());
+  return BX_OK;
+}
+int bx_kf_boost_update(int n, double* x, double* P, const double* z, void* stream) {
+  if (n < 0 || (n && (!z || !x || !P))) return bx_record_error(BX_ERR_INVALID, "bad arguments");
+  if (!n) return BX_OK;
+  hipLaunchKernelGGL(kf_boost_kernel, dim3((8 * n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     2, n, x, P, z);
+  BCHK(hipGetLastError());
+  return BX_OK;
+}
+int bx_kf_boost_mh_dist(int nd, const double* dets, int nt, const double* x, const double* P,
+                        double* out, void* stream) {
+  if (nd < 0 || nt < 0 || ((size_t)nd * nt && (!dets || !x || !P || !out)))
+    return bx_record_error(BX_ERR_INVALID, "bad arguments");
+  const size_t m = (size_t)nd * nt;
+  if (!m) return BX_OK;
+  hipLaunchKernelGGL(kf_boost_mh_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, nd, dets, nt, x, P, out);
+  BCHK(hipGetLastError());
   return BX_OK;
 }
 

@@ -922,6 +922,45 @@ __global__ void ocsort_reset_kernel(OcsDev g, int seq0, int nseq) {
 
 thread_local std::string g_ocs_err;
 
+// Op-level XYSR filter (bx_kf_xysr_*): one octet per track running the frame kernel's octet code
+// (kfo_predict / kfo_update), so the op and the tracker are bit-identical.  op 0 initiate
+// (ocsort.py:83-111 from xyxy boxes), 1 predict (ocsort.py:177-180: the s + ds <= 0 clamp, then
+// F/Q of the tracker), 2 update (xysr_kf.py:256-283 with R = diag(1, 1, 10, 10)).
+__global__ __launch_bounds__(256) void kf_xysr_kernel(int op, int n, double* __restrict__ x,
+                                                      double* __restrict__ P,
+                                                      const double* __restrict__ arg, double q_xy,
+                                                      double q_s) {
+  const int gt = blockIdx.x * 256 + threadIdx.x;
+  const int k = gt >> 3, r = gt & 7, rr = r < 7 ? r : 6;
+  if (k >= n) return;  // whole octets leave together
+  double* xk = x + 7 * (size_t)k;
+  double* Pk = P + 49 * (size_t)k;
+  if (op == 0) {
+    const double* b = arg + 4 * (size_t)k;
+    const double w = b[2] - b[0], h = b[3] - b[1];
+    const double z[4] = {b[0] + w / 2.0, b[1] + h / 2.0, w * h, w / (h + 1e-6)};
+    if (r < 7) {
+      xk[r] = r < 4 ? z[r] : 0.0;
+      for (int j = 0; j < 7; j++) Pk[7 * r + j] = j == r ? (r < 4 ? 10.0 : 10000.0) : 0.0;
+    }
+    return;
+  }
+  KfRow kr;
+  row_load(xk, Pk, rr, kr);
+  if (op == 1) {
+    OcsDev g;
+    g.q_xy = q_xy;
+    g.q_s = q_s;
+    if (rr == 6 && xk[6] + xk[2] <= 0) kr.x *= 0.0;
+    kfo_predict(g, rr, kr);
+  } else {
+    const double* zk = arg + 4 * (size_t)k;
+    const double z[4] = {zk[0], zk[1], zk[2], zk[3]};
+    kfo_update(rr, kr, z);
+  }
+  row_store(xk, Pk, r, kr);
+}
+
 }  // namespace
 
 struct bx_ocsort {
@@ -1207,6 +1246,28 @@ int bx_ocsort_update_classes_host(bx_ocsort* e, int seq0, int n_classes, const f
     }
   *n_out = k;
   return BX_OK;
+}
+
+static int kf_xysr_launch(int op, int n, double* x, double* P, const double* arg, double q_xy,
+                          double q_s, void* stream) {
+  if (n < 0 || !x || !P || (op != 1 && n && !arg))
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_kf_xysr_*");
+  if (!n) return BX_OK;
+  hipLaunchKernelGGL(kf_xysr_kernel, dim3((8 * n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     op, n, x, P, arg, q_xy, q_s);
+  OCHK(hipGetLastError());
+  return BX_OK;
+}
+
+int bx_kf_xysr_initiate(int n, const double* bbox, double* x, double* P, void* stream) {
+  return kf_xysr_launch(0, n, x, P, bbox, 0.0, 0.0, stream);
+}
+int bx_kf_xysr_predict(int n, double* x, double* P, double q_xy_scaling, double q_s_scaling,
+                       void* stream) {
+  return kf_xysr_launch(1, n, x, P, nullptr, q_xy_scaling, q_s_scaling, stream);
+}
+int bx_kf_xysr_update(int n, double* x, double* P, const double* z, void* stream) {
+  return kf_xysr_launch(2, n, x, P, z, 0.0, 0.0, stream);
 }
 
 int bx_ocsort_status(bx_ocsort* e, int* status) {

@@ -83,6 +83,19 @@ int bx_boost_update_host(bx_boost *e, int seq, const float *dets, int n, const d
 int bx_boost_update_classes_host(bx_boost *e, int seq, const float *dets, int n,
                                  const double *embs, const double *warp, int n_classes,
                                  double *out, int *n_out, void *stream);
+/* Op-level BoostTrack filter (device arrays, async on `stream`), the frame kernel's octet code.
+ * x [n][8], P [n][8][8] row-major, z [n][4] = convert_bbox_to_z (x, y, h, w/(h+1e-6)).
+ *   bx_kf_boost_initiate  KalmanFilter.__init__   boxmot/trackers/boosttrack/kalmanfilter.py:47-73
+ *   bx_kf_boost_predict   KalmanFilter.predict    kalmanfilter.py:75-107 (F(PF^T) + Q, constant Q)
+ *   bx_kf_boost_update    KalmanFilter.update     kalmanfilter.py:127-157 (cho_factor / cho_solve,
+ *                         R = diag(1, 1, 10, 0.01))
+ *   bx_kf_boost_mh_dist   BoostTrack.get_mh_dist_matrix  boosttrack.py:356-369: detections
+ *                         dets [nd][4] xyxy against the n filters -> out [nd][nt] */
+int bx_kf_boost_initiate(int n, const double *z, double *x, double *P, void *stream);
+int bx_kf_boost_predict(int n, double *x, double *P, void *stream);
+int bx_kf_boost_update(int n, double *x, double *P, const double *z, void *stream);
+int bx_kf_boost_mh_dist(int nd, const double *dets, int nt, const double *x, const double *P,
+                        double *out, void *stream);
 int bx_boost_status(bx_boost *e, int *status);
 int bx_boost_counters_host(bx_boost *e, int seq, int *frame_count, int *id_count, int *n_tracks);
 /* KalmanBoxTracker.count is class-global in the reference (boosttrack.py:50,53-56, never reset

@@ -74,6 +74,19 @@ int bx_ocsort_update_host(bx_ocsort *e, int seq, const float *dets, int n, doubl
  * class-global KalmanBoxTracker.count, read and advanced.  out must hold n rows. */
 int bx_ocsort_update_classes_host(bx_ocsort *e, int seq0, int n_classes, const float *dets,
                                   int n, int *id_count, double *out, int *n_out, void *stream);
+/* Op-level XYSR filter of OCSort's KalmanBoxTracker (device arrays, async on `stream`), the
+ * same octet code as the frame kernel.  x [n][7], P [n][7][7] row-major.
+ *   bx_kf_xysr_initiate  KalmanBoxTracker.__init__ filter setup   ocsort.py:83-111
+ *                        (x[:4] = xyxy2xysr(bbox [n][4]) (P1), P = 10*diag(1,1,1,1,1e3,1e3,1e3))
+ *   bx_kf_xysr_predict   KalmanBoxTracker.predict's filter part  ocsort.py:177-180 +
+ *                        KalmanFilterXYSR.predict  xysr_kf.py:137-175 (Q[4:6,4:6] *= q_xy,
+ *                        Q[-1,-1] *= q_s; the s + ds <= 0 velocity clamp first)
+ *   bx_kf_xysr_update    KalmanFilterXYSR.update's filter part xysr_kf.py:256-283 (R = diag(1,1,
+ *                        10,10), explicit inv(S), Joseph form; z [n][4]; no history / ORU) */
+int bx_kf_xysr_initiate(int n, const double *bbox, double *x, double *P, void *stream);
+int bx_kf_xysr_predict(int n, double *x, double *P, double q_xy_scaling, double q_s_scaling,
+                       void *stream);
+int bx_kf_xysr_update(int n, double *x, double *P, const double *z, void *stream);
 /* Latched device status (BX_OK, BX_ERR_TRACK_OVERFLOW or BX_ERR_CAPACITY). */
 int bx_ocsort_status(bx_ocsort *e, int *status);
 int bx_ocsort_counters_host(bx_ocsort *e, int seq, int *frame_count, int *id_count,

@@ -106,6 +106,10 @@ int bxo_ocsort_tracks(bxo_ocsort *o, int cap, int *ids, double *x, double *P);
 /* dets[n,6] float64 (float32-rounded); out[M,8]; returns M or -2 if out_cap is too small */
 int bxo_ocsort_update(bxo_ocsort *o, const double *dets, int n, double *out, int out_cap);
 double bxo_acos(double x);
+/* op-level XYSR filter of KalmanBoxTracker (mirrors bx_kf_xysr_*): x [n][7], P [n][49] */
+void bxo_kf_xysr_initiate(int n, const double *bbox, double *x, double *P);
+void bxo_kf_xysr_predict(int n, double *x, double *P, double q_xy, double q_s);
+void bxo_kf_xysr_update(int n, double *x, double *P, const double *z);
 
 /* BoostTrack / BoostTrack++ (trackers/boosttrack/boosttrack.py:123-456, assoc.py,            */
 /* kalmanfilter.py), as shipped (see bxo_boost.c for the fixed orders).                        */
@@ -128,6 +132,12 @@ int bxo_boost_tracks(const bxo_boost *b, int cap, int *ids, double *x, double *P
 int bxo_boost_update(bxo_boost *b, const double *dets, int n, const double *embs, int emb_dim,
                      const double *warp, double *out, int out_cap);
 double bxo_exp(double x);
+/* op-level BoostTrack filter (mirrors bx_kf_boost_*): x [n][8], P [n][64], z [n][4] */
+void bxo_kf_boost_initiate(int n, const double *z, double *x, double *P);
+void bxo_kf_boost_predict(int n, double *x, double *P);
+void bxo_kf_boost_update(int n, double *x, double *P, const double *z);
+void bxo_kf_boost_mh_dist(int nd, const double *dets, int nt, const double *x, const double *P,
+                          double *out);
 double bxo_pow15(double x);
 
 /* StrongSort, the fork's "enhanced" tracker (trackers/strongsort/strongsort.py:17-232, sort/...)

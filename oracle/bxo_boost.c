@@ -256,6 +256,49 @@ static double mh_dist(const double *det, const double *x, const double *sinv) {
     return s;
 }
 
+/* Op-level entries (mirrors of bx_kf_boost_*): KalmanFilter.__init__ (kalmanfilter.py:47-73)
+ * from a measurement z = convert_bbox_to_z, predict (:75-107), update (:127-157), and
+ * get_mh_dist_matrix (boosttrack.py:356-369) of detections [nd][4] xyxy against tracks. */
+void bxo_kf_boost_initiate(int n, const double *z, double *x, double *P) {
+    for (int k = 0; k < n; k++) {
+        bkf b;
+        bkf_init(&b, z + 4 * k);
+        memcpy(x + 8 * k, b.x, sizeof b.x);
+        memcpy(P + 64 * k, b.P, sizeof b.P);
+    }
+}
+
+void bxo_kf_boost_predict(int n, double *x, double *P) {
+    for (int k = 0; k < n; k++) {
+        bkf b;
+        memcpy(b.x, x + 8 * k, sizeof b.x);
+        memcpy(b.P, P + 64 * k, sizeof b.P);
+        bkf_predict(&b);
+        memcpy(x + 8 * k, b.x, sizeof b.x);
+        memcpy(P + 64 * k, b.P, sizeof b.P);
+    }
+}
+
+void bxo_kf_boost_update(int n, double *x, double *P, const double *z) {
+    for (int k = 0; k < n; k++) {
+        bkf b;
+        memcpy(b.x, x + 8 * k, sizeof b.x);
+        memcpy(b.P, P + 64 * k, sizeof b.P);
+        bkf_update(&b, z + 4 * k);
+        memcpy(x + 8 * k, b.x, sizeof b.x);
+        memcpy(P + 64 * k, b.P, sizeof b.P);
+    }
+}
+
+void bxo_kf_boost_mh_dist(int nd, const double *dets, int nt, const double *x, const double *P,
+                          double *out) {
+    for (int t = 0; t < nt; t++) {
+        double sinv[4];
+        for (int q = 0; q < 4; q++) sinv[q] = 1.0 / P[64 * t + 9 * q];
+        for (int d = 0; d < nd; d++) out[(size_t)d * nt + t] = mh_dist(dets + 4 * d, x + 8 * t, sinv);
+    }
+}
+
 #define MH_LIMIT 13.2767
 
 /* MhDist_similarity (assoc.py:37-47): softmax over axis 0 (detections) per tracker column;

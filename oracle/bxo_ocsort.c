@@ -338,6 +338,44 @@ static void xyxy2xysr(const double *b, double *z) {
     z[3] = w / (h + 1e-6);
 }
 
+/* Op-level entries (mirrors of bx_kf_xysr_*): KalmanBoxTracker's filter without the tracker's
+ * history/ORU bookkeeping.  initiate = ocsort.py:83-111 (P = eye; P[4:,4:] *= 1000; P *= 10;
+ * x[:4] = xyxy2xysr(bbox)); predict = ocsort.py:177-180 (the s + ds <= 0 clamp, then
+ * xysr_kf.py:137-175 with Q[4:6,4:6] *= q_xy, Q[-1,-1] *= q_s); update = xysr_kf.py:256-283. */
+void bxo_kf_xysr_initiate(int n, const double *bbox, double *x, double *P) {
+    for (int k = 0; k < n; k++) {
+        double *xk = x + 7 * k, *Pk = P + 49 * k;
+        memset(xk, 0, sizeof(double) * 7);
+        memset(Pk, 0, sizeof(double) * 49);
+        xyxy2xysr(bbox + 4 * k, xk);
+        for (int i = 0; i < 7; i++) Pk[8 * i] = i < 4 ? 10.0 : 10000.0;
+    }
+}
+
+void bxo_kf_xysr_predict(int n, double *x, double *P, double q_xy, double q_s) {
+    const kf_params kp = {q_xy, q_s, 50};
+    for (int k = 0; k < n; k++) {
+        kf_state s;
+        memcpy(s.x, x + 7 * k, sizeof s.x);
+        memcpy(s.P, P + 49 * k, sizeof s.P);
+        if (s.x[6] + s.x[2] <= 0) s.x[6] *= 0.0;
+        kf_predict7(&kp, &s);
+        memcpy(x + 7 * k, s.x, sizeof s.x);
+        memcpy(P + 49 * k, s.P, sizeof s.P);
+    }
+}
+
+void bxo_kf_xysr_update(int n, double *x, double *P, const double *z) {
+    for (int k = 0; k < n; k++) {
+        kf_state s;
+        memcpy(s.x, x + 7 * k, sizeof s.x);
+        memcpy(s.P, P + 49 * k, sizeof s.P);
+        kf_update7_core(&s, z + 4 * k);
+        memcpy(x + 7 * k, s.x, sizeof s.x);
+        memcpy(P + 49 * k, s.P, sizeof s.P);
+    }
+}
+
 /* ocsort.py:31-45 convert_x_to_bbox */
 static void x_to_bbox(const double *x, double *b) {
     const double w = sqrt(x[2] * x[3]);

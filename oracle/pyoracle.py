@@ -160,6 +160,12 @@ def lib():
                                  _dp, C.c_int]
         L.bxo_id_count.argtypes = [C.c_void_p]
         L.bxo_frame_count.argtypes = [C.c_void_p]
+        for fn in ("bxo_kf_xysr_initiate", "bxo_kf_xysr_update", "bxo_kf_boost_initiate",
+                   "bxo_kf_boost_update"):
+            getattr(L, fn).argtypes = [C.c_int, _dp, _dp, _dp]
+        L.bxo_kf_xysr_predict.argtypes = [C.c_int, _dp, _dp, C.c_double, C.c_double]
+        L.bxo_kf_boost_predict.argtypes = [C.c_int, _dp, _dp]
+        L.bxo_kf_boost_mh_dist.argtypes = [C.c_int, _dp, C.c_int, _dp, _dp, _dp]
         L.bxo_select_class.argtypes = [C.c_void_p, C.c_int]
         L.bxo_set_frame_count.argtypes = [C.c_void_p, C.c_int]
         L.bxo_ocsort_set_id_count.argtypes = [C.c_void_p, C.c_int]
@@ -322,6 +328,45 @@ def linear_assignment(cost, thresh):
     lib().bxo_linear_assignment(_d(cost), nr, nc, float(thresh), ip(m), C.byref(nm), ip(ua),
                                 C.byref(nua), ip(ub), C.byref(nub))
     return m[: 2 * nm.value].reshape(-1, 2), ua[: nua.value], ub[: nub.value]
+
+
+def kf_xysr(op, x, P, arg=None, q_xy=0.01, q_s=0.0001):
+    """Op-level XYSR filter (bxo_kf_xysr_*): op in initiate (arg = boxes [n,4]), predict,
+    update (arg = z [n,4]); returns new (x [n,7], P [n,7,7])."""
+    L = lib()
+    n = (arg if op == "initiate" else x).shape[0]
+    x = np.zeros((n, 7)) if op == "initiate" else np.array(x, np.float64).reshape(n, 7)
+    P = np.zeros((n, 7, 7)) if op == "initiate" else np.array(P, np.float64).reshape(n, 7, 7)
+    if op == "initiate":
+        L.bxo_kf_xysr_initiate(n, _d(np.ascontiguousarray(arg, np.float64)), _d(x), _d(P))
+    elif op == "predict":
+        L.bxo_kf_xysr_predict(n, _d(x), _d(P), q_xy, q_s)
+    else:
+        L.bxo_kf_xysr_update(n, _d(x), _d(P), _d(np.ascontiguousarray(arg, np.float64)))
+    return x, P
+
+
+def kf_boost(op, x, P, arg=None):
+    """Op-level BoostTrack filter (bxo_kf_boost_*): initiate (arg = z [n,4]), predict, update
+    (arg = z), mh_dist (arg = xyxy detections [m,4]; returns [m,n])."""
+    L = lib()
+    if op == "mh_dist":
+        d = np.ascontiguousarray(arg, np.float64)
+        x = np.ascontiguousarray(x, np.float64)
+        P = np.ascontiguousarray(P, np.float64)
+        out = np.zeros((d.shape[0], x.shape[0]))
+        L.bxo_kf_boost_mh_dist(d.shape[0], _d(d), x.shape[0], _d(x), _d(P), _d(out))
+        return out
+    n = (arg if op == "initiate" else x).shape[0]
+    x = np.zeros((n, 8)) if op == "initiate" else np.array(x, np.float64).reshape(n, 8)
+    P = np.zeros((n, 8, 8)) if op == "initiate" else np.array(P, np.float64).reshape(n, 8, 8)
+    if op == "initiate":
+        L.bxo_kf_boost_initiate(n, _d(np.ascontiguousarray(arg, np.float64)), _d(x), _d(P))
+    elif op == "predict":
+        L.bxo_kf_boost_predict(n, _d(x), _d(P))
+    else:
+        L.bxo_kf_boost_update(n, _d(x), _d(P), _d(np.ascontiguousarray(arg, np.float64)))
+    return x, P
 
 
 NR_CLASSES = 80  # BaseTracker(nr_classes=80) (basetracker.py:23)

@@ -167,6 +167,56 @@ def test_kalman_ops(torch_cuda, K, kind):
     np.testing.assert_allclose(host(out), K[f"kf_{kind}_gate_out"], rtol=1e-10)
 
 
+@pytest.mark.gpu
+def test_kf_xysr_boost_ops(torch_cuda):
+    """Op-level XYSR (OCSort) and BoostTrack filters: bitwise equal to the oracle on the
+    reference-captured chains of kf_ops.npz (initiate, predict incl. the clamp, update, MhDist),
+    and through it pinned to the reference (tests/test_oracle.py)."""
+    torch = torch_cuda
+    from boxmot_amd import _native as N
+
+    L = N.load()
+    fx = np.load(GOLDEN / "kf_ops.npz")
+    ptr = lambda t: t.data_ptr()  # noqa: E731
+    n = fx["xysr_init_box"].shape[0]
+    x = torch.empty((n, 7), dtype=torch.float64, device="cuda")
+    P = torch.empty((n, 7, 7), dtype=torch.float64, device="cuda")
+    N.check(L.bx_kf_xysr_initiate(n, ptr(dev(torch, fx["xysr_init_box"])), ptr(x), ptr(P), None))
+    np.testing.assert_array_equal(host(x), fx["xysr_init_x"])
+    np.testing.assert_array_equal(host(P), fx["xysr_init_P"])
+    for s in range(int(fx["xysr_steps"])):
+        x, P = dev(torch, fx[f"xysr_s{s}_in_x"]), dev(torch, fx[f"xysr_s{s}_in_P"])
+        N.check(L.bx_kf_xysr_predict(n, ptr(x), ptr(P), 0.01, 0.0001, None))
+        np.testing.assert_array_equal(host(x), fx[f"xysr_s{s}_pred_x"])
+        np.testing.assert_array_equal(host(P), fx[f"xysr_s{s}_pred_P"])
+        z = fx[f"xysr_s{s}_z"]
+        N.check(L.bx_kf_xysr_update(n, ptr(x), ptr(P), ptr(dev(torch, z)), None))
+        ox, oP = po.kf_xysr("update", fx[f"xysr_s{s}_pred_x"], fx[f"xysr_s{s}_pred_P"], z)
+        np.testing.assert_array_equal(host(x), ox)
+        np.testing.assert_array_equal(host(P), oP)
+    n = fx["boost_init_z"].shape[0]
+    x = torch.empty((n, 8), dtype=torch.float64, device="cuda")
+    P = torch.empty((n, 8, 8), dtype=torch.float64, device="cuda")
+    N.check(L.bx_kf_boost_initiate(n, ptr(dev(torch, fx["boost_init_z"])), ptr(x), ptr(P), None))
+    np.testing.assert_array_equal(host(x), fx["boost_init_x"])
+    np.testing.assert_array_equal(host(P), fx["boost_init_P"])
+    for s in range(int(fx["boost_steps"])):
+        x, P = dev(torch, fx[f"boost_s{s}_in_x"]), dev(torch, fx[f"boost_s{s}_in_P"])
+        N.check(L.bx_kf_boost_predict(n, ptr(x), ptr(P), None))
+        np.testing.assert_array_equal(host(x), fx[f"boost_s{s}_pred_x"])
+        np.testing.assert_array_equal(host(P), fx[f"boost_s{s}_pred_P"])
+        d = fx[f"boost_s{s}_mh_dets"]
+        mh = torch.empty((d.shape[0], n), dtype=torch.float64, device="cuda")
+        N.check(L.bx_kf_boost_mh_dist(d.shape[0], ptr(dev(torch, d)), n, ptr(x), ptr(P), ptr(mh),
+                                      None))
+        np.testing.assert_array_equal(host(mh), fx[f"boost_s{s}_mh"])
+        z = fx[f"boost_s{s}_z"]
+        N.check(L.bx_kf_boost_update(n, ptr(x), ptr(P), ptr(dev(torch, z)), None))
+        ox, oP = po.kf_boost("update", fx[f"boost_s{s}_pred_x"], fx[f"boost_s{s}_pred_P"], z)
+        np.testing.assert_array_equal(host(x), ox)
+        np.testing.assert_array_equal(host(P), oP)
+
+
 def gpu_linear_assignment(torch, cost, thr):
     from boxmot_amd import _native as N
 

@@ -285,3 +285,39 @@ def test_aw_max_metric_matches_reference():
     for k in range(int(g["aw_count"])):
         got = po.aw_max_metric(g[f"aw{k}_in"], float(g[f"aw{k}_w"]), 0.5)
         np.testing.assert_array_equal(got, g[f"aw{k}_out"])
+
+
+def test_kf_xysr_ops_vs_reference():
+    """Op-level XYSR filter of OCSort's KalmanBoxTracker (ocsort.py:83-111,177-180,
+    xysr_kf.py:137-175,256-283) against the reference objects (kf_ops.npz): initiate and predict
+    (incl. the s + ds <= 0 clamp) bitwise; update (np.linalg.inv, unpinned BLAS order) <= 1e-12."""
+    fx = np.load(GOLDEN / "kf_ops.npz")
+    x, P = po.kf_xysr("initiate", None, None, fx["xysr_init_box"])
+    np.testing.assert_array_equal(x, fx["xysr_init_x"])
+    np.testing.assert_array_equal(P, fx["xysr_init_P"])
+    for s in range(int(fx["xysr_steps"])):
+        x, P = po.kf_xysr("predict", fx[f"xysr_s{s}_in_x"], fx[f"xysr_s{s}_in_P"])
+        np.testing.assert_array_equal(x, fx[f"xysr_s{s}_pred_x"])
+        np.testing.assert_array_equal(P, fx[f"xysr_s{s}_pred_P"])
+        x, P = po.kf_xysr("update", x, P, fx[f"xysr_s{s}_z"])
+        np.testing.assert_allclose(x, fx[f"xysr_s{s}_upd_x"], rtol=1e-12, atol=1e-9)
+        np.testing.assert_allclose(P, fx[f"xysr_s{s}_upd_P"], rtol=1e-12, atol=1e-9)
+
+
+def test_kf_boost_ops_vs_reference():
+    """Op-level BoostTrack filter (kalmanfilter.py:47-157) and get_mh_dist_matrix
+    (boosttrack.py:356-369) against the reference objects: initiate/predict/mh_dist bitwise,
+    update (scipy cho_factor/cho_solve, unpinned LAPACK order) <= 1e-12."""
+    fx = np.load(GOLDEN / "kf_ops.npz")
+    x, P = po.kf_boost("initiate", None, None, fx["boost_init_z"])
+    np.testing.assert_array_equal(x, fx["boost_init_x"])
+    np.testing.assert_array_equal(P, fx["boost_init_P"])
+    for s in range(int(fx["boost_steps"])):
+        x, P = po.kf_boost("predict", fx[f"boost_s{s}_in_x"], fx[f"boost_s{s}_in_P"])
+        np.testing.assert_array_equal(x, fx[f"boost_s{s}_pred_x"])
+        np.testing.assert_array_equal(P, fx[f"boost_s{s}_pred_P"])
+        mh = po.kf_boost("mh_dist", x, P, fx[f"boost_s{s}_mh_dets"])
+        np.testing.assert_array_equal(mh, fx[f"boost_s{s}_mh"])
+        x, P = po.kf_boost("update", x, P, fx[f"boost_s{s}_z"])
+        np.testing.assert_allclose(x, fx[f"boost_s{s}_upd_x"], rtol=1e-12, atol=1e-9)
+        np.testing.assert_allclose(P, fx[f"boost_s{s}_upd_P"], rtol=1e-12, atol=1e-9)
