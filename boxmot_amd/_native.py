@@ -131,7 +131,8 @@ EXPORTS = [
     "bx_engine_update_classes_host", "bx_ocsort_update_classes_host",
     "bx_boost_update_classes_host", "bx_kf_xysr_initiate", "bx_kf_xysr_predict",
     "bx_kf_xysr_update", "bx_kf_boost_initiate", "bx_kf_boost_predict", "bx_kf_boost_update",
-    "bx_kf_boost_mh_dist",
+    "bx_kf_boost_mh_dist", "bx_ss_track_attrs_host", "bx_ss_track_attrs_set_host",
+    "bx_ss_last_feature_host", "bx_ss_last_feature_set_host",
 ]
 
 _vp, _ip, _dp, _fp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_float)
@@ -223,6 +224,10 @@ _SIGS = {
     "bx_kf_boost_predict": ([C.c_int, _vp, _vp, _vp], C.c_int),
     "bx_kf_boost_update": ([C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "bx_kf_boost_mh_dist": ([C.c_int, _vp, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_ss_track_attrs_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _ip], C.c_int),
+    "bx_ss_track_attrs_set_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "bx_ss_last_feature_host": ([_vp, C.c_int, C.c_int, _vp, _vp], C.c_int),
+    "bx_ss_last_feature_set_host": ([_vp, C.c_int, C.c_int, _vp, _vp, C.c_int], C.c_int),
 }
 
 _lib = None

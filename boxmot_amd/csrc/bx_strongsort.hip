@@ -2298,6 +2298,50 @@ __global__ void ss_reset_kernel(SsDev g, int seq0, int nseq) {
   }
 }
 
+// OcclusionAwareTracker._handle_emerging_track's `track.features[-1] = blended`
+// (utils/occlusion_handler.py:405-413) for the host post-process: one wave per edited track.
+// The vector replaces features[-1]; a pool entry the gallery also references keeps its old
+// content (the reference's gallery holds copies) and the feature moves to a fresh entry.  The
+// blend is normalised here when asked (`/= np.linalg.norm + 1e-8`, the engine's wave order) and
+// the entry gets the norms every stored feature carries (wave norm, numpy pairwise + 1e-8, the
+// NN-normalised copy).
+__global__ void __launch_bounds__(64) ss_feat_set_kernel(SsDev g, int seq, const int* __restrict__ slots,
+                                                         const double* __restrict__ src,
+                                                         int normalize) {
+  __shared__ int lo[PW_MAXLEAF], ln[PW_MAXLEAF];
+  __shared__ double leaf[PW_MAXLEAF];
+  __shared__ int sv;
+  const int lane = threadIdx.x, F = g.F, slot = slots[blockIdx.x];
+  SsTrk& t = g.trk[(size_t)seq * g.T + slot];
+  const double* x = src + (size_t)blockIdx.x * F;
+  if (lane == 0) {
+    int v = -1;
+    if (t.nfeat > 0) {
+      const int lv = t.feat[t.nfeat - 1];
+      v = ((t.gmask >> lv) & 1ull) ? pool_alloc(t, g.VP) : lv;
+      if (v < 0) atomicExch(g.status, (int)BX_ERR_TRACK_OVERFLOW);
+    }
+    sv = v;
+  }
+  __syncthreads();
+  const int v = sv;
+  if (v < 0) return;
+  double* dst = vecp(g, seq, slot, v);
+  const double ns = normalize ? sqrt(wdot(x, x, F)) + 1e-8 : 1.0;
+  for (int q = lane; q < F; q += 64) dst[q] = normalize ? x[q] / ns : x[q];
+  __syncthreads();
+  const double wn = sqrt(wdot(dst, dst, F));
+  const double pn = wpw_norm(dst, F, lo, ln, leaf) + 1e-8;
+  double* dstn = vecnp(g, seq, slot, v);
+  for (int q = lane; q < F; q += 64) dstn[q] = dst[q] / pn;
+  if (lane == 0) {
+    const size_t vi = vidx(g, seq, slot, v);
+    g.vwn[vi] = wn;
+    g.vden[vi] = pn;
+    t.feat[t.nfeat - 1] = v;
+  }
+}
+
 }  // namespace
 
 struct bx_ss {
@@ -2687,6 +2731,116 @@ int bx_ss_tracks_host(bx_ss* e, int seq, int cap, int32_t* ids, int32_t* state, 
     if (cov) memcpy(cov + 64 * k, t.cov, sizeof(t.cov));
   }
   *n = nt;
+  return BX_OK;
+}
+
+// the sequence's track list (slots in list order) and its track records, one copy each
+static int ss_read_list(bx_ss* e, int seq, std::vector<int>& ord, std::vector<SsTrk>& trk) {
+  SCHK(hipDeviceSynchronize());
+  int s[SQS];
+  SCHK(hipMemcpy(s, e->dev.sq + (size_t)seq * SQS, sizeof(s), hipMemcpyDeviceToHost));
+  ord.assign(s[Q_NTR], 0);
+  if (!ord.empty())
+    SCHK(hipMemcpy(ord.data(), e->dev.order + (size_t)seq * e->dev.T, sizeof(int) * ord.size(),
+                   hipMemcpyDeviceToHost));
+  trk.resize(e->dev.T);
+  SCHK(hipMemcpy(trk.data(), e->dev.trk + (size_t)seq * e->dev.T, sizeof(SsTrk) * e->dev.T,
+                 hipMemcpyDeviceToHost));
+  return BX_OK;
+}
+
+static int ss_find(const std::vector<int>& ord, const std::vector<SsTrk>& trk, int id) {
+  for (int k : ord)
+    if (trk[k].id == id) return k;
+  return -1;
+}
+
+int bx_ss_track_attrs_host(bx_ss* e, int seq, int cap, int32_t* ids, double* quality,
+                           double* conf, int32_t* max_age, int32_t* n_features, int* n) {
+  if (!e || seq < 0 || seq >= e->dev.S || cap < 0 || !n)
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_track_attrs_host");
+  std::vector<int> ord;
+  std::vector<SsTrk> trk;
+  if (int rc = ss_read_list(e, seq, ord, trk)) return rc;
+  for (int k = 0; k < (int)ord.size() && k < cap; k++) {
+    const SsTrk& t = trk[ord[k]];
+    if (ids) ids[k] = t.id;
+    if (quality) quality[k] = t.quality;
+    if (conf) conf[k] = t.conf;
+    if (max_age) max_age[k] = t.max_age;
+    if (n_features) n_features[k] = t.nfeat;
+  }
+  *n = (int)ord.size();
+  return BX_OK;
+}
+
+int bx_ss_track_attrs_set_host(bx_ss* e, int seq, int n, const int32_t* ids, const double* quality,
+                               const double* conf, const int32_t* max_age) {
+  if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && !ids))
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_track_attrs_set_host");
+  std::vector<int> ord;
+  std::vector<SsTrk> trk;
+  if (int rc = ss_read_list(e, seq, ord, trk)) return rc;
+  for (int j = 0; j < n; j++) {
+    const int k = ss_find(ord, trk, ids[j]);
+    if (k < 0) return bx_record_error(BX_ERR_INVALID, "track_attrs_set: no live track with that id");
+    SsTrk* dt = e->dev.trk + (size_t)seq * e->dev.T + k;
+    if (quality) SCHK(hipMemcpy(&dt->quality, quality + j, sizeof(double), hipMemcpyHostToDevice));
+    if (conf) SCHK(hipMemcpy(&dt->conf, conf + j, sizeof(double), hipMemcpyHostToDevice));
+    if (max_age) SCHK(hipMemcpy(&dt->max_age, max_age + j, sizeof(int), hipMemcpyHostToDevice));
+  }
+  return BX_OK;
+}
+
+int bx_ss_last_feature_host(bx_ss* e, int seq, int n, const int32_t* ids, double* feats) {
+  if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && (!ids || !feats)))
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_last_feature_host");
+  std::vector<int> ord;
+  std::vector<SsTrk> trk;
+  if (int rc = ss_read_list(e, seq, ord, trk)) return rc;
+  const int F = e->dev.F;
+  for (int j = 0; j < n; j++) {
+    const int k = ss_find(ord, trk, ids[j]);
+    if (k < 0 || trk[k].nfeat < 1)
+      return bx_record_error(BX_ERR_INVALID, "last_feature: no live track with features and that id");
+    const size_t vi = ((size_t)seq * e->dev.T + k) * e->dev.VP + trk[k].feat[trk[k].nfeat - 1];
+    SCHK(hipMemcpy(feats + (size_t)j * F, e->dev.vec + vi * F, sizeof(double) * F,
+                   hipMemcpyDeviceToHost));
+  }
+  return BX_OK;
+}
+
+int bx_ss_last_feature_set_host(bx_ss* e, int seq, int n, const int32_t* ids, const double* feats,
+                                int normalize) {
+  if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && (!ids || !feats)))
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_last_feature_set_host");
+  if (!n) return BX_OK;
+  std::vector<int> ord;
+  std::vector<SsTrk> trk;
+  if (int rc = ss_read_list(e, seq, ord, trk)) return rc;
+  std::vector<int> slots(n);
+  for (int j = 0; j < n; j++) {
+    slots[j] = ss_find(ord, trk, ids[j]);
+    if (slots[j] < 0 || trk[slots[j]].nfeat < 1)
+      return bx_record_error(BX_ERR_INVALID, "last_feature_set: no live track with features and that id");
+    for (int q = 0; q < j; q++)
+      if (slots[q] == slots[j]) return bx_record_error(BX_ERR_INVALID, "last_feature_set: repeated id");
+  }
+  const int F = e->dev.F;
+  void* buf = nullptr;
+  SCHK(hipMalloc(&buf, sizeof(int) * n + sizeof(double) * (size_t)n * F + 256));
+  int* d_slots = (int*)buf;
+  double* d_src = (double*)((char*)buf + ((sizeof(int) * n + 255) & ~(size_t)255));
+  SCHK(hipMemcpy(d_slots, slots.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+  SCHK(hipMemcpy(d_src, feats, sizeof(double) * (size_t)n * F, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(ss_feat_set_kernel, dim3(n), dim3(64), 0, 0, e->dev, seq, d_slots, d_src,
+                     normalize);
+  SCHK(hipGetLastError());
+  SCHK(hipDeviceSynchronize());
+  SCHK(hipFree(buf));
+  int status = 0;
+  SCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
+  if (status) return bx_record_error(status, "a track's feature pool is exhausted (raise vec_cap)");
   return BX_OK;
 }
 

@@ -660,6 +660,43 @@ class SsEngine:
         N.check(self._L.bx_ss_state_set_host(self._h, seq, n, ids.ctypes.data, _p(m), _p(c)),
                 "state_set")
 
+    def track_attrs(self, seq: int = 0) -> dict:
+        """Per track in list order: id, quality_score, conf, _max_age, len(features)."""
+        cap = self.track_cap
+        ids, mx, nf = (np.zeros(cap, np.int32) for _ in range(3))
+        q, cf = np.zeros(cap), np.zeros(cap)
+        n = C.c_int()
+        N.check(self._L.bx_ss_track_attrs_host(self._h, seq, cap, ids.ctypes.data, q.ctypes.data,
+                                               cf.ctypes.data, mx.ctypes.data, nf.ctypes.data,
+                                               C.byref(n)), "track_attrs")
+        k = min(n.value, cap)
+        return {"id": ids[:k], "quality": q[:k], "conf": cf[:k], "max_age": mx[:k],
+                "n_features": nf[:k]}
+
+    def track_attrs_set(self, seq: int, ids, quality=None, conf=None, max_age=None) -> None:
+        ids = np.ascontiguousarray(ids, np.int32).reshape(-1)
+        q = None if quality is None else np.ascontiguousarray(quality, np.float64).reshape(-1)
+        c = None if conf is None else np.ascontiguousarray(conf, np.float64).reshape(-1)
+        m = None if max_age is None else np.ascontiguousarray(max_age, np.int32).reshape(-1)
+        N.check(self._L.bx_ss_track_attrs_set_host(self._h, seq, ids.size, ids.ctypes.data,
+                                                   _p(q), _p(c), _p(m)), "track_attrs_set")
+
+    def last_features(self, seq: int, ids) -> np.ndarray:
+        """features[-1] of the tracks `ids` ([n, emb_dim] float64)."""
+        ids = np.ascontiguousarray(ids, np.int32).reshape(-1)
+        out = np.zeros((ids.size, self.emb_dim))
+        if ids.size:
+            N.check(self._L.bx_ss_last_feature_host(self._h, seq, ids.size, ids.ctypes.data,
+                                                    out.ctypes.data), "last_features")
+        return out
+
+    def last_features_set(self, seq: int, ids, feats, normalize: bool = True) -> None:
+        ids = np.ascontiguousarray(ids, np.int32).reshape(-1)
+        f = np.ascontiguousarray(feats, np.float64).reshape(ids.size, self.emb_dim)
+        N.check(self._L.bx_ss_last_feature_set_host(self._h, seq, ids.size, ids.ctypes.data,
+                                                    f.ctypes.data, int(bool(normalize))),
+                "last_features_set")
+
     def frame_stats(self, seq0: int = 0, nseq: int | None = None) -> dict:
         nseq = self.n_seq - seq0 if nseq is None else nseq
         a = (C.c_int64 * 7)()

@@ -144,8 +144,11 @@ def _batched_engine(tracker_type: str, n_seq: int, emb_dim: int, tracker_kwargs:
                            params=tr._params), np.float32, 8
     if tracker_type == "strongsort":
         tc, dc, vc = tr._caps
-        return SsEngine(n_seq=n_seq, track_cap=tc, det_cap=dc, emb_dim=emb_dim, vec_cap=vc,
-                        params=tr._params), np.float64, 10
+        eng = SsEngine(n_seq=n_seq, track_cap=tc, det_cap=dc, emb_dim=emb_dim, vec_cap=vc,
+                       params=tr._params)
+        # handle_occlusions: the host post-process runs per sequence after each batched step
+        eng.occlusion_threshold = tr.occlusion_threshold if tr.handle_occlusions else None
+        return eng, np.float64, 10
     raise NotImplementedError(f"{tracker_type} is not on the engine")
 
 
@@ -172,6 +175,12 @@ def run_sequences(tracker_type: str, sequences: dict, exp_dir, frame_ids: dict |
     fids = [np.asarray(frame_ids[nm]) if frame_ids and nm in frame_ids else s.frame_ids
             for nm, s in zip(names, seqs)]
     results = [[] for _ in range(S)]
+    occ = None
+    if getattr(eng, "occlusion_threshold", None) is not None:
+        from .occlusion import OcclusionHandler
+
+        occ = [OcclusionHandler(eng, k, eng.occlusion_threshold) for k in range(S)]
+    nupd = [0] * S
     dev = torch.device("cuda")
     for t in range(max([len(f) for f in fids] + [0])):
         frame = []
@@ -208,6 +217,9 @@ def run_sequences(tracker_type: str, sequences: dict, exp_dir, frame_ids: dict |
             o, c = out.cpu().numpy(), cnt.cpu().numpy()
             for q in range(k, k1):
                 rows = o[off[q - k]: off[q - k] + c[q - k]]
+                nupd[q] += 1
+                if occ is not None:
+                    rows = occ[q](nupd[q], rows)
                 if rows.shape[0]:
                     results[q].append(convert_to_mot_format(rows, int(fids[q][t])))
             k = k1

@@ -10,10 +10,12 @@ Every frame is generated from its own ``numpy.random.default_rng([seed, frame])`
 frame can be produced independently of the frames before it (bench shards, GPU-side staging and
 the golden-fixture script all regenerate identical inputs from ``(seed, frame)``).
 
-Two layouts:
+Three layouts:
 * ``grid``   — objects on a regular grid, little overlap (the survey's C2/C3/C4 scene);
 * ``crowded``— uniformly random centres with heavy overlap: many non-trivial LAP components and
-  near-threshold costs (the stress variant §8(d) asks for).
+  near-threshold costs (the stress variant §8(d) asks for);
+* ``corner`` — ``crowded`` plus the ``corner`` objects held at the top-left corner (StrongSort's
+  occlusion-handler fixtures).
 """
 from __future__ import annotations
 
@@ -39,6 +41,7 @@ class SyntheticScene:
     height: float = 1080.0
     emb_dtype: type = np.float32
     classes: tuple = ()  # per-identity class ids (identity k -> classes[k % len]); () = class 0
+    corner: tuple = ()  # layout "corner": (width, a) of the objects parked at the top-left corner
 
     def __post_init__(self):
         rng = np.random.default_rng([self.seed, 0x5CE7E])
@@ -52,16 +55,25 @@ class SyntheticScene:
             cy = (idx // cols + 0.5) * ch
             w = 0.45 * cw * rng.uniform(0.8, 1.2, n)
             h = 0.80 * ch * rng.uniform(0.8, 1.2, n)
-        elif self.layout == "crowded":
+        elif self.layout in ("crowded", "corner"):
             cx = rng.uniform(0.1, 0.9, n) * self.width
             cy = rng.uniform(0.1, 0.9, n) * self.height
             w = rng.uniform(30.0, 90.0, n)
             h = w * rng.uniform(1.5, 3.0, n)
+            # corner: objects 0..k-1 nearly still at the top-left corner, where a tlwh row has
+            # x < w and y < h — the only place OcclusionAwareTracker's xyxy reading of tlwh
+            # boxes (occlusion_handler.py:49-56, 297-299) sees overlaps
+            # (centre at a * size: the box's tlwh row reads as the xyxy rect [(a-.5)w, w] x ...)
+            for i, (cw, a) in enumerate(self.corner if self.layout == "corner" else ()):
+                w[i], h[i] = cw, 2.5 * cw
+                cx[i], cy[i] = a * w[i], a * h[i]
         else:
             raise ValueError(f"unknown layout {self.layout!r}")
         self.c0 = np.stack([cx, cy], 1)
         self.size = np.stack([w, h], 1)
         self.vel = rng.uniform(-0.5, 0.5, (n, 2))
+        if self.layout == "corner":
+            self.vel[: len(self.corner)] *= 0.05
         if self.emb_dim:
             base = rng.standard_normal((n, self.emb_dim))
             self.base_emb = base / np.linalg.norm(base, axis=1, keepdims=True)

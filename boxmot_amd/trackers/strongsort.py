@@ -9,9 +9,10 @@ similarities and one wave per sequence for everything else (include/bxstrongsort
 Differences from the reference, by design or because the fork cannot run otherwise
 (SURVEY.md Appendix A):
 * the fork crashes on frame 1 (D5); the engine applies the minimal patch P6;
-* ``handle_occlusions`` (the OcclusionAwareTracker post-process, utils/occlusion_handler.py)
-  is not on the engine: it crashes on mutual occlusion (D7); only ``False`` is accepted and the
-  occlusion column is 0;
+* ``handle_occlusions`` (default True, as the reference): the OcclusionAwareTracker post-process
+  (utils/occlusion_handler.py:312-439) runs on the host over the engine's track state
+  (``boxmot_amd.occlusion``) and raises TypeError where the reference crashes on mutual
+  occlusion (D7); with False the occlusion column is 0;
 * tracks are born Confirmed when ``GITHUB_ACTIONS=true`` (and GITHUB_JOB is not the MOT
   benchmark), Tentative otherwise — read from the environment like the reference (D8);
 * ReID features are inputs (``embs`` required, used as float64).  CMC: ``self.cmc.apply(img,
@@ -24,6 +25,7 @@ import os
 import numpy as np
 
 from ..engine import SsEngine, SsParams
+from ..occlusion import OcclusionHandler
 from .basetracker import BaseTracker
 from .boosttrack import IdentityCMC
 
@@ -40,18 +42,14 @@ class StrongSort:
                  n_init=2, nn_budget=150, mc_lambda=0.995, ema_alpha=0.9, conf_thresh_high=0.7,
                  conf_thresh_low=0.3, id_preservation_weight=0.1, adaptive_matching=True,
                  appearance_weight=0.6, motion_weight=0.4, occlusion_threshold=0.3,
-                 handle_occlusions=False, crowd_detection=True, track_cap: int = 512,
-                 det_cap: int = 256, vec_cap: int = 32):
+                 handle_occlusions=True, crowd_detection=True, track_cap: int = 512,
+                 det_cap: int = 256, vec_cap: int = 64):
         if per_class:
             # create_tracker pops per_class for StrongSort (tracker_zoo.py:84-85); constructed
             # directly with per_class=True the reference fails in its first update (StrongSort
             # never runs BaseTracker.__init__, so the decorator's nr_classes does not exist)
             raise NotImplementedError("StrongSort has no per-class mode (the reference's "
                                       "create_tracker drops per_class for it)")
-        if handle_occlusions:
-            raise NotImplementedError(
-                "handle_occlusions=True (OcclusionAwareTracker) is not on the engine: the fork's "
-                "handler crashes on mutual occlusion (SURVEY.md App. A D7)")
         self.per_class = per_class
         self.min_conf = min_conf
         self.conf_thresh_high = conf_thresh_high
@@ -74,6 +72,8 @@ class StrongSort:
         self._caps = (track_cap, det_cap, vec_cap)
         self.engine = None
         self._pending = 0
+        self.occlusion_tracker = None  # OcclusionHandler, created with the engine
+        self.occlusion_stats = {}
 
     @BaseTracker.per_class_decorator
     def update(self, dets: np.ndarray, img: np.ndarray, embs: np.ndarray = None) -> np.ndarray:
@@ -98,12 +98,18 @@ class StrongSort:
                                    params=self._params)
             for _ in range(self._pending):  # replay the empty frames (predict + bookkeeping)
                 self.engine.update_host(0, np.empty((0, 6)), np.empty((0, self.engine.emb_dim)))
+            if self.handle_occlusions:
+                self.occlusion_tracker = OcclusionHandler(self.engine, 0, self.occlusion_threshold)
         warp = None
         if self.cmc is not None:
             warp = np.asarray(self.cmc.apply(img, dets[:, :4]), np.float64)
             warp = warp[:2] if warp.shape == (3, 3) else warp
         e = embs if embs is not None else np.empty((dets.shape[0], self.engine.emb_dim))
         out = self.engine.update_host(0, dets, e, warp)
+        if self.occlusion_tracker is not None:  # strongsort.py:150-154, 195-201
+            out = self.occlusion_tracker(self.frame_count, out)
+            if np.any(dets[:, 4] >= self.min_conf):  # not refreshed by the no-detection branch
+                self.occlusion_stats = self.occlusion_tracker.statistics()
         return out if out.shape[0] else np.array([])
 
     def reset(self):

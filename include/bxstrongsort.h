@@ -24,8 +24,10 @@
  *     NearestNeighborDistanceMetric sort/linear_assignment.py:14-618
  *     iou_cost                     sort/iou_matching.py:10-87
  *     detect_crowd_situations      utils/occlusion_handler.py:45-87, 464-490
- * The fork needs the minimal patch P6 and runs with
- * handle_occlusions=False (D7); `born_confirmed` stands for its GITHUB_ACTIONS=true switch (D8).
+ * The fork needs the minimal patch P6; `born_confirmed` stands for its
+ * GITHUB_ACTIONS=true switch (D8).  handle_occlusions=True (OcclusionAwareTracker,
+ * utils/occlusion_handler.py:312-439) is a host post-process (boxmot_amd/occlusion.py) over the
+ * track-attribute calls below; it raises where the reference crashes on mutual occlusion (D7).
  * Bit-identical to oracle/bxo_strongsort.c (pinned by tests/golden/trk_strongsort_*.npz).
  *
  * Conventions as in bxassoc.h: device pointers unless a name ends in _host, asynchronous on
@@ -96,6 +98,23 @@ int bx_ss_tracks_host(bx_ss *e, int seq, int cap, int32_t *ids, int32_t *state, 
  * BX_ERR_INVALID for an unknown id. */
 int bx_ss_state_set_host(bx_ss *e, int seq, int n, const int32_t *ids, const double *mean,
                          const double *cov);
+/* Track attributes the host-side OcclusionAwareTracker reads and edits
+ * (utils/occlusion_handler.py:341-417; sort/track.py:76-131 attributes), host and synchronous,
+ * list order / by id:
+ *   bx_ss_track_attrs_host      ids, quality_score, conf, _max_age, len(features) (any NULL)
+ *   bx_ss_track_attrs_set_host  quality_score / conf / _max_age by id (NULL arrays untouched)
+ *   bx_ss_last_feature_host     features[-1] [n][emb_dim] by id
+ *   bx_ss_last_feature_set_host `features[-1] = v` [n][emb_dim] by id (normalize: v / (wave-order
+ *                               norm + 1e-8) first, the engine's np.linalg.norm order); the
+ *                               gallery keeps the replaced vector's content
+ * BX_ERR_INVALID for an unknown id (or a track without features for the feature calls). */
+int bx_ss_track_attrs_host(bx_ss *e, int seq, int cap, int32_t *ids, double *quality,
+                           double *conf, int32_t *max_age, int32_t *n_features, int *n);
+int bx_ss_track_attrs_set_host(bx_ss *e, int seq, int n, const int32_t *ids, const double *quality,
+                               const double *conf, const int32_t *max_age);
+int bx_ss_last_feature_host(bx_ss *e, int seq, int n, const int32_t *ids, double *feats);
+int bx_ss_last_feature_set_host(bx_ss *e, int seq, int n, const int32_t *ids, const double *feats,
+                                int normalize);
 /* Last-frame statistics over sequences [seq0, seq0+nseq) (host): sums[7] = {detections kept,
  * tracks entering the frame, confirmed tracks queried next frame, gallery sample rows compared,
  * output rows, max frame counter, matches} — bench.py's unit counts. */

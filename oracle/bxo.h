@@ -152,6 +152,11 @@ typedef struct bxo_ss bxo_ss;
 bxo_ss *bxo_ss_new(const bxo_ss_params *p);
 void bxo_ss_free(bxo_ss *s);
 int bxo_ss_next_id(const bxo_ss *s);
+/* handle_occlusions=True: the OcclusionAwareTracker post-process after every update (then
+ * bxo_ss_update returns -5 where the reference raises TypeError on mutual occlusion, D7) */
+void bxo_ss_set_occlusion(bxo_ss *s, int on, double threshold);
+/* CPython set iteration order of small positive ints added in order (returns the count) */
+int bxo_pyset_order(const long *adds, int nadd, long *out);
 /* host edits of the Kalman state by track id (mirrors of the engines' bx_*_state_set_host);
  * each returns the number of ids found */
 int bxo_state_set(bxo_tracker *T, int n, const int *ids, const double *mean, const double *cov);

@@ -150,7 +150,20 @@ struct bxo_ss {
     int nlost;
     ss_gallery *gal;
     int ngal, capgal;
+    /* OcclusionAwareTracker state (handle_occlusions=True): track_visibility by id, and the
+     * occlusion_buffer (id -> deque(maxlen=10) of features[-1] copies) */
+    int occ_on;
+    double occ_thr;
+    double *vis;
+    int nvis;
+    struct occ_buf *ob;
+    int nob, capob;
 };
+
+typedef struct occ_buf {
+    int id, n;
+    double *f[10];
+} occ_buf;
 
 static double *vdup(const double *x, int F) {
     double *y = (double *)malloc(sizeof(double) * F);
@@ -186,6 +199,10 @@ bxo_ss *bxo_ss_new(const bxo_ss_params *p) {
 
 void bxo_ss_free(bxo_ss *s) {
     if (!s) return;
+    for (int b = 0; b < s->nob; b++)
+        for (int k = 0; k < s->ob[b].n; k++) free(s->ob[b].f[k]);
+    free(s->ob);
+    free(s->vis);
     for (int i = 0; i < s->ntrk; i++) track_free(s->trk[i]);
     for (int i = 0; i < s->nlost; i++) track_free(s->lost[i]);
     for (int g = 0; g < s->ngal; g++) {
@@ -1041,6 +1058,237 @@ static void tracker_update(bxo_ss *s, ss_frame *fr, int frame_id) {
     free(ud);
 }
 
+/* ------------------------------------------------------------------------------------------ */
+/* OcclusionAwareTracker.update_with_occlusion_handling (utils/occlusion_handler.py:324-339),
+ * run after the tracker update when handle_occlusions=True (strongsort.py:150-154, 195-201). */
+
+void bxo_ss_set_occlusion(bxo_ss *s, int on, double threshold) {
+    s->occ_on = on;
+    s->occ_thr = threshold;
+}
+
+/* Iteration order of a CPython (3.10) set of small positive ints after adding `adds` in order:
+ * Objects/setobject.c set_add_entry (linear probes of 9, then perturbation; hash(i) = i),
+ * growth to 4x used when fill*5 >= mask*3 (set_table_resize + set_insert_clean), iteration in
+ * table order.  Returns the number of distinct keys written to out. */
+static int pyset_order(const long *adds, int nadd, long *out) {
+    size_t mask = 7;
+    long *tab = (long *)calloc(8, sizeof(long));
+    int fill = 0;
+    for (int a = 0; a < nadd; a++) {
+        const long key = adds[a];
+        size_t perturb = (size_t)key, i = (size_t)key & mask;
+        long *e = NULL;
+        int dup = 0;
+        for (;;) {
+            e = &tab[i];
+            int probes = (i + 9 <= mask) ? 9 : 0;
+            int hit = 0;
+            do {
+                if (*e == 0) { hit = 1; break; }
+                if (*e == key) { hit = 1; dup = 1; break; }
+                e++;
+            } while (probes--);
+            if (hit) break;
+            perturb >>= 5;
+            i = (i * 5 + 1 + perturb) & mask;
+        }
+        if (dup) continue;
+        *e = key;
+        fill++;
+        if ((size_t)fill * 5 < mask * 3) continue;
+        size_t nsz = 8;
+        while (nsz <= (size_t)fill * 4) nsz <<= 1;
+        long *nt = (long *)calloc(nsz, sizeof(long));
+        const size_t nmask = nsz - 1;
+        for (size_t q = 0; q <= mask; q++) {
+            if (!tab[q]) continue;
+            size_t pp = (size_t)tab[q], j = (size_t)tab[q] & nmask;
+            for (;;) {
+                long *f = &nt[j];
+                if (*f == 0) { *f = tab[q]; break; }
+                int done = 0;
+                if (j + 9 <= nmask)
+                    for (int l = 0; l < 9; l++) {
+                        f++;
+                        if (*f == 0) { *f = tab[q]; done = 1; break; }
+                    }
+                if (done) break;
+                pp >>= 5;
+                j = (j * 5 + 1 + pp) & nmask;
+            }
+        }
+        free(tab);
+        tab = nt;
+        mask = nmask;
+    }
+    int m = 0;
+    for (size_t q = 0; q <= mask; q++)
+        if (tab[q]) out[m++] = tab[q];
+    free(tab);
+    return m;
+}
+
+/* exported for tests/test_oracle.py (checked against CPython's own sets) */
+int bxo_pyset_order(const long *adds, int nadd, long *out) { return pyset_order(adds, nadd, out); }
+
+static double occ_vis(const bxo_ss *s, int id) { return id < s->nvis ? s->vis[id] : 1.0; }
+
+static occ_buf *occ_find(bxo_ss *s, int id) {
+    for (int b = 0; b < s->nob; b++)
+        if (s->ob[b].id == id) return &s->ob[b];
+    return NULL;
+}
+
+/* Returns 0, or -5 where the reference raises TypeError (_resolve_mutual_occlusion, D7). */
+static int occlusion_update(bxo_ss *s) {
+    const int n = s->ntrk, F = s->F;
+    if (n == 0) return 0;
+    double(*b)[4] = (double(*)[4])malloc(sizeof(double) * 4 * n);
+    double *area = (double *)malloc(sizeof(double) * n);
+    double *ov = (double *)calloc((size_t)n * n, sizeof(double));
+    double *sr = (double *)calloc((size_t)n * n, sizeof(double));
+    long *adds = (long *)malloc(sizeof(long) * (size_t)n * n);
+    int *nadd = (int *)calloc(n, sizeof(int));
+    for (int i = 0; i < n; i++) {
+        to_tlwh(s->trk[i], b[i]);
+        /* the tlwh rows are read as xyxy (compute_overlap_matrix :49-56,
+         * analyze_spatial_relationships :109-113) */
+        area[i] = (b[i][2] - b[i][0]) * (b[i][3] - b[i][1]);
+    }
+    for (int i = 0; i < n; i++)
+        for (int j = i + 1; j < n; j++) {
+            const double xx1 = pymax(b[i][0], b[j][0]), yy1 = pymax(b[i][1], b[j][1]);
+            const double xx2 = pymin(b[i][2], b[j][2]), yy2 = pymin(b[i][3], b[j][3]);
+            const double inter = pymax(0, xx2 - xx1) * pymax(0, yy2 - yy1);
+            if (inter > 0) {
+                const double m = pymax(inter / area[i], inter / area[j]);
+                ov[(size_t)i * n + j] = ov[(size_t)j * n + i] = m;
+            }
+            const double r = area[j] > 0 ? area[i] / area[j] : 1.0; /* size_ratio_matrix */
+            sr[(size_t)i * n + j] = r;
+            sr[(size_t)j * n + i] = 1.0 / r;
+        }
+    int rc = 0;
+    double *vis = (double *)malloc(sizeof(double) * n);
+    for (int i = 0; i < n && !rc; i++) { /* update_occlusion_state :163-207 */
+        double v = 1.0;
+        for (int j = 0; j < n; j++) {
+            if (i == j) continue;
+            const double o = ov[(size_t)i * n + j];
+            if (!(o > s->occ_thr)) continue;
+            const double r = sr[(size_t)i * n + j];
+            int occluder, occluded;
+            if (r > 1.2) occluder = i, occluded = j;
+            else if (r < 0.8) occluder = j, occluded = i;
+            else { rc = -5; break; } /* MUTUAL: `list(int)` raises TypeError (D7) */
+            adds[(size_t)occluded * n + nadd[occluded]++] = s->trk[occluder]->id;
+            if (occluded == i) v *= (1.0 - o);
+        }
+        vis[i] = v;
+    }
+    if (!rc) {
+        for (int i = 0; i < n; i++) { /* track_visibility[track_i] = visibility_score */
+            const int id = s->trk[i]->id;
+            if (id >= s->nvis) {
+                int nn = s->nvis ? s->nvis : 64;
+                while (nn <= id) nn *= 2;
+                s->vis = (double *)realloc(s->vis, sizeof(double) * nn);
+                for (int q = s->nvis; q < nn; q++) s->vis[q] = 1.0;
+                s->nvis = nn;
+            }
+            s->vis[id] = vis[i];
+        }
+        /* _apply_occlusion_modifications (:341-371), tracks in list order */
+        for (int i = 0; i < n; i++) {
+            ss_track *t = s->trk[i];
+            const double level = 1.0 - occ_vis(s, t->id);
+            if (level > 0.3) {
+                /* int(track._max_age * 2.0): doubles every occluded frame; held at 2^30 (the
+                 * deletion threshold int(max_age * 1.5) then still fits an int and is never
+                 * reached) */
+                t->max_age = t->max_age >= (1 << 29) ? (1 << 30) : (int)(t->max_age * 2.0);
+                if (t->nfeat) {
+                    occ_buf *q = occ_find(s, t->id);
+                    if (!q) {
+                        if (s->nob == s->capob) {
+                            s->capob = s->capob ? 2 * s->capob : 16;
+                            s->ob = (occ_buf *)realloc(s->ob, sizeof(occ_buf) * s->capob);
+                        }
+                        q = &s->ob[s->nob++];
+                        q->id = t->id;
+                        q->n = 0;
+                    }
+                    if (q->n == 10) { /* deque(maxlen=10) drops the oldest */
+                        free(q->f[0]);
+                        memmove(q->f, q->f + 1, sizeof(double *) * 9);
+                        q->n--;
+                    }
+                    q->f[q->n++] = vdup(t->feat[t->nfeat - 1], F);
+                }
+                t->quality = pymax(t->quality, 0.6);
+                if (level > 0.8) { /* predict_track_position (:268-305) + :373-392 */
+                    long *order = (long *)malloc(sizeof(long) * (nadd[i] + 1));
+                    const int k = pyset_order(adds + (size_t)i * n, nadd[i], order);
+                    double c0 = 0.0, c1 = 0.0;
+                    int kc = 0;
+                    for (int q = 0; q < k; q++)
+                        for (int j = 0; j < n; j++) {
+                            if (j == i || s->trk[j]->id != order[q]) continue;
+                            double bb[4];
+                            to_tlwh(s->trk[j], bb); /* the current (possibly edited) mean */
+                            const double cx = (bb[0] + bb[2]) / 2, cy = (bb[1] + bb[3]) / 2;
+                            c0 = kc ? c0 + cx : cx;
+                            c1 = kc ? c1 + cy : cy;
+                            kc++;
+                        }
+                    free(order);
+                    if (kc) {
+                        const double px = c0 / kc - 50 / 2.0, py = c1 / kc - 100 / 2.0;
+                        const double pw = 50.0, ph = 100.0;
+                        t->mean[0] = px + pw / 2;
+                        t->mean[1] = py + ph / 2;
+                        t->mean[2] = pw / ph;
+                        t->mean[3] = ph;
+                        for (int r = 0; r < 4; r++)
+                            for (int c = 0; c < 4; c++) t->cov[8 * r + c] *= 1.5;
+                    }
+                }
+            } else {
+                occ_buf *q = occ_find(s, t->id);
+                if (q) { /* _handle_emerging_track (:394-417) */
+                    t->conf = pymin(t->conf + 0.1, 1.0);
+                    if (q->n && t->nfeat) {
+                        int best = 0;
+                        double bn = wave_norm(q->f[0], F);
+                        for (int k = 1; k < q->n; k++) {
+                            const double v = wave_norm(q->f[k], F);
+                            if (v > bn) bn = v, best = k;
+                        }
+                        double *cur = t->feat[t->nfeat - 1];
+                        double *bl = (double *)malloc(sizeof(double) * F);
+                        for (int k = 0; k < F; k++) bl[k] = 0.7 * cur[k] + 0.3 * q->f[best][k];
+                        const double nb = wave_norm(bl, F) + 1e-8;
+                        for (int k = 0; k < F; k++) bl[k] /= nb;
+                        free(cur);
+                        t->feat[t->nfeat - 1] = bl;
+                    }
+                    for (int k = 0; k < q->n; k++) free(q->f[k]);
+                    *q = s->ob[--s->nob]; /* del self.occlusion_buffer[track.id] */
+                }
+            }
+        }
+    }
+    free(vis);
+    free(b);
+    free(area);
+    free(ov);
+    free(sr);
+    free(adds);
+    free(nadd);
+    return rc;
+}
+
 static int format_outputs(const bxo_ss *s, double *out, int cap) {
     int m = 0;
     for (int i = 0; i < s->ntrk; i++) {
@@ -1052,7 +1300,8 @@ static int format_outputs(const bxo_ss *s, double *out, int cap) {
         double *o = out + 10 * m++;
         o[0] = b[0], o[1] = b[1], o[2] = b[2], o[3] = b[3];
         o[4] = t->id, o[5] = t->conf, o[6] = t->cls, o[7] = t->det_ind;
-        o[8] = t->quality, o[9] = 0.0; /* occlusion level: handle_occlusions=False */
+        /* occlusion level (strongsort.py:345-348): 0 unless handle_occlusions */
+        o[8] = t->quality, o[9] = s->occ_on ? 1.0 - occ_vis(s, t->id) : 0.0;
     }
     return m;
 }
@@ -1130,7 +1379,8 @@ int bxo_ss_update(bxo_ss *s, const double *dets, int n, const double *embs, int 
         for (int i = 0; i < s->ntrk; i++) track_predict(s->trk[i]);
         tracker_update(s, &fr, s->frame_count);
     }
-    const int m = format_outputs(s, out, out_cap);
+    const int occ = s->occ_on ? occlusion_update(s) : 0;
+    const int m = occ ? occ : format_outputs(s, out, out_cap);
     for (int k = 0; k < fr.nd; k++) {
         free(fr.d[k].feat);
         free(fr.dn[k]);

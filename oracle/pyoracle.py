@@ -167,6 +167,8 @@ def lib():
         L.bxo_kf_boost_predict.argtypes = [C.c_int, _dp, _dp]
         L.bxo_kf_boost_mh_dist.argtypes = [C.c_int, _dp, C.c_int, _dp, _dp, _dp]
         L.bxo_select_class.argtypes = [C.c_void_p, C.c_int]
+        L.bxo_ss_set_occlusion.argtypes = [C.c_void_p, C.c_int, C.c_double]
+        L.bxo_pyset_order.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         L.bxo_set_frame_count.argtypes = [C.c_void_p, C.c_int]
         L.bxo_ocsort_set_id_count.argtypes = [C.c_void_p, C.c_int]
         L.bxo_boost_set_frame_count.argtypes = [C.c_void_p, C.c_int]
@@ -330,6 +332,14 @@ def linear_assignment(cost, thresh):
     return m[: 2 * nm.value].reshape(-1, 2), ua[: nua.value], ub[: nub.value]
 
 
+def pyset_order(adds):
+    """The oracle's emulation of CPython's set iteration order (bxo_pyset_order)."""
+    a = np.ascontiguousarray(adds, np.int64)
+    out = np.zeros(max(a.size, 1), np.int64)
+    m = lib().bxo_pyset_order(a.ctypes.data, a.size, out.ctypes.data)
+    return out[:m].tolist()
+
+
 def kf_xysr(op, x, P, arg=None, q_xy=0.01, q_s=0.0001):
     """Op-level XYSR filter (bxo_kf_xysr_*): op in initiate (arg = boxes [n,4]), predict,
     update (arg = z [n,4]); returns new (x [n,7], P [n,7,7])."""
@@ -414,10 +424,10 @@ class OracleTracker:
             self._bp = boost_params(**p)
             self.h = L.bxo_boost_new(C.byref(self._bp))
         elif kind == "strongsort":
-            if p.get("handle_occlusions", False):
-                raise NotImplementedError("oracle StrongSort: handle_occlusions=False only")
             self._sp = ss_params(**p)
             self.h = L.bxo_ss_new(C.byref(self._sp))
+            if p.get("handle_occlusions", False):  # OcclusionAwareTracker post-process
+                L.bxo_ss_set_occlusion(self.h, 1, float(p.get("occlusion_threshold", 0.3)))
         else:
             raise KeyError(kind)
         self._cap = 1024
@@ -494,6 +504,8 @@ class OracleTracker:
             cap = max(self._cap, 2 * n + 64)
             out = np.zeros((cap, 10))
             m = lib().bxo_ss_update(self.h, _d(dets), n, ep, fd, w, _d(out), cap)
+            if m == -5:  # the reference's _resolve_mutual_occlusion
+                raise TypeError("'int' object is not iterable")
             if m < 0:
                 raise RuntimeError(f"oracle update failed ({m})")
             return out[:m].copy()

@@ -19,6 +19,16 @@ def fixture_frames(fx):
             yield t, d, e
 
 
+def fixture_crash(fx):
+    """(frame_no, dets, embs) of the frame where the reference raised TypeError (the StrongSort
+    occlusion handler's mutual-occlusion crash, D7), or None."""
+    if "crash_frame" not in fx.files or not int(fx["crash_frame"]):
+        return None
+    t = int(fx["crash_frame"])
+    d, e, _ = SyntheticScene(**ast.literal_eval(str(fx["scene"]))).frame(t)
+    return t, d, e
+
+
 def fixture_warp(fx, f):
     """The 2x3 CMC warp a fixture's frame ``f`` was captured with (None = identity CMC)."""
     if "warps" not in fx.files:

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from oracle import pyoracle as po
-from tests.golden_util import (compare_outputs, fixture_frames, fixture_tracker_args,
+from tests.golden_util import (compare_outputs, fixture_crash, fixture_frames, fixture_tracker_args,
                                fixture_warp)
 
 pytestmark = pytest.mark.gpu
@@ -386,7 +386,12 @@ def test_tracker_fixture_parity(torch_cuda, path):
             oo = orc.update(d, e, fixture_warp(fx, f)).reshape(-1, ncol)
             np.testing.assert_array_equal(o, oo, err_msg=f"frame {f}: GPU != oracle")
         rows.append(np.concatenate([np.full((o.shape[0], 1), f), o], 1))
-    compare_outputs(np.concatenate(rows, 0), fx["outputs"], box_atol=1e-9,
+    crash = fixture_crash(fx)
+    if crash is not None:  # the reference raised TypeError here (occlusion handler, D7)
+        with pytest.raises(TypeError, match="not iterable"):
+            tr.update(crash[1], img, crash[2])
+    got = np.concatenate(rows, 0) if rows else np.zeros((0, fx["outputs"].shape[1]))
+    compare_outputs(got, fx["outputs"], box_atol=1e-9,
                     conf_atol=1e-9 if kind == "boosttrack" else None)
 
 
@@ -1040,8 +1045,8 @@ def test_strongsort_dropin(torch_cuda, monkeypatch):
     monkeypatch.setenv("GITHUB_ACTIONS", "true")
     monkeypatch.delenv("GITHUB_JOB", raising=False)
     img = np.zeros((720, 1280, 3), np.uint8)
-    t = create_tracker("strongsort", handle_occlusions=False) if False else StrongSort()
-    orc = po.OracleTracker("strongsort", **SS_ARGS)
+    t = StrongSort()  # the reference's defaults: handle_occlusions=True
+    orc = po.OracleTracker("strongsort", **SS_ARGS, handle_occlusions=True)
     rng = np.random.default_rng(5)
     base = rng.standard_normal((3, 32))
     d = np.array([[10, 10, 60, 120, 0.9, 0], [200, 50, 260, 170, 0.8, 2],
@@ -1094,12 +1099,19 @@ def test_run_sequences_matches_per_sequence_dropins(torch_cuda, tmp_path, kind):
         np.savetxt(ep, e, fmt="%f")
         packed[nm] = motio.pack_sequence(dp, ep, tmp_path / f"{nm}.bxmot")
         frame_ids[nm] = list(range(1, int(r[:, 0].max()) + 2))  # image frames, some empty
-    motio.run_sequences(kind, packed, tmp_path / "batched", frame_ids=frame_ids)
+    # StrongSort: MOT17-02 has mutually occluding tracks at the top-left corner, where the
+    # default handle_occlusions=True raises (D7) in the runner and the drop-in alike
+    kw = dict(handle_occlusions=False) if kind == "strongsort" else {}
+    if kind == "strongsort":
+        with pytest.raises(TypeError, match="not iterable"):
+            motio.run_sequences(kind, packed, tmp_path / "crash", frame_ids=frame_ids)
+    motio.run_sequences(kind, packed, tmp_path / "batched", frame_ids=frame_ids,
+                        tracker_kwargs=kw)
     img = np.zeros((1080, 1920, 3), np.uint8)
     for nm in rows:
         ByteTrack.clear_count()
         BoostTrack._id_count = 0
-        tr = create_tracker(kind)
+        tr = create_tracker(kind, evolve_param_dict=kw) if kw else create_tracker(kind)
         dets = np.loadtxt(tmp_path / f"{nm}.dets.txt", comments="#")
         embs = np.loadtxt(tmp_path / f"{nm}.embs.txt", comments="#")
         out = []
