@@ -292,6 +292,55 @@ def load_traffic(config, stage):
         return None
 
 
+def run_dropin(args):
+    """The drop-in single-stream path: `create_tracker(kind).update(dets, img, embs)` per frame on
+    one sequence, numpy inputs in host memory (how val.py and Ultralytics call the trackers), the
+    wall time of the update calls only (input generation excluded).  One JSON line."""
+    from boxmot_amd.synth import SyntheticScene
+    from boxmot_amd.tracker_zoo import create_tracker
+
+    kind, n_obj, F, params = CONFIGS[args.config]
+    os.environ.setdefault("GITHUB_ACTIONS", "true")  # StrongSort born Confirmed, as its fixtures
+    extra = dict(conf_lo=OCS_CONF_LO) if kind in ("ocsort", "boosttrack", "strongsort") else {}
+    if kind in ("boosttrack", "strongsort"):
+        extra["emb_dtype"] = np.float64
+    sc = SyntheticScene(n_obj=n_obj, seed=777, emb_dim=F,
+                        layout="crowded" if args.config.endswith("_crowded") else "grid", **extra)
+    kw = {k: v for k, v in params.items() if k != "born_confirmed"}
+    if kind == "strongsort":
+        kw.update(handle_occlusions=False, **ss_caps(args.config, n_obj))
+    tr = create_tracker(kind, evolve_param_dict=kw)
+    img = np.zeros((1080, 1920, 3), np.uint8)
+    frames = [sc.frame(t) for t in range(1, args.warmup + args.steps + 1)]
+    for d, e, _ in frames[: args.warmup]:
+        tr.update(d, img, e) if F else tr.update(d, img)
+    t0 = time.perf_counter()
+    for d, e, _ in frames[args.warmup:]:
+        tr.update(d, img, e) if F else tr.update(d, img)
+    wall = time.perf_counter() - t0
+    mean_d = float(np.mean([f[0].shape[0] for f in frames[args.warmup:]]))
+    ref = REFERENCE_CPU_FPS.get(args.config)
+    line = {
+        "metric": METRIC, "value": round(args.steps / wall, 1), "unit": "frames/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "none", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (numpy scenes in host memory, as the drop-in contract takes them)",
+        "config": {"workload": f"{args.config} drop-in: one sequence x {n_obj} tracks x "
+                               f"~{mean_d:.0f} dets" + (f" x {F}-d ReID" if F else "") +
+                               ", tracker.update() per frame",
+                   "tracker": kind, "n_seq_per_gpu": 1, "n_tracks": n_obj,
+                   "n_dets_mean": round(mean_d, 1), "feat_dim": F, "parallelism": "single stream"},
+        "roofline": {"bound": "latency", "note": "one sequence per call: launch and host<->device "
+                                                 "latency bound, not an HBM/MFMA roofline"},
+        "cpu_baseline": None if ref is None else {
+            "value": ref[0], "unit": "frames/s", "cores": 1, "kind": "reference",
+            "sample": f"the reference's Python tracker, {ref[1]}, survey container Intel Xeon "
+                      f"(BASELINE.md §2)"},
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -305,10 +354,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--dropin", action="store_true",
+                    help="time the drop-in tracker.update() on one sequence instead")
     args = ap.parse_args()
     if args.cpu_worker:
         print(json.dumps(cpu_worker(json.loads(args.cpu_worker))), flush=True)
         return
+    if args.dropin:
+        return run_dropin(args)
 
     import torch
 

@@ -1089,6 +1089,15 @@ struct bx_boost {
   double* h_warp = nullptr;
   double* h_out = nullptr;
   int* h_cnt = nullptr;
+  // pinned mirrors for update_host (asynchronous copies, one sync per frame) and the counters
+  // row of the last update_host sequence (bx_boost_counters_host answers from it)
+  float* p_dets = nullptr;
+  double* p_embs = nullptr;
+  double* p_warp = nullptr;
+  double* p_out = nullptr;
+  int* p_cnt = nullptr;
+  int* p_sq = nullptr;
+  int cache_seq = -1;
   // per_class host path (bx_boost_update_classes_host): class offsets [C][2], counts [C], the
   // held frame counter
   int n_classes = 0;
@@ -1256,6 +1265,12 @@ int bx_boost_create(const bx_boost_config* c, bx_boost** out) {
   BCHK(hipMalloc(&e->h_warp, sizeof(double) * 6));
   BCHK(hipMalloc(&e->h_out, sizeof(double) * 8 * D));
   BCHK(hipMalloc(&e->h_cnt, sizeof(int)));
+  BCHK(hipHostMalloc(&e->p_dets, sizeof(float) * 6 * d.D));
+  BCHK(hipHostMalloc(&e->p_embs, sizeof(double) * (size_t)d.D * (d.F ? d.F : 1)));
+  BCHK(hipHostMalloc(&e->p_warp, sizeof(double) * 8));
+  BCHK(hipHostMalloc(&e->p_out, sizeof(double) * 8 * d.D));
+  BCHK(hipHostMalloc(&e->p_cnt, sizeof(int) * 4));
+  BCHK(hipHostMalloc(&e->p_sq, sizeof(int) * SQB));
   *out = e;
   return BX_OK;
 }
@@ -1273,6 +1288,12 @@ int bx_boost_destroy(bx_boost* e) {
   (void)hipFree(e->h_warp);
   (void)hipFree(e->h_out);
   (void)hipFree(e->h_cnt);
+  (void)hipHostFree(e->p_dets);
+  (void)hipHostFree(e->p_embs);
+  (void)hipHostFree(e->p_warp);
+  (void)hipHostFree(e->p_out);
+  (void)hipHostFree(e->p_cnt);
+  (void)hipHostFree(e->p_sq);
   (void)hipFree(e->h_coff);
   (void)hipFree(e->h_ccnt);
   (void)hipFree(e->h_hold);
@@ -1284,6 +1305,7 @@ int bx_boost_reset(bx_boost* e, int seq0, int nseq, void* stream) {
   if (!e || seq0 < 0 || nseq < 0 || seq0 + nseq > e->dev.S)
     return bx_record_error(BX_ERR_INVALID, "bad sequence range");
   if (!nseq) return BX_OK;
+  e->cache_seq = -1;
   hipLaunchKernelGGL(boost_reset_kernel, dim3((nseq * SQB + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, e->dev, seq0, nseq);
   BCHK(hipGetLastError());
@@ -1295,6 +1317,7 @@ int bx_boost_step(bx_boost* e, int seq0, int nseq, const float* dets, const int3
                   void* stream) {
   if (!e || seq0 < 0 || nseq <= 0 || seq0 + nseq > e->dev.S || !det_off || !out || !out_count)
     return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_boost_step");
+  e->cache_seq = -1;
   return launch(e, seq0, nseq, dets, det_off, embs, warps, out, out_count, (hipStream_t)stream);
 }
 
@@ -1306,23 +1329,38 @@ int bx_boost_update_host(bx_boost* e, int seq, const float* dets, int n, const d
   if (e->dev.reid && n && !embs)
     return bx_record_error(BX_ERR_SHAPE, "with_reid BoostTrack needs embeddings");
   hipStream_t st = (hipStream_t)stream;
-  const int off[2] = {0, n};
-  if (n) BCHK(hipMemcpyAsync(e->h_dets, dets, sizeof(float) * 6 * n, hipMemcpyHostToDevice, st));
-  if (n && e->dev.reid)
-    BCHK(hipMemcpyAsync(e->h_embs, embs, sizeof(double) * (size_t)n * e->dev.F,
+  // pinned mirrors: asynchronous copies in, the frame, rows (at most n) + count + status +
+  // counters back, one synchronisation
+  if (n) {
+    memcpy(e->p_dets, dets, sizeof(float) * 6 * n);
+    BCHK(hipMemcpyAsync(e->h_dets, e->p_dets, sizeof(float) * 6 * n, hipMemcpyHostToDevice, st));
+  }
+  if (n && e->dev.reid) {
+    memcpy(e->p_embs, embs, sizeof(double) * (size_t)n * e->dev.F);
+    BCHK(hipMemcpyAsync(e->h_embs, e->p_embs, sizeof(double) * (size_t)n * e->dev.F,
                         hipMemcpyHostToDevice, st));
-  if (warp) BCHK(hipMemcpyAsync(e->h_warp, warp, sizeof(double) * 6, hipMemcpyHostToDevice, st));
-  BCHK(hipMemcpyAsync(e->h_off, off, sizeof(off), hipMemcpyHostToDevice, st));
+  }
+  if (warp) {
+    memcpy(e->p_warp, warp, sizeof(double) * 6);
+    BCHK(hipMemcpyAsync(e->h_warp, e->p_warp, sizeof(double) * 6, hipMemcpyHostToDevice, st));
+  }
+  e->p_cnt[2] = 0;
+  e->p_cnt[3] = n;
+  BCHK(hipMemcpyAsync(e->h_off, e->p_cnt + 2, sizeof(int) * 2, hipMemcpyHostToDevice, st));
+  e->cache_seq = -1;
   int rc = launch(e, seq, 1, e->h_dets, e->h_off, e->dev.reid ? e->h_embs : nullptr,
                   warp ? e->h_warp : nullptr, e->h_out, e->h_cnt, st);
   if (rc) return rc;
-  int cnt = 0;
-  BCHK(hipMemcpyAsync(&cnt, e->h_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+  BCHK(hipMemcpyAsync(e->p_cnt, e->h_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+  BCHK(hipMemcpyAsync(e->p_cnt + 1, e->dev.status, sizeof(int), hipMemcpyDeviceToHost, st));
+  if (n) BCHK(hipMemcpyAsync(e->p_out, e->h_out, sizeof(double) * 8 * n, hipMemcpyDeviceToHost, st));
+  BCHK(hipMemcpyAsync(e->p_sq, e->dev.seqst + (size_t)seq * SQB, sizeof(int) * SQB,
+                      hipMemcpyDeviceToHost, st));
   BCHK(hipStreamSynchronize(st));
-  if (cnt) BCHK(hipMemcpy(out, e->h_out, sizeof(double) * 8 * cnt, hipMemcpyDeviceToHost));
+  const int cnt = e->p_cnt[0], status = e->p_cnt[1];
+  e->cache_seq = seq;
+  if (cnt) memcpy(out, e->p_out, sizeof(double) * 8 * cnt);
   *n_out = cnt;
-  int status = 0;
-  BCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
   if (status)
     return bx_record_error(status, status == BX_ERR_CAPACITY ? "detections exceed det_cap"
                                                              : "a sequence ran out of track slots (raise track_cap)");
@@ -1347,6 +1385,7 @@ int bx_boost_update_classes_host(bx_boost* e, int seq, const float* dets, int n,
   const int C = n_classes, F = e->dev.F;
   if (e->n_classes && e->n_classes != C)
     return bx_record_error(BX_ERR_INVALID, "n_classes differs from the engine's first per-class call");
+  e->cache_seq = -1;
   if (!e->n_classes) {
     e->n_classes = C;
     BCHK(hipMalloc(&e->h_coff, sizeof(int) * 2 * C));
@@ -1451,8 +1490,12 @@ int bx_boost_status(bx_boost* e, int* status) {
 int bx_boost_counters_host(bx_boost* e, int seq, int* frame_count, int* id_count, int* n_tracks) {
   if (!e || seq < 0 || seq >= e->dev.S) return bx_record_error(BX_ERR_INVALID, "bad sequence");
   int s[SQB];
-  BCHK(hipDeviceSynchronize());
-  BCHK(hipMemcpy(s, e->dev.seqst + (size_t)seq * SQB, sizeof(s), hipMemcpyDeviceToHost));
+  if (seq == e->cache_seq) {
+    memcpy(s, e->p_sq, sizeof(s));
+  } else {
+    BCHK(hipDeviceSynchronize());
+    BCHK(hipMemcpy(s, e->dev.seqst + (size_t)seq * SQB, sizeof(s), hipMemcpyDeviceToHost));
+  }
   if (frame_count) *frame_count = s[SB_FRAME];
   if (id_count) *id_count = s[SB_IDS];
   if (n_tracks) *n_tracks = s[SB_NTR];
@@ -1461,6 +1504,7 @@ int bx_boost_counters_host(bx_boost* e, int seq, int* frame_count, int* id_count
 
 int bx_boost_set_id_count(bx_boost* e, int seq, int id_count, void* stream) {
   if (!e || seq < 0 || seq >= e->dev.S) return bx_record_error(BX_ERR_INVALID, "bad sequence");
+  e->cache_seq = -1;
   BCHK(hipMemcpyAsync(e->dev.seqst + (size_t)seq * SQB + SB_IDS, &id_count, sizeof(int),
                       hipMemcpyHostToDevice, (hipStream_t)stream));
   BCHK(hipStreamSynchronize((hipStream_t)stream));

@@ -1672,6 +1672,16 @@ struct bx_engine {
   double* h_out;
   int* h_cnt;
   double* h_warp;
+  // pinned host mirrors of the staging buffers (update_host: true async copies, one sync):
+  // dets, embs, offsets + counters, warp, output rows, out count + status
+  float* p_dets = nullptr;
+  char* p_embs = nullptr;
+  int* p_off = nullptr;
+  double* p_warp = nullptr;
+  double* p_out = nullptr;
+  int* p_cnt = nullptr;
+  int* p_seq = nullptr;     // the sequence's counters row after the last update_host
+  int cache_seq = -1;       // sequence whose counters p_seq holds (-1: none / stale)
   // side stream of the frame's fork-join (launch_frame): the ReID feature kernels K1 and K5 run
   // there beside the Kalman/list kernels they share no data with
   hipStream_t side = nullptr;
@@ -1946,6 +1956,13 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
   HIPCHK(hipMalloc(&e->h_out, sizeof(double) * 8 * D));
   HIPCHK(hipMalloc(&e->h_cnt, sizeof(int)));
   HIPCHK(hipMalloc(&e->h_warp, sizeof(double) * 6));
+  HIPCHK(hipHostMalloc(&e->p_dets, sizeof(float) * 6 * D));
+  HIPCHK(hipHostMalloc(&e->p_embs, fs * (size_t)D * (F ? F : 1)));
+  HIPCHK(hipHostMalloc(&e->p_off, sizeof(int) * 2));
+  HIPCHK(hipHostMalloc(&e->p_warp, sizeof(double) * 6));
+  HIPCHK(hipHostMalloc(&e->p_out, sizeof(double) * 8 * D));
+  HIPCHK(hipHostMalloc(&e->p_cnt, sizeof(int) * 2));
+  HIPCHK(hipHostMalloc(&e->p_seq, sizeof(int) * SQ_STRIDE));
   *out = e;
   return BX_OK;
 }
@@ -1971,6 +1988,13 @@ int bx_engine_destroy(bx_engine* e) {
   (void)hipFree(e->h_out);
   (void)hipFree(e->h_cnt);
   (void)hipFree(e->h_warp);
+  (void)hipHostFree(e->p_dets);
+  (void)hipHostFree(e->p_embs);
+  (void)hipHostFree(e->p_off);
+  (void)hipHostFree(e->p_warp);
+  (void)hipHostFree(e->p_out);
+  (void)hipHostFree(e->p_cnt);
+  (void)hipHostFree(e->p_seq);
   for (char* p : e->park) (void)hipFree(p);
   (void)hipFree(e->h_coff);
   (void)hipFree(e->h_ccnt);
@@ -1981,6 +2005,7 @@ int bx_engine_destroy(bx_engine* e) {
 int bx_engine_reset(bx_engine* e, int seq0, int nseq, void* stream) {
   if (!e || seq0 < 0 || nseq <= 0 || seq0 + nseq > e->dev.S)
     return set_err(BX_ERR_INVALID, "bad sequence range");
+  e->cache_seq = -1;
   hipLaunchKernelGGL(reset_kernel, dim3(nseq), dim3(256), 0, (hipStream_t)stream, e->dev.seq,
                      e->dev.flags, e->dev.T, seq0, nseq);
   HIPCHK(hipGetLastError());
@@ -2000,6 +2025,7 @@ int bx_engine_step(bx_engine* e, int seq0, int nseq, const float* dets, const in
     return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_step");
   if (e->dev.with_reid && !embs) return set_err(BX_ERR_SHAPE, "BoT-SORT with_reid needs embs");
   hipStream_t st = (hipStream_t)stream;
+  e->cache_seq = -1;
   if (e->dev.kind == BX_BYTETRACK)
     return launch_frame<KIND_BYTE, float, true>(e, seq0, nseq, dets, det_off, embs, warps, out,
                                                 out_count, st);
@@ -2025,23 +2051,32 @@ int bx_engine_update_host(bx_engine* e, int seq, const float* dets, int n, const
   std::lock_guard<std::mutex> lk(e->mu);
   hipStream_t st = (hipStream_t)stream;
   const size_t fs = e->cfg.emb_f64 ? 8 : 4;
-  int off[2] = {0, n};
-  if (n) HIPCHK(hipMemcpyAsync(e->h_dets, dets, sizeof(float) * 6 * n, hipMemcpyHostToDevice, st));
-  if (n && e->dev.with_reid)
-    HIPCHK(hipMemcpyAsync(e->h_embs, embs, fs * (size_t)n * e->dev.F, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(e->h_off, off, sizeof(off), hipMemcpyHostToDevice, st));
-  if (warp) HIPCHK(hipMemcpyAsync(e->h_warp, warp, sizeof(double) * 6, hipMemcpyHostToDevice, st));
+  // inputs through pinned mirrors (asynchronous DMA), the frame, then the rows (at most n), the
+  // count and the status back in one go: a single synchronisation per frame
+  const bool ecopy = n && e->dev.with_reid;
+  if (n) memcpy(e->p_dets, dets, sizeof(float) * 6 * n);
+  if (ecopy) memcpy(e->p_embs, embs, fs * (size_t)n * e->dev.F);
+  e->p_off[0] = 0;
+  e->p_off[1] = n;
+  if (warp) memcpy(e->p_warp, warp, sizeof(double) * 6);
+  if (n) HIPCHK(hipMemcpyAsync(e->h_dets, e->p_dets, sizeof(float) * 6 * n, hipMemcpyHostToDevice, st));
+  if (ecopy)
+    HIPCHK(hipMemcpyAsync(e->h_embs, e->p_embs, fs * (size_t)n * e->dev.F, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(e->h_off, e->p_off, sizeof(int) * 2, hipMemcpyHostToDevice, st));
+  if (warp) HIPCHK(hipMemcpyAsync(e->h_warp, e->p_warp, sizeof(double) * 6, hipMemcpyHostToDevice, st));
   int rc = bx_engine_step(e, seq, 1, e->h_dets, e->h_off, e->h_embs, warp ? e->h_warp : nullptr,
                           e->h_out, e->h_cnt, stream);
   if (rc) return rc;
-  int cnt = 0;
-  HIPCHK(hipMemcpyAsync(&cnt, e->h_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(e->p_cnt, e->h_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(e->p_cnt + 1, e->dev.status, sizeof(int), hipMemcpyDeviceToHost, st));
+  if (n) HIPCHK(hipMemcpyAsync(e->p_out, e->h_out, sizeof(double) * 8 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(e->p_seq, e->dev.seq + (size_t)seq * SQ_STRIDE, sizeof(int) * SQ_STRIDE,
+                        hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  if (cnt && out)
-    HIPCHK(hipMemcpy(out, e->h_out, sizeof(double) * 8 * cnt, hipMemcpyDeviceToHost));
+  e->cache_seq = seq;  // bx_engine_counters_host answers from it until the next device change
+  const int cnt = e->p_cnt[0], status = e->p_cnt[1];
+  if (cnt && out) memcpy(out, e->p_out, sizeof(double) * 8 * cnt);
   *n_out = cnt;
-  int status = 0;
-  HIPCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
   if (status & (1 << BX_ERR_TRACK_OVERFLOW))
     return set_err(BX_ERR_TRACK_OVERFLOW, "a sequence ran out of track slots (raise track_cap)");
   return BX_OK;
@@ -2202,7 +2237,10 @@ int bx_engine_counters_host(bx_engine* e, int seq, int* frame_count, int* id_cou
                             int* n_lost) {
   if (!e || seq < 0 || seq >= e->dev.S) return set_err(BX_ERR_INVALID, "bad sequence");
   int v[SQ_STRIDE];
-  HIPCHK(hipMemcpy(v, e->dev.seq + (size_t)seq * SQ_STRIDE, sizeof(v), hipMemcpyDeviceToHost));
+  if (seq == e->cache_seq)
+    memcpy(v, e->p_seq, sizeof(v));
+  else
+    HIPCHK(hipMemcpy(v, e->dev.seq + (size_t)seq * SQ_STRIDE, sizeof(v), hipMemcpyDeviceToHost));
   if (frame_count) *frame_count = v[SQ_FC];
   if (id_count) *id_count = v[SQ_IDC];
   if (n_active) *n_active = v[SQ_NA];
@@ -2212,6 +2250,7 @@ int bx_engine_counters_host(bx_engine* e, int seq, int* frame_count, int* id_cou
 
 int bx_engine_set_id_count(bx_engine* e, int seq, int id_count, void* stream) {
   if (!e || seq < 0 || seq >= e->dev.S) return set_err(BX_ERR_INVALID, "bad sequence");
+  e->cache_seq = -1;
   hipLaunchKernelGGL(set_id_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, e->dev.seq, seq,
                      id_count);
   HIPCHK(hipGetLastError());

@@ -974,6 +974,13 @@ struct bx_ocsort {
   int* h_off = nullptr;
   double* h_out = nullptr;
   int* h_cnt = nullptr;
+  // pinned mirrors for update_host (asynchronous copies, one sync per frame) and the counters
+  // row of the last update_host sequence (bx_ocsort_counters_host answers from it)
+  float* p_dets = nullptr;
+  double* p_out = nullptr;
+  int* p_cnt = nullptr;
+  int* p_sq = nullptr;
+  int cache_seq = -1;
   // per_class host path (bx_ocsort_update_classes_host): per sequence the local -> class-global
   // track id map and the local id counter the map covers; class offsets [C+1], counts [C]
   std::vector<std::vector<int>> gid;
@@ -1107,6 +1114,10 @@ int bx_ocsort_create(const bx_ocsort_config* c, bx_ocsort** out) {
   OCHK(hipMalloc(&e->h_off, sizeof(int) * 2));
   OCHK(hipMalloc(&e->h_out, sizeof(double) * 8 * d.D));
   OCHK(hipMalloc(&e->h_cnt, sizeof(int)));
+  OCHK(hipHostMalloc(&e->p_dets, sizeof(float) * 6 * d.D));
+  OCHK(hipHostMalloc(&e->p_out, sizeof(double) * 8 * d.D));
+  OCHK(hipHostMalloc(&e->p_cnt, sizeof(int) * 4));
+  OCHK(hipHostMalloc(&e->p_sq, sizeof(int) * SQO));
   *out = e;
   return BX_OK;
 }
@@ -1122,6 +1133,10 @@ int bx_ocsort_destroy(bx_ocsort* e) {
   (void)hipFree(e->h_off);
   (void)hipFree(e->h_out);
   (void)hipFree(e->h_cnt);
+  (void)hipHostFree(e->p_dets);
+  (void)hipHostFree(e->p_out);
+  (void)hipHostFree(e->p_cnt);
+  (void)hipHostFree(e->p_sq);
   (void)hipFree(e->h_coff);
   (void)hipFree(e->h_ccnt);
   delete e;
@@ -1132,6 +1147,7 @@ int bx_ocsort_reset(bx_ocsort* e, int seq0, int nseq, void* stream) {
   if (!e || seq0 < 0 || nseq < 0 || seq0 + nseq > e->dev.S)
     return bx_record_error(BX_ERR_INVALID, "bad sequence range");
   if (!nseq) return BX_OK;
+  e->cache_seq = -1;
   hipLaunchKernelGGL(ocsort_reset_kernel, dim3((nseq * SQO + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, e->dev, seq0, nseq);
   OCHK(hipGetLastError());
@@ -1146,6 +1162,7 @@ int bx_ocsort_step(bx_ocsort* e, int seq0, int nseq, const float* dets, const in
                    double* out, int32_t* out_count, void* stream) {
   if (!e || seq0 < 0 || nseq <= 0 || seq0 + nseq > e->dev.S || !det_off || !out || !out_count)
     return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ocsort_step");
+  e->cache_seq = -1;
   return launch(e, seq0, nseq, dets, det_off, out, out_count, (hipStream_t)stream);
 }
 
@@ -1155,18 +1172,28 @@ int bx_ocsort_update_host(bx_ocsort* e, int seq, const float* dets, int n, doubl
     return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ocsort_update_host");
   if (n > e->dev.D) return bx_record_error(BX_ERR_CAPACITY, "detections exceed det_cap");
   hipStream_t st = (hipStream_t)stream;
-  const int off[2] = {0, n};
-  if (n) OCHK(hipMemcpyAsync(e->h_dets, dets, sizeof(float) * 6 * n, hipMemcpyHostToDevice, st));
-  OCHK(hipMemcpyAsync(e->h_off, off, sizeof(off), hipMemcpyHostToDevice, st));
+  // pinned mirrors: asynchronous copies in, the frame, rows (at most n) + count + status +
+  // counters back, one synchronisation
+  if (n) {
+    memcpy(e->p_dets, dets, sizeof(float) * 6 * n);
+    OCHK(hipMemcpyAsync(e->h_dets, e->p_dets, sizeof(float) * 6 * n, hipMemcpyHostToDevice, st));
+  }
+  e->p_cnt[2] = 0;
+  e->p_cnt[3] = n;
+  OCHK(hipMemcpyAsync(e->h_off, e->p_cnt + 2, sizeof(int) * 2, hipMemcpyHostToDevice, st));
+  e->cache_seq = -1;
   int rc = launch(e, seq, 1, e->h_dets, e->h_off, e->h_out, e->h_cnt, st);
   if (rc) return rc;
-  int cnt = 0;
-  OCHK(hipMemcpyAsync(&cnt, e->h_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+  OCHK(hipMemcpyAsync(e->p_cnt, e->h_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+  OCHK(hipMemcpyAsync(e->p_cnt + 1, e->dev.status, sizeof(int), hipMemcpyDeviceToHost, st));
+  if (n) OCHK(hipMemcpyAsync(e->p_out, e->h_out, sizeof(double) * 8 * n, hipMemcpyDeviceToHost, st));
+  OCHK(hipMemcpyAsync(e->p_sq, e->dev.seqst + (size_t)seq * SQO, sizeof(int) * SQO,
+                      hipMemcpyDeviceToHost, st));
   OCHK(hipStreamSynchronize(st));
-  if (cnt) OCHK(hipMemcpy(out, e->h_out, sizeof(double) * 8 * cnt, hipMemcpyDeviceToHost));
+  const int cnt = e->p_cnt[0], status = e->p_cnt[1];
+  e->cache_seq = seq;
+  if (cnt) memcpy(out, e->p_out, sizeof(double) * 8 * cnt);
   *n_out = cnt;
-  int status = 0;
-  OCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
   if (status)
     return bx_record_error(BX_ERR_TRACK_OVERFLOW, "a sequence ran out of track slots (raise track_cap)");
   return BX_OK;
@@ -1214,6 +1241,7 @@ int bx_ocsort_update_classes_host(bx_ocsort* e, int seq0, int n_classes, const f
   }
   if (m) OCHK(hipMemcpyAsync(e->h_dets, hd.data(), sizeof(float) * 6 * m, hipMemcpyHostToDevice, st));
   OCHK(hipMemcpyAsync(e->h_coff, cnt.data(), sizeof(int) * (C + 1), hipMemcpyHostToDevice, st));
+  e->cache_seq = -1;
   int rc = launch(e, seq0, C, e->h_dets, e->h_coff, e->h_out, e->h_ccnt, st);
   if (rc) return rc;
   std::vector<int> oc(C), sq((size_t)C * SQO);
@@ -1280,8 +1308,12 @@ int bx_ocsort_counters_host(bx_ocsort* e, int seq, int* frame_count, int* id_cou
                             int* n_tracks) {
   if (!e || seq < 0 || seq >= e->dev.S) return bx_record_error(BX_ERR_INVALID, "bad sequence");
   int s[SQO];
-  OCHK(hipDeviceSynchronize());
-  OCHK(hipMemcpy(s, e->dev.seqst + (size_t)seq * SQO, sizeof(s), hipMemcpyDeviceToHost));
+  if (seq == e->cache_seq) {
+    memcpy(s, e->p_sq, sizeof(s));
+  } else {
+    OCHK(hipDeviceSynchronize());
+    OCHK(hipMemcpy(s, e->dev.seqst + (size_t)seq * SQO, sizeof(s), hipMemcpyDeviceToHost));
+  }
   if (frame_count) *frame_count = s[SO_FRAME];
   if (id_count) *id_count = s[SO_IDS];
   if (n_tracks) *n_tracks = s[SO_NTR];
@@ -1290,6 +1322,7 @@ int bx_ocsort_counters_host(bx_ocsort* e, int seq, int* frame_count, int* id_cou
 
 int bx_ocsort_set_id_count(bx_ocsort* e, int seq, int id_count, void* stream) {
   if (!e || seq < 0 || seq >= e->dev.S) return bx_record_error(BX_ERR_INVALID, "bad sequence");
+  e->cache_seq = -1;
   OCHK(hipMemcpyAsync(e->dev.seqst + (size_t)seq * SQO + SO_IDS, &id_count, sizeof(int),
                       hipMemcpyHostToDevice, (hipStream_t)stream));
   OCHK(hipStreamSynchronize((hipStream_t)stream));

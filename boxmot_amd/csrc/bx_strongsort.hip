@@ -2354,6 +2354,15 @@ struct bx_ss {
   double* h_warp = nullptr;
   double* h_out = nullptr;
   int* h_cnt = nullptr;
+  // pinned mirrors for update_host (asynchronous copies, one sync per frame) and the counters
+  // row of the last update_host sequence (bx_ss_counters_host answers from it)
+  double* p_dets = nullptr;
+  double* p_embs = nullptr;
+  double* p_warp = nullptr;
+  double* p_out = nullptr;
+  int* p_cnt = nullptr;
+  int* p_sq = nullptr;
+  int cache_seq = -1;
   int probe_stage = -1;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   int ev_used = 0;
@@ -2623,6 +2632,12 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   SCHK(hipMalloc(&e->h_warp, sizeof(double) * 6));
   SCHK(hipMalloc(&e->h_out, sizeof(double) * 10 * D));
   SCHK(hipMalloc(&e->h_cnt, sizeof(int)));
+  SCHK(hipHostMalloc(&e->p_dets, sizeof(double) * 6 * d.D));
+  SCHK(hipHostMalloc(&e->p_embs, sizeof(double) * (size_t)d.D * d.F));
+  SCHK(hipHostMalloc(&e->p_warp, sizeof(double) * 8));
+  SCHK(hipHostMalloc(&e->p_out, sizeof(double) * 10 * d.D));
+  SCHK(hipHostMalloc(&e->p_cnt, sizeof(int) * 4));
+  SCHK(hipHostMalloc(&e->p_sq, sizeof(int) * SQS));
   *out = e;
   return BX_OK;
 }
@@ -2640,6 +2655,12 @@ int bx_ss_destroy(bx_ss* e) {
   (void)hipFree(e->h_warp);
   (void)hipFree(e->h_out);
   (void)hipFree(e->h_cnt);
+  (void)hipHostFree(e->p_dets);
+  (void)hipHostFree(e->p_embs);
+  (void)hipHostFree(e->p_warp);
+  (void)hipHostFree(e->p_out);
+  (void)hipHostFree(e->p_cnt);
+  (void)hipHostFree(e->p_sq);
   delete e;
   return BX_OK;
 }
@@ -2648,6 +2669,7 @@ int bx_ss_reset(bx_ss* e, int seq0, int nseq, void* stream) {
   if (!e || seq0 < 0 || nseq < 0 || seq0 + nseq > e->dev.S)
     return bx_record_error(BX_ERR_INVALID, "bad sequence range");
   if (!nseq) return BX_OK;
+  e->cache_seq = -1;
   hipLaunchKernelGGL(ss_reset_kernel, dim3((nseq + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      e->dev, seq0, nseq);
   SCHK(hipGetLastError());
@@ -2659,6 +2681,7 @@ int bx_ss_step(bx_ss* e, int seq0, int nseq, const double* dets, const int32_t* 
                void* stream) {
   if (!e || seq0 < 0 || nseq <= 0 || seq0 + nseq > e->dev.S || !det_off || !out || !out_count)
     return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_step");
+  e->cache_seq = -1;
   return ss_launch(e, seq0, nseq, dets, det_off, embs, warps, out, out_count, (hipStream_t)stream);
 }
 
@@ -2668,24 +2691,36 @@ int bx_ss_update_host(bx_ss* e, int seq, const double* dets, int n, const double
     return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_update_host");
   if (n > e->dev.D) return bx_record_error(BX_ERR_CAPACITY, "detections exceed det_cap");
   hipStream_t st = (hipStream_t)stream;
-  const int off[2] = {0, n};
+  // pinned mirrors: asynchronous copies in, the frame, rows (at most n) + count + status +
+  // counters back, one synchronisation
   if (n) {
-    SCHK(hipMemcpyAsync(e->h_dets, dets, sizeof(double) * 6 * n, hipMemcpyHostToDevice, st));
-    SCHK(hipMemcpyAsync(e->h_embs, embs, sizeof(double) * (size_t)n * e->dev.F,
+    memcpy(e->p_dets, dets, sizeof(double) * 6 * n);
+    memcpy(e->p_embs, embs, sizeof(double) * (size_t)n * e->dev.F);
+    SCHK(hipMemcpyAsync(e->h_dets, e->p_dets, sizeof(double) * 6 * n, hipMemcpyHostToDevice, st));
+    SCHK(hipMemcpyAsync(e->h_embs, e->p_embs, sizeof(double) * (size_t)n * e->dev.F,
                         hipMemcpyHostToDevice, st));
   }
-  if (warp) SCHK(hipMemcpyAsync(e->h_warp, warp, sizeof(double) * 6, hipMemcpyHostToDevice, st));
-  SCHK(hipMemcpyAsync(e->h_off, off, sizeof(off), hipMemcpyHostToDevice, st));
+  if (warp) {
+    memcpy(e->p_warp, warp, sizeof(double) * 6);
+    SCHK(hipMemcpyAsync(e->h_warp, e->p_warp, sizeof(double) * 6, hipMemcpyHostToDevice, st));
+  }
+  e->p_cnt[2] = 0;
+  e->p_cnt[3] = n;
+  SCHK(hipMemcpyAsync(e->h_off, e->p_cnt + 2, sizeof(int) * 2, hipMemcpyHostToDevice, st));
+  e->cache_seq = -1;
   int rc = ss_launch(e, seq, 1, e->h_dets, e->h_off, e->h_embs, warp ? e->h_warp : nullptr,
                      e->h_out, e->h_cnt, st);
   if (rc) return rc;
-  int cnt = 0;
-  SCHK(hipMemcpyAsync(&cnt, e->h_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+  SCHK(hipMemcpyAsync(e->p_cnt, e->h_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+  SCHK(hipMemcpyAsync(e->p_cnt + 1, e->dev.status, sizeof(int), hipMemcpyDeviceToHost, st));
+  if (n) SCHK(hipMemcpyAsync(e->p_out, e->h_out, sizeof(double) * 10 * n, hipMemcpyDeviceToHost, st));
+  SCHK(hipMemcpyAsync(e->p_sq, e->dev.sq + (size_t)seq * SQS, sizeof(int) * SQS,
+                      hipMemcpyDeviceToHost, st));
   SCHK(hipStreamSynchronize(st));
-  if (cnt) SCHK(hipMemcpy(out, e->h_out, sizeof(double) * 10 * cnt, hipMemcpyDeviceToHost));
+  const int cnt = e->p_cnt[0], status = e->p_cnt[1];
+  e->cache_seq = seq;
+  if (cnt) memcpy(out, e->p_out, sizeof(double) * 10 * cnt);
   *n_out = cnt;
-  int status = 0;
-  SCHK(hipMemcpy(&status, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
   if (status) return bx_record_error(status, "StrongSort engine status latched (see bx_ss_status)");
   return BX_OK;
 }
@@ -2700,8 +2735,12 @@ int bx_ss_counters_host(bx_ss* e, int seq, int* frame_count, int* next_id, int* 
                         int* n_lost) {
   if (!e || seq < 0 || seq >= e->dev.S) return bx_record_error(BX_ERR_INVALID, "bad sequence");
   int s[SQS];
-  SCHK(hipDeviceSynchronize());
-  SCHK(hipMemcpy(s, e->dev.sq + (size_t)seq * SQS, sizeof(s), hipMemcpyDeviceToHost));
+  if (seq == e->cache_seq) {
+    memcpy(s, e->p_sq, sizeof(s));
+  } else {
+    SCHK(hipDeviceSynchronize());
+    SCHK(hipMemcpy(s, e->dev.sq + (size_t)seq * SQS, sizeof(s), hipMemcpyDeviceToHost));
+  }
   if (frame_count) *frame_count = s[Q_FRAME];
   if (next_id) *next_id = s[Q_NEXTID];
   if (n_tracks) *n_tracks = s[Q_NTR];
