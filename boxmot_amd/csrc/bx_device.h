@@ -23,14 +23,14 @@ enum : uint32_t { ST_NEW = 0, ST_TRACKED = 1, ST_LOST = 2, ST_REMOVED = 3 };
 // (lets the slot-parallel kernels select joint(tracked, lost) without walking the lists)
 // F_PRED / F_GMC / F_REC are frame-transient: mean predicted (covariance predict pending), CMC
 // warp applied to the mean (covariance warp pending), slot has an update record this frame.
-// F_PEND (bits 16-23, persistent): covariance predicts applied to the mean but not yet to the
+// F_PEND (bits 16-31, persistent): covariance predicts applied to the mean but not yet to the
 // covariance — a track without an update keeps them pending until it is updated again (or its
 // state is read), see bx_engine.hip K2/K4.
 enum : uint32_t {
   F_STATE = 0x7u, F_ACT = 0x8u, F_INREM = 0x10u, F_INUSE = 0x20u, F_INACT = 0x40u,
   F_INLOST = 0x80u, F_PRED = 0x100u, F_GMC = 0x200u, F_REC = 0x400u, F_TRANSIENT = 0x700u,
   F_PARKED = 0x800u,  // per_class mode: on another class's (parked) active list — kept alive
-  F_PEND1 = 0x10000u, F_PEND_MASK = 0xFF0000u
+  F_PEND1 = 0x10000u, F_PEND_MASK = 0xFFFF0000u
 };
 
 __device__ __forceinline__ uint32_t st_of(uint32_t f) { return f & F_STATE; }

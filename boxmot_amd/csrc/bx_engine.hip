@@ -645,6 +645,31 @@ __device__ __forceinline__ void kf_predict_cov(int kind, const double* qm, doubl
 __device__ inline void kf_materialize(int kind, double* m, int n) {
   for (int k = 0; k < n; k++) kf_predict_cov(kind, m + (k ? KF_QM2 : KF_QM), m + 8);
 }
+// kf_materialize for K2's counter-overflow path, quad by quad through memory with no unrolling:
+// the same expressions as kf_predict_quad, but it keeps the predict kernel's register budget
+// (inlined, the 64-entry covariance in registers cost it 190 VGPRs and 2 waves/SIMD)
+__device__ __noinline__ void kf_materialize_mem(int kind, double* m, int n) {
+  double* c = m + 8;
+#pragma nounroll
+  for (int k = 0; k < n; k++) {
+    const double* qm = m + (k ? KF_QM2 : KF_QM);
+    double mv[4] = {0.0, 0.0, qm[0], qm[1]}, q[8];
+    kf_process_noise(kind, mv, q);
+#pragma nounroll
+    for (int ij = 0; ij < 16; ij++) {
+      const int i = ij >> 2, j = ij & 3;
+      const double p00 = c[8 * i + j], p10 = c[8 * (i + 4) + j], p01 = c[8 * i + j + 4],
+                   p11 = c[8 * (i + 4) + j + 4];
+      double v = (p00 + p10) + (p01 + p11);
+      double v11 = p11;
+      if (i == j) { v = v + q[i]; v11 = v11 + q[i + 4]; }
+      c[8 * i + j] = v;
+      c[8 * i + j + 4] = p01 + p11;
+      c[8 * (i + 4) + j] = p10 + p11;
+      c[8 * (i + 4) + j + 4] = v11;
+    }
+  }
+}
 // multi_gmc covariance part: cov = R8·cov·R8ᵀ, R8 = kron(I4, R) (botsort.py:192-195)
 __device__ inline void gmc_cov(const double* H, double* c) {
   double RP[64];
@@ -688,8 +713,8 @@ __device__ __forceinline__ void predict_slot(Dev& P, int s, int slot, uint32_t f
     // Lost from its next predict on, which zeroes the size velocities (v_w, v_h | v_h) first —
     // so two operand pairs describe any number of pending predicts exactly.
     int pend = pend_of(f);
-    if (pend == 255) {  // never reached (tracks are removed after max_time_lost frames)
-      kf_materialize(KIND, m, pend);
+    if (pend == 65535) {  // counter full (a lost track predicted 65535 times without an update)
+      kf_materialize_mem(KIND, m, pend);
       pend = 0;
       nf &= ~F_PEND_MASK;
     }
