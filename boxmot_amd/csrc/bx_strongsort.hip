@@ -936,36 +936,58 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
   for (int j = lane; j < CC; j += 64) w.v[j] = 0.0, w.path[j] = -1, w.row4col[j] = -1;
   __syncthreads();
   constexpr int NONE = 0x7fffffff;
+  // Row `cur`'s costs are loaded into registers (element lane + 64 q, the first 64 * LQ columns)
+  // while row cur - 1 is still being solved: the first Dijkstra step — where most rows end — runs
+  // from registers without waiting on memory (the wave's loads were its critical path).  Columns
+  // past 64 * LQ (more than 512 of them) are read from memory.
+  constexpr int LQ = 8;
+  const double* __restrict__ ctail = nullptr;
+  double nx[LQ];
+  auto load_row = [&](int r, double* dst) {
+    const double* __restrict__ p = C + (size_t)r * CC;
+#pragma unroll
+    for (int q = 0; q < LQ; q++) {
+      const int j = lane + 64 * q;
+      dst[q] = j < CC ? p[j] : 0.0;
+    }
+  };
+  if (R > 0) load_row(0, nx);
   for (int cur = 0; cur < R; cur++) {
     // The first Dijkstra step from row `cur` starts from scipy's fresh state (spc = INF,
     // remaining[it] = CC-1-it), so it runs from registers: relax, minimum, tie rule.  Most rows
     // end there on an unassigned column; only otherwise is the state written out and the search
     // continued as below.
+    double rv[LQ];
     const double ucur = w.u[cur];
-    const double* __restrict__ crow = C + (size_t)cur * CC;
     double lmin = INF;
-    for (int j0 = 0; j0 < CC; j0 += 256) {
-      double cv[4];
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int j = j0 + 64 * q + lane;
-        cv[q] = j < CC ? crow[j] : 0.0;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int j = j0 + 64 * q + lane;
-        if (j < CC) {
-          const double r = 0.0 + cv[q] - ucur - w.v[j];
-          lmin = fmin(lmin, r < INF ? r : INF);
-        }
-      }
+    for (int q = 0; q < LQ; q++) {
+      const int j = lane + 64 * q;
+      const double r = 0.0 + nx[q] - ucur - (j < CC ? w.v[j] : 0.0);
+      rv[q] = j < CC ? (r < INF ? r : INF) : INF;
+      lmin = fmin(lmin, rv[q]);
     }
+    ctail = C + (size_t)cur * CC;
+    for (int j = 64 * LQ + lane; j < CC; j += 64) {
+      const double r = 0.0 + ctail[j] - ucur - w.v[j];
+      lmin = fmin(lmin, r < INF ? r : INF);
+    }
+    if (cur + 1 < R) load_row(cur + 1, nx);  // in flight during this row's reductions
     const double m0 = wave_min_dpp(lmin);
     // scipy's tie rule among the columns at the minimum (fresh positions CC-1-j)
     int lfirst = NONE, llast = -1;
     if (lmin == m0) {
-      for (int j = lane; j < CC; j += 64) {
-        const double r = 0.0 + crow[j] - ucur - w.v[j];
+#pragma unroll
+      for (int q = 0; q < LQ; q++) {
+        const int j = lane + 64 * q;
+        if (j < CC && rv[q] == m0) {
+          const int p = CC - 1 - j;
+          lfirst = p < lfirst ? p : lfirst;
+          if (w.row4col[j] == -1 && p > llast) llast = p;
+        }
+      }
+      for (int j = 64 * LQ + lane; j < CC; j += 64) {
+        const double r = 0.0 + ctail[j] - ucur - w.v[j];
         if ((r < INF ? r : INF) == m0) {
           const int p = CC - 1 - j;
           lfirst = p < lfirst ? p : lfirst;
@@ -1001,8 +1023,16 @@ __device__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
     }
     for (int i = lane; i < R; i += 64) w.SR[i] = 0;
     __syncthreads();
-    for (int j = lane; j < CC; j += 64) {  // the first step's relaxation, recomputed
-      const double r = 0.0 + crow[j] - ucur - w.v[j];
+#pragma unroll
+    for (int q = 0; q < LQ; q++) {  // the first step's relaxation, from registers
+      const int j = lane + 64 * q;
+      if (j < CC && rv[q] < INF) {
+        w.path[j] = cur;
+        w.spc[j] = rv[q];
+      }
+    }
+    for (int j = 64 * LQ + lane; j < CC; j += 64) {
+      const double r = 0.0 + ctail[j] - ucur - w.v[j];
       if (r < INF) {
         w.path[j] = cur;
         w.spc[j] = r;
