@@ -929,7 +929,7 @@ struct SsCtx {
 // row — and picks the minimum with scipy's tie rule: the last unassigned column at the minimum in
 // `remaining` order, else the first at the minimum (pos[] tracks each column's place in scipy's
 // swap-remove `remaining` array).  Pairs sorted by row into w.rows/w.cols; returns their count.
-__device__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
+__device__ __forceinline__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
   SsWs& w = x.w;
   const int lane = x.lane;
   for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
@@ -1281,7 +1281,7 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
 // matches appended to w.mt at x.nm; unmatched tracks to ut_out (if non-null), detections to
 // ud_out.  Cost rows lane per track (gated_metric + gate_cost_matrix + id preservation, or
 // iou_cost), _enhance_cost_matrix and the max_distance clamp fused per entry.
-__device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* ti, int nt,
+__device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* ti, int nt,
                                   const int* di, int nd, int* ut_out, int& nut, int* ud_out,
                                   int& nud) {
   const SsDev& g = x.g;
@@ -1317,18 +1317,20 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
     int* roff = x.flt;  // the rows' matrix indices, staged in LDS (free during the levels)
     for (int o = lane; o < no; o += 64) roff[o] = tr ? oi[o] : rk[oi[o]];
     __syncthreads();
+    // the wave's reads are its critical path: GQ rows of loads in flight per lane
+    constexpr int GQ = 8;
     for (int c = lane; c < nl; c += 64) {  // this lane's column, then every row
       const int v = li[c];
       const int idx = tr ? rk[v] : v;
-      for (int o = 0; o < no; o += 4) {
-        double e[4];
+      for (int o = 0; o < no; o += GQ) {
+        double e[GQ];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < GQ; u++) {
           const int oo = o + u < no ? o + u : o;
           e[u] = cf[(size_t)roff[oo] * ld + idx];
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++)
+        for (int u = 0; u < GQ; u++)
           if (o + u < no) C[(size_t)(o + u) * nl + c] = e[u] > max_d ? max_d + 1e-5 : e[u];
       }
     }
@@ -1424,7 +1426,7 @@ __device__ void min_cost_matching(SsCtx& x, int kind, double max_d, const int* t
 
 // matching_cascade (linear_assignment.py:96-171): levels by time_since_update ascending (up to
 // tracker.max_age), each level's tracks ordered by -(quality + stability), stable
-__device__ void matching_cascade(SsCtx& x, double max_d, const int* ti, int nt, const int* di,
+__device__ __forceinline__ void matching_cascade(SsCtx& x, double max_d, const int* ti, int nt, const int* di,
                                  int nd) {
   SsWs& w = x.w;
   const int lane = x.lane;
