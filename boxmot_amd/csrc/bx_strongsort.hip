@@ -120,7 +120,7 @@ struct SsDev {
   int* wsi;       // [S][WSI] int scratch
   double* wsd;    // [S][WSD] double scratch
   int wsi_n, wsd_n;
-  int ws_lds;     // 1: the frame kernel's workspace lives in LDS
+  int ws_lds;     // 1: the whole frame-kernel workspace in LDS, 2: its LSAP state only
   int* status;
   unsigned long long* dbg;  // [S][SS_DBG] phase stamps (diagnostic builds only, else null)
 };
@@ -490,6 +490,11 @@ __device__ int pool_alloc(SsTrk& t, int VP) {
   return -1;
 }
 
+// ---- the match kernel's code generation ---------------------------------------------------
+#ifndef SS_MATCH_ATTR  // everything inlined: a call left by the inliner keeps its frame in scratch
+#define SS_MATCH_ATTR __attribute__((flatten))
+#endif
+
 // ---- the frame kernel's scratch -----------------------------------------------------------
 struct SsWs {
   // ints
@@ -501,8 +506,10 @@ struct SsWs {
 };
 
 // The scratch of one sequence: the LSAP state (3N doubles u v spc, 7N ints path col4row row4col
-// rem pos SR SC) and the rest.  ws_lds: 0 = all in HBM, 1 = all in LDS, 2 = the LSAP state in LDS.
-int ws_lsap_bytes(int N) { return 3 * N * 8 + 7 * N * 4; }
+// rem pos SR SC) and the rest.  The LSAP state always leads the dynamic LDS block (N <= 2048:
+// 106 KB at most); ws_lds: 1 = the rest in LDS after it, 2 = the rest in HBM.
+__host__ __device__ inline int ws_lsap_bytes(int N) { return 3 * N * 8 + 7 * N * 4; }
+// (the LSAP state's 7N ints and 3N doubles are counted in the sizes below: the LDS block's total)
 int ws_ints(int T, int D, int N) {
   return T /*lst*/ + T + T + T + 2 * T /*cand*/ + 2 * T /*ut3*/ + 3 * D +
          D /*rd*/ + 2 * (D + 2 * T) /*ud ud2*/ + T /*lvl*/ + T /*ages*/ +
@@ -523,13 +530,23 @@ __device__ void ws_frame(const SsDev& g, int seq, SsWs& w) {
 }
 
 __device__ void ws_carve(const SsDev& g, int seq, SsWs& w, char* lds) {
+  const int T = g.T, D = g.D, N = g.N;
+  // The LSAP state is carved from LDS unconditionally, so its accesses compile to ds_* LDS
+  // instructions: a generic (flat) access counts against the vector-memory counter too, and every
+  // wait on one would also wait for the solver's in-flight row loads.
+  {
+    double* ld = (double*)lds;
+    int* li = (int*)(lds + (size_t)3 * N * 8);
+    w.u = ld; w.v = ld + N; w.spc = ld + 2 * N;
+    w.path = li; w.col4row = li + N; w.row4col = li + 2 * N; w.rem = li + 3 * N;
+    w.pos = li + 4 * N; w.SR = li + 5 * N; w.SC = li + 6 * N;
+  }
   int* pi = g.wsi + (size_t)seq * g.wsi_n;
   double* pd = g.wsd + (size_t)seq * g.wsd_n;
-  if (g.ws_lds == 1) {  // doubles first (8-byte alignment), then ints
-    pd = (double*)lds;
-    pi = (int*)(lds + (size_t)g.wsd_n * 8);
+  if (g.ws_lds == 1) {  // the rest after the LSAP state: doubles first (8-byte alignment), ints
+    pd = (double*)(lds + ws_lsap_bytes(N));
+    pi = (int*)(lds + ws_lsap_bytes(N) + (size_t)(g.wsd_n - 3 * N) * 8);
   }
-  const int T = g.T, D = g.D, N = g.N;
   auto I = [&](int n) { int* p = pi; pi += n; return p; };
   auto Dd = [&](int n) { double* p = pd; pd += n; return p; };
   w.lst = I(T); w.conf_t = I(T); w.unconf_t = I(T); w.aut = I(T); w.cand = I(2 * T);
@@ -539,13 +556,6 @@ __device__ void ws_carve(const SsDev& g, int seq, SsWs& w, char* lds) {
   w.ti2 = I(2 * T); w.pwlo = I(PW_MAXLEAF); w.pwln = I(PW_MAXLEAF); w.sc = I(32);
   ws_frame(g, seq, w);
   w.meas = Dd(4 * D); w.key = Dd(2 * T); w.pwleaf = Dd(PW_MAXLEAF); w.sd = Dd(8);
-  if (g.ws_lds == 2) {  // the LSAP state alone in LDS
-    pd = (double*)lds;
-    pi = (int*)(lds + (size_t)3 * N * 8);
-  }
-  w.u = Dd(N); w.v = Dd(N); w.spc = Dd(N);
-  w.path = I(N); w.col4row = I(N); w.row4col = I(N); w.rem = I(N); w.pos = I(N); w.SR = I(N);
-  w.SC = I(N);
 }
 
 // broadcast an int from lane 0 (all lanes call)
@@ -918,101 +928,121 @@ struct SsCtx {
   int ncf;      // confirmed tracks
   int* flt;     // match kernel: scratch table (LDS, 1024 ints)
   double* ks;   // match kernel: sort-key scratch (LDS)
+  int* cidx;    // match kernel: the solver's column indices (LDS, 1024 ints)
   __device__ const double* det(int i) const { return w.dt + (size_t)w.dord[i] * DTW; }
   __device__ int det_in(int i) const { return (int)det(i)[6]; }
 };
 
 // scipy.optimize.linear_sum_assignment (Crouse's shortest augmenting path, rectangular),
-// wave-parallel, on C given in the solver's orientation: R x CC row-major, R <= CC (`tr`: the
-// caller's matrix was transposed to get there, so the output pairs are argsorted by the original
-// row).  Each row's Dijkstra relaxes the remaining columns lane-parallel — coalesced reads of the
-// row — and picks the minimum with scipy's tie rule: the last unassigned column at the minimum in
-// `remaining` order, else the first at the minimum (pos[] tracks each column's place in scipy's
-// swap-remove `remaining` array).  Pairs sorted by row into w.rows/w.cols; returns their count.
-__device__ __forceinline__ int lsap_wave(SsCtx& x, const double* C, int R, int CC, bool tr) {
+// wave-parallel, in the solver's orientation: R x CC, R <= CC (`tr`: the caller's matrix was
+// transposed to get there, so the output pairs are argsorted by the original row).  Entry (r, j)
+// is P[roff[r] + cidx[j]], clamped at max_d (min_cost_matching's clamp: above max_d ->
+// max_d + 1e-5; max_d = INF: none), read straight from the stage's matrix — no per-level copy.
+//
+// Lane l owns the columns j = l + 64 q (q < LQ, CC <= 64 LQ): their matrix index (cidx, or j
+// itself when !IDX), v[j] and an assigned bit stay in registers.  Each row's first Dijkstra step — where most rows end — runs
+// from registers: relax against v, wave minimum, scipy's tie rule (the last unassigned column at
+// the minimum in `remaining` order, else the first; fresh positions are CC-1-j, so the smallest
+// unassigned j, else the largest j), assignment.  The next row's costs are loaded meanwhile.
+// Only a row whose minimum lands on an assigned column writes the search state out (rem / pos /
+// SC / spc / path in LDS) and continues Crouse's search as scipy does; u[cur] is 0 before row cur
+// (only rows already assigned are ever on a path).  Pairs sorted by row into w.rows / w.cols.
+template <int LQ, bool IDX>
+__device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P, const int* roff,
+                                         const int* cidx, double max_d, int R, int CC, bool tr) {
   SsWs& w = x.w;
   const int lane = x.lane;
+#ifdef BX_PHASE_TIMING
+  const SsDev& g = x.g;
+  const int seq = x.seq;
+  SCOUNT(7, R);
+  SCOUNT(8, CC);
+  unsigned long long t_slow = 0, t_s0 = 0, t_all = SS_NOW();
+#endif
+  const double clampv = max_d + 1e-5;
   for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
   for (int j = lane; j < CC; j += 64) w.v[j] = 0.0, w.path[j] = -1, w.row4col[j] = -1;
+  int ci[LQ];
+  double vr[LQ];
+  unsigned asg = 0;
+#pragma unroll
+  for (int q = 0; q < LQ; q++) {
+    const int j = lane + 64 * q;
+    ci[q] = IDX ? (j < CC ? cidx[j] : 0) : j;
+    vr[q] = 0.0;
+  }
   __syncthreads();
-  constexpr int NONE = 0x7fffffff;
-  // Row `cur`'s costs are loaded into registers (element lane + 64 q, the first 64 * LQ columns)
-  // while row cur - 1 is still being solved: the first Dijkstra step — where most rows end — runs
-  // from registers without waiting on memory (the wave's loads were its critical path).  Columns
-  // past 64 * LQ (more than 512 of them) are read from memory.
-  constexpr int LQ = 8;
-  const double* __restrict__ ctail = nullptr;
-  double nx[LQ];
-  auto load_row = [&](int r, double* dst) {
-    const double* __restrict__ p = C + (size_t)r * CC;
+  auto load_row = [&](int off, double* dst) {
 #pragma unroll
     for (int q = 0; q < LQ; q++) {
-      const int j = lane + 64 * q;
-      dst[q] = j < CC ? p[j] : 0.0;
+      const double e = lane + 64 * q < CC ? P[off + ci[q]] : 0.0;
+      dst[q] = e;  // raw: clamped where used, so the load is waited for only then
     }
   };
-  if (R > 0) load_row(0, nx);
+  // the next row's loads are issued during this one's reductions, except at LQ = 32 (IoU stage of
+  // more than 1024 candidates, rare) where the registers would not hold both rows
+  constexpr bool PF = LQ <= 16;
+  double nx[LQ];
+  int off1 = R > 1 ? roff[1] : 0;
+  if (PF && R > 0) load_row(roff[0], nx);
   for (int cur = 0; cur < R; cur++) {
-    // The first Dijkstra step from row `cur` starts from scipy's fresh state (spc = INF,
-    // remaining[it] = CC-1-it), so it runs from registers: relax, minimum, tie rule.  Most rows
-    // end there on an unassigned column; only otherwise is the state written out and the search
-    // continued as below.
+    if (!PF) load_row(roff[cur], nx);
+    // scipy's minVal + cost - u[cur] - v[j] with minVal = u[cur] = 0 (up to the sign of a zero,
+    // which no comparison and no later sum can tell)
     double rv[LQ];
-    const double ucur = w.u[cur];
-    double lmin = INF;
 #pragma unroll
     for (int q = 0; q < LQ; q++) {
-      const int j = lane + 64 * q;
-      const double r = 0.0 + nx[q] - ucur - (j < CC ? w.v[j] : 0.0);
-      rv[q] = j < CC ? (r < INF ? r : INF) : INF;
-      lmin = fmin(lmin, rv[q]);
+      const double c = nx[q] > max_d ? clampv : nx[q];
+      const double r = c - vr[q];
+      rv[q] = lane + 64 * q < CC ? (r < INF ? r : INF) : INF;
     }
-    ctail = C + (size_t)cur * CC;
-    for (int j = 64 * LQ + lane; j < CC; j += 64) {
-      const double r = 0.0 + ctail[j] - ucur - w.v[j];
-      lmin = fmin(lmin, r < INF ? r : INF);
-    }
-    if (cur + 1 < R) load_row(cur + 1, nx);  // in flight during this row's reductions
-    const double m0 = wave_min_dpp(lmin);
-    // scipy's tie rule among the columns at the minimum (fresh positions CC-1-j)
-    int lfirst = NONE, llast = -1;
-    if (lmin == m0) {
+    double lmin = rv[0];
 #pragma unroll
-      for (int q = 0; q < LQ; q++) {
-        const int j = lane + 64 * q;
-        if (j < CC && rv[q] == m0) {
-          const int p = CC - 1 - j;
-          lfirst = p < lfirst ? p : lfirst;
-          if (w.row4col[j] == -1 && p > llast) llast = p;
-        }
-      }
-      for (int j = 64 * LQ + lane; j < CC; j += 64) {
-        const double r = 0.0 + ctail[j] - ucur - w.v[j];
-        if ((r < INF ? r : INF) == m0) {
-          const int p = CC - 1 - j;
-          lfirst = p < lfirst ? p : lfirst;
-          if (w.row4col[j] == -1 && p > llast) llast = p;
-        }
-      }
+    for (int q = 1; q < LQ; q++) lmin = fmin(lmin, rv[q]);
+    if (PF && cur + 1 < R) {  // the next row in flight during this one's reductions
+      load_row(off1, nx);
+      off1 = cur + 2 < R ? roff[cur + 2] : 0;
     }
-    lfirst = wave_min_i(lfirst);
-    llast = -wave_min_i(-llast);
+    const double m0 = wave_min_dpp(lmin);
     if (!(m0 < INF)) {  // infeasible (cannot happen with finite costs)
       if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
       return 0;
     }
-    const int index0 = llast >= 0 ? llast : lfirst;
-    const int j0 = CC - 1 - index0;
-    if (w.row4col[j0] == -1) {  // sink reached: u[cur] += minVal, v[j0] -= 0, augment
-      __syncthreads();
+    unsigned eq = 0;
+#pragma unroll
+    for (int q = 0; q < LQ; q++) eq |= rv[q] == m0 ? 1u << q : 0u;
+    const unsigned un = eq & ~asg;
+    int j0;
+    bool sink;
+    const unsigned long long lm = __ballot(eq != 0);
+    if ((lm & (lm - 1)) == 0) {  // one lane holds the columns at the minimum (the usual case)
+      const int L = __ffsll((long long)lm) - 1;
+      const unsigned eL = (unsigned)rl_i((int)eq, L), uL = (unsigned)rl_i((int)un, L);
+      sink = uL != 0;
+      j0 = L + 64 * (sink ? __ffs(uL) - 1 : 31 - __clz(eL));
+    } else {
+      constexpr int BIG = 0x7fffffff;
+      const int a = un ? lane + 64 * (__ffs(un) - 1) : BIG;
+      const int b = eq ? lane + 64 * (31 - __clz(eq)) : -1;
+      const int ja = wave_min_i(a), jb = -wave_min_i(-b);
+      sink = ja != BIG;
+      j0 = sink ? ja : jb;
+    }
+    if (sink) {  // an unassigned column: u[cur] += minVal, v[j0] -= 0, augment
+      if (lane == (j0 & 63)) asg |= 1u << (j0 >> 6);
       if (lane == 0) {
-        w.u[cur] += m0;
+        w.u[cur] = m0;
         w.row4col[j0] = cur;
         w.col4row[cur] = j0;
       }
-      __syncthreads();
       continue;
     }
+#ifdef BX_PHASE_TIMING
+    SCOUNT(9, 1);
+    t_s0 = SS_NOW();
+#endif
+    // the search continues: scipy's state after the first step, written out
+    const int index0 = CC - 1 - j0;
     double minVal = m0;
     int nrem = CC;
     for (int j = lane; j < CC; j += 64) {
@@ -1024,18 +1054,11 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* C, int R, int C
     for (int i = lane; i < R; i += 64) w.SR[i] = 0;
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < LQ; q++) {  // the first step's relaxation, from registers
+    for (int q = 0; q < LQ; q++) {  // the first step's relaxation
       const int j = lane + 64 * q;
       if (j < CC && rv[q] < INF) {
         w.path[j] = cur;
         w.spc[j] = rv[q];
-      }
-    }
-    for (int j = 64 * LQ + lane; j < CC; j += 64) {
-      const double r = 0.0 + ctail[j] - ucur - w.v[j];
-      if (r < INF) {
-        w.path[j] = cur;
-        w.spc[j] = r;
       }
     }
     if (lane == 0) {
@@ -1047,24 +1070,27 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* C, int R, int C
     }
     nrem--;
     __syncthreads();
-    int sink = -1, i = w.row4col[j0];
-    while (sink == -1) {
+    int sk = -1, i = w.row4col[j0];
+    while (sk == -1) {
       if (lane == 0) w.SR[i] = 1;
       const double ui = w.u[i];
-      const double* __restrict__ crow = C + (size_t)i * CC;
+      const int offi = roff[i];
       double m = INF;
-      for (int j0 = 0; j0 < CC; j0 += 256) {  // the row's loads issued four at a time
-        double cv[4];
+      constexpr int QB = LQ < 8 ? LQ : 8;  // loads in flight per lane
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const int j = j0 + 64 * u + lane;
-          cv[u] = j < CC ? crow[j] : 0.0;
+      for (int q0 = 0; q0 < LQ; q0 += QB) {
+        double cv[QB];
+#pragma unroll
+        for (int u = 0; u < QB; u++) {
+          const int q = q0 + u;
+          const double e = lane + 64 * q < CC ? P[offi + ci[q]] : 0.0;
+          cv[u] = e > max_d ? clampv : e;
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const int j = j0 + 64 * u + lane;
+        for (int u = 0; u < QB; u++) {
+          const int q = q0 + u, j = lane + 64 * q;
           if (j >= CC || w.SC[j]) continue;
-          const double r = minVal + cv[u] - ui - w.v[j];
+          const double r = minVal + cv[u] - ui - vr[q];
           double sp = w.spc[j];
           if (r < sp) {
             w.path[j] = i;
@@ -1075,10 +1101,12 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* C, int R, int C
       }
       m = wave_min_dpp(m);
       int last_un = -1, first_eq = 0x7fffffff;
-      for (int j = lane; j < CC; j += 64) {
-        if (!w.SC[j] && w.spc[j] == m) {
+#pragma unroll
+      for (int q = 0; q < LQ; q++) {
+        const int j = lane + 64 * q;
+        if (j < CC && !w.SC[j] && w.spc[j] == m) {
           const int p = w.pos[j];
-          if (w.row4col[j] == -1) last_un = p > last_un ? p : last_un;
+          if (!((asg >> q) & 1u)) last_un = p > last_un ? p : last_un;
           first_eq = p < first_eq ? p : first_eq;
         }
       }
@@ -1092,7 +1120,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* C, int R, int C
       minVal = m;
       const int j = w.rem[index];
       if (w.row4col[j] == -1)
-        sink = j;
+        sk = j;
       else
         i = w.row4col[j];
       __syncthreads();
@@ -1117,7 +1145,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* C, int R, int C
       if (w.SC[j]) w.v[j] -= minVal - w.spc[j];
     __syncthreads();
     if (lane == 0) {
-      int j = sink;
+      int j = sk;
       for (;;) {
         const int q = w.path[j];
         w.row4col[j] = q;
@@ -1127,8 +1155,22 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* C, int R, int C
         if (q == cur) break;
       }
     }
+    if (lane == (sk & 63)) asg |= 1u << (sk >> 6);
+#ifdef BX_PHASE_TIMING
+    t_slow += SS_NOW() - t_s0;
+#endif
+#pragma unroll
+    for (int q = 0; q < LQ; q++) {
+      const int j = lane + 64 * q;
+      vr[q] = j < CC ? w.v[j] : 0.0;
+    }
     __syncthreads();
   }
+  __syncthreads();
+#ifdef BX_PHASE_TIMING
+  SCOUNT(10, t_slow);
+  SCOUNT(11, SS_NOW() - t_all);
+#endif
   if (tr) {  // argsort(col4row): pairs ordered by the original row
     for (int q = lane; q < R; q += 64) {
       const int orow = w.col4row[q];
@@ -1150,16 +1192,20 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* C, int R, int C
 enum { M_GATED = 0, M_IOU = 1 };
 
 // _enhance_cost_matrix (linear_assignment.py:251-273) of one entry, unclamped
-__device__ __forceinline__ double enhance(const SsTrk& t, const double* d, double e) {
-  const double cq = (t.quality + d[7]) / 2.0;
+__device__ __forceinline__ double enhance_v(double tq, double tcls, double tconf, const double* d,
+                                            double e) {
+  const double cq = (tq + d[7]) / 2.0;
   e *= clipd(1.0 - (cq - 0.5) * 0.2, 0.8, 1.2);
-  if (t.cls == d[5]) e *= 0.9;
+  if (tcls == d[5]) e *= 0.9;
   double cf = 1.0;
-  if (t.conf > 0.7 && d[4] > 0.7)
+  if (tconf > 0.7 && d[4] > 0.7)
     cf = 0.9;
-  else if (t.conf < 0.3 || d[4] < 0.3)
+  else if (tconf < 0.3 || d[4] < 0.3)
     cf = 1.1;
   return e * cf;
+}
+__device__ __forceinline__ double enhance(const SsTrk& t, const double* d, double e) {
+  return enhance_v(t.quality, t.cls, t.conf, d, e);
 }
 // ... and min_cost_matching's clamp at max_distance (linear_assignment.py:62-64)
 __device__ __forceinline__ double enhance_clamp(const SsTrk& t, const double* d, double e,
@@ -1298,44 +1344,38 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
   }
   // the solver's orientation: R x CC with R <= CC, transposed (tr) when detections are fewer
   const bool tr = nd < nt;
-  double* C = g.cost + (size_t)x.seq * 4 * g.T * g.D;
-  double* C2 = C + (size_t)2 * g.T * g.D;
+  const int R = tr ? nd : nt, CC = tr ? nt : nd;
+  if (CC > 2048 || R > 1024) {  // track_cap, det_cap <= 1024
+    if (lane == 0) atomicExch(g.status, (int)BX_ERR_INVALID);
+    nut = nud = 0;
+    return;
+  }
+  int* roff = x.flt;   // the solver rows' element offsets into P (LDS)
+  int* cidx = x.cidx;  // the solver columns' element indices (LDS)
+  const double* P;
+  double mx;
 #ifdef BX_PHASE_TIMING
   const int seq = x.seq;
   __syncthreads();
   unsigned long long t0 = SS_NOW();
 #endif
   if (kind == M_GATED) {
-    // ss_cost_kernel's gated + shaped + enhanced cost of (list position, sorted detection); the
-    // clamp at max_distance is this level's.  The lane's gather indices stay in registers.
-    const int nl = tr ? nt : nd, no = tr ? nd : nt;
-    const int* li = tr ? ti : di;
-    const int* oi = tr ? di : ti;
-    const int* rk = x.rank;  // track list position -> cascade rank (the matrix's track index)
-    const double* cf = tr ? g.cfullT + (size_t)x.seq * g.D * g.T : g.cfull + (size_t)x.seq * g.T * g.D;
+    // ss_cost_kernel's gated + shaped + enhanced cost of (cascade rank, sorted detection), read
+    // in place by the solver (its rows: tracks, or detections when tr, through cfullT); the
+    // clamp at max_distance is this level's.
+    const int* li = tr ? ti : di;  // columns
+    const int* oi = tr ? di : ti;  // rows
+    const int* rk = x.rank;        // track list position -> cascade rank
+    P = tr ? g.cfullT + (size_t)x.seq * g.D * g.T : g.cfull + (size_t)x.seq * g.T * g.D;
     const int ld = tr ? g.T : g.D;
-    int* roff = x.flt;  // the rows' matrix indices, staged in LDS (free during the levels)
-    for (int o = lane; o < no; o += 64) roff[o] = tr ? oi[o] : rk[oi[o]];
-    __syncthreads();
-    // the wave's reads are its critical path: GQ rows of loads in flight per lane
-    constexpr int GQ = 8;
-    for (int c = lane; c < nl; c += 64) {  // this lane's column, then every row
-      const int v = li[c];
-      const int idx = tr ? rk[v] : v;
-      for (int o = 0; o < no; o += GQ) {
-        double e[GQ];
-#pragma unroll
-        for (int u = 0; u < GQ; u++) {
-          const int oo = o + u < no ? o + u : o;
-          e[u] = cf[(size_t)roff[oo] * ld + idx];
-        }
-#pragma unroll
-        for (int u = 0; u < GQ; u++)
-          if (o + u < no) C[(size_t)(o + u) * nl + c] = e[u] > max_d ? max_d + 1e-5 : e[u];
-      }
-    }
+    for (int o = lane; o < R; o += 64) roff[o] = (tr ? oi[o] : rk[oi[o]]) * ld;
+    for (int c = lane; c < CC; c += 64) cidx[c] = tr ? rk[li[c]] : li[c];
+    mx = max_d;
   } else {
-    double* Cr = tr ? C2 : C;  // row-major nt x nd, transposed below when tr
+    // iou_cost + _enhance_cost_matrix + the clamp of every (track, detection), written straight
+    // in the solver's orientation R x CC: lanes over the solver's columns (coalesced stores), the
+    // rows' operands uniform per iteration
+    double* C = g.cost + (size_t)x.seq * 4 * g.T * g.D;
     // the detections' rows staged in LDS when they fit (x.sdet: 256 x DTW)
     const bool staged = x.sdet && nd <= 256;
     if (staged) {
@@ -1346,32 +1386,34 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
       __syncthreads();
     }
     auto dq = [&](int c) { return staged ? x.sdet + (size_t)c * DTW : x.det(di[c]); };
+    // lanes over tracks, the track's operands in registers (the stores could alias them);
+    // transposed (tr) the lanes' stores are coalesced
     for (int r = lane; r < nt; r += 64) {
-      const int slot = w.lst[ti[r]];
-      const SsTrk& t = x.trk[slot];
-      double* row = Cr + (size_t)r * nd;
-      if (t.tsu > 1) {
-        for (int c = 0; c < nd; c++) row[c] = SS_INFTY;
-      } else {
-        double b[4];
-        to_tlwh(t, b);
-        const double br0 = b[0] + b[2], br1 = b[1] + b[3];
-        for (int c = 0; c < nd; c++) {
-          const double* q = dq(c);
+      const SsTrk& t = x.trk[w.lst[ti[r]]];
+      const bool near = t.tsu <= 1;
+      double b[4];
+      to_tlwh(t, b);
+      const double br0 = b[0] + b[2], br1 = b[1] + b[3], ab = b[2] * b[3];
+      const double tq = t.quality, tcls = t.cls, tconf = t.conf;
+      double* out = tr ? C + r : C + (size_t)r * nd;
+      const size_t st = tr ? (size_t)nt : 1;
+      for (int c = 0; c < nd; c++) {
+        const double* q = dq(c);
+        double e = SS_INFTY;
+        if (near) {
           const double tl0 = fmax(b[0], q[0]), tl1 = fmax(b[1], q[1]);
           const double e0 = fmin(br0, q[0] + q[2]), e1 = fmin(br1, q[1] + q[3]);
           const double ww = fmax(0.0, e0 - tl0), hh = fmax(0.0, e1 - tl1);
           const double ai = ww * hh;
-          row[c] = 1.0 - ai / ((b[2] * b[3] + q[2] * q[3]) - ai);
+          e = 1.0 - ai / ((ab + q[2] * q[3]) - ai);
         }
+        e = enhance_v(tq, tcls, tconf, q, e);
+        out[c * st] = e > max_d ? max_d + 1e-5 : e;
       }
-      for (int c = 0; c < nd; c++) row[c] = enhance_clamp(t, dq(c), row[c], max_d);
     }
-    if (tr) {
-      __syncthreads();
-      for (int c = 0; c < nd; c++)
-        for (int r = lane; r < nt; r += 64) C[(size_t)c * nt + r] = C2[(size_t)r * nd + c];
-    }
+    P = C;
+    for (int o = lane; o < R; o += 64) roff[o] = o * CC;
+    mx = INF;  // clamped above
   }
   __syncthreads();
 #ifdef BX_PHASE_TIMING
@@ -1381,7 +1423,14 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
   SCOUNT(3, nt);
   SCOUNT(4, nd);
 #endif
-  const int np_ = lsap_wave(x, C, tr ? nd : nt, tr ? nt : nd, tr);
+  // gated levels: CC <= max(track_cap, det_cap) <= 1024; the IoU stage's candidates can list a
+  // track twice (up to 2 track_cap columns), its matrix is its own (identity column index)
+  const int np_ = kind == M_GATED
+                      ? (CC <= 256 ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr)
+                                   : lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr))
+                      : (CC <= 256    ? lsap_wave<4, false>(x, P, roff, cidx, mx, R, CC, tr)
+                         : CC <= 1024 ? lsap_wave<16, false>(x, P, roff, cidx, mx, R, CC, tr)
+                                      : lsap_wave<32, false>(x, P, roff, cidx, mx, R, CC, tr));
 #ifdef BX_PHASE_TIMING
   __syncthreads();
   SCOUNT(1, SS_NOW() - t1);
@@ -1402,7 +1451,8 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
     if (q < np_) {
       r = w.rows[q];
       c = w.cols[q];
-      rej = (tr ? C[(size_t)c * nt + r] : C[(size_t)r * nd + c]) > max_d;
+      const int cr = kind == M_GATED ? cidx[r] : r, cc = kind == M_GATED ? cidx[c] : c;
+      rej = (tr ? P[roff[c] + cr] : P[roff[r] + cc]) > max_d;
       ok = !rej;
     }
     const unsigned long long mo = __ballot(ok), mr = __ballot(rej);
@@ -1862,12 +1912,12 @@ __global__ void __launch_bounds__(64)
 // ss_match_kernel (one wave per sequence): the three matching stages of Tracker._enhanced_match
 // (stage 1/2 costs gathered from ss_cost_kernel's matrix).  Hands the matches (fmt), the unmatched
 // tracks (ffut) and detections (faud) to the next launches.
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) SS_MATCH_ATTR
     ss_match_kernel(SsDev g, int seq0) {
   extern __shared__ __align__(16) char ss_lds[];
   __shared__ int srank[1024], sgpos[1024], sinset[1024];
   __shared__ double ssdet[256 * DTW];
-  __shared__ int flt[1024], fld[1024];  // membership tables: track positions, sorted detections
+  __shared__ int flt[1024], fld[1024];  // solver column indices; sorted-detection membership
   __shared__ int stsu[1024], sage[1024];
   const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
   SsWs w;
@@ -1892,6 +1942,7 @@ __global__ void __launch_bounds__(64)
   x.ncf = g.ncf[seq];
   x.tsu = stsu;
   x.flt = sage;
+  x.cidx = flt;
   x.rank = srank;
   x.gpos = sgpos;
   x.inset = sinset;
@@ -2425,8 +2476,7 @@ static int ss_probe_end(bx_ss* e, int stage, hipStream_t st) {
 }
 
 static size_t ss_lds_bytes(const SsDev& d) {
-  return d.ws_lds == 1 ? (size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4
-                       : (d.ws_lds == 2 ? (size_t)ws_lsap_bytes(d.N) : 0);
+  return d.ws_lds == 1 ? (size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4 : (size_t)ws_lsap_bytes(d.N);
 }
 
 template <int G>
@@ -2550,8 +2600,8 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   // the frame kernel's workspace in LDS when it fits beside ~3 other workgroups per CU
   const size_t ws_bytes = (size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4;
   // all of it in LDS when it fits beside ~3 other workgroups per CU; else the LSAP state alone
-  // (the solver's inner loops) when that fits in one CU's 160 KB with room to spare
-  d.ws_lds = ws_bytes <= 48 * 1024 ? 1 : (ws_lsap_bytes(d.N) <= 120 * 1024 ? 2 : 0);
+  // (the solver's inner loops; track_cap, det_cap <= 1024 keep it within 106 KB)
+  d.ws_lds = ws_bytes <= 48 * 1024 ? 1 : 2;
   const size_t S = d.S, T = d.T, D = d.D, F = d.F, VP = d.VP, GB = d.GB;
   size_t off = 0;
   auto cb = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };

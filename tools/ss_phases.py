@@ -22,7 +22,8 @@ PHASES = ["setup", "crowd", "camera+quality+sort+predict", "lists", "stage1 casc
           "stage2 cascade", "stage3 iou", "updates+misses", "recovery", "births", "deaths",
           "partial_fit", "masks+outputs"]
 COUNTERS = ["cost build cyc", "lsap cyc", "lsap calls", "sum rows (tracks)", "sum cols (dets)",
-            "dijkstra steps", "matches"]
+            "dijkstra steps", "matches", "solver rows R", "solver cols CC", "slow rows",
+            "slow-row cyc", "lsap loop cyc"]
 
 
 def build():
@@ -39,10 +40,11 @@ def main():
     ap.add_argument("--seqs", type=int, default=None)
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--no-build", action="store_true")
+    ap.add_argument("--lib", default=None, help="a timing build of tools/build_variant.py")
     a = ap.parse_args()
     if not a.no_build:
         build()
-    os.environ["BX_LIB_PATH"] = str(LIB)
+    os.environ["BX_LIB_PATH"] = a.lib or str(LIB)
     import torch
 
     from bench import CONFIGS, DEFAULT_SEQS, OCS_CONF_LO
