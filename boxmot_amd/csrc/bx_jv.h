@@ -443,6 +443,35 @@ __device__ __forceinline__ double perm_d(double v, int dst) {
 __device__ __forceinline__ double wave_min_dpp(double a) {  // no NaNs (fmin drops them anyway)
   return rl_d(scan_min_d(a), 63);
 }
+// The wave minimum in every lane, returned uniform: a butterfly — row rotations by 8/4/2/1 within
+// rows of 16 (every lane stays valid, no identity to preload), then gfx950's row-pair and half
+// swaps.  fmin ignores NaNs (an all-NaN wave gives NaN).
+__device__ __forceinline__ double swap_min(double r, bool half) {
+  const long long b = __double_as_longlong(r);
+  const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+  unsigned a0, a1, h0, h1;
+  if (half) {
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a0 = l[0], a1 = l[1], h0 = h[0], h1 = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a0 = l[0], a1 = l[1], h0 = h[0], h1 = h[1];
+  }
+  const double x = __longlong_as_double(((long long)h0 << 32) | a0);
+  const double y = __longlong_as_double(((long long)h1 << 32) | a1);
+  return fmin(x, y);
+}
+__device__ __forceinline__ double wave_min_bfly(double r) {
+  r = fmin(r, dpp_d<0x128, 0xf, 0xf>(r, r));
+  r = fmin(r, dpp_d<0x124, 0xf, 0xf>(r, r));
+  r = fmin(r, dpp_d<0x122, 0xf, 0xf>(r, r));
+  r = fmin(r, dpp_d<0x121, 0xf, 0xf>(r, r));
+  r = swap_min(r, false);
+  r = swap_min(r, true);
+  return rl_d(r, 0);
+}
 
 __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
   const int n = nr > nc ? nr : nc;

@@ -962,22 +962,22 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
   const double clampv = max_d + 1e-5;
   for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
   for (int j = lane; j < CC; j += 64) w.v[j] = 0.0, w.path[j] = -1, w.row4col[j] = -1;
-  int ci[LQ];
-  double vr[LQ];
+  unsigned cb[LQ];  // byte offset of the lane's column q in a row (column 0's past CC)
+  double vr[LQ];    // v[j]; -INF past CC, so those columns relax to +INF
   unsigned asg = 0;
 #pragma unroll
   for (int q = 0; q < LQ; q++) {
     const int j = lane + 64 * q;
-    ci[q] = IDX ? (j < CC ? cidx[j] : 0) : j;
-    vr[q] = 0.0;
+    cb[q] = 8u * (unsigned)(j < CC ? (IDX ? cidx[j] : j) : 0);
+    vr[q] = j < CC ? 0.0 : -INF;
   }
   __syncthreads();
+  // raw loads, unconditional (in-row offsets): clamped where used, so a load is waited for only
+  // when its value is needed
   auto load_row = [&](int off, double* dst) {
+    const char* base = (const char*)(P + off);
 #pragma unroll
-    for (int q = 0; q < LQ; q++) {
-      const double e = lane + 64 * q < CC ? P[off + ci[q]] : 0.0;
-      dst[q] = e;  // raw: clamped where used, so the load is waited for only then
-    }
+    for (int q = 0; q < LQ; q++) dst[q] = *(const double*)(base + cb[q]);
   };
   // the next row's loads are issued during this one's reductions, except at LQ = 32 (IoU stage of
   // more than 1024 candidates, rare) where the registers would not hold both rows
@@ -988,14 +988,11 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
   for (int cur = 0; cur < R; cur++) {
     if (!PF) load_row(roff[cur], nx);
     // scipy's minVal + cost - u[cur] - v[j] with minVal = u[cur] = 0 (up to the sign of a zero,
-    // which no comparison and no later sum can tell)
+    // which no comparison and no later sum can tell).  A NaN cost stays NaN here and loses every
+    // comparison below, as the INF that scipy's `r < INF` test would make of it.
     double rv[LQ];
 #pragma unroll
-    for (int q = 0; q < LQ; q++) {
-      const double c = nx[q] > max_d ? clampv : nx[q];
-      const double r = c - vr[q];
-      rv[q] = lane + 64 * q < CC ? (r < INF ? r : INF) : INF;
-    }
+    for (int q = 0; q < LQ; q++) rv[q] = (nx[q] > max_d ? clampv : nx[q]) - vr[q];
     double lmin = rv[0];
 #pragma unroll
     for (int q = 1; q < LQ; q++) lmin = fmin(lmin, rv[q]);
@@ -1003,24 +1000,31 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       load_row(off1, nx);
       off1 = cur + 2 < R ? roff[cur + 2] : 0;
     }
-    const double m0 = wave_min_dpp(lmin);
+    const double m0 = wave_min_bfly(lmin);
     if (!(m0 < INF)) {  // infeasible (cannot happen with finite costs)
       if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
       return 0;
     }
-    unsigned eq = 0;
+    // the columns at the minimum, one wave mask per q
+    int cnt = 0, q0 = 0;
+    unsigned long long e0 = 0;
 #pragma unroll
-    for (int q = 0; q < LQ; q++) eq |= rv[q] == m0 ? 1u << q : 0u;
-    const unsigned un = eq & ~asg;
+    for (int q = 0; q < LQ; q++) {
+      const unsigned long long e = __ballot(rv[q] == m0);
+      cnt += __popcll(e);
+      if (e) q0 = q, e0 = e;
+    }
     int j0;
     bool sink;
-    const unsigned long long lm = __ballot(eq != 0);
-    if ((lm & (lm - 1)) == 0) {  // one lane holds the columns at the minimum (the usual case)
-      const int L = __ffsll((long long)lm) - 1;
-      const unsigned eL = (unsigned)rl_i((int)eq, L), uL = (unsigned)rl_i((int)un, L);
-      sink = uL != 0;
-      j0 = L + 64 * (sink ? __ffs(uL) - 1 : 31 - __clz(eL));
-    } else {
+    if (cnt == 1) {  // a unique minimum (the usual case)
+      const int L = __ffsll((long long)e0) - 1;
+      j0 = L + 64 * q0;
+      sink = !((rl_i((int)asg, L) >> q0) & 1);
+    } else {  // scipy's tie rule over the lanes
+      unsigned eq = 0;
+#pragma unroll
+      for (int q = 0; q < LQ; q++) eq |= rv[q] == m0 ? 1u << q : 0u;
+      const unsigned un = eq & ~asg;
       constexpr int BIG = 0x7fffffff;
       const int a = un ? lane + 64 * (__ffs(un) - 1) : BIG;
       const int b = eq ? lane + 64 * (31 - __clz(eq)) : -1;
@@ -1074,7 +1078,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     while (sk == -1) {
       if (lane == 0) w.SR[i] = 1;
       const double ui = w.u[i];
-      const int offi = roff[i];
+      const char* rowi = (const char*)(P + roff[i]);
       double m = INF;
       constexpr int QB = LQ < 8 ? LQ : 8;  // loads in flight per lane
 #pragma unroll
@@ -1083,7 +1087,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
 #pragma unroll
         for (int u = 0; u < QB; u++) {
           const int q = q0 + u;
-          const double e = lane + 64 * q < CC ? P[offi + ci[q]] : 0.0;
+          const double e = *(const double*)(rowi + cb[q]);
           cv[u] = e > max_d ? clampv : e;
         }
 #pragma unroll
@@ -1162,7 +1166,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
 #pragma unroll
     for (int q = 0; q < LQ; q++) {
       const int j = lane + 64 * q;
-      vr[q] = j < CC ? w.v[j] : 0.0;
+      vr[q] = j < CC ? w.v[j] : -INF;
     }
     __syncthreads();
   }
