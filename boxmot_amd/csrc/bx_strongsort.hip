@@ -961,7 +961,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
 #endif
   const double clampv = max_d + 1e-5;
   for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
-  for (int j = lane; j < CC; j += 64) w.v[j] = 0.0, w.path[j] = -1, w.row4col[j] = -1;
+  for (int j = lane; j < CC; j += 64) w.path[j] = -1, w.row4col[j] = -1;
   unsigned cb[LQ];  // byte offset of the lane's column q in a row (column 0's past CC)
   double vr[LQ];    // v[j]; -INF past CC, so those columns relax to +INF
   unsigned asg = 0;
@@ -1045,38 +1045,36 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     SCOUNT(9, 1);
     t_s0 = SS_NOW();
 #endif
-    // the search continues: scipy's state after the first step, written out
+    // The search continues as scipy's does, its per-column state in registers: spc (rv, NaN as
+    // INF), the SC bits, v; `remaining` (rem / pos, for the tie rule), path and the visited rows
+    // (with the minimum each was reached at: spc of its column) in LDS.
     const int index0 = CC - 1 - j0;
     double minVal = m0;
     int nrem = CC;
-    for (int j = lane; j < CC; j += 64) {
-      w.rem[CC - 1 - j] = j;
-      w.pos[j] = CC - 1 - j;
-      w.SC[j] = 0;
-      w.spc[j] = INF;
-    }
-    for (int i = lane; i < R; i += 64) w.SR[i] = 0;
-    __syncthreads();
+    unsigned sc = lane == (j0 & 63) ? 1u << (j0 >> 6) : 0u;
 #pragma unroll
     for (int q = 0; q < LQ; q++) {  // the first step's relaxation
       const int j = lane + 64 * q;
-      if (j < CC && rv[q] < INF) {
-        w.path[j] = cur;
-        w.spc[j] = rv[q];
+      const bool ok = rv[q] < INF;
+      rv[q] = ok ? rv[q] : INF;
+      if (j < CC) {
+        w.rem[CC - 1 - j] = j;
+        w.pos[j] = CC - 1 - j;
+        if (ok) w.path[j] = cur;
       }
     }
+    __syncthreads();
     if (lane == 0) {
-      w.SR[cur] = 1;
-      w.SC[j0] = 1;
       const int jl = w.rem[nrem - 1];
       w.rem[index0] = jl;
       w.pos[jl] = index0;
     }
     nrem--;
-    __syncthreads();
+    int nvis = 0;  // visited rows other than cur: w.SR[k] (row), w.spc[k] (its minimum)
     int sk = -1, i = w.row4col[j0];
+    if (lane == 0) w.SR[0] = i, w.spc[0] = m0;
+    nvis = 1;
     while (sk == -1) {
-      if (lane == 0) w.SR[i] = 1;
       const double ui = w.u[i];
       const char* rowi = (const char*)(P + roff[i]);
       double m = INF;
@@ -1086,76 +1084,93 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
         double cv[QB];
 #pragma unroll
         for (int u = 0; u < QB; u++) {
-          const int q = q0 + u;
-          const double e = *(const double*)(rowi + cb[q]);
+          const double e = *(const double*)(rowi + cb[q0 + u]);
           cv[u] = e > max_d ? clampv : e;
         }
 #pragma unroll
         for (int u = 0; u < QB; u++) {
-          const int q = q0 + u, j = lane + 64 * q;
-          if (j >= CC || w.SC[j]) continue;
-          const double r = minVal + cv[u] - ui - vr[q];
-          double sp = w.spc[j];
-          if (r < sp) {
-            w.path[j] = i;
-            w.spc[j] = sp = r;
+          const int q = q0 + u;
+          if ((sc >> q) & 1u) continue;
+          const double r = minVal + cv[u] - ui - vr[q];  // +INF past CC
+          if (r < rv[q]) {
+            rv[q] = r;
+            w.path[lane + 64 * q] = i;
           }
-          m = fmin(m, sp);
+          m = fmin(m, rv[q]);
         }
       }
-      m = wave_min_dpp(m);
-      int last_un = -1, first_eq = 0x7fffffff;
-#pragma unroll
-      for (int q = 0; q < LQ; q++) {
-        const int j = lane + 64 * q;
-        if (j < CC && !w.SC[j] && w.spc[j] == m) {
-          const int p = w.pos[j];
-          if (!((asg >> q) & 1u)) last_un = p > last_un ? p : last_un;
-          first_eq = p < first_eq ? p : first_eq;
-        }
-      }
-      last_un = -wave_min_i(-last_un);
-      first_eq = wave_min_i(first_eq);
+      m = wave_min_bfly(m);
       if (!(m < INF)) {  // infeasible (cannot happen with finite costs)
         if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
         return 0;
       }
-      const int index = last_un >= 0 ? last_un : first_eq;
+      int c1 = 0, qs = 0;
+      unsigned long long es = 0;
+#pragma unroll
+      for (int q = 0; q < LQ; q++) {
+        const unsigned long long e = __ballot(!((sc >> q) & 1u) && rv[q] == m);
+        c1 += __popcll(e);
+        if (e) qs = q, es = e;
+      }
+      int j;
+      if (c1 == 1) {
+        j = __ffsll((long long)es) - 1 + 64 * qs;
+      } else {  // the last unassigned column at the minimum in `remaining` order, else the first
+        int last_un = -1, first_eq = 0x7fffffff;
+#pragma unroll
+        for (int q = 0; q < LQ; q++) {
+          const int jq = lane + 64 * q;
+          if (!((sc >> q) & 1u) && rv[q] == m) {
+            const int p = w.pos[jq];
+            if (!((asg >> q) & 1u)) last_un = p > last_un ? p : last_un;
+            first_eq = p < first_eq ? p : first_eq;
+          }
+        }
+        last_un = -wave_min_i(-last_un);
+        first_eq = wave_min_i(first_eq);
+        j = w.rem[last_un >= 0 ? last_un : first_eq];
+      }
       minVal = m;
-      const int j = w.rem[index];
-      if (w.row4col[j] == -1)
+      const bool un = !((rl_i((int)asg, j & 63) >> (j >> 6)) & 1);
+      if (un) {
         sk = j;
-      else
+      } else {
         i = w.row4col[j];
-      __syncthreads();
+        if (lane == 0) w.SR[nvis] = i, w.spc[nvis] = m;
+        nvis++;
+      }
+      if (lane == (j & 63)) sc |= 1u << (j >> 6);
       if (lane == 0) {
-        w.SC[j] = 1;
+        const int index = w.pos[j];
         const int jl = w.rem[nrem - 1];
         w.rem[index] = jl;
         w.pos[jl] = index;
       }
       nrem--;
-      __syncthreads();
 #ifdef BX_PHASE_TIMING
       if (threadIdx.x == 0 && x.g.dbg) x.g.dbg[(size_t)x.seq * SS_DBG + 16 + 5] += 1;
 #endif
     }
-    for (int q = lane; q < R; q += 64)
-      if (q == cur)
-        w.u[q] += minVal;
-      else if (w.SR[q])
-        w.u[q] += minVal - w.spc[w.col4row[q]];
-    for (int j = lane; j < CC; j += 64)
-      if (w.SC[j]) w.v[j] -= minVal - w.spc[j];
+    __syncthreads();
+    // duals: u[cur] = minVal (it was 0), u[i] += minVal - spc[col4row[i]] for the visited rows,
+    // v[j] -= minVal - spc[j] for the SC columns; then the augmentation along path
+    for (int k = lane; k < nvis; k += 64) {
+      const int r = w.SR[k];
+      w.u[r] += minVal - w.spc[k];
+    }
+    if (lane == 0) w.u[cur] = 0.0 + minVal;
+#pragma unroll
+    for (int q = 0; q < LQ; q++)
+      if ((sc >> q) & 1u) vr[q] -= minVal - rv[q];
     __syncthreads();
     if (lane == 0) {
-      int j = sk;
+      int jj = sk;
       for (;;) {
-        const int q = w.path[j];
-        w.row4col[j] = q;
+        const int q = w.path[jj];
+        w.row4col[jj] = q;
         const int t = w.col4row[q];
-        w.col4row[q] = j;
-        j = t;
+        w.col4row[q] = jj;
+        jj = t;
         if (q == cur) break;
       }
     }
@@ -1163,11 +1178,6 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
 #ifdef BX_PHASE_TIMING
     t_slow += SS_NOW() - t_s0;
 #endif
-#pragma unroll
-    for (int q = 0; q < LQ; q++) {
-      const int j = lane + 64 * q;
-      vr[q] = j < CC ? w.v[j] : -INF;
-    }
     __syncthreads();
   }
   __syncthreads();
