@@ -924,11 +924,10 @@ struct SsCtx {
   int* rank;    // match kernel: cascade rank by list position (LDS)
   int* gpos;    // match kernel: list position by cascade rank (LDS)
   int* inset;   // match kernel: membership table by list position (LDS)
-  double* sdet; // match kernel: staged detection rows for the IoU stage (LDS, 256 x DTW)
   int ncf;      // confirmed tracks
   int* flt;     // match kernel: scratch table (LDS, 1024 ints)
   double* ks;   // match kernel: sort-key scratch (LDS)
-  int* cidx;    // match kernel: the solver's column indices (LDS, 1024 ints)
+  int* cidx;    // match kernel: the solver's column indices (LDS, 2048 ints)
   __device__ const double* det(int i) const { return w.dt + (size_t)w.dord[i] * DTW; }
   __device__ int det_in(int i) const { return (int)det(i)[6]; }
 };
@@ -1232,8 +1231,10 @@ __device__ __forceinline__ double enhance_clamp(const SsTrk& t, const double* d,
 // lanes over detections in quality order): gated_metric's NN distance, gate_cost_matrix with the
 // motion / adaptive-lambda / track-specific shaping (linear_assignment.py:174-352), the
 // id-preservation weight (tracker.py:283-298) and _enhance_cost_matrix — everything but the
-// level's clamp.  Only depends on the predicted tracks and the detections, so the cascade levels
-// of ss_match_kernel gather from it.
+// level's clamp.  And stage 3's cost of every listed track: iou_cost (iou_matching.py:55-87,
+// INFTY past time_since_update 1) with _enhance_cost_matrix, unclamped.  Both only depend on the
+// predicted tracks and the detections, so ss_match_kernel's solver reads them in place (by
+// cascade rank / list position and sorted detection, in both orientations).
 __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
   __shared__ double sh[32];
   const int b = blockIdx.y, seq = seq0 + b, k = blockIdx.x, lane = threadIdx.x;
@@ -1242,7 +1243,32 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
   const int nk = sq[Q_NK];
   const int slot = g.order[(size_t)seq * g.T + k];
   const SsTrk& t = g.trk[(size_t)seq * g.T + slot];
-  if (t.state != 2 || nk == 0) return;
+  if (nk == 0) return;
+  {
+    const double* dt = g.fdt + (size_t)seq * g.D * DTW;
+    const int* dord = g.fdord + (size_t)seq * g.D;
+    double* io = g.cost + (size_t)seq * 4 * g.T * g.D;  // [T][D] by list position
+    double* ioT = io + (size_t)g.T * g.D;               // [D][T]
+    const bool near = t.tsu <= 1;
+    double bx[4];
+    to_tlwh(t, bx);
+    const double br0 = bx[0] + bx[2], br1 = bx[1] + bx[3], ab = bx[2] * bx[3];
+    for (int c = lane; c < nk; c += 64) {
+      const double* q = dt + (size_t)dord[c] * DTW;
+      double e = SS_INFTY;
+      if (near) {
+        const double tl0 = fmax(bx[0], q[0]), tl1 = fmax(bx[1], q[1]);
+        const double e0 = fmin(br0, q[0] + q[2]), e1 = fmin(br1, q[1] + q[3]);
+        const double ww = fmax(0.0, e0 - tl0), hh = fmax(0.0, e1 - tl1);
+        const double ai = ww * hh;
+        e = 1.0 - ai / ((ab + q[2] * q[3]) - ai);
+      }
+      e = enhance(t, q, e);
+      io[(size_t)k * g.D + c] = e;
+      ioT[(size_t)c * g.T + k] = e;
+    }
+  }
+  if (t.state != 2) return;
   // this track's cascade rank: time_since_update ascending, -(quality + stability), list order
   int rk = 0;
   {
@@ -1386,48 +1412,16 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
     for (int c = lane; c < CC; c += 64) cidx[c] = tr ? rk[li[c]] : li[c];
     mx = max_d;
   } else {
-    // iou_cost + _enhance_cost_matrix + the clamp of every (track, detection), written straight
-    // in the solver's orientation R x CC: lanes over the solver's columns (coalesced stores), the
-    // rows' operands uniform per iteration
-    double* C = g.cost + (size_t)x.seq * 4 * g.T * g.D;
-    // the detections' rows staged in LDS when they fit (x.sdet: 256 x DTW)
-    const bool staged = x.sdet && nd <= 256;
-    if (staged) {
-      for (int k = lane; k < nd * DTW; k += 64) {
-        const int c = k / DTW, f = k - c * DTW;
-        x.sdet[k] = x.det(di[c])[f];
-      }
-      __syncthreads();
-    }
-    auto dq = [&](int c) { return staged ? x.sdet + (size_t)c * DTW : x.det(di[c]); };
-    // lanes over tracks, the track's operands in registers (the stores could alias them);
-    // transposed (tr) the lanes' stores are coalesced
-    for (int r = lane; r < nt; r += 64) {
-      const SsTrk& t = x.trk[w.lst[ti[r]]];
-      const bool near = t.tsu <= 1;
-      double b[4];
-      to_tlwh(t, b);
-      const double br0 = b[0] + b[2], br1 = b[1] + b[3], ab = b[2] * b[3];
-      const double tq = t.quality, tcls = t.cls, tconf = t.conf;
-      double* out = tr ? C + r : C + (size_t)r * nd;
-      const size_t st = tr ? (size_t)nt : 1;
-      for (int c = 0; c < nd; c++) {
-        const double* q = dq(c);
-        double e = SS_INFTY;
-        if (near) {
-          const double tl0 = fmax(b[0], q[0]), tl1 = fmax(b[1], q[1]);
-          const double e0 = fmin(br0, q[0] + q[2]), e1 = fmin(br1, q[1] + q[3]);
-          const double ww = fmax(0.0, e0 - tl0), hh = fmax(0.0, e1 - tl1);
-          const double ai = ww * hh;
-          e = 1.0 - ai / ((ab + q[2] * q[3]) - ai);
-        }
-        e = enhance_v(tq, tcls, tconf, q, e);
-        out[c * st] = e > max_d ? max_d + 1e-5 : e;
-      }
-    }
-    P = C;
-    for (int o = lane; o < R; o += 64) roff[o] = o * CC;
-    mx = INF;  // clamped above
+    // ss_cost_kernel's iou_cost + _enhance_cost_matrix of (list position, sorted detection),
+    // read in place; the clamp at max_iou_distance here
+    const double* io = g.cost + (size_t)x.seq * 4 * g.T * g.D;
+    P = tr ? io + (size_t)g.T * g.D : io;
+    const int ld = tr ? g.T : g.D;
+    const int* li = tr ? ti : di;  // columns
+    const int* oi = tr ? di : ti;  // rows
+    for (int o = lane; o < R; o += 64) roff[o] = oi[o] * ld;
+    for (int c = lane; c < CC; c += 64) cidx[c] = li[c];
+    mx = max_d;
   }
   __syncthreads();
 #ifdef BX_PHASE_TIMING
@@ -1437,14 +1431,11 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
   SCOUNT(3, nt);
   SCOUNT(4, nd);
 #endif
-  // gated levels: CC <= max(track_cap, det_cap) <= 1024; the IoU stage's candidates can list a
-  // track twice (up to 2 track_cap columns), its matrix is its own (identity column index)
-  const int np_ = kind == M_GATED
-                      ? (CC <= 256 ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr)
-                                   : lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr))
-                      : (CC <= 256    ? lsap_wave<4, false>(x, P, roff, cidx, mx, R, CC, tr)
-                         : CC <= 1024 ? lsap_wave<16, false>(x, P, roff, cidx, mx, R, CC, tr)
-                                      : lsap_wave<32, false>(x, P, roff, cidx, mx, R, CC, tr));
+  // CC <= max(track_cap, det_cap) <= 1024, but for the IoU stage's candidates, which can list a
+  // track twice (up to 2 track_cap columns)
+  const int np_ = CC <= 256    ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr)
+                  : CC <= 1024 ? lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr)
+                               : lsap_wave<32, true>(x, P, roff, cidx, mx, R, CC, tr);
 #ifdef BX_PHASE_TIMING
   __syncthreads();
   SCOUNT(1, SS_NOW() - t1);
@@ -1465,8 +1456,7 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
     if (q < np_) {
       r = w.rows[q];
       c = w.cols[q];
-      const int cr = kind == M_GATED ? cidx[r] : r, cc = kind == M_GATED ? cidx[c] : c;
-      rej = (tr ? P[roff[c] + cr] : P[roff[r] + cc]) > max_d;
+      rej = (tr ? P[roff[c] + cidx[r]] : P[roff[r] + cidx[c]]) > max_d;
       ok = !rej;
     }
     const unsigned long long mo = __ballot(ok), mr = __ballot(rej);
@@ -1822,10 +1812,6 @@ __global__ void __launch_bounds__(64)
     n = g.D;
   }
   const int frame = sq[Q_FRAME] + 1;
-  if (lane == 0) {  // gallery rows compared by this frame's ss_nn_kernel (a statistic)
-    sq[Q_ROWSL] = sq[Q_ROWS];
-    sq[Q_ROWS] = 0;
-  }
   x.ntr = sq[Q_NTR];
   x.nlost = sq[Q_NLOST];
   const int nt0 = x.ntr;
@@ -1930,8 +1916,7 @@ __global__ void __launch_bounds__(64) SS_MATCH_ATTR
     ss_match_kernel(SsDev g, int seq0) {
   extern __shared__ __align__(16) char ss_lds[];
   __shared__ int srank[1024], sgpos[1024], sinset[1024];
-  __shared__ double ssdet[256 * DTW];
-  __shared__ int flt[1024], fld[1024];  // solver column indices; sorted-detection membership
+  __shared__ int flt[2048], fld[1024];  // solver column indices; sorted-detection membership
   __shared__ int stsu[1024], sage[1024];
   const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
   SsWs w;
@@ -1946,6 +1931,10 @@ __global__ void __launch_bounds__(64) SS_MATCH_ATTR
   x.ntr = sq[Q_NTR];
   x.nlost = sq[Q_NLOST];
   x.nk = sq[Q_NK];
+  if (lane == 0) {  // gallery rows compared by this frame's ss_nn_kernel (a statistic)
+    sq[Q_ROWSL] = sq[Q_ROWS];
+    sq[Q_ROWS] = 0;
+  }
   for (int p = lane; p < x.ntr; p += 64) {
     w.lst[p] = order[p];
     stsu[p] = x.trk[order[p]].tsu;
@@ -1960,7 +1949,6 @@ __global__ void __launch_bounds__(64) SS_MATCH_ATTR
   x.rank = srank;
   x.gpos = sgpos;
   x.inset = sinset;
-  x.sdet = ssdet;
   __syncthreads();
 
   // ---- Tracker._enhanced_match (tracker.py:183-281, P6) --------------------------------------
@@ -2463,6 +2451,10 @@ struct bx_ss {
   int probe_stage = -1;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   int ev_used = 0;
+  // crowd test + ss_pre_kernel run on `side` beside ss_nn_kernel / ss_rec_kernel (neither reads
+  // what the other writes); fork after ss_prep_kernel, join before ss_cost_kernel
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 #define SCHK(x)                                                                    \
@@ -2513,6 +2505,18 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   hipLaunchKernelGGL(ss_prep_kernel, dim3(d.D, nseq), dim3(64), 0, st, d, seq0, off, embs);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 0, st))) return rc;
+  // fork: the crowd test and ss_pre_kernel (camera, quality + sort, predict) on the side stream
+  const size_t lds = ss_lds_bytes(d);
+  SCHK(hipEventRecord(e->ev_fork, st));
+  SCHK(hipStreamWaitEvent(e->side, e->ev_fork, 0));
+  if ((rc = ss_probe_begin(e, 3, e->side))) return rc;
+  if (d.crowd)
+    hipLaunchKernelGGL(ss_crowd_kernel, dim3(CROWD_BLOCKS, nseq), dim3(256), 0, e->side, d, seq0);
+  hipLaunchKernelGGL(ss_pre_kernel, dim3(nseq), dim3(64), lds, e->side, d, seq0, dets, off,
+                     warps);
+  SCHK(hipGetLastError());
+  if ((rc = ss_probe_end(e, 3, e->side))) return rc;
+  SCHK(hipEventRecord(e->ev_join, e->side));
   if ((rc = ss_probe_begin(e, 1, st))) return rc;
   // tracks per wave: 4 share every detection load (the detection blocks' split over waves
   // below restores the wave count), fewer only for a handful of tracks
@@ -2540,13 +2544,7 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   hipLaunchKernelGGL(ss_rec_kernel, dim3(LOSTN, nseq), dim3(256), 0, st, d, seq0, off, embs);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 2, st))) return rc;
-  const size_t lds = ss_lds_bytes(d);
-  if ((rc = ss_probe_begin(e, 3, st))) return rc;
-  if (d.crowd)
-    hipLaunchKernelGGL(ss_crowd_kernel, dim3(CROWD_BLOCKS, nseq), dim3(256), 0, st, d, seq0);
-  hipLaunchKernelGGL(ss_pre_kernel, dim3(nseq), dim3(64), lds, st, d, seq0, dets, off, warps);
-  SCHK(hipGetLastError());
-  if ((rc = ss_probe_end(e, 3, st))) return rc;
+  SCHK(hipStreamWaitEvent(st, e->ev_join, 0));  // join
   if ((rc = ss_probe_begin(e, 4, st))) return rc;
   hipLaunchKernelGGL(ss_cost_kernel, dim3(d.T, nseq), dim3(64), 0, st, d, seq0);
   SCHK(hipGetLastError());
@@ -2722,6 +2720,9 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
     SCHK(hipFuncSetAttribute((const void*)ss_post_kernel,
                              hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   }
+  SCHK(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+  SCHK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+  SCHK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
   SCHK(hipMalloc(&e->h_dets, sizeof(double) * 6 * D));
   SCHK(hipMalloc(&e->h_off, sizeof(int) * 2));
   SCHK(hipMalloc(&e->h_embs, sizeof(double) * D * F));
@@ -2740,6 +2741,9 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
 
 int bx_ss_destroy(bx_ss* e) {
   if (!e) return BX_OK;
+  if (e->side) (void)hipStreamDestroy(e->side);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   for (auto& p : e->ev) {
     (void)hipEventDestroy(p.first);
     (void)hipEventDestroy(p.second);
