@@ -693,58 +693,69 @@ __global__ void __launch_bounds__(64)
 }
 
 typedef double d4 __attribute__((ext_vector_type(4)));
-#ifndef BX_NN_KU
-#define BX_NN_KU 2
-#endif
 
-// The NN contraction's k loop for RT row tiles x NDT detection tiles: straight-line blocks of
-// KU MFMA k-steps, the next block's operands loaded before this block's MFMAs; padded rows (past a track's
-// samples) read valid rows and are discarded by the caller, so no branch splits the chains.
+// Operands of two k-steps from one 16-byte load per lane: lane group m (lanes 16m..16m+15) loaded
+// elements (k0 + 2m, k0 + 2m + 1) of its row; the MFMA wants k0 + m for the first step and
+// k0 + 4 + m for the second (each step's k-slots ascending, so the accumulation stays the oracle's
+// ascending fma chain).  Two gfx950 row swaps transpose the 4 x 2 blocks:
+// swap16 -> [x0 y0 x2 y2] / [x1 y1 x3 y3], swap32 -> [x0 y0 x1 y1] / [x2 y2 x3 y3] (rows of 16 lanes).
+__device__ __forceinline__ void kpair(const double2 v, double& s0, double& s1) {
+  const long long a = __double_as_longlong(v.x), b = __double_as_longlong(v.y);
+  const auto l16 = __builtin_amdgcn_permlane16_swap((unsigned)a, (unsigned)b, false, false);
+  const auto h16 = __builtin_amdgcn_permlane16_swap((unsigned)(a >> 32), (unsigned)(b >> 32),
+                                                    false, false);
+  const auto l32 = __builtin_amdgcn_permlane32_swap(l16[0], l16[1], false, false);
+  const auto h32 = __builtin_amdgcn_permlane32_swap(h16[0], h16[1], false, false);
+  s0 = __longlong_as_double(((long long)h32[0] << 32) | l32[0]);
+  s1 = __longlong_as_double(((long long)h32[1] << 32) | l32[1]);
+}
+
+// The NN contraction's k loop for RT row tiles x NDT detection tiles (ap / bp: the lane's row
+// bases): blocks of 8 k, one 16-byte load per tile and lane transposed into two MFMA k-steps
+// (kpair), the next block's loads in flight during this block's MFMAs; padded rows (past a
+// track's samples) read valid rows and are discarded by the caller, so no branch splits the chains.
 template <int RT, int NDT, int NA>
 __device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT],
                                          const double* const (&bp)[NA], int F, int kl,
                                          d4 (&acc)[RT][NA]) {
-  constexpr int KU = BX_NN_KU, KS = 4 * KU;
-  const int FB = F - F % KS;
-  if (FB > 0) {  // software-pipelined: block k+1's operands in flight during block k's MFMAs
-    double a[KU][RT], bb[KU][NDT];
+  const int FB = (F & 1) ? 0 : F - F % 8;  // 16-byte loads need even rows
+  if (FB > 0) {
+    double2 a[RT], bb[NDT];
 #pragma unroll
-    for (int u = 0; u < KU; u++) {
+    for (int rt = 0; rt < RT; rt++) a[rt] = *(const double2*)(ap[rt] + 2 * kl);
 #pragma unroll
-      for (int rt = 0; rt < RT; rt++) a[u][rt] = ap[rt][4 * u];
+    for (int dt = 0; dt < NDT; dt++) bb[dt] = *(const double2*)(bp[dt] + 2 * kl);
+    for (int k = 0; k < FB; k += 8) {
+      const int kn = k + 8 < FB ? k + 8 : k;  // the last block re-reads its own operands
+      double2 na[RT], nb[NDT];
 #pragma unroll
-      for (int dt = 0; dt < NDT; dt++) bb[u][dt] = bp[dt][4 * u];
-    }
-    for (int k = 0; k < FB; k += KS) {
-      const int kn = k + KS < FB ? k + KS : k;  // the last block re-reads its own operands
-      double na[KU][RT], nb[KU][NDT];
+      for (int rt = 0; rt < RT; rt++) na[rt] = *(const double2*)(ap[rt] + kn + 2 * kl);
 #pragma unroll
-      for (int u = 0; u < KU; u++) {
+      for (int dt = 0; dt < NDT; dt++) nb[dt] = *(const double2*)(bp[dt] + kn + 2 * kl);
+      double a0[RT], a1[RT], b0[NDT], b1[NDT];
 #pragma unroll
-        for (int rt = 0; rt < RT; rt++) na[u][rt] = ap[rt][kn + 4 * u];
+      for (int rt = 0; rt < RT; rt++) kpair(a[rt], a0[rt], a1[rt]);
 #pragma unroll
-        for (int dt = 0; dt < NDT; dt++) nb[u][dt] = bp[dt][kn + 4 * u];
-      }
+      for (int dt = 0; dt < NDT; dt++) kpair(bb[dt], b0[dt], b1[dt]);
 #pragma unroll
-      for (int u = 0; u < KU; u++)
+      for (int rt = 0; rt < RT; rt++)
 #pragma unroll
-        for (int rt = 0; rt < RT; rt++)
+        for (int dt = 0; dt < NDT; dt++)
+          acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[rt], b0[dt], acc[rt][dt], 0, 0, 0);
 #pragma unroll
-          for (int dt = 0; dt < NDT; dt++)
-            acc[rt][dt] =
-                __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][rt], bb[u][dt], acc[rt][dt], 0, 0, 0);
+      for (int rt = 0; rt < RT; rt++)
 #pragma unroll
-      for (int u = 0; u < KU; u++) {
+        for (int dt = 0; dt < NDT; dt++)
+          acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[rt], b1[dt], acc[rt][dt], 0, 0, 0);
 #pragma unroll
-        for (int rt = 0; rt < RT; rt++) a[u][rt] = na[u][rt];
+      for (int rt = 0; rt < RT; rt++) a[rt] = na[rt];
 #pragma unroll
-        for (int dt = 0; dt < NDT; dt++) bb[u][dt] = nb[u][dt];
-      }
+      for (int dt = 0; dt < NDT; dt++) bb[dt] = nb[dt];
     }
   }
   for (int k = FB; k < F; k += 4) {  // tail: lanes past F multiply zeros (a clamped read)
     const bool in = k + kl < F;
-    const int kk = in ? k : F - 1 - kl;
+    const int kk = in ? k + kl : F - 1;
     double a[RT], bb[NDT];
 #pragma unroll
     for (int rt = 0; rt < RT; rt++) { const double v = ap[rt][kk]; a[rt] = in ? v : 0.0; }
@@ -821,7 +832,7 @@ __global__ void __launch_bounds__(64)
 #pragma unroll
     for (int dt = 0; dt < NDT; dt++) {
       const int col = db + 16 * dt + cl;
-      bp[dt] = dnb + (size_t)(col < n ? col : 0) * F + kl;
+      bp[dt] = dnb + (size_t)(col < n ? col : 0) * F;
     }
     for (int p0 = 0; p0 < ntile; p0 += RT) {
       const double* ap[RT];
@@ -831,7 +842,7 @@ __global__ void __launch_bounds__(64)
         const int ti = p0 + rt < ntile ? p0 + rt : p0;
         const int q = tt[ti], row = tr0[ti] + cl;
         const int slot = slot_s[q];
-        ap[rt] = vecnp(g, seq, slot, rowv[q][row < nrow_s[q] ? row : 0]) + kl;
+        ap[rt] = vecnp(g, seq, slot, rowv[q][row < nrow_s[q] ? row : 0]);
         nrt += p0 + rt < ntile;
       }
       d4 acc[RT][NDT];
