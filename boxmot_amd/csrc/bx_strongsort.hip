@@ -99,6 +99,8 @@ struct SsDev {
   int* order;     // [S][T] track list (slots)
   int* lost;      // [S][LOSTN] lost buffer (slots)
   int* nnl;       // [S][T] confirmed slots queried by the next frame's gallery distance
+  int* pk;        // [S][T+3] packs of nnl for ss_nn_kernel: starts pk[0..P], P at pk[T+1];
+                  // pk[T+2]: a detection passes min_conf this frame (ss_motion_kernel)
   double* nnd;    // [S][T][D] NN distance by (slot, input detection)
   double* dprep;  // [S][D][4] wave norm, pairwise norm of feat; wave norm, den of nf
   double* dn;     // [S][D][F] feat / (pairwise norm + 1e-8)
@@ -625,10 +627,59 @@ __device__ __forceinline__ bool in_list(const int* a, int n, int v) {
 // pairwise norm of feat, wave norm of nf, pairwise norm of nf + 1e-8], dn, nf
 __global__ void __launch_bounds__(64)
     ss_prep_kernel(SsDev g, int seq0, const int* __restrict__ det_off,
-                   const double* __restrict__ embs) {
+                   const double* __restrict__ embs, const double* __restrict__ dets) {
   __shared__ int lo[PW_MAXLEAF], ln[PW_MAXLEAF];
   __shared__ double leaf[PW_MAXLEAF];
   const int b = blockIdx.y, seq = seq0 + b, k = blockIdx.x;
+  if (k == g.D) {  // the extra block: pack the gallery queries for ss_nn_kernel
+    // greedy in list order, a pack holding <= 64 rows (4 MFMA row tiles): the pack starting at
+    // track i ends before the first j with rows(i..j) > 64 — found for every i at once by a binary
+    // search of the row prefix sums, then the chain of pack starts walked from track 0
+    __shared__ int pre[1025], nxt[1024];
+    const int nl = g.sq[(size_t)seq * SQS + Q_NNL], lane = threadIdx.x;
+    const int* nnl = g.nnl + (size_t)seq * g.T;
+    int carry = 0;
+    if (lane == 0) pre[0] = 0;
+    for (int i0 = 0; i0 < nl; i0 += 64) {
+      const int i = i0 + lane;
+      int v = i < nl ? __popcll(g.trk[(size_t)seq * g.T + nnl[i]].gmask) : 0;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+      }
+      if (i < nl) pre[i + 1] = carry + v;  // rows of tracks [0, i]
+      carry += __shfl(v, 63);
+    }
+    __syncthreads();
+    for (int i = lane; i < nl; i += 64) {  // first j > i with pre[j + 1] - pre[i] > 64
+      const int lim = pre[i] + 64;
+      int lo2 = i + 1, hi2 = nl;  // answer in [i + 1, nl]
+      while (lo2 < hi2) {
+        const int mid = (lo2 + hi2) >> 1;
+        if (pre[mid + 1] > lim) hi2 = mid; else lo2 = mid + 1;
+      }
+      nxt[i] = lo2;
+    }
+    __syncthreads();
+    int keep = 0;  // ss_motion_kernel: does a detection pass min_conf (ss_pre_kernel's nk > 0)
+    {
+      const int r0 = det_off[b];
+      int n = det_off[b + 1] - r0;
+      if (n > g.D) n = g.D;
+      for (int q = lane; q < n; q += 64) keep |= dets[(size_t)(r0 + q) * 6 + 4] >= g.min_conf;
+      keep = __any(keep);
+    }
+    if (lane == 0) {
+      int* pk = g.pk + (size_t)seq * (g.T + 3);
+      int np = 0;
+      for (int i = 0; i < nl; i = nxt[i]) pk[np++] = i;
+      pk[np] = nl;
+      pk[g.T + 1] = np;
+      pk[g.T + 2] = keep;
+    }
+    return;
+  }
   const int r0 = det_off[b];
   int n = det_off[b + 1] - r0;
   if (n > g.D) n = g.D;
@@ -769,127 +820,127 @@ __device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT],
   }
 }
 
-// NearestNeighborDistanceMetric.distance (linear_assignment.py:468-497, 595-618) for G listed
-// confirmed tracks per wave: rows = each track's distinct gallery vectors (pre-normalised x/den),
-// columns = this frame's normalised detections; out = 1 - clip(max over the track's rows).
-// A pass multiplies RT row tiles (16 rows each, a track's <= 64 rows are <= 4 tiles; tiles of
-// the G tracks concatenated) by up to 4 detection tiles (64 detections) on the fp64 matrix cores,
-// so every detection row loaded serves up to RT tiles and every sample row 4 detection tiles.
-// Each output's k-chain is the oracle's ascending fma chain whatever the tiling.
-template <int G, int RT, int NDT>
+// NearestNeighborDistanceMetric.distance (linear_assignment.py:468-497, 595-618) for one pack of
+// listed confirmed tracks per wave (ss_prep_kernel's greedy packing: <= 64 gallery rows, so up to
+// four 16-row tiles with the tracks' rows back to back instead of a padded tile per track): rows =
+// the tracks' distinct gallery vectors (pre-normalised x/den), columns = this frame's normalised
+// detections in blocks of NDT 16-detection tiles; out = 1 - clip(max over the track's rows), the
+// max taken per track over its row range by wave shuffles.  Each output's k-chain is the oracle's
+// ascending fma chain whatever the tiling.
+template <int NDT>
 __global__ void __launch_bounds__(64)
     ss_nn_kernel(SsDev g, int seq0, const int* __restrict__ det_off) {
-  __shared__ int rowv[G][64];
-  __shared__ int nrow_s[G], slot_s[G], tt[4 * G], tr0[4 * G], ntile_s;
-  const int b = blockIdx.y, seq = seq0 + b, k0 = blockIdx.x * G, lane = threadIdx.x;
-  const int nl = g.sq[(size_t)seq * SQS + Q_NNL];
-  if (k0 >= nl) return;
-  const int ng = nl - k0 < G ? nl - k0 : G;
+  __shared__ int rowv[64], rowq[64], qoff[65], qslot[64];
+  const int b = blockIdx.y, seq = seq0 + b, lane = threadIdx.x;
+  const int* pk = g.pk + (size_t)seq * (g.T + 3);
+  const int np = pk[g.T + 1];
+  if ((int)blockIdx.x >= np) return;
   const int r0 = det_off[b];
   int n = det_off[b + 1] - r0;
   if (n > g.D) n = g.D;
   if (n <= 0) return;
   const int F = g.F;
-  if (lane < ng && blockIdx.z == 0) {  // (the statistic counted once per track)
-    unsigned long long m = g.trk[(size_t)seq * g.T + g.nnl[(size_t)seq * g.T + k0 + lane]].gmask;
-    atomicAdd(g.sq + (size_t)seq * SQS + Q_ROWS, __popcll(m));
-  }
-  if (lane < ng) {  // distinct pool entries referenced by each gallery
-    const int slot = g.nnl[(size_t)seq * g.T + k0 + lane];
-    unsigned long long m = g.trk[(size_t)seq * g.T + slot].gmask;
-    int c = 0;
-    while (m) {
-      rowv[lane][c++] = __ffsll((long long)m) - 1;
-      m &= m - 1;
-    }
-    nrow_s[lane] = c;
-    slot_s[lane] = slot;
-  }
-  __syncthreads();
-  if (lane == 0) {  // the tile list: (track, first row) per 16-row tile
-    int nt = 0;
-    for (int q = 0; q < ng; q++)
-      for (int r = 0; r < nrow_s[q]; r += 16) {
-        tt[nt] = q;
-        tr0[nt] = r;
-        nt++;
-      }
-    ntile_s = nt;
-  }
-  __syncthreads();
-  const int ntile = ntile_s;
   const double* dnb = g.dn + (size_t)seq * g.D * F;
   const int kl = lane >> 4, cl = lane & 15;
-  constexpr int DB = 16 * NDT;  // detections per block: NDT tiles of 16
-  for (int db = DB * blockIdx.z; db < n; db += DB * gridDim.z) {  // this wave's detection blocks
-    const int ndt = n - db >= DB ? NDT : (n - db + 15) / 16;  // detection tiles in this block
-    double best[G][NDT];
-#pragma unroll
-    for (int q = 0; q < G; q++)
-#pragma unroll
-      for (int dt = 0; dt < NDT; dt++) best[q][dt] = -INF;
-    const double* bp[NDT];
-#pragma unroll
-    for (int dt = 0; dt < NDT; dt++) {
-      const int col = db + 16 * dt + cl;
-      bp[dt] = dnb + (size_t)(col < n ? col : 0) * F;
+  constexpr int DB = 16 * NDT;  // detections per block
+  for (int p = blockIdx.x; p < np; p += gridDim.x) {
+    const int t0 = pk[p], nq = pk[p + 1] - t0;  // this pack's tracks (<= 64)
+    int slot = 0, c = 0;
+    unsigned long long m = 0;
+    if (lane < nq) {
+      slot = g.nnl[(size_t)seq * g.T + t0 + lane];
+      m = g.trk[(size_t)seq * g.T + slot].gmask;
+      c = __popcll(m);
     }
-    for (int p0 = 0; p0 < ntile; p0 += RT) {
-      const double* ap[RT];
-      int nrt = 0;
+    int inc = c;  // inclusive prefix of the row counts over the lanes
 #pragma unroll
-      for (int rt = 0; rt < RT; rt++) {
-        const int ti = p0 + rt < ntile ? p0 + rt : p0;
-        const int q = tt[ti], row = tr0[ti] + cl;
-        const int slot = slot_s[q];
-        ap[rt] = vecnp(g, seq, slot, rowv[q][row < nrow_s[q] ? row : 0]);
-        nrt += p0 + rt < ntile;
-      }
-      d4 acc[RT][NDT];
-#pragma unroll
-      for (int rt = 0; rt < RT; rt++)
-#pragma unroll
-        for (int dt = 0; dt < NDT; dt++) acc[rt][dt] = (d4){0.0, 0.0, 0.0, 0.0};
-      // detection tiles as a compile-time count: no MFMA on absent tiles
-      if constexpr (NDT == 4) {
-        if (ndt == 4) nn_kloop<RT, 4, NDT>(ap, bp, F, kl, acc);
-        else if (ndt == 3) nn_kloop<RT, 3, NDT>(ap, bp, F, kl, acc);
-        else if (ndt == 2) nn_kloop<RT, 2, NDT>(ap, bp, F, kl, acc);
-        else nn_kloop<RT, 1, NDT>(ap, bp, F, kl, acc);
-      } else {
-        if (ndt == 2) nn_kloop<RT, 2, NDT>(ap, bp, F, kl, acc);
-        else nn_kloop<RT, 1, NDT>(ap, bp, F, kl, acc);
-      }
-      // lane holds column cl of each detection tile, rows kl + 4 j of each row tile
-#pragma unroll
-      for (int rt = 0; rt < RT; rt++) {
-        if (rt >= nrt) break;
-        const int ti = p0 + rt, q = tt[ti];
-        const int nr = nrow_s[q] - tr0[ti];
-#pragma unroll
-        for (int dt = 0; dt < NDT; dt++) {
-          double m = -INF;
-#pragma unroll
-          for (int j = 0; j < 4; j++)
-            if (kl + 4 * j < nr) m = acc[rt][dt][j] > m ? acc[rt][dt][j] : m;
-          const double o1 = __shfl_xor(m, 16);
-          m = o1 > m ? o1 : m;
-          const double o2 = __shfl_xor(m, 32);
-          m = o2 > m ? o2 : m;
-#pragma unroll
-          for (int qq = 0; qq < G; qq++)
-            if (qq == q && m > best[qq][dt]) best[qq][dt] = m;
-        }
-      }
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(inc, o);
+      if (lane >= o) inc += t;
     }
+    const int nrows = __shfl(inc, 63);
+    __syncthreads();  // (the previous pack's tables are read no more)
+    if (lane < nq) {
+      int r = inc - c;
+      qoff[lane] = r;
+      qslot[lane] = slot;
+      while (m) {
+        rowv[r] = __ffsll((long long)m) - 1;
+        rowq[r] = lane;
+        r++;
+        m &= m - 1;
+      }
+      if (blockIdx.z == 0) atomicAdd(g.sq + (size_t)seq * SQS + Q_ROWS, c);  // a statistic
+    }
+    if (lane == 0) qoff[nq] = nrows;
+    __syncthreads();
+    const int ntile = (nrows + 15) / 16;
+    if (ntile == 0) continue;
+    const double* ap[4];
 #pragma unroll
-    for (int q = 0; q < G; q++) {
-      if (q >= ng) break;
-      double* out = g.nnd + ((size_t)seq * g.T + slot_s[q]) * g.D;
+    for (int rt = 0; rt < 4; rt++) {  // padded rows read row 0 and are discarded below
+      const int row = 16 * rt + cl, rr = row < nrows ? row : 0;
+      ap[rt] = vecnp(g, seq, qslot[rowq[rr]], rowv[rr]);
+    }
+    for (int db = DB * blockIdx.z; db < n; db += DB * gridDim.z) {  // this wave's blocks
+      const int ndt = n - db >= DB ? NDT : (n - db + 15) / 16;
+      const double* bp[NDT];
 #pragma unroll
       for (int dt = 0; dt < NDT; dt++) {
         const int col = db + 16 * dt + cl;
-        if (kl == 0 && col < n) out[col] = 1.0 - clipd(best[q][dt], -1.0, 1.0);
+        bp[dt] = dnb + (size_t)(col < n ? col : 0) * F;
+      }
+      d4 acc[4][NDT];
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int dt = 0; dt < NDT; dt++) acc[rt][dt] = (d4){0.0, 0.0, 0.0, 0.0};
+      // row / detection tile counts as compile-time parameters: no MFMA on absent tiles
+      auto run = [&](auto rtc, auto ndc) {
+        constexpr int RTN = decltype(rtc)::value, NDN = decltype(ndc)::value;
+        const double* const(&apr)[RTN] = *reinterpret_cast<const double* const(*)[RTN]>(&ap);
+        d4(&accr)[RTN][NDT] = *reinterpret_cast<d4(*)[RTN][NDT]>(&acc);
+        nn_kloop<RTN, NDN, NDT>(apr, bp, F, kl, accr);
+      };
+      using I1 = std::integral_constant<int, 1>;
+      using I2 = std::integral_constant<int, 2>;
+      using I3 = std::integral_constant<int, 3>;
+      using I4 = std::integral_constant<int, 4>;
+      if (ndt == NDT) {
+        if (ntile == 4) run(I4{}, std::integral_constant<int, NDT>{});
+        else if (ntile == 3) run(I3{}, std::integral_constant<int, NDT>{});
+        else if (ntile == 2) run(I2{}, std::integral_constant<int, NDT>{});
+        else run(I1{}, std::integral_constant<int, NDT>{});
+      } else {
+        if (ntile == 4) run(I4{}, I1{});
+        else if (ntile == 3) run(I3{}, I1{});
+        else if (ntile == 2) run(I2{}, I1{});
+        else run(I1{}, I1{});
+      }
+      // per track: max over its rows (lane holds rows 16 rt + kl + 4 j of column cl)
+      for (int q = 0; q < nq; q++) {
+        const int o = qoff[q], e = qoff[q + 1];
+        if (o == e) continue;  // no gallery rows (never read by the cost kernel)
+        double* out = g.nnd + ((size_t)seq * g.T + qslot[q]) * g.D;
+#pragma unroll
+        for (int dt = 0; dt < NDT; dt++) {
+          double mx = -INF;
+#pragma unroll
+          for (int rt = 0; rt < 4; rt++) {
+            if (16 * rt >= e || 16 * rt + 16 <= o) continue;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              const int row = 16 * rt + kl + 4 * j;
+              if (row >= o && row < e && acc[rt][dt][j] > mx) mx = acc[rt][dt][j];
+            }
+          }
+          const double o1 = __shfl_xor(mx, 16);
+          mx = o1 > mx ? o1 : mx;
+          const double o2 = __shfl_xor(mx, 32);
+          mx = o2 > mx ? o2 : mx;
+          const int col = db + 16 * dt + cl;
+          if (kl == 0 && dt < ndt && col < n) out[col] = 1.0 - clipd(mx, -1.0, 1.0);
+        }
       }
     }
   }
@@ -1801,6 +1852,52 @@ __global__ void __launch_bounds__(256) ss_crowd_kernel(SsDev g, int seq0) {
 // ss_pre_kernel (one wave per sequence): detections, crowd mode, CMC warp, quality + stable sort,
 // Kalman predict.  The detection table (fdt, fdord) and the predicted tracks are the input of
 // ss_cost_kernel and ss_match_kernel.
+// Tracker.camera_update + Tracker.predict of every listed track (strongsort.py:144-149,
+// tracker.py:63-70): wave per track, lane 8i + j owning covariance entry (i, j) — the row sums of
+// F P F^T come by two shuffles, each entry the expression track_predict evaluates; the mean, the
+// histories and the consistency scalars on lane 0.  With no detection kept the reference skips
+// the camera update (tracker.update([]) path).  Runs before ss_pre_kernel on its stream.
+__global__ void __launch_bounds__(64)
+    ss_motion_kernel(SsDev g, int seq0, const double* __restrict__ warps) {
+  const int b = blockIdx.y, seq = seq0 + b, p = blockIdx.x, lane = threadIdx.x;
+  if (p >= g.sq[(size_t)seq * SQS + Q_NTR]) return;
+  const bool keep = g.pk[(size_t)seq * (g.T + 3) + g.T + 2] != 0;
+  SsTrk& t = g.trk[(size_t)seq * g.T + g.order[(size_t)seq * g.T + p]];
+  if (keep && lane == 0) {
+    double wm[6] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0};
+    if (warps)
+      for (int q = 0; q < 6; q++) wm[q] = warps[(size_t)b * 6 + q];
+    track_camera(t, wm);
+  }
+  __syncthreads();
+  // track_predict: q from the (camera-updated) mean, then P = F (P F^T) + Q entrywise
+  double q[8];
+  kf_process_noise(KIND_BYTE, t.mean, q);
+  const int i = lane >> 3, j = lane & 7;
+  const double pij = t.cov[lane];
+  const double pj4 = __shfl(pij, (lane & ~7) | ((j + 4) & 7));
+  const double mij = j < 4 ? pij + pj4 : pij;
+  const double m4 = __shfl(mij, (lane + 32) & 63);
+  double v;
+  if (i < 4) {
+    const double s2 = mij + m4;
+    v = i == j ? s2 + q[i] : s2;
+  } else {
+    v = i == j ? mij + q[i] : mij;
+  }
+  __syncthreads();  // every lane read its operands (and q read the mean) before the writes
+  t.cov[lane] = v;
+  if (lane == 0) {
+    double* m = t.mean;
+    for (int k = 0; k < 4; k++) m[k] = m[k] + m[k + 4];
+    t.age++;
+    t.tsu++;
+    push2(t.vel, t.nvel, t.mean + 4);
+    push2(t.pos, t.npos, t.mean);
+    if (t.npos >= 2) motion_cons(t, t.pos[t.npos - 2], t.pos[t.npos - 1]);
+  }
+}
+
 __global__ void __launch_bounds__(64)
     ss_pre_kernel(SsDev g, int seq0, const double* __restrict__ dets,
                   const int* __restrict__ det_off, const double* __restrict__ warps) {
@@ -1839,9 +1936,7 @@ __global__ void __launch_bounds__(64)
       });
   int fid = frame;
   SSTAMP(0);
-  if (x.nk == 0) {
-    for (int p = lane; p < x.ntr; p += 64) track_predict(x.trk[w.lst[p]]);
-    __syncthreads();
+  if (x.nk == 0) {  // (the tracks were predicted by ss_motion_kernel)
     fid = 0;  // tracker.update([]) passes frame_id=None
   } else {
     if (g.crowd) {  // detect_crowd_situations (reads the tlwh boxes as xyxy)
@@ -1869,12 +1964,6 @@ __global__ void __launch_bounds__(64)
       __syncthreads();
     }
     SSTAMP(1);
-    if (x.ntr >= 1) {
-      double wm[6] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0};
-      if (warps)
-        for (int q = 0; q < 6; q++) wm[q] = warps[(size_t)b * 6 + q];
-      for (int p = lane; p < x.ntr; p += 64) track_camera(x.trk[w.lst[p]], wm);
-    }
     const int crowd_mode = sq[Q_CROWD];
     for (int i = lane; i < x.nk; i += 64) {  // _compute_detection_quality
       double* d = w.dt + (size_t)i * DTW;
@@ -1891,7 +1980,6 @@ __global__ void __launch_bounds__(64)
     }
     __syncthreads();
     stable_sort_desc(w.dord, x.nk, [&](int r) { return w.dt[(size_t)r * DTW + 7]; }, w.tmp, sbox);
-    for (int p = lane; p < x.ntr; p += 64) track_predict(x.trk[w.lst[p]]);
     __syncthreads();
   }
   if (!fid) fid = sq[Q_HIST];
@@ -2496,16 +2584,6 @@ static size_t ss_lds_bytes(const SsDev& d) {
   return d.ws_lds == 1 ? (size_t)d.wsd_n * 8 + (size_t)d.wsi_n * 4 : (size_t)ws_lsap_bytes(d.N);
 }
 
-template <int G>
-static void launch_nn(const SsDev& d, int seq0, int nseq, int zb, int ndt, const int* off,
-                      hipStream_t st) {
-  const dim3 grid((d.T + G - 1) / G, nseq, zb);
-  if (ndt == 2)
-    hipLaunchKernelGGL((ss_nn_kernel<G, G, 2>), grid, dim3(64), 0, st, d, seq0, off);
-  else
-    hipLaunchKernelGGL((ss_nn_kernel<G, G, 4>), grid, dim3(64), 0, st, d, seq0, off);
-}
-
 static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int* off,
                      const double* embs, const double* warps, double* out, int* cnt,
                      hipStream_t st) {
@@ -2513,42 +2591,47 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   int rc;
   if (!embs) return bx_record_error(BX_ERR_SHAPE, "StrongSort needs embeddings");
   if ((rc = ss_probe_begin(e, 0, st))) return rc;
-  hipLaunchKernelGGL(ss_prep_kernel, dim3(d.D, nseq), dim3(64), 0, st, d, seq0, off, embs);
+  hipLaunchKernelGGL(ss_prep_kernel, dim3(d.D + 1, nseq), dim3(64), 0, st, d, seq0, off, embs,
+                     dets);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 0, st))) return rc;
-  // fork: the crowd test and ss_pre_kernel (camera, quality + sort, predict) on the side stream
+  // fork: ss_pre_kernel (crowd mode, quality + sort, cascade keys; one wave per sequence) on the
+  // side stream beside the gallery distance
   const size_t lds = ss_lds_bytes(d);
-  SCHK(hipEventRecord(e->ev_fork, st));
-  SCHK(hipStreamWaitEvent(e->side, e->ev_fork, 0));
-  if ((rc = ss_probe_begin(e, 3, e->side))) return rc;
+  // The crowd test and the camera update + predict are short grids.  With few sequences they go
+  // on the main stream before the gallery distance: queued beside its waves they wait for their
+  // slots and become the critical path (C4: 1 sequence).  With many sequences they overlap it on
+  // the side stream (measured: 256 sequences 0.654 -> 0.612 ms per step, C4 the reverse).
+  const bool side_all = nseq >= 8;
+  hipStream_t sm = side_all ? e->side : st;
+  if (side_all) {
+    SCHK(hipEventRecord(e->ev_fork, st));
+    SCHK(hipStreamWaitEvent(e->side, e->ev_fork, 0));
+  }
+  if ((rc = ss_probe_begin(e, 3, sm))) return rc;
   if (d.crowd)
-    hipLaunchKernelGGL(ss_crowd_kernel, dim3(CROWD_BLOCKS, nseq), dim3(256), 0, e->side, d, seq0);
+    hipLaunchKernelGGL(ss_crowd_kernel, dim3(CROWD_BLOCKS, nseq), dim3(256), 0, sm, d, seq0);
+  hipLaunchKernelGGL(ss_motion_kernel, dim3(d.T, nseq), dim3(64), 0, sm, d, seq0, warps);
+  SCHK(hipGetLastError());
+  if (!side_all) {
+    if ((rc = ss_probe_end(e, 3, st))) return rc;
+    SCHK(hipEventRecord(e->ev_fork, st));
+    SCHK(hipStreamWaitEvent(e->side, e->ev_fork, 0));
+    if ((rc = ss_probe_begin(e, 3, e->side))) return rc;
+  }
   hipLaunchKernelGGL(ss_pre_kernel, dim3(nseq), dim3(64), lds, e->side, d, seq0, dets, off,
                      warps);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 3, e->side))) return rc;
   SCHK(hipEventRecord(e->ev_join, e->side));
   if ((rc = ss_probe_begin(e, 1, st))) return rc;
-  // tracks per wave: 4 share every detection load (the detection blocks' split over waves
-  // below restores the wave count), fewer only for a handful of tracks
-  const long qtracks = (long)d.T * nseq;
-  int gsel = qtracks >= 256 ? 4 : (qtracks >= 64 ? 2 : 1);
-  if (const char* ev = std::getenv("BX_SS_NN_G")) gsel = std::atoi(ev);  // diagnostics
-  // detection blocks of 16·ndt (ndt = 2 tiles when the detection capacity is <= 64: half the
-  // accumulators, more resident waves), split over waves too when the tracks alone give too few
-  int ndtsel = d.D <= 64 ? 2 : 4;
-  if (const char* ev = std::getenv("BX_SS_NN_NDT")) ndtsel = std::atoi(ev) <= 2 ? 2 : 4;
-  const long waves = (long)((d.T + gsel - 1) / gsel) * nseq;
-  int zb = (int)((4096 + waves - 1) / waves);
-  const int nblk = (d.D + 16 * ndtsel - 1) / (16 * ndtsel);
+  // packs per sequence <= listed tracks; a wave per (pack, detection-block split), waves looping
+  // over packs past the grid; the detection blocks split over waves for ~4k waves in all
+  const int gx = d.T < 4 ? d.T : (d.T + 3) / 4;
+  const int nblk = (d.D + 31) / 32;
+  int zb = (int)((4096 + (long)gx * nseq - 1) / ((long)gx * nseq));
   zb = zb < 1 ? 1 : (zb > nblk ? nblk : zb);
-
-  if (gsel >= 4)
-    launch_nn<4>(d, seq0, nseq, zb, ndtsel, off, st);
-  else if (gsel == 2)
-    launch_nn<2>(d, seq0, nseq, zb, ndtsel, off, st);
-  else
-    launch_nn<1>(d, seq0, nseq, zb, ndtsel, off, st);
+  hipLaunchKernelGGL((ss_nn_kernel<2>), dim3(gx, nseq, zb), dim3(64), 0, st, d, seq0, off);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 1, st))) return rc;
   if ((rc = ss_probe_begin(e, 2, st))) return rc;
@@ -2641,6 +2724,7 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   const size_t o_ord = cb(S * T * sizeof(int));
   const size_t o_lost = cb(S * LOSTN * sizeof(int));
   const size_t o_nnl = cb(S * T * sizeof(int));
+  const size_t o_pk = cb(S * (T + 3) * sizeof(int));
   const size_t o_nnd = cb(S * T * D * sizeof(double));
   const size_t o_prep = cb(S * D * 4 * sizeof(double));
   const size_t o_dn = cb(S * D * F * sizeof(double));
@@ -2684,6 +2768,7 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   d.order = (int*)(base + o_ord);
   d.lost = (int*)(base + o_lost);
   d.nnl = (int*)(base + o_nnl);
+  d.pk = (int*)(base + o_pk);
   d.nnd = (double*)(base + o_nnd);
   d.dprep = (double*)(base + o_prep);
   d.dn = (double*)(base + o_dn);
