@@ -50,7 +50,8 @@ def main():
     kind, n_obj, F, params = CONFIGS[a.config]
     eng = Engine(kind, n_seq=a.seqs, track_cap=512, det_cap=256, emb_dim=F,
                  params=EngineParams(**params))
-    gen = TorchSceneBatch(a.seqs, n_obj, emb_dim=F, seed=7, device="cuda")
+    layout = "crowded" if a.config.endswith("_crowded") else "grid"
+    gen = TorchSceneBatch(a.seqs, n_obj, emb_dim=F, seed=7, device="cuda", layout=layout)
     L = N.load()
     L.bx_debug_stamps_host.argtypes = [C.c_void_p, C.c_void_p]
     out = torch.empty((a.seqs * n_obj, 8), dtype=torch.float64, device="cuda")
