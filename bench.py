@@ -352,6 +352,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=0,
                     help="sequences per pipeline launch (0 = all; BoT-SORT/ByteTrack)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="join each step's feature EMA before it returns (bx_engine_set_overlap off)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--dropin", action="store_true",
@@ -406,6 +408,9 @@ def main():
     else:
         eng = Engine(kind, n_seq=S, track_cap=512, det_cap=256, emb_dim=F,
                      params=EngineParams(**params))
+        # every step's inputs are their own resident tensors, so the feature EMA may stay
+        # unjoined into the next step (bx_engine_set_overlap)
+        eng.set_overlap(not args.no_overlap)
         stages = [s for s in Engine.STAGES
                   if F or s not in ("det_features", "gate", "cosine", "features")]
     # this rank's shard: global sequences [rank*S, (rank+1)*S) — weak scaling, no exchange
@@ -533,7 +538,9 @@ def main():
                        "tracker": kind, "n_seq_per_gpu": S, "n_tracks": n_obj,
                        "n_dets_mean": round(mean_d, 1), "feat_dim": F,
                        "emb_dtype": "f64" if emb_bytes == 8 else "f32",
-                       "parallelism": f"seq-sharded x{world}"},
+                       "parallelism": f"seq-sharded x{world}",
+                       **({"feature_overlap": not args.no_overlap}
+                          if kind == "botsort" and F else {})},
             "roofline": {**roof, "kernel": dominant,
                          "kernel_ms": round(dom_ms, 4), "probe_steps": n_probe,
                          "launches_per_step": len(bounds),

@@ -115,7 +115,7 @@ EXPORTS = [
     "bx_engine_counters_host", "bx_engine_set_id_count", "bx_engine_tracks_host",
     "bx_engine_state_set_host", "bx_ocsort_state_set_host", "bx_boost_state_set_host",
     "bx_ss_state_set_host",
-    "bx_engine_probe", "bx_engine_probe_read", "bx_engine_frame_stats_host",
+    "bx_engine_probe", "bx_engine_probe_read", "bx_engine_set_overlap", "bx_engine_frame_stats_host",
     "bx_iou_batch", "bx_pairwise_cost", "bx_aw_max_metric", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
     "bx_kf_multi_predict", "bx_kf_update", "bx_kf_gating_distance", "bx_linear_assignment", "bx_lapjv",
     "bx_nn_cosine_distance", "bx_ocsort_create", "bx_ocsort_destroy", "bx_ocsort_reset", "bx_ocsort_step",
@@ -147,6 +147,7 @@ _SIGS = {
     "bx_engine_update_host": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp, _vp, _ip, _vp], C.c_int),
     "bx_engine_status": ([_vp, _ip], C.c_int),
     "bx_engine_probe": ([_vp, C.c_int], C.c_int),
+    "bx_engine_set_overlap": ([_vp, C.c_int], C.c_int),
     "bx_engine_probe_read": ([_vp, _dp, _ip], C.c_int),
     "bx_engine_frame_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_engine_counters_host": ([_vp, C.c_int, _ip, _ip, _ip, _ip], C.c_int),

@@ -1711,6 +1711,10 @@ struct bx_engine {
   // there beside the Kalman/list kernels they share no data with
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
+  // overlap mode (bx_engine_set_overlap): a step leaves K5 on the side stream unjoined; the next
+  // step's K1 queues behind it there and its K1c join covers both, every other entry point
+  // settles it first (side_pending)
+  bool overlap = false, side_pending = false;
   std::mutex mu;
   // per_class mode (bx_engine_update_classes_host), allocated on first use: per sequence the
   // parked active lists [C][T] + their lengths [C] + the held frame counter, the class that ran
@@ -1760,7 +1764,10 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
   // Fork-join: K1 (detection norms) only feeds K1c, and K5 (feature EMA) only reads K3's records
   // and K1's norms and writes smooth_feat / tdn, which nothing else in the frame touches — so K1
   // runs on the side stream beside K2/K1b, and K5 beside K4/K4b/K6.  Both joins land on `st`
-  // before the frame returns (the next frame's K1 rewrites the norms K5 reads).
+  // before the frame returns (the next frame's K1 rewrites the norms K5 reads) — except in
+  // overlap mode (bx_engine_set_overlap), where K5 stays unjoined: the next frame's K1 queues
+  // behind it on the side stream and that frame's join before K1c covers both (measured: 0.615
+  // -> 0.599 ms/step at C3; a greater or lesser side-stream priority measured slower).
   if (reid && !e->side) {
     HIPCHK(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
     for (int k = 0; k < 2; k++) {
@@ -1861,8 +1868,12 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
   BX_PROBED(BX_STAGE_FINISH,
             hipLaunchKernelGGL(finish_kernel<KIND>, dim3(nseq), dim3(WG), e->lds_finish, st, d,
                                seq0, det_off, out, out_count));
-  if (reid)
-    if (int rc = join(1)) return rc;
+  if (reid) {
+    if (e->overlap)
+      e->side_pending = true;  // joined by the next step's K1c join, or settle()
+    else if (int rc = join(1))
+      return rc;
+  }
 #undef BX_PROBED
 #undef BX_PROBED_ON
   return BX_OK;
@@ -1872,6 +1883,15 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
 
 // shared by the other translation units of the library (bx_ocsort.hip) so that bx_last_error
 // reports their failures too
+// overlap mode: wait for a step's unjoined K5 (side stream) before any other use of the engine
+static int settle(bx_engine* e) {
+  if (e && e->side_pending) {
+    e->side_pending = false;
+    HIPCHK(hipStreamSynchronize(e->side));
+  }
+  return BX_OK;
+}
+
 int bx_record_error(int code, const char* msg) { return set_err(code, msg); }
 
 extern "C" {
@@ -2028,6 +2048,7 @@ int bx_engine_destroy(bx_engine* e) {
 }
 
 int bx_engine_reset(bx_engine* e, int seq0, int nseq, void* stream) {
+  if (int rc = settle(e)) return rc;
   if (!e || seq0 < 0 || nseq <= 0 || seq0 + nseq > e->dev.S)
     return set_err(BX_ERR_INVALID, "bad sequence range");
   e->cache_seq = -1;
@@ -2068,6 +2089,7 @@ int bx_engine_step(bx_engine* e, int seq0, int nseq, const float* dets, const in
 
 int bx_engine_update_host(bx_engine* e, int seq, const float* dets, int n, const void* embs,
                           const double* warp, double* out, int* n_out, void* stream) {
+  if (int rc = settle(e)) return rc;
   if (!e || seq < 0 || seq >= e->dev.S || n < 0 || !n_out)
     return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_update_host");
   if (n > e->dev.D) return set_err(BX_ERR_CAPACITY, "detections exceed det_cap");
@@ -2116,6 +2138,7 @@ int bx_engine_update_host(bx_engine* e, int seq, const float* dets, int n, const
 int bx_engine_update_classes_host(bx_engine* e, int seq, const float* dets, int n,
                                   const void* embs, const double* warp, int n_classes,
                                   double* out, int* n_out, void* stream) {
+  if (int rc = settle(e)) return rc;
   if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && !dets) || !n_out || n_classes <= 0 ||
       n_classes > 4096)
     return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_update_classes_host");
@@ -2204,6 +2227,7 @@ int bx_engine_update_classes_host(bx_engine* e, int seq, const float* dets, int 
 #ifdef BX_PHASE_TIMING
 // diagnostic only: copy the [S][32] phase stamps of the last launch to the host
 int bx_debug_stamps_host(bx_engine* e, unsigned long long* out) {
+  if (int rc = settle(e)) return rc;
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(out, e->dev.dbg, sizeof(unsigned long long) * BX_DBG_STRIDE * e->dev.S,
                    hipMemcpyDeviceToHost));
@@ -2212,6 +2236,7 @@ int bx_debug_stamps_host(bx_engine* e, unsigned long long* out) {
 #endif
 
 int bx_engine_status(bx_engine* e, int* status) {
+  if (int rc = settle(e)) return rc;
   if (!e || !status) return set_err(BX_ERR_INVALID, "null argument");
   int s = 0;
   HIPCHK(hipMemcpy(&s, e->dev.status, sizeof(int), hipMemcpyDeviceToHost));
@@ -2222,6 +2247,7 @@ int bx_engine_status(bx_engine* e, int* status) {
 }
 
 int bx_engine_frame_stats_host(bx_engine* e, int seq0, int nseq, int64_t* sums) {
+  if (int rc = settle(e)) return rc;
   if (!e || !sums || seq0 < 0 || nseq <= 0 || seq0 + nseq > e->dev.S)
     return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_frame_stats_host");
   std::vector<int> v((size_t)nseq * SQ_STRIDE);
@@ -2244,6 +2270,7 @@ int bx_engine_probe(bx_engine* e, int stage) {
 }
 
 int bx_engine_probe_read(bx_engine* e, double* total_ms, int* count) {
+  if (int rc = settle(e)) return rc;
   if (!e || !total_ms || !count) return set_err(BX_ERR_INVALID, "null argument");
   double t = 0.0;
   for (size_t k = 0; k < e->probe_used; k++) {
@@ -2260,6 +2287,7 @@ int bx_engine_probe_read(bx_engine* e, double* total_ms, int* count) {
 
 int bx_engine_counters_host(bx_engine* e, int seq, int* frame_count, int* id_count, int* n_active,
                             int* n_lost) {
+  if (int rc = settle(e)) return rc;
   if (!e || seq < 0 || seq >= e->dev.S) return set_err(BX_ERR_INVALID, "bad sequence");
   int v[SQ_STRIDE];
   if (seq == e->cache_seq)
@@ -2274,6 +2302,7 @@ int bx_engine_counters_host(bx_engine* e, int seq, int* frame_count, int* id_cou
 }
 
 int bx_engine_set_id_count(bx_engine* e, int seq, int id_count, void* stream) {
+  if (int rc = settle(e)) return rc;
   if (!e || seq < 0 || seq >= e->dev.S) return set_err(BX_ERR_INVALID, "bad sequence");
   e->cache_seq = -1;
   hipLaunchKernelGGL(set_id_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, e->dev.seq, seq,
@@ -2285,6 +2314,7 @@ int bx_engine_set_id_count(bx_engine* e, int seq, int id_count, void* stream) {
 int bx_engine_tracks_host(bx_engine* e, int seq, int cap, int32_t* ids, int32_t* state,
                           int32_t* is_activated, int32_t* frame_id, int32_t* start_frame,
                           double* mean, double* cov, int* n_active, int* n_lost) {
+  if (int rc = settle(e)) return rc;
   if (!e || seq < 0 || seq >= e->dev.S) return set_err(BX_ERR_INVALID, "bad sequence");
   HIPCHK(hipDeviceSynchronize());
   const int T = e->dev.T;
@@ -2332,6 +2362,7 @@ int bx_engine_tracks_host(bx_engine* e, int seq, int cap, int32_t* ids, int32_t*
 
 int bx_engine_state_set_host(bx_engine* e, int seq, int n, const int32_t* ids, const double* mean,
                              const double* cov) {
+  if (int rc = settle(e)) return rc;
   if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && !ids))
     return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_state_set_host");
   HIPCHK(hipDeviceSynchronize());
@@ -2373,6 +2404,13 @@ int bx_engine_state_set_host(bx_engine* e, int seq, int n, const int32_t* ids, c
     if (cov) HIPCHK(hipMemcpy(kf + 8, cov + 64 * j, 64 * 8, hipMemcpyHostToDevice));
   }
   HIPCHK(hipDeviceSynchronize());
+  return BX_OK;
+}
+
+int bx_engine_set_overlap(bx_engine* e, int on) {
+  if (!e) return set_err(BX_ERR_INVALID, "null engine");
+  if (int rc = settle(e)) return rc;
+  e->overlap = on != 0;
   return BX_OK;
 }
 

@@ -153,6 +153,11 @@ class Engine:
         k = -1 if stage is None else (self.STAGES.index(stage) if isinstance(stage, str) else stage)
         N.check(self._L.bx_engine_probe(self._h, k), "bx_engine_probe")
 
+    def set_overlap(self, on: bool = True) -> None:
+        """Leave each step's feature EMA (K5) unjoined on the side stream (bx_engine_set_overlap):
+        the caller keeps a step's input tensors unmodified until the next step is enqueued."""
+        N.check(self._L.bx_engine_set_overlap(self._h, int(bool(on))), "bx_engine_set_overlap")
+
     def probe_read(self):
         """(total ms, launches) of the probed stage since the last read."""
         t, n = C.c_double(), C.c_int()

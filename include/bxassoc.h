@@ -98,6 +98,16 @@ int bx_engine_step(bx_engine *e, int seq0, int nseq, const float *dets, const in
                    const void *embs, const double *warps, double *out, int32_t *out_count,
                    void *stream);
 
+/* Overlap mode (default off; bench.py turns it on): bx_engine_step
+ * returns with the BoT-SORT feature EMA (K5) of that frame still running on the engine's side
+ * stream instead of joining it onto `stream`.  The next bx_engine_step orders its own K1 after
+ * it and its cosine pass (the first reader of smooth_feat) waits for it; every other bx_engine_*
+ * call synchronises it first.  The caller must keep that step's dets / det_off / embs unmodified
+ * until the next bx_engine_step is enqueued (or any other bx_engine_* call returns);
+ * hipDeviceSynchronize covers it.  Saves the join and lets the next frame's K1 start as soon as
+ * K5 ends instead of after the caller's stream drains. */
+int bx_engine_set_overlap(bx_engine *e, int on);
+
 /* Host-memory convenience for one sequence (the drop-in `update` path): copies in, launches,
  * copies out and synchronises.  dets [n][6] float32; embs [n][emb_dim] or NULL; warp [6] or
  * NULL; out must hold n rows; *n_out receives the row count. */

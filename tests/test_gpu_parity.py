@@ -439,14 +439,20 @@ def test_per_class_vs_oracle(torch_cuda, kind, args, skw):
     assert rows > 0
 
 
-def run_batched(torch, kind, scenes, n_frames, args, emb_dim=0, seq_frames=None, warps=None):
+def run_batched(torch, kind, scenes, n_frames, args, emb_dim=0, seq_frames=None, warps=None,
+                overlap=False):
     """Drive an Engine with len(scenes) sequences in one launch per frame (``warps(s, t)``: the
-    2x3 CMC warp of sequence s at frame t, BoT-SORT's multi_gmc)."""
+    2x3 CMC warp of sequence s at frame t, BoT-SORT's multi_gmc).  ``overlap``: the engine leaves
+    each step's feature EMA unjoined (bx_engine_set_overlap), so a step's input tensors are kept
+    alive until the next step is enqueued."""
     from boxmot_amd.engine import Engine, EngineParams
 
     S = len(scenes)
     eng = Engine(kind, n_seq=S, track_cap=1024, det_cap=384, emb_dim=emb_dim,
                  params=EngineParams(**args))
+    if overlap:
+        eng.set_overlap(True)
+    keep = None
     outs = [[] for _ in range(S)]
     for t in range(1, n_frames + 1):
         frames = [sc.frame(t) for sc in scenes]
@@ -461,10 +467,12 @@ def run_batched(torch, kind, scenes, n_frames, args, emb_dim=0, seq_frames=None,
         w = None if warps is None else dev(torch, np.stack([warps(s, t).reshape(6)
                                                             for s in range(S)]))
         eng.step(dd, do, de, w, out, cnt)
+        keep = (dd, do, de, w)  # the previous step's inputs are released only now
         o, c = host(out), host(cnt)
         for s in range(S):
             outs[s].append(o[off[s]: off[s] + c[s]])
     assert eng.status() == 0
+    del keep
     run_batched.engine = eng  # the last run's engine (Kalman-state checks)
     return outs
 
@@ -516,6 +524,30 @@ def test_botsort_batched_warps_vs_oracle(torch_cuda):
         for t in range(1, 51):
             d, e, _ = sc.frame(t)
             np.testing.assert_array_equal(outs[s][t - 1], orc.update(d, e, warps(s, t)),
+                                          err_msg=f"seq {s} frame {t}")
+        assert_kalman_state_equal(eng, s, orc)
+
+
+@pytest.mark.parametrize("warped", [False, True])
+def test_botsort_overlap_mode_vs_oracle(torch_cuda, warped):
+    """bx_engine_set_overlap: each step returns with its feature EMA (K5) still on the side
+    stream; the next step's K1 queues behind it and its cosine pass joins it.  Outputs (whose
+    appearance costs read the previous frame's smooth_feat) and Kalman state bitwise vs the
+    oracle, with and without warp frames; state reads settle the side stream first."""
+    from boxmot_amd.synth import SyntheticScene, synth_warp
+
+    scenes = [SyntheticScene(n_obj=40 + 11 * s, seed=170 + s, emb_dim=128,
+                             layout="crowded" if s % 2 else "grid") for s in range(5)]
+    args = dict(track_high_thresh=0.6, new_track_thresh=0.7, match_thresh=0.8)
+    warps = (lambda s, t: synth_warp(170 + s, t)) if warped else None  # noqa: E731
+    outs = run_batched(torch_cuda, "botsort", scenes, 40, args, 128, warps=warps, overlap=True)
+    eng = run_batched.engine
+    for s, sc in enumerate(scenes):
+        orc = po.OracleTracker("botsort", **args)
+        for t in range(1, 41):
+            d, e, _ = sc.frame(t)
+            np.testing.assert_array_equal(outs[s][t - 1],
+                                          orc.update(d, e, warps(s, t) if warped else None),
                                           err_msg=f"seq {s} frame {t}")
         assert_kalman_state_equal(eng, s, orc)
 
