@@ -353,7 +353,10 @@ __device__ __forceinline__ void det_measurement(const float* r, double* meas) {
 // recomputes f2 = (f / n1) / n2 elementwise from the input row, bit-identically.
 // Grid (n_seq, ceil(D/K1_DETS)); each wave walks its block's detections with stride 4 (no
 // prefetch of the next row: the lower VGPR count buys more resident waves, which hide more).
-constexpr int K1_DETS = 8;  // detections per K1 block (2 per wave)
+#ifndef BX_K1_DETS
+#define BX_K1_DETS 8
+#endif
+constexpr int K1_DETS = BX_K1_DETS;  // detections per K1 block (2 per wave)
 template <typename FT, bool NPF>
 __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
                                                          const float* __restrict__ dets,
