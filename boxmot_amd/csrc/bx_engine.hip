@@ -1858,6 +1858,7 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
     BX_PROBED_ON(BX_STAGE_FEATURES, side,
                  hipLaunchKernelGGL((feature_kernel<FT, NPF>), dim3(nseq, FEAT_BLOCKS), dim3(WG),
                                     0, side, d, seq0, det_off, (const FT*)embs));
+    e->side_pending = true;  // until joined below (or, in overlap mode, by the next frame)
   }
   BX_PROBED(BX_STAGE_UPDATE,
             hipLaunchKernelGGL(update_kernel<KIND>,
@@ -1871,11 +1872,9 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
   BX_PROBED(BX_STAGE_FINISH,
             hipLaunchKernelGGL(finish_kernel<KIND>, dim3(nseq), dim3(WG), e->lds_finish, st, d,
                                seq0, det_off, out, out_count));
-  if (reid) {
-    if (e->overlap)
-      e->side_pending = true;  // joined by the next step's K1c join, or settle()
-    else if (int rc = join(1))
-      return rc;
+  if (reid && !e->overlap) {  // overlap mode: joined by the next step's K1c join, or settle()
+    if (int rc = join(1)) return rc;
+    e->side_pending = false;
   }
 #undef BX_PROBED
 #undef BX_PROBED_ON
