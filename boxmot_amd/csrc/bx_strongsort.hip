@@ -1495,7 +1495,12 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
 #endif
   // CC <= max(track_cap, det_cap) <= 1024, but for the IoU stage's candidates, which can list a
   // track twice (up to 2 track_cap columns)
+  // (column slots per lane sized to CC: every slot past CC is a relaxation, a minimum and a
+  // ballot per row for nothing — measured at C4: 16 -> 8 slots for CC <= 512, match 1.63 -> 1.52
+  // ms; more instantiations (1, 2, 10, 12 slots) measured slower, 1.83 ms: the kernel's code and
+  // register allocation grow with every inlined copy)
   const int np_ = CC <= 256    ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr)
+                  : CC <= 512  ? lsap_wave<8, true>(x, P, roff, cidx, mx, R, CC, tr)
                   : CC <= 1024 ? lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr)
                                : lsap_wave<32, true>(x, P, roff, cidx, mx, R, CC, tr);
 #ifdef BX_PHASE_TIMING
