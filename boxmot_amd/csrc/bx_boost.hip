@@ -1104,6 +1104,7 @@ struct bx_boost {
   int* h_coff = nullptr;
   int* h_ccnt = nullptr;
   int* h_hold = nullptr;
+  double* h_cwarp = nullptr;  // [C][6] the class calls' warps
   // timing probe
   int probe_stage = -1;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -1297,6 +1298,7 @@ int bx_boost_destroy(bx_boost* e) {
   (void)hipFree(e->h_coff);
   (void)hipFree(e->h_ccnt);
   (void)hipFree(e->h_hold);
+  (void)hipFree(e->h_cwarp);
   delete e;
   return BX_OK;
 }
@@ -1373,7 +1375,7 @@ int bx_boost_update_host(bx_boost* e, int seq, const float* dets, int n, const d
 // Restated as one engine sequence stepped once per class id 0..C-1 with the frame counter held;
 // rows stacked in class order, det_ind indexing the class's subset.  One sync at the end.
 int bx_boost_update_classes_host(bx_boost* e, int seq, const float* dets, int n,
-                                 const double* embs, const double* warp, int n_classes,
+                                 const double* embs, const double* warps, int n_classes,
                                  double* out, int* n_out, void* stream) {
   if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && !dets) || !n_out || n_classes <= 0 ||
       n_classes > 4096)
@@ -1391,6 +1393,7 @@ int bx_boost_update_classes_host(bx_boost* e, int seq, const float* dets, int n,
     BCHK(hipMalloc(&e->h_coff, sizeof(int) * 2 * C));
     BCHK(hipMalloc(&e->h_ccnt, sizeof(int) * C));
     BCHK(hipMalloc(&e->h_hold, sizeof(int)));
+    BCHK(hipMalloc(&e->h_cwarp, sizeof(double) * 6 * C));
   }
   auto cls_of = [&](int i) -> int {
     const float v = dets[6 * i + 5];
@@ -1417,13 +1420,15 @@ int bx_boost_update_classes_host(bx_boost* e, int seq, const float* dets, int n,
   if (m && reid)
     BCHK(hipMemcpyAsync(e->h_embs, he.data(), sizeof(double) * (size_t)m * F, hipMemcpyHostToDevice, st));
   BCHK(hipMemcpyAsync(e->h_coff, hoff.data(), sizeof(int) * 2 * C, hipMemcpyHostToDevice, st));
-  if (warp) BCHK(hipMemcpyAsync(e->h_warp, warp, sizeof(double) * 6, hipMemcpyHostToDevice, st));
+  if (warps) BCHK(hipMemcpyAsync(e->h_cwarp, warps, sizeof(double) * 6 * C, hipMemcpyHostToDevice, st));
   for (int c = 0; c < C; c++) {
     hipLaunchKernelGGL(boost_hold_frame_kernel, dim3(1), dim3(1), 0, st, e->dev.seqst, seq,
                        e->h_hold, c == 0 ? 1 : 0);
     BCHK(hipGetLastError());
+    // class call c's camera_update warp (boosttrack.py:243-246 runs cmc.apply per class call)
+    const double* wc = warps ? e->h_cwarp + 6 * (size_t)c : nullptr;
     int rc = launch(e, seq, 1, e->h_dets + 6 * (size_t)cnt[c], e->h_coff + 2 * c,
-                    reid ? e->h_embs + (size_t)F * cnt[c] : nullptr, warp ? e->h_warp : nullptr,
+                    reid ? e->h_embs + (size_t)F * cnt[c] : nullptr, wc,
                     e->h_out + 8 * (size_t)cnt[c], e->h_ccnt + c, st);
     if (rc) return rc;
   }

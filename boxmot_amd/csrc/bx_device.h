@@ -17,6 +17,11 @@ constexpr int WG = 256;  // threads per workgroup: 4 waves of 64
 constexpr int WAVE = 64;
 constexpr double INF = __builtin_huge_val();
 
+// host: is a 2x3 row-major warp exactly the identity (what a static camera's CMC returns)?
+inline bool is_identity_warp(const double* w) {
+  return w[0] == 1.0 && w[1] == 0.0 && w[2] == 0.0 && w[3] == 0.0 && w[4] == 1.0 && w[5] == 0.0;
+}
+
 enum : int { KIND_BYTE = 0, KIND_BOT = 1 };
 enum : uint32_t { ST_NEW = 0, ST_TRACKED = 1, ST_LOST = 2, ST_REMOVED = 3 };
 // per-slot persistent flag word; F_INACT / F_INLOST: the slot is on the active / lost list
@@ -999,10 +1004,16 @@ __device__ __forceinline__ bool lap_component_regs(const int (&rr)[LAP_RM], int 
   }
 #pragma unroll
   for (int q = 0; q < RM; q++)
-    if (q < m) w.col4row[rr[q]] = (int16_t)(c4r[q] >= 0 ? rsel(cols, c4r[q]) : -1);
+    if (q < m) {
+      w.col4row[rr[q]] = (int16_t)(c4r[q] >= 0 ? rsel(cols, c4r[q]) : -1);
+      w.u[rr[q]] = u[q];  // the duals, for lap_tied_block
+    }
 #pragma unroll
   for (int t = 0; t < CM; t++)
-    if (t < nc) w.row4col[cols[t]] = (int16_t)(r4c[t] >= 0 ? rsel(rr, r4c[t]) : -1);
+    if (t < nc) {
+      w.row4col[cols[t]] = (int16_t)(r4c[t] >= 0 ? rsel(rr, r4c[t]) : -1);
+      w.v[cols[t]] = v[t];
+    }
   return true;
 }
 
@@ -1102,6 +1113,8 @@ __device__ __forceinline__ int lap_prepare_block(int R, int C, double L, const L
       if (w.colmin[jj] == r) {
         w.col4row[r] = (int16_t)jj;
         w.row4col[jj] = (int16_t)r;
+        w.v[jj] = cc - L;  // optimal duals u = 0, v = c - L: every other row's edge has
+                           // reduced cost c_r - c >= 0, zero exactly on a tie (lap_tied_block)
       } else {
         w.col4row[r] = -2;  // settled unmatched
       }
@@ -1230,6 +1243,109 @@ __device__ __forceinline__ void lap_solve_roots_wave(int R, int nroots, double L
     w.dbg[6] = iters;
     w.dbg[7] = __builtin_amdgcn_s_memtime();  // after labels+solve
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Is the solved matching the UNIQUE optimum?  The sparse solver above equals lapx whenever the
+// optimal pair set is unique; on a tie lapx's pick depends on its whole dense run, so the caller
+// re-solves with lapx itself (bx_jv.h).  Max-gain view: gains g = L - c, duals U = -u >= 0,
+// V = -v >= 0, reduced cost rc = U_i + V_j - g_ij = (c - L) - u_i - v_j >= 0, zero on every
+// matched edge; unmatched rows/columns have zero duals.  Another optimum exists iff, in the
+// directed graph of tight edges (unmatched edge row -> column, matched edge column -> row), there
+// is a cycle or a path from a source (an unmatched row, or a matched column with V = 0) to a sink
+// (an unmatched column, or a matched row with U = 0): swapping along it keeps the gain.  Tight
+// and zero are taken within BX_TIE_EPS (float duals; a near-tie is re-solved too), and `pre`
+// carries the caller's own flag (a pair whose cost is within BX_TIE_EPS of L: gain 0, which the
+// CSR drops as inadmissible).  Called by ALL threads after lap_solve_block; returns a uniform
+// answer.  Uses rlab / coldeg as scratch.
+constexpr double BX_TIE_EPS = 1e-12;
+__device__ inline bool lap_tied_block(int R, int C, double L, const LapWS& w, int* scan_tmp,
+                                      bool pre) {
+  const int tid = threadIdx.x;
+  auto extra_tight = [&](int r, int e, int& j) {  // a tight unmatched edge of row r
+    double c;
+    lap_edge(w, e, j, c);
+    if (!(c < INF) || j == w.col4row[r]) return false;
+    return (c - L) - w.u[r] - w.v[j] <= BX_TIE_EPS;
+  };
+  // pass 0: a matched edge with both duals zero (gain 0) is a tie by itself; tight unmatched
+  // edges decide whether the graph search runs at all (after a multi-step augmentation the
+  // formerly matched edges stay tight, so they are common but rarely part of a swap)
+  bool tie = pre, extra = false;
+  for (int r = tid; r < R; r += WG) {
+    const int jm = w.col4row[r];
+    if (jm >= 0 && w.u[r] > -BX_TIE_EPS && w.v[jm] > -BX_TIE_EPS) tie = true;
+    for (int e = w.row_ptr[r]; e < w.row_ptr[r + 1] && !extra; e++) {
+      int j;
+      extra |= extra_tight(r, e, j);
+    }
+  }
+  int ntie, nextra;
+  block_scan_flag(tie, scan_tmp, ntie);
+  block_scan_flag(extra, scan_tmp, nextra);
+  if (ntie) return true;
+  if (!nextra) return false;
+  // reach-T: hc[j] = column j leads to a sink, hr[r] = row r does
+  int* hr = w.rlab;
+  int* hc = w.coldeg;
+  for (int r = tid; r < R; r += WG) hr[r] = 0;
+  for (int j = tid; j < C; j += WG) {
+    const int r = w.row4col[j];
+    hc[j] = r < 0 || w.u[r] > -BX_TIE_EPS;
+  }
+  __syncthreads();
+  while (true) {
+    bool ch = false;
+    for (int r = tid; r < R; r += WG) {
+      if (hr[r]) continue;
+      for (int e = w.row_ptr[r]; e < w.row_ptr[r + 1]; e++) {
+        int j;
+        if (extra_tight(r, e, j) && hc[j]) { hr[r] = 1; ch = true; break; }
+      }
+    }
+    __syncthreads();
+    for (int j = tid; j < C; j += WG) {
+      const int r = w.row4col[j];
+      if (!hc[j] && r >= 0 && hr[r]) { hc[j] = 1; ch = true; }
+    }
+    int nch;
+    block_scan_flag(ch, scan_tmp, nch);
+    if (!nch) break;
+  }
+  bool st = false;
+  for (int r = tid; r < R; r += WG) st |= w.col4row[r] < 0 && hr[r];
+  for (int j = tid; j < C; j += WG) st |= w.row4col[j] >= 0 && w.v[j] > -BX_TIE_EPS && hc[j];
+  int nst;
+  block_scan_flag(st, scan_tmp, nst);
+  if (nst) return true;
+  // cycles: peel rows without a live successor (row -> the row matched to a tight column);
+  // whatever survives lies on or leads into a cycle
+  int* al = w.rlab;
+  for (int r = tid; r < R; r += WG) al[r] = 1;
+  __syncthreads();
+  while (true) {
+    bool ch = false;
+    for (int r = tid; r < R; r += WG) {
+      if (!al[r]) continue;
+      bool live = false;
+      for (int e = w.row_ptr[r]; e < w.row_ptr[r + 1] && !live; e++) {
+        int j;
+        if (extra_tight(r, e, j)) {
+          const int r2 = w.row4col[j];
+          live = r2 >= 0 && al[r2];
+        }
+      }
+      if (!live) { al[r] = 0; ch = true; }
+    }
+    int nch;
+    block_scan_flag(ch, scan_tmp, nch);
+    if (!nch) break;
+  }
+  bool cyc = false;
+  for (int r = tid; r < R; r += WG) cyc |= al[r] != 0;
+  int ncyc;
+  block_scan_flag(cyc, scan_tmp, ncyc);
+  return ncyc != 0;
 }
 
 // Whole solve, called by ALL threads of the workgroup.

@@ -35,6 +35,8 @@ using namespace bx;
 
 namespace {
 
+#include "bx_jv.h"
+
 constexpr int CLS_HIST = 8;  // BoT-SORT per-track class-history entries (update_cls)
 constexpr int ELDS_DEFAULT = 1024;  // LAP edges kept in LDS; the rest spill to global scratch
 constexpr int REG_F = 512;   // feature rows up to this width live in registers: 8 per lane
@@ -208,6 +210,8 @@ struct Dev {
   uint32_t* pairs;    // [S][T*D] frame scratch: gated (slot << 16 | det) pairs
   int* npair;         // [S] gated pair count (zeroed by K6 for the next frame)
   double* etab;       // [S][T][D] frame scratch: embedding distance of gated pairs
+  unsigned char* jvs; // [S][jvs_stride] lapx lapjv state for tied associations (n = T + D)
+  size_t jvs_stride;
   void* fscr;         // [S][D][F] frame scratch for F > REG_F only: twice-normalised det rows
   int* status;        // [1] latched engine status
   unsigned long long* dbg;  // [S][32] phase stamps (diagnostic builds only, else null)
@@ -230,6 +234,7 @@ constexpr int BX_DBG_STRIDE = 64;  // stamps + counters per sequence
 enum {
   SQ_NA = 0, SQ_NL, SQ_FC, SQ_IDC, SQ_STATUS, SQ_NA2, SQ_NL2, SQ_NREC, SQ_SKIP,
   SQ_NHIGH, SQ_NPAIR, SQ_NDET,  // last frame's high dets, gated pairs, dets (statistics)
+  SQ_NTIE,                       // associations re-solved by lapx's lapjv (tied optimum), total
   SQ_STRIDE = 16
 };
 // update records: x = slot | kind << 16, y = detection index within the sequence's frame
@@ -931,18 +936,23 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
   auto associate = [&](const uint16_t* rows, int R, const uint16_t* cols, int C, double L,
                        int mode, int stamp) {
     const bool reid = REID && (mode == 2 || mode == 3);
-    // non-overlapping pairs have IoU 0: cost >= 1, never admissible, never gated (prox < 1)
-    const bool prefilter = L <= 1.0 && (!reid || P.prox < 1.0);
-    auto pair_cost = [&](const double* tb, int dk, bool& gated, bool& cand) -> double {
+    // non-overlapping pairs have IoU 0: cost >= 1, never admissible nor tied with L (so L below
+    // 1 by more than the tie tolerance), never gated (prox < 1)
+    const bool prefilter = L < 1.0 - BX_TIE_EPS && (!reid || P.prox < 1.0);
+    // the reference's cost of (track box tb, detection dk) — iou_distance, fuse_score, and for
+    // BoT-SORT with ReID np.minimum with the gated embedding distance (1 where not gated)
+    auto pair_cost = [&](const double* tb, int slot, int dk) -> double {
       double c = 1 - iou_pair(tb, s_dbox + 4 * dk);
-      gated = false;
       if (mode == 1) {
         c = fuse_one(c, s_dconf[dk]);
       } else if (mode >= 2) {
-        gated = reid && !(c > P.prox);
+        const bool gated = reid && !(c > P.prox);
         if (mode == 3 || P.fuse_first) c = fuse_one(c, s_dconf[dk]);
+        if (reid) {
+          const double ed = gated ? P.etab[((size_t)s * T + slot) * D + dk] : 1.0;
+          c = c < ed ? c : ed;  // np.minimum(ious_dists, emb_dists)
+        }
       }
-      cand = c < L || gated;
       return c;
     };
     // Candidates: a conservative fp32 intersection test on outward-rounded boxes (never misses
@@ -1075,9 +1085,10 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
     __syncthreads();
     if (stamp == 4) BX_STAMP(23);
     // pass 3: exact fp64 cost per candidate; a gated pair (botsort.py:209-214) takes
-    // min(iou cost, embedding distance) with the distance K1c precomputed for it
+    // min(iou cost, embedding distance) with the distance K1c precomputed for it.  A cost within
+    // the tie tolerance of L (gain 0) makes the optimum non-unique by itself.
     const int E = s_rowptr[R];
-    const double* etab = P.etab + (size_t)s * T * D;
+    bool at_limit = false;
     for (int e = tid; e < E; e += WG) {
       int j;
       double ri;
@@ -1085,14 +1096,9 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
       const int i = (int)ri;
       double tb[4];
       track_box<KIND>(g_kf, rows[i], tb);
-      bool g, cand;
-      double c = pair_cost(tb, cols[j], g, cand);
-      if (g && cand) {
-        const double ed = etab[(size_t)rows[i] * D + cols[j]];
-        c = c < ed ? c : ed;  // np.minimum(ious_dists, emb_dists)
-        cand = c < L;
-      }
-      put_edge(e, j, cand ? c : INF);
+      const double c = pair_cost(tb, rows[i], cols[j]);
+      at_limit |= fabs(c - L) <= BX_TIE_EPS;
+      put_edge(e, j, c < L ? c : INF);
     }
     __syncthreads();
     BX_STAMP(stamp);
@@ -1100,6 +1106,38 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
     W.dbg = (stamp == 4 && P.dbg) ? P.dbg + (size_t)s * BX_DBG_STRIDE + 26 : nullptr;
 #endif
     lap_solve_block(R, C, L, W, scan_tmp);
+    if (lap_tied_block(R, C, L, W, scan_tmp, at_limit)) {
+      // Tied optimum: lapx's own lapjv on the (R+C)^2 extension (matching.py:54-61), its state
+      // in this sequence's global scratch, the exact R x C cost block in gcost (the CSR is done).
+      double* M = e_gcost;
+      for (int k = tid; k < R * C; k += WG) {
+        const int i = k / C, j = k - i * C;
+        double tb[4];
+        track_box<KIND>(g_kf, rows[i], tb);
+        M[k] = pair_cost(tb, rows[i], cols[j]);
+      }
+      __syncthreads();
+      JvLds jw = jv_bind(P.jvs + (size_t)s * P.jvs_stride, R + C);
+      if (wave_id() == 0) {
+        const double half = L / 2.;
+        jv_wave_t([&](int i, int j) {
+                    return (i < R && j < C) ? M[(size_t)i * C + j]
+                                            : (i >= R && j >= C) ? 0.0 : half;
+                  },
+                  R + C, jw, SyncWaveG{});
+      }
+      __syncthreads();
+      // x >= C: unmatched (-1); a real partner above L is neither matched nor listed (-3)
+      for (int i = tid; i < R; i += WG) {
+        const int j = jw.x[i];
+        s_c4r[i] = (int16_t)(j >= C ? -1 : (M[(size_t)i * C + j] <= L ? j : -3));
+      }
+      for (int j = tid; j < C; j += WG) {
+        const int i = jw.y[j];
+        s_r4c[j] = (int16_t)(i >= R ? -1 : (M[(size_t)i * C + j] <= L ? i : -3));
+      }
+      if (tid == 0) seq[SQ_NTIE]++;
+    }
     __syncthreads();
   };
 
@@ -1145,7 +1183,7 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
     if (stage == 2) {
       BX_STAMP(10);
       for (int i = tid; i < nun; i += WG) {
-        if (s_c4r[i] >= 0) continue;
+        if (s_c4r[i] != -1) continue;  // u_unconfirmed = rows with x < 0 (-3: neither)
         const int slot = s_unconf[i];
         s_flags[slot] = (s_flags[slot] & ~F_STATE) | ST_REMOVED;  // mark_removed
         s_mark[slot] |= M_REMNOW;
@@ -1157,16 +1195,16 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
       nref = block_compact(npool, [&](int k) { return (s_mark[s_pool[k]] & M_TMP) != 0; },
                            [&](int k, int p) { s_refind[p] = s_pool[k]; }, scan_tmp);
       // remaining high dets (u_detection, ascending) — saved before the next solve reuses r4c
-      nrem = block_compact(Dh, [&](int j) { return s_r4c[j] < 0; },
+      nrem = block_compact(Dh, [&](int j) { return s_r4c[j] == -1; },
                            [&](int j, int p) { s_rem[p] = s_hd[j]; }, scan_tmp);
       for (int k = tid; k < nref; k += WG) s_mark[s_refind[k]] &= ~M_TMP;
       // r_tracked = unmatched pool rows still Tracked
       nrtr = block_compact(
-          npool, [&](int k) { return s_c4r[k] < 0 && st_of(s_flags[s_pool[k]]) == ST_TRACKED; },
+          npool, [&](int k) { return s_c4r[k] == -1 && st_of(s_flags[s_pool[k]]) == ST_TRACKED; },
           [&](int k, int p) { s_rtr[p] = s_pool[k]; }, scan_tmp);
     } else if (stage == 1) {
       nlostl = block_compact(
-          nrtr, [&](int k) { return s_c4r[k] < 0; },
+          nrtr, [&](int k) { return s_c4r[k] == -1; },
           [&](int k, int p) {
             const int slot = s_rtr[k];
             s_lostl[p] = (uint16_t)slot;
@@ -1178,7 +1216,7 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
 
   // ---------------- P9: new tracks from the detections left over (conf >= det/new thresh)
   const int nnew = block_compact(
-      nrem, [&](int k) { return s_r4c[k] < 0 && s_dconf[s_rem[k]] >= P.new_thresh; },
+      nrem, [&](int k) { return s_r4c[k] == -1 && s_dconf[s_rem[k]] >= P.new_thresh; },
       [&](int k, int p) { s_newt[p] = s_rem[k]; /* det index for now */ }, scan_tmp);
   // allocate the first nnew free slots (ascending)
   {
@@ -1718,7 +1756,9 @@ struct bx_engine {
   // step's K1 queues behind it there and its K1c join covers both, every other entry point
   // settles it first (side_pending)
   bool overlap = false, side_pending = false;
-  std::mutex mu;
+  // serialises every entry point that touches side_pending / the host staging buffers
+  // (recursive: the host paths call bx_engine_step while holding it)
+  std::recursive_mutex mu;
   // per_class mode (bx_engine_update_classes_host), allocated on first use: per sequence the
   // parked active lists [C][T] + their lengths [C] + the held frame counter, the class that ran
   // last; host-path class offsets [C][2] and output counts [C]
@@ -1727,6 +1767,7 @@ struct bx_engine {
   std::vector<int> cur_cls;
   int* h_coff = nullptr;
   int* h_ccnt = nullptr;
+  double* h_cwarp = nullptr;  // [C][6] the class calls' warps
 };
 
 namespace {
@@ -1887,7 +1928,9 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
 // reports their failures too
 // overlap mode: wait for a step's unjoined K5 (side stream) before any other use of the engine
 static int settle(bx_engine* e) {
-  if (e && e->side_pending) {
+  if (!e) return BX_OK;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  if (e->side_pending) {
     e->side_pending = false;
     HIPCHK(hipStreamSynchronize(e->side));
   }
@@ -1931,6 +1974,7 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
   d.S = S; d.T = T; d.D = D; d.F = F; d.kind = cfg->kind; d.emb_f64 = cfg->emb_f64;
   d.with_reid = reid; d.fuse_first = cfg->fuse_first_associate;
   d.elds = ELDS_DEFAULT;
+  d.jvs_stride = (jv_bytes(T + D) + 255) & ~size_t(255);
   d.match_thresh = cfg->match_thresh;
   d.max_time_lost = (int)(cfg->frame_rate / 30.0 * cfg->track_buffer);
   if (cfg->kind == BX_BYTETRACK) {
@@ -1972,6 +2016,7 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
     d.pairs = carve<uint32_t>(p, reid ? ST * D : 1);
     d.npair = carve<int>(p, S);
     d.etab = carve<double>(p, reid ? ST * D : 1);
+    d.jvs = carve<unsigned char>(p, (size_t)S * d.jvs_stride);
     d.fscr = carve<char>(p, fs * SD * FS);
     d.status = carve<int>(p, 16);
     return (size_t)(p - p0);
@@ -2045,6 +2090,7 @@ int bx_engine_destroy(bx_engine* e) {
   for (char* p : e->park) (void)hipFree(p);
   (void)hipFree(e->h_coff);
   (void)hipFree(e->h_ccnt);
+  (void)hipFree(e->h_cwarp);
   delete e;
   return BX_OK;
 }
@@ -2073,6 +2119,7 @@ int bx_engine_step(bx_engine* e, int seq0, int nseq, const float* dets, const in
     return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_step");
   if (e->dev.with_reid && !embs) return set_err(BX_ERR_SHAPE, "BoT-SORT with_reid needs embs");
   hipStream_t st = (hipStream_t)stream;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   e->cache_seq = -1;
   if (e->dev.kind == BX_BYTETRACK)
     return launch_frame<KIND_BYTE, float, true>(e, seq0, nseq, dets, det_off, embs, warps, out,
@@ -2097,7 +2144,7 @@ int bx_engine_update_host(bx_engine* e, int seq, const float* dets, int n, const
   if (n > e->dev.D) return set_err(BX_ERR_CAPACITY, "detections exceed det_cap");
   if (e->dev.with_reid && n > 0 && !embs)
     return set_err(BX_ERR_SHAPE, "BoT-SORT with_reid needs embs");
-  std::lock_guard<std::mutex> lk(e->mu);
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   hipStream_t st = (hipStream_t)stream;
   const size_t fs = e->cfg.emb_f64 ? 8 : 4;
   // inputs through pinned mirrors (asynchronous DMA), the frame, then the rows (at most n), the
@@ -2138,7 +2185,7 @@ int bx_engine_update_host(bx_engine* e, int seq, const float* dets, int n, const
 // stacked in class order.  All C class calls are enqueued back to back on `stream` (no host sync
 // between them); one synchronisation at the end.
 int bx_engine_update_classes_host(bx_engine* e, int seq, const float* dets, int n,
-                                  const void* embs, const double* warp, int n_classes,
+                                  const void* embs, const double* warps, int n_classes,
                                   double* out, int* n_out, void* stream) {
   if (int rc = settle(e)) return rc;
   if (!e || seq < 0 || seq >= e->dev.S || n < 0 || (n && !dets) || !n_out || n_classes <= 0 ||
@@ -2147,7 +2194,7 @@ int bx_engine_update_classes_host(bx_engine* e, int seq, const float* dets, int 
   if (n > e->dev.D) return set_err(BX_ERR_CAPACITY, "detections exceed det_cap");
   const bool reid = e->dev.with_reid;
   if (reid && n > 0 && !embs) return set_err(BX_ERR_SHAPE, "BoT-SORT with_reid needs embs");
-  std::lock_guard<std::mutex> lk(e->mu);
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   hipStream_t st = (hipStream_t)stream;
   const int C = n_classes, F = e->dev.F;
   if (e->n_classes && e->n_classes != C)
@@ -2158,6 +2205,7 @@ int bx_engine_update_classes_host(bx_engine* e, int seq, const float* dets, int 
     e->cur_cls.assign(e->dev.S, 0);
     HIPCHK(hipMalloc(&e->h_coff, sizeof(int) * 2 * C));
     HIPCHK(hipMalloc(&e->h_ccnt, sizeof(int) * C));
+    HIPCHK(hipMalloc(&e->h_cwarp, sizeof(double) * 6 * C));
   }
   if (!e->park[seq]) {
     const size_t bytes = park_npark_off(e) + sizeof(int) * (C + 1);
@@ -2197,16 +2245,18 @@ int bx_engine_update_classes_host(bx_engine* e, int seq, const float* dets, int 
   if (m) HIPCHK(hipMemcpyAsync(e->h_dets, hd.data(), sizeof(float) * 6 * m, hipMemcpyHostToDevice, st));
   if (m && reid) HIPCHK(hipMemcpyAsync(e->h_embs, he.data(), fs * (size_t)m * F, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(e->h_coff, hoff.data(), sizeof(int) * 2 * C, hipMemcpyHostToDevice, st));
-  if (warp) HIPCHK(hipMemcpyAsync(e->h_warp, warp, sizeof(double) * 6, hipMemcpyHostToDevice, st));
+  if (warps) HIPCHK(hipMemcpyAsync(e->h_cwarp, warps, sizeof(double) * 6 * C, hipMemcpyHostToDevice, st));
   for (int c = 0; c < C; c++) {
     hipLaunchKernelGGL(class_swap_kernel, dim3(1), dim3(WG), 0, st, e->dev, seq, park, npark, C,
                        e->cur_cls[seq], c, c == 0 ? 1 : 0);
     HIPCHK(hipGetLastError());
     e->cur_cls[seq] = c;
     const char* ep = reid ? (const char*)e->h_embs + fs * F * (size_t)cnt[c] : nullptr;
+    // class call c's warp (an identity warp is no warp, as in bx_engine_update_host's callers)
+    const bool wc = warps && !is_identity_warp(warps + 6 * (size_t)c);
     int rc = bx_engine_step(e, seq, 1, e->h_dets + 6 * (size_t)cnt[c], e->h_coff + 2 * c, ep,
-                            warp ? e->h_warp : nullptr, e->h_out + 8 * (size_t)cnt[c],
-                            e->h_ccnt + c, stream);
+                            wc ? e->h_cwarp + 6 * (size_t)c : nullptr,
+                            e->h_out + 8 * (size_t)cnt[c], e->h_ccnt + c, stream);
     if (rc) return rc;
   }
   std::vector<int> oc(C);
@@ -2261,6 +2311,19 @@ int bx_engine_frame_stats_host(bx_engine* e, int seq0, int nseq, int64_t* sums) 
     for (int q = 0; q < nseq; q++) t += v[(size_t)q * SQ_STRIDE + idx[k]];
     sums[k] = t;
   }
+  return BX_OK;
+}
+
+int bx_engine_lap_ties_host(bx_engine* e, int seq0, int nseq, int64_t* total) {
+  if (int rc = settle(e)) return rc;
+  if (!e || !total || seq0 < 0 || nseq <= 0 || seq0 + nseq > e->dev.S)
+    return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_lap_ties_host");
+  std::vector<int> v((size_t)nseq * SQ_STRIDE);
+  HIPCHK(hipMemcpy(v.data(), e->dev.seq + (size_t)seq0 * SQ_STRIDE, sizeof(int) * v.size(),
+                   hipMemcpyDeviceToHost));
+  int64_t t = 0;
+  for (int q = 0; q < nseq; q++) t += v[(size_t)q * SQ_STRIDE + SQ_NTIE];
+  *total = t;
   return BX_OK;
 }
 
@@ -2413,6 +2476,16 @@ int bx_engine_set_overlap(bx_engine* e, int on) {
   if (!e) return set_err(BX_ERR_INVALID, "null engine");
   if (int rc = settle(e)) return rc;
   e->overlap = on != 0;
+  return BX_OK;
+}
+
+int bx_engine_inputs_released(bx_engine* e, void* stream) {
+  if (!e) return set_err(BX_ERR_INVALID, "null engine");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  if (!e->side_pending) return BX_OK;
+  // the last step's K5 is the last reader of its dets / det_off / embs: order `stream` after it
+  HIPCHK(hipEventRecord(e->ev_join[1], e->side));
+  HIPCHK(hipStreamWaitEvent((hipStream_t)stream, e->ev_join[1], 0));
   return BX_OK;
 }
 

@@ -19,6 +19,30 @@ struct JvLds {
   unsigned long long* dc;  // diagnostic counters (timing builds) or null
 };
 
+// JvLds state of an n-column problem carved from `p` (LDS or global), jv_bytes(n) bytes.
+__host__ __device__ constexpr size_t jv_ints_bytes(int n) { return (((size_t)n * 4 + 7) / 8) * 8; }
+__host__ __device__ constexpr size_t jv_bytes(int n) {
+  return 2 * 8 * (size_t)n + 16 + 6 * jv_ints_bytes(n) + 32;
+}
+__device__ inline JvLds jv_bind(unsigned char* p, int n) {
+  JvLds w;
+  size_t o = 0;
+  auto takeD = [&](int k) { double* q = (double*)(p + o); o += (size_t)k * 8; return q; };
+  auto takeI = [&](int k) { int* q = (int*)(p + o); o += jv_ints_bytes(k); return q; };
+  w.v = takeD(n);
+  w.d = takeD(n);
+  w.sd = takeD(2);
+  w.x = takeI(n);
+  w.y = takeI(n);
+  w.matches = takeI(n);
+  w.freer = takeI(n);
+  w.pred = takeI(n);
+  w.col = takeI(n);
+  w.sc = takeI(8);
+  w.dc = nullptr;
+  return w;
+}
+
 __device__ __forceinline__ double cget(const double* C, int nr, int nc, int i, int j) {
   return (i < nr && j < nc) ? C[i * nc + j] : 0.0;
 }
@@ -41,9 +65,30 @@ __device__ __forceinline__ void wave_argmin(double& m, int& j) {
   }
 }
 
+// Cross-lane hand-off points of the wave solvers: the whole (one-wave) workgroup, or only the
+// calling wave of a larger one with its state in global memory (workgroup-scope fence: the
+// stores are complete and visible to the wave's later loads through the CU's L1).
+// after_atomics(): global atomics are performed in L2 and need not update a line the CU's L1
+// still holds, so a global-state solver invalidates L1 (agent-scope fence) before reading what
+// its atomics wrote; plain stores and loads of one wave meet in the same L1.
+struct SyncBlock {
+  __device__ void operator()() const { __syncthreads(); }
+  __device__ void after_atomics() const {}
+};
+struct SyncWaveG {
+  __device__ void operator()() const {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ void after_atomics() const {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    __builtin_amdgcn_wave_barrier();
+  }
+};
+
 // Wave-order-preserving compaction: emit(k, pos) for k < n with pred(k); returns the count.
-template <class P, class E>
-__device__ int wave_compact(int n, P pred, E emit) {
+template <class P, class E, class SY>
+__device__ int wave_compact_s(int n, P pred, E emit, SY sync) {
   const int lane = threadIdx.x;
   int base = 0;
   for (int c = 0; c < n; c += OW) {
@@ -53,23 +98,29 @@ __device__ int wave_compact(int n, P pred, E emit) {
     if (f) emit(k, base + __popcll(m & ((1ull << lane) - 1ull)));
     base += __popcll(m);
   }
-  __syncthreads();
+  sync();
   return base;
 }
+template <class P, class E>
+__device__ int wave_compact(int n, P pred, E emit) {
+  return wave_compact_s(n, pred, emit, SyncBlock{});
+}
 
-constexpr int JV_CH = 8;  // 64-position chunks of one relaxation (assignment sizes <= 512)
+constexpr int JV_CH = 8;  // 64-position chunks of one relaxation loaded together
 
 // ------------------------------------------------------------------------------------------
-// Any n <= 64 * JV_CH, state in LDS.
-__device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
-  const int n = nr > nc ? nr : nc;
+// Any n, state in `w` (LDS, or global memory with a SyncWaveG); the cost of (i, j) from cf(i, j)
+// and every cross-lane hand-off through sync() (the whole workgroup when it is one wave, else
+// the calling wave only).
+template <class CF, class SY>
+__device__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync) {
   const int lane = threadIdx.x;
   // ---- _ccrrt_dense.  Column minima from LARGE, first row on ties (lane per column) ...
   for (int j = lane; j < n; j += OW) {
     double mn = LAPX_LARGE;
     int im = 0;
     for (int i = 0; i < n; i++) {
-      const double c = cget(C, nr, nc, i, j);
+      const double c = cf(i, j);
       if (c < mn) mn = c, im = i;
     }
     w.v[j] = mn;
@@ -77,18 +128,19 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
     w.x[j] = -1;
     w.matches[j] = 0;
   }
-  __syncthreads();
+  sync();
   // ... the sweep j = n-1..0 leaves each row the LARGEST column whose minimum it holds and
   // releases the others; `matches` counts them (lapx's unique[] is a count of one)
   for (int j = lane; j < n; j += OW) {
     atomicMax(&w.x[w.y[j]], j);
     atomicAdd(&w.matches[w.y[j]], 1);
   }
-  __syncthreads();
+  sync();
+  sync.after_atomics();
   for (int j = lane; j < n; j += OW)
     if (w.x[w.y[j]] != j) w.y[j] = -1;
-  int nfree = wave_compact(
-      n, [&](int i) { return w.x[i] < 0; }, [&](int i, int p) { w.freer[p] = i; });
+  int nfree = wave_compact_s(
+      n, [&](int i) { return w.x[i] < 0; }, [&](int i, int p) { w.freer[p] = i; }, sync);
   // reduction transfer, uniquely-assigned rows in order (each lowers v[x[i]], which the rows
   // after it read)
   for (int i = 0; i < n; i++) {
@@ -96,13 +148,13 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
     if (j1 < 0 || w.matches[i] != 1) continue;
     double mn = LAPX_LARGE;
     for (int j = lane; j < n; j += OW) {
-      const double h = cget(C, nr, nc, i, j) - w.v[j];
+      const double h = cf(i, j) - w.v[j];
       if (j != j1 && h < mn) mn = h;
     }
     mn = wave_min_d(mn);
-    __syncthreads();
+    sync();
     if (lane == 0) w.v[j1] = w.v[j1] - mn;
-    __syncthreads();
+    sync();
   }
   // ---- _carr_dense, at most two passes over the free rows (lapjv_internal)
   for (int pass = 0; pass < 2 && nfree > 0; pass++) {
@@ -117,7 +169,7 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
       int k1 = JV_IMAX;
       bool odd = false;
       for (int j = lane; j < n; j += OW) {
-        const double h = cget(C, nr, nc, fi, j) - w.v[j];
+        const double h = cf(fi, j) - w.v[j];
         odd |= !(h < LAPX_LARGE);
         if (h < m1) m1 = h, k1 = j;
       }
@@ -129,14 +181,14 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
         double m2 = INF;
         int k2 = JV_IMAX;
         for (int j = lane; j < n; j += OW) {
-          const double h = cget(C, nr, nc, fi, j) - w.v[j];
+          const double h = cf(fi, j) - w.v[j];
           if (j != j1 && h < m2) m2 = h, k2 = j;
         }
         wave_argmin(m2, k2);
-        v1 = cget(C, nr, nc, fi, j1) - w.v[j1];
+        v1 = cf(fi, j1) - w.v[j1];
         if (n >= 2) {
           j2 = k2;
-          v2 = cget(C, nr, nc, fi, j2) - w.v[j2];
+          v2 = cf(fi, j2) - w.v[j2];
         } else {
           j2 = -1;
           v2 = LAPX_LARGE;
@@ -144,10 +196,10 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
       } else {  // NaN or huge reduced costs: lapx's scan as written
         j1 = 0;
         j2 = -1;
-        v1 = cget(C, nr, nc, fi, 0) - w.v[0];
+        v1 = cf(fi, 0) - w.v[0];
         v2 = LAPX_LARGE;
         for (int j = 1; j < n; j++) {
-          const double h = cget(C, nr, nc, fi, j) - w.v[j];
+          const double h = cf(fi, j) - w.v[j];
           if (h < v2) {
             if (h >= v1) {
               v2 = h;
@@ -185,12 +237,12 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
         if (lane == 0) w.freer[nnew] = i0;
         nnew++;
       }
-      __syncthreads();
+      sync();
       if (lane == 0) {
         w.x[fi] = j1;
         w.y[j1] = fi;
       }
-      __syncthreads();
+      sync();
     }
     nfree = nnew;
   }
@@ -201,11 +253,11 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
   for (int f = 0; f < nfree; f++) {
     const int start = w.freer[f];
     for (int j = lane; j < n; j += OW) {
-      w.d[j] = cget(C, nr, nc, start, j) - w.v[j];
+      w.d[j] = cf(start, j) - w.v[j];
       w.pred[j] = start;
       w.col[j] = j;
     }
-    __syncthreads();
+    sync();
     int low = 0, up = 0, last = 0, endofpath = -1, found = 0;
     double mn = 0.0;
     do {
@@ -277,13 +329,13 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
             w.sc[3] = found;
             w.sd[0] = mn;
           }
-          __syncthreads();
+          sync();
           last = w.sc[0];
           up = w.sc[1];
           endofpath = w.sc[2];
           found = w.sc[3];
           mn = w.sd[0];
-          __syncthreads();
+          sync();
         }
       }
       if (!found) {
@@ -295,68 +347,71 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
         const int j1 = w.col[low++];
         const int i = w.y[j1];
         const double mind = w.d[j1];
-        const double h = cget(C, nr, nc, i, j1) - w.v[j1] - mind;
-        const int up0 = up;
-        int jc[JV_CH];
-        double v2c[JV_CH], dc[JV_CH];
-        bool yc[JV_CH];
+        const double h = cf(i, j1) - w.v[j1] - mind;
+        // groups of JV_CH chunks (a swap only writes positions up to the chunk in flight, so a
+        // later group's operands are still the sequential loop's)
+        for (int g0 = up; g0 < n && !found; g0 += JV_CH * OW) {
+          int jc[JV_CH];
+          double v2c[JV_CH], dc[JV_CH];
+          bool yc[JV_CH];
 #pragma unroll
-        for (int c = 0; c < JV_CH; c++) {
-          const int k = up0 + c * OW + lane;
-          jc[c] = -1;
-          if (k < n) {
-            const int j = w.col[k];
-            jc[c] = j;
-            v2c[c] = cget(C, nr, nc, i, j) - w.v[j] - h;
-            dc[c] = w.d[j];
-            yc[c] = w.y[j] < 0;
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < JV_CH; c++) {
-          const int base = up0 + c * OW;
-          if (base >= n || found) break;
-          const int j = jc[c];
-          const double v2 = v2c[c];
-          bool A = false, B = false, E = false;
-          if (j >= 0) {
-            A = v2 < dc[c];
-            B = A && v2 == mind;
-            E = B && yc[c];
-          }
-          const unsigned long long em = __ballot(E);
-          int kE = OW;
-          if (em) kE = __ffsll((long long)em) - 1;
-          if (A && lane <= kE) {
-            w.pred[j] = i;
-            w.d[j] = v2;
-          }
-          unsigned long long hm = __ballot(B && !E && lane < kE);
-          if (hm) {
-            while (hm) {  // the swaps, in position order (lane 0 owns col)
-              const int bb = __ffsll((long long)hm) - 1;
-              hm &= hm - 1;
-              const int jb = __shfl(j, bb);
-              if (lane == 0) {
-                w.col[base + bb] = w.col[up];
-                w.col[up] = jb;
-              }
-              up++;
+          for (int c = 0; c < JV_CH; c++) {
+            const int k = g0 + c * OW + lane;
+            jc[c] = -1;
+            if (k < n) {
+              const int j = w.col[k];
+              jc[c] = j;
+              v2c[c] = cf(i, j) - w.v[j] - h;
+              dc[c] = w.d[j];
+              yc[c] = w.y[j] < 0;
             }
           }
-          if (em) {
-            endofpath = __shfl(j, kE);
-            found = 1;
+#pragma unroll
+          for (int c = 0; c < JV_CH; c++) {
+            const int base = g0 + c * OW;
+            if (base >= n || found) break;
+            const int j = jc[c];
+            const double v2 = v2c[c];
+            bool A = false, B = false, E = false;
+            if (j >= 0) {
+              A = v2 < dc[c];
+              B = A && v2 == mind;
+              E = B && yc[c];
+            }
+            const unsigned long long em = __ballot(E);
+            int kE = OW;
+            if (em) kE = __ffsll((long long)em) - 1;
+            if (A && lane <= kE) {
+              w.pred[j] = i;
+              w.d[j] = v2;
+            }
+            unsigned long long hm = __ballot(B && !E && lane < kE);
+            if (hm) {
+              while (hm) {  // the swaps, in position order (lane 0 owns col)
+                const int bb = __ffsll((long long)hm) - 1;
+                hm &= hm - 1;
+                const int jb = __shfl(j, bb);
+                if (lane == 0) {
+                  w.col[base + bb] = w.col[up];
+                  w.col[up] = jb;
+                }
+                up++;
+              }
+            }
+            if (em) {
+              endofpath = __shfl(j, kE);
+              found = 1;
+            }
           }
         }
-        __syncthreads();
+        sync();
       }
     } while (!found);
     for (int k = lane; k <= last; k += OW) {
       const int j1 = w.col[k];
-      w.v[j1] = w.v[j1] + w.d[j1] - mn;
+      w.v[j1] = w.v[j1] + (w.d[j1] - mn);  // lapx: v[j] += d[j] - mind
     }
-    __syncthreads();
+    sync();
     if (lane == 0) {
       int i;
       do {
@@ -367,8 +422,13 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
         w.x[i] = j1;
       } while (i != start);
     }
-    __syncthreads();
+    sync();
   }
+}
+
+__device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
+  jv_wave_t([&](int i, int j) { return cget(C, nr, nc, i, j); }, nr > nc ? nr : nc, w,
+            SyncBlock{});
 }
 
 // ------------------------------------------------------------------------------------------
@@ -746,7 +806,7 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
       }
       JVT(6);
     } while (!found);
-    if (own && lane <= last) v = v + d - mn;
+    if (own && lane <= last) v = v + (d - mn);  // lapx: v[j] += d[j] - mind
     int i;
     do {
       const int le = first_lane(own && col == endofpath);

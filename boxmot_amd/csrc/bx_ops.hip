@@ -151,10 +151,18 @@ __global__ void kf_gate_kernel(int kind, int n, const double* mean, const double
   kf_gating_soa(kind, mean + 8 * t, cov + 64 * t, 1, z, nz, out + (size_t)t * nz);
 }
 
-// One dense problem: CSR of admissible edges (cost < thresh) in LDS, then the wave LAP.
+#include "bx_jv.h"
+
+// One dense problem: CSR of admissible edges (cost < thresh) in LDS, then the wave LAP.  When
+// the optimum is not unique (lap_tied_block) the problem is re-solved by lapx's own lapjv on the
+// (nr+nc)^2 extension (matching.py:54-61: lap.lapjv(extend_cost=True, cost_limit=thresh)), read
+// through an accessor with its state in `jvs` (global memory), so ties resolve as lapx's do.
+// Outputs: x[i] = column, -1 unmatched, -3 assigned by lapx to a real column above thresh (the
+// reference neither matches nor lists such a row: matching.py:56-61); y likewise.
 __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int nr, int nc,
                                                        double thr, int elds, uint16_t* gcol,
-                                                       double* gcost, int32_t* x, int32_t* y) {
+                                                       double* gcost, unsigned char* jvs,
+                                                       int32_t* x, int32_t* y, int32_t* tied) {
   extern __shared__ __align__(16) unsigned char smem[];
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -181,9 +189,14 @@ __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int n
   int* cmin = (int*)take(4 * nc);
   int* scan_tmp = (int*)take(4 * 8);
   const int tid = threadIdx.x;
+  bool pre = false;  // a cost within BX_TIE_EPS of the limit: gain 0, a tie by itself
   for (int i = tid; i < nr; i += WG) {
     int cnt = 0;
-    for (int j = 0; j < nc; j++) cnt += cost[(size_t)i * nc + j] < thr;
+    for (int j = 0; j < nc; j++) {
+      const double c = cost[(size_t)i * nc + j];
+      cnt += c < thr;
+      pre |= fabs(c - thr) <= BX_TIE_EPS;
+    }
     rowptr[i] = cnt;
   }
   __syncthreads();
@@ -209,8 +222,33 @@ __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int n
   W.colaux = caux;
   W.colmin = cmin;
   lap_solve_block(nr, nc, thr, W, scan_tmp);
-  for (int i = tid; i < nr; i += WG) x[i] = c4r[i];
-  for (int j = tid; j < nc; j += WG) y[j] = r4c[j];
+  const bool tie = lap_tied_block(nr, nc, thr, W, scan_tmp, pre);
+  if (!tie) {
+    for (int i = tid; i < nr; i += WG) x[i] = c4r[i];
+    for (int j = tid; j < nc; j += WG) y[j] = r4c[j];
+    if (tid == 0) *tied = 0;
+    return;
+  }
+  const int n = nr + nc;
+  JvLds jw = jv_bind(jvs, n);
+  if (wave_id() == 0) {
+    const double half = thr / 2.;
+    jv_wave_t([&](int i, int j) {
+                return (i < nr && j < nc) ? cost[(size_t)i * nc + j]
+                                          : (i >= nr && j >= nc) ? 0.0 : half;
+              },
+              n, jw, SyncWaveG{});
+  }
+  __syncthreads();
+  for (int i = tid; i < nr; i += WG) {
+    const int j = jw.x[i];
+    x[i] = j >= nc ? -1 : (cost[(size_t)i * nc + j] <= thr ? j : -3);
+  }
+  for (int j = tid; j < nc; j += WG) {
+    const int i = jw.y[j];
+    y[j] = i >= nr ? -1 : (cost[(size_t)i * nc + j] <= thr ? i : -3);
+  }
+  if (tid == 0) *tied = 1;
 }
 
 int grid_for(size_t n) {
@@ -218,46 +256,28 @@ int grid_for(size_t n) {
   return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
 }
 
-#include "bx_jv.h"
-
 // lapx.lapjv(cost, extend_cost, cost_limit) on one dense problem, one wave: mode 0 = square,
 // 1 = extend_cost (zero padding to max(nr, nc), read through cget), 2 = cost_limit (the
-// (nr+nc)^2 extension with cost_limit / 2 off the diagonal blocks, built in E first).
+// (nr+nc)^2 extension with cost_limit / 2 off the diagonal blocks, read through an accessor).
+// State in LDS when gst is null, else in global memory at gst.
 __global__ __launch_bounds__(OW) void lapjv_kernel(const double* cost, int nr, int nc, int mode,
-                                                   double lim, double* E, int32_t* x, int32_t* y) {
+                                                   double lim, unsigned char* gst, int32_t* x,
+                                                   int32_t* y) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = mode == 2 ? nr + nc : (nr > nc ? nr : nc);
-  const double* C = cost;
-  int cr = nr, cc = nc;
+  JvLds w = jv_bind(gst ? gst : smem, n);
   if (mode == 2) {
     const double half = lim / 2.;
-    for (int k = threadIdx.x; k < n * n; k += OW) {
-      const int i = k / n, j = k % n;
-      E[k] = (i < nr && j < nc) ? cost[(size_t)i * nc + j] : (i >= nr && j >= nc) ? 0.0 : half;
-    }
-    __syncthreads();
-    C = E;
-    cr = cc = n;
+    jv_wave_t([&](int i, int j) {
+                return (i < nr && j < nc) ? cost[(size_t)i * nc + j]
+                                          : (i >= nr && j >= nc) ? 0.0 : half;
+              },
+              n, w, SyncBlock{});
+  } else if (n <= OW) {
+    jv_wave64(cost, nr, nc, w);
+  } else {
+    jv_wave(cost, nr, nc, w);
   }
-  JvLds w;
-  size_t o = 0;
-  auto takeD = [&](int k) { double* p = (double*)(smem + o); o += (size_t)k * 8; return p; };
-  auto takeI = [&](int k) { int* p = (int*)(smem + o); o += (((size_t)k * 4 + 7) / 8) * 8; return p; };
-  w.v = takeD(n);
-  w.d = takeD(n);
-  w.sd = takeD(2);
-  w.x = takeI(n);
-  w.y = takeI(n);
-  w.matches = takeI(n);
-  w.freer = takeI(n);
-  w.pred = takeI(n);
-  w.col = takeI(n);
-  w.sc = takeI(8);
-  w.dc = nullptr;
-  if (n <= OW)
-    jv_wave64(C, cr, cc, w);
-  else
-    jv_wave(C, cr, cc, w);
   const bool cut = mode != 0;  // lapx: x >= n_cols -> -1, y >= n_rows -> -1, then [:nr] / [:nc]
   for (int i = threadIdx.x; i < nr; i += OW) x[i] = (cut && w.x[i] >= nc) ? -1 : w.x[i];
   for (int j = threadIdx.x; j < nc; j += OW) y[j] = (cut && w.y[j] >= nr) ? -1 : w.y[j];
@@ -372,6 +392,11 @@ int bx_kf_gating_distance(int kind, int n, const double* mean, const double* cov
 
 int bx_linear_assignment(const double* cost, int nr, int nc, double thresh, int32_t* x,
                          int32_t* y, void* stream) {
+  return bx_linear_assignment_ex(cost, nr, nc, thresh, x, y, nullptr, stream);
+}
+
+int bx_linear_assignment_ex(const double* cost, int nr, int nc, double thresh, int32_t* x,
+                            int32_t* y, int32_t* tied_out, void* stream) {
   if (nr < 0 || nc < 0 || nr > 8192 || nc > 8192)
     return op_err(BX_ERR_INVALID, "nr/nc out of range (0..8192)");
   hipStream_t st = (hipStream_t)stream;
@@ -398,15 +423,19 @@ int bx_linear_assignment(const double* cost, int nr, int nc, double thresh, int3
   if (lds > 160 * 1024) return op_err(BX_ERR_INVALID, "problem too large for LDS");
   void* ws = nullptr;
   const size_t ne = (size_t)nr * nc;
-  OPCHK(hipMallocAsync(&ws, ne * 10 + 64, st));
-  double* gcost = (double*)ws;
+  const size_t jvb = (jv_bytes(nr + nc) + 255) & ~size_t(255);
+  OPCHK(hipMallocAsync(&ws, jvb + 64 + ne * 10 + 64, st));
+  unsigned char* jvs = (unsigned char*)ws;
+  int32_t* tied = (int32_t*)(jvs + jvb);
+  double* gcost = (double*)(jvs + jvb + 64);
   uint16_t* gcol = (uint16_t*)(gcost + ne);
   if (lds > 65536)
     OPCHK(hipFuncSetAttribute((const void*)lap_dense_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(lap_dense_kernel, dim3(1), dim3(WG), lds, st, cost, nr, nc, thresh, elds,
-                     gcol, gcost, x, y);
+                     gcol, gcost, jvs, x, y, tied);
   OPCHK(hipGetLastError());
+  if (tied_out) OPCHK(hipMemcpyAsync(tied_out, tied, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
   OPCHK(hipFreeAsync(ws, st));
   return BX_OK;
 }
@@ -421,20 +450,24 @@ int bx_lapjv(const double* cost, int nr, int nc, int extend_cost, double cost_li
                   "extend_cost=True.");
   const int mode = lim ? 2 : (extend_cost ? 1 : 0);
   const int n = mode == 2 ? nr + nc : (nr > nc ? nr : nc);
-  if (n > OW * JV_CH) return op_err(BX_ERR_INVALID, "lapjv: extended size above 512");
+  if (n > 32768) return op_err(BX_ERR_INVALID, "lapjv: extended size above 32768");
   hipStream_t st = (hipStream_t)stream;
   if (!nr || !nc) {
     if (nr) OPCHK(hipMemsetAsync(x, 0xff, sizeof(int32_t) * nr, st));
     if (nc) OPCHK(hipMemsetAsync(y, 0xff, sizeof(int32_t) * nc, st));
     return BX_OK;
   }
-  double* E = nullptr;
-  if (mode == 2) OPCHK(hipMallocAsync((void**)&E, sizeof(double) * (size_t)n * n, st));
-  const size_t lds = 2 * 8 * (size_t)n + 16 + 6 * (((size_t)n * 4 + 7) / 8) * 8 + 32;
-  hipLaunchKernelGGL(lapjv_kernel, dim3(1), dim3(OW), lds, st, cost, nr, nc, mode, cost_limit, E,
-                     x, y);
+  const size_t lds = jv_bytes(n);
+  unsigned char* gst = nullptr;
+  if (lds > 160 * 1024) OPCHK(hipMallocAsync((void**)&gst, lds, st));
+  const size_t dyn = gst ? 0 : lds;
+  if (dyn > 65536)
+    OPCHK(hipFuncSetAttribute((const void*)lapjv_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+  hipLaunchKernelGGL(lapjv_kernel, dim3(1), dim3(OW), dyn, st, cost, nr, nc, mode, cost_limit,
+                     gst, x, y);
   OPCHK(hipGetLastError());
-  if (E) OPCHK(hipFreeAsync(E, st));
+  if (gst) OPCHK(hipFreeAsync(gst, st));
   return BX_OK;
 }
 

@@ -57,6 +57,7 @@ class Engine:
             appearance_thresh=p.appearance_thresh,
             fuse_first_associate=int(bool(p.fuse_first_associate)), with_reid=int(self.with_reid))
         self._L = N.load()
+        self._overlap, self._inflight = False, None
         h = C.c_void_p()
         N.check(self._L.bx_engine_create(C.byref(cfg), C.byref(h)), "bx_engine_create")
         self._h = h
@@ -93,6 +94,24 @@ class Engine:
         N.check(self._L.bx_engine_step(self._h, seq0, nseq, ptr(dets), ptr(det_off), ptr(embs),
                                        ptr(warps), ptr(out), ptr(out_count), stream),
                 "bx_engine_step")
+        # overlap mode: this step's K5 still reads its inputs after the call returns — hold them
+        # so the caching allocator cannot hand their memory out before the next step
+        self._inflight = (dets, det_off, embs) if self._overlap else None
+
+    def inputs_released(self, stream=None) -> None:
+        """Overlap mode: order ``stream`` after the last step's last read of its inputs
+        (bx_engine_inputs_released) — before refilling a reused input buffer in place."""
+        if stream is None:
+            stream = _current_stream()
+        N.check(self._L.bx_engine_inputs_released(self._h, stream), "bx_engine_inputs_released")
+
+    def lap_ties(self, seq0: int = 0, nseq: int | None = None) -> int:
+        """Associations re-solved by lapx's lapjv because their optimum was tied
+        (bx_engine_lap_ties_host), summed over sequences [seq0, seq0+nseq)."""
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        t = C.c_int64(0)
+        N.check(self._L.bx_engine_lap_ties_host(self._h, seq0, nseq, C.byref(t)), "lap_ties")
+        return int(t.value)
 
     def update_host(self, seq: int, dets: np.ndarray, embs: np.ndarray | None = None,
                     warp: np.ndarray | None = None) -> np.ndarray:
@@ -119,7 +138,9 @@ class Engine:
     def update_classes_host(self, seq: int, dets: np.ndarray, embs: np.ndarray | None = None,
                             warp: np.ndarray | None = None, n_classes: int = 80) -> np.ndarray:
         """per_class=True frame of one sequence (bx_engine_update_classes_host): one update per
-        class id on that class's detections, active lists per class, lost list shared."""
+        class id on that class's detections, active lists per class, lost list shared.  ``warp``:
+        None, one 2x3 warp for every class call, or [n_classes, 2, 3] — the reference calls
+        cmc.apply once per class call (botsort.py:218)."""
         d = np.ascontiguousarray(dets, dtype=np.float32).reshape(-1, 6)
         n = d.shape[0]
         e = None
@@ -130,7 +151,7 @@ class Engine:
             e = np.ascontiguousarray(embs, dtype=np.float64 if self.emb_f64 else np.float32)
             if e.shape != (n, self.emb_dim):
                 raise ValueError(f"embs shape {e.shape} != ({n}, {self.emb_dim})")
-        w = None if warp is None else np.ascontiguousarray(warp, np.float64).reshape(6)
+        w = _class_warps(warp, n_classes)
         out = np.empty((max(n, 1), 8), np.float64)
         m = C.c_int(0)
         N.check(self._L.bx_engine_update_classes_host(
@@ -157,6 +178,9 @@ class Engine:
         """Leave each step's feature EMA (K5) unjoined on the side stream (bx_engine_set_overlap):
         the caller keeps a step's input tensors unmodified until the next step is enqueued."""
         N.check(self._L.bx_engine_set_overlap(self._h, int(bool(on))), "bx_engine_set_overlap")
+        self._overlap = bool(on)
+        if not on:
+            self._inflight = None
 
     def probe_read(self):
         """(total ms, launches) of the probed stage since the last read."""
@@ -209,6 +233,18 @@ class Engine:
         N.check(self._L.bx_engine_state_set_host(self._h, seq, n, ids.ctypes.data, _p(m), _p(c)),
                 "state_set")
 
+
+
+def _class_warps(warp, n_classes: int):
+    """Per-class-call warps as the C ABI takes them: [n_classes][6] float64 or None."""
+    if warp is None:
+        return None
+    w = np.asarray(warp, np.float64)
+    if w.size == 6:
+        w = np.broadcast_to(w.reshape(1, 6), (int(n_classes), 6))
+    if w.shape[0] != int(n_classes) or w.size != 6 * int(n_classes):
+        raise ValueError(f"warps must be one 2x3 warp or [n_classes, 2, 3], got {w.shape}")
+    return np.ascontiguousarray(w.reshape(int(n_classes), 6))
 
 
 def _state_arrays(ids, a, b, na, nb):
@@ -478,7 +514,7 @@ class BoostEngine:
             e = np.ascontiguousarray(embs, dtype=np.float64).reshape(n, -1)
             if e.shape[1] != self.emb_dim:
                 raise ValueError(f"embedding dim {e.shape[1]} != engine emb_dim {self.emb_dim}")
-        w = None if warp is None else np.ascontiguousarray(warp, np.float64).reshape(6)
+        w = _class_warps(warp, n_classes)
         out = np.empty((max(n, 1), 8), np.float64)
         m = C.c_int(0)
         N.check(self._L.bx_boost_update_classes_host(

@@ -24,7 +24,8 @@ from dataclasses import dataclass
 
 import numpy as np
 
-__all__ = ["SyntheticScene", "SyntheticCMC", "TorchSceneBatch", "load_mot_dets", "synth_warp"]
+__all__ = ["SyntheticScene", "SyntheticCMC", "StatefulCMC", "TorchSceneBatch", "load_mot_dets",
+           "synth_warp"]
 
 
 @dataclass
@@ -42,6 +43,9 @@ class SyntheticScene:
     emb_dtype: type = np.float32
     classes: tuple = ()  # per-identity class ids (identity k -> classes[k % len]); () = class 0
     corner: tuple = ()  # layout "corner": (width, a) of the objects parked at the top-left corner
+    # every k-th detection is emitted twice (identical row and embedding, the copy right after
+    # it) — a detector without NMS; the duplicates tie the linear assignment (0 = off)
+    dup_every: int = 0
 
     def __post_init__(self):
         rng = np.random.default_rng([self.seed, 0x5CE7E])
@@ -107,6 +111,12 @@ class SyntheticScene:
             )
             e /= np.linalg.norm(e, axis=1, keepdims=True)
             embs = e.astype(self.emb_dtype)
+        if self.dup_every > 0 and m:
+            rep = np.ones(m, np.int64)
+            rep[:: self.dup_every] = 2
+            order = np.repeat(np.arange(m), rep)
+            dets, ids = dets[order], ids[order]
+            embs = embs[order] if embs is not None else None
         return dets, embs, ids
 
 
@@ -136,6 +146,24 @@ class SyntheticCMC:
     def apply(self, img, dets=None):
         w = self.warps(self.t) if callable(self.warps) else self.warps[self.t]
         return np.array(w, np.float64).reshape(2, 3)
+
+
+class StatefulCMC(SyntheticCMC):
+    """ECC-like state (``motion/cmc/ecc.py`` keeps the previous frame): the first ``apply`` of a
+    frame returns that frame's warp, every later call on the same frame compares the image with
+    itself and returns the identity.  Under ``per_class=True`` the reference calls ``apply`` once
+    per class call (basetracker.py:175-189 -> botsort.py:218 / boosttrack.py:244), so only class
+    0 sees the real inter-frame warp."""
+
+    def __init__(self, warps):
+        super().__init__(warps)
+        self._last = None
+
+    def apply(self, img, dets=None):
+        if self._last == self.t:
+            return np.eye(2, 3)
+        self._last = self.t
+        return super().apply(img, dets)
 
 
 class TorchSceneBatch:

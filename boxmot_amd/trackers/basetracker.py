@@ -12,6 +12,30 @@ from __future__ import annotations
 import numpy as np
 
 
+def _with_index(dets: np.ndarray) -> np.ndarray:
+    """dets with the detection-index column the reference appends before its CMC call
+    (botsort.py:169, boosttrack.py:239)."""
+    d = np.asarray(dets).reshape(-1, np.asarray(dets).shape[-1] if np.asarray(dets).ndim else 6)
+    return np.hstack([d, np.arange(len(d)).reshape(-1, 1)])
+
+
+def _reshape_warp(w) -> np.ndarray:
+    return np.asarray(w, np.float64).reshape(2, 3)
+
+
+def class_warps(cmc, img, dets: np.ndarray, nr_classes: int, conv=_reshape_warp) -> np.ndarray:
+    """The warps of one frame's class calls under per_class=True: the reference calls
+    ``cmc.apply(img, class_dets)`` once per class id (basetracker.py:175-189 ->
+    botsort.py:218 / boosttrack.py:243-246), class_dets = dets[dets[:, 5] == c]
+    (get_class_dets_n_embs, basetracker.py:83-106).  Returns [nr_classes, 2, 3]."""
+    d = np.asarray(dets)
+    d = d.reshape(-1, 6) if d.size else np.empty((0, 6))
+    out = np.empty((int(nr_classes), 2, 3), np.float64)
+    for c in range(int(nr_classes)):
+        out[c] = conv(cmc.apply(img, _with_index(d[d[:, 5] == c])))
+    return out
+
+
 class TrackView:
     """Read-only host view of one engine track (what ``active_tracks`` entries expose)."""
 

@@ -20,7 +20,17 @@ from __future__ import annotations
 import numpy as np
 
 from ..engine import BoostEngine, BoostParams
-from .basetracker import BaseTracker
+from .basetracker import BaseTracker, _with_index, class_warps
+
+
+def _boost_warp(w) -> np.ndarray:
+    """camera_update's transform (boosttrack.py:243-246): a 2x3 or 3x3 affine, as 2x3."""
+    w = np.asarray(w, np.float64)
+    if w.shape == (3, 3):
+        w = w[:2]
+    if w.shape != (2, 3):
+        raise ValueError(f"Expected 2x3 or 3x3 matrix, got {w.shape}")
+    return w
 
 
 class IdentityCMC:
@@ -92,7 +102,13 @@ class BoostTrack(BaseTracker):
         if self.engine is None:  # with_reid: the embedding dimension arrives with the first frame
             if embs is None or not len(dets):
                 # nothing can be associated before the first embeddings; the reference's
-                # frame counter still advances
+                # frame counter still advances and its CMC still sees the frame (a stateful CMC
+                # keeps it as the previous image), with no tracker to warp
+                if self.cmc is not None:
+                    if self.per_class:
+                        class_warps(self.cmc, img, dets, self.nr_classes, _boost_warp)
+                    else:
+                        self.cmc.apply(img, _with_index(dets))
                 self.frame_count += 1
                 self._pending_frames = getattr(self, "_pending_frames", 0) + 1
                 return np.empty((0, 8))
@@ -104,16 +120,16 @@ class BoostTrack(BaseTracker):
             self.engine.set_id_count(0, BoostTrack._id_count)
         self.frame_count += 1
         warp = None
-        if self.cmc is not None:
-            warp = np.asarray(self.cmc.apply(img, dets), np.float64)
-            if warp.shape == (3, 3):
-                warp = warp[:2]
-            if warp.shape != (2, 3):
-                raise ValueError(f"Expected 2x3 or 3x3 matrix, got {warp.shape}")
         if self.per_class:  # every class call sees every track (D10; basetracker.py:155-201)
-            out = self.engine.update_classes_host(0, dets, embs if self.with_reid else None, warp,
-                                                  n_classes=self.nr_classes)
+            # cmc.apply runs once per class call (boosttrack.py:243-246), each warp applied to
+            # every tracker
+            warps = None if self.cmc is None else class_warps(self.cmc, img, dets,
+                                                              self.nr_classes, _boost_warp)
+            out = self.engine.update_classes_host(0, dets, embs if self.with_reid else None,
+                                                  warps, n_classes=self.nr_classes)
         else:
+            if self.cmc is not None:
+                warp = _boost_warp(self.cmc.apply(img, _with_index(dets)))
             out = self.engine.update_host(0, dets, embs if self.with_reid else None, warp)
         self._engine_ids = BoostTrack._id_count = self.engine.counters(0)["id_count"]
         return out if out.shape[0] else np.empty((0, 8))

@@ -13,7 +13,7 @@ from __future__ import annotations
 import numpy as np
 
 from ..engine import Engine, EngineParams
-from .basetracker import BaseTracker
+from .basetracker import BaseTracker, _with_index, class_warps
 
 
 class IdentityCMC:
@@ -76,13 +76,15 @@ class BotSort(BaseTracker):
             else:
                 self.engine = self._make_engine(embs.shape[1], embs.dtype == np.float64)
         self.frame_count += 1
-        warp = np.asarray(self.cmc.apply(img, dets), np.float64).reshape(2, 3)
-        warp = None if np.array_equal(warp, np.eye(2, 3)) else warp
         if self.per_class:  # one update per class id, lost list shared (basetracker.py:155-201)
-            # (the reference's cmc.apply runs once per class call on the frame's image; the warp
-            # object here is per frame, so every class call applies the same warp)
+            # the reference's cmc.apply runs once per class call (botsort.py:218) on the class's
+            # detections: a stateful CMC (ECC keeps the previous frame) gives class 0 the frame's
+            # warp and the identity to the later calls
+            warps = class_warps(self.cmc, img, dets, self.nr_classes)
             return self.engine.update_classes_host(0, dets, embs if self.with_reid else None,
-                                                   warp, n_classes=self.nr_classes)
+                                                   warps, n_classes=self.nr_classes)
+        warp = np.asarray(self.cmc.apply(img, _with_index(dets)), np.float64).reshape(2, 3)
+        warp = None if np.array_equal(warp, np.eye(2, 3)) else warp
         out = self.engine.update_host(0, dets, embs if self.with_reid else None, warp)
         return out if out.shape[0] else np.asarray([])
 

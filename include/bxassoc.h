@@ -107,6 +107,10 @@ int bx_engine_step(bx_engine *e, int seq0, int nseq, const float *dets, const in
  * hipDeviceSynchronize covers it.  Saves the join and lets the next frame's K1 start as soon as
  * K5 ends instead of after the caller's stream drains. */
 int bx_engine_set_overlap(bx_engine *e, int on);
+/* Overlap mode: make `stream` wait (stream-ordered, no host sync) until the last step's inputs
+ * are no longer read — call it before refilling a reused dets / det_off / embs buffer on
+ * `stream`.  A no-op when nothing is pending. */
+int bx_engine_inputs_released(bx_engine *e, void *stream);
 
 /* Host-memory convenience for one sequence (the drop-in `update` path): copies in, launches,
  * copies out and synchronises.  dets [n][6] float32; embs [n][emb_dim] or NULL; warp [6] or
@@ -119,9 +123,12 @@ int bx_engine_update_host(bx_engine *e, int seq, const float *dets, int n, const
  * detections whose float32 class equals it (det_ind then indexes that subset, as in the
  * reference), each with the class's own active list while the lost list and the id counter stay
  * shared, and the frame counter held across the frame's class calls; rows stacked in class
- * order.  Arguments as bx_engine_update_host; n_classes must stay the same for an engine. */
+ * order.  Arguments as bx_engine_update_host except warps: [n_classes][6] float64, the warp of
+ * each class call (the reference calls cmc.apply once per class call, botsort.py:218, so a
+ * stateful CMC such as ECC returns the inter-frame warp to class 0 only), or NULL = identity;
+ * n_classes must stay the same for an engine. */
 int bx_engine_update_classes_host(bx_engine *e, int seq, const float *dets, int n,
-                                  const void *embs, const double *warp, int n_classes,
+                                  const void *embs, const double *warps, int n_classes,
                                   double *out, int *n_out, void *stream);
 
 /* Stage timing probe (benchmarks): while enabled, bx_engine_step records a HIP event pair
@@ -139,6 +146,9 @@ int bx_engine_probe(bx_engine *e, int stage);
  * gated (track, det) pairs, frame counter} — the unit counts bench.py prices bytes with. */
 int bx_engine_frame_stats_host(bx_engine *e, int seq0, int nseq, int64_t *sums);
 int bx_engine_probe_read(bx_engine *e, double *total_ms, int *count);
+/* Associations of sequences [seq0, seq0+nseq) whose optimum was tied and that were therefore
+ * re-solved by lapx's own lapjv (see bx_linear_assignment), summed since creation / reset. */
+int bx_engine_lap_ties_host(bx_engine *e, int seq0, int nseq, int64_t *total);
 
 /* Latched device-side status of the whole engine (BX_OK or BX_ERR_TRACK_OVERFLOW). */
 int bx_engine_status(bx_engine *e, int *status);
@@ -189,8 +199,6 @@ int bx_kf_update(int kind, int n, double *mean, double *cov, const double *z, co
                  void *stream);
 int bx_kf_gating_distance(int kind, int n, const double *mean, const double *cov,
                           const double *z, int nz, double *out, void *stream);
-/* lapx extend_cost + cost_limit semantics on a dense [nr][nc] cost: x [nr] (col or -1),
- * y [nc] (row or -1); matches are the pairs with x>=0 (all have cost < thresh). */
 /* StrongSort appearance metric (NearestNeighborDistanceMetric.distance with the cosine metric,
  * trackers/strongsort/sort/linear_assignment.py:468-497,595-618): samples [G][F] float64 is every
  * target's gallery packed by target (target t owns rows off[t]..off[t+1], off [T+1] int32 on the
@@ -201,13 +209,25 @@ int bx_kf_gating_distance(int kind, int n, const double *mean, const double *cov
 #define BX_NN_SAMPLES_NORMALIZED 1
 int bx_nn_cosine_distance(const double *samples, int G, const int32_t *off, int T,
                           const double *feats, int D, int F, int flags, double *out, void *stream);
+/* matching.enhanced_linear_assignment (matching.py:30-61: lap.lapjv(cost, extend_cost=True,
+ * cost_limit=thresh), matches = rows with x >= 0 and cost <= thresh) on a dense [nr][nc] cost:
+ * x [nr] = matched column, -1 = unmatched (in unmatched_a); y [nc] likewise.  Solved sparse (exact
+ * shortest augmenting paths over the admissible pairs); when the optimal pair set is not unique
+ * the problem is re-solved by lapx's own lapjv on the (nr+nc)^2 extension so ties resolve as
+ * lapx's do.  -3 marks a row/column lapx assigned to a real partner above thresh (possible only
+ * within rounding of a tie at thresh): the reference neither matches it nor lists it unmatched.
+ * nr, nc <= 8192.  bx_linear_assignment_ex also writes tied[0] (device) = 1 when the lapx
+ * re-solve ran, else 0. */
 int bx_linear_assignment(const double *cost, int nr, int nc, double thresh, int32_t *x,
                          int32_t *y, void *stream);
+int bx_linear_assignment_ex(const double *cost, int nr, int nc, double thresh, int32_t *x,
+                            int32_t *y, int32_t *tied, void *stream);
 /* lapx 0.5.11 lapjv(cost, extend_cost, cost_limit) on a dense [nr][nc] float64 cost, solved by
  * lapx's algorithm (_ccrrt_dense, two _carr_dense passes, _ca_dense) on one wave, so tied
  * problems return lapx's optimum.  cost_limit = +inf for none (then nr == nc unless
  * extend_cost).  x [nr] = column or -1, y [nc] = row or -1 (lapx's post-processing when
- * extended).  The (possibly extended) size must be <= 512.  BX_ERR_INVALID carries lapx's
+ * extended).  The (possibly extended) size must be <= 32768 (state in LDS up to ~4k, else in
+ * global memory).  BX_ERR_INVALID carries lapx's
  * ValueError text for a non-square cost without extend_cost. */
 int bx_lapjv(const double *cost, int nr, int nc, int extend_cost, double cost_limit, int32_t *x,
              int32_t *y, void *stream);

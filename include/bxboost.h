@@ -79,9 +79,10 @@ int bx_boost_update_host(bx_boost *e, int seq, const float *dets, int n, const d
  * id 0..n_classes-1 on that class's detections with the frame counter held, rows stacked in class
  * order (det_ind indexes the class's subset).  BoostTrack keeps its tracks outside the swapped
  * active_tracks, so every class call sees every track.  Arguments as
- * bx_boost_update_host. */
+ * bx_boost_update_host except warps: [n_classes][6] float64, the camera_update warp of each class
+ * call (boosttrack.py:243-246 calls cmc.apply per class call), or NULL = no CMC. */
 int bx_boost_update_classes_host(bx_boost *e, int seq, const float *dets, int n,
-                                 const double *embs, const double *warp, int n_classes,
+                                 const double *embs, const double *warps, int n_classes,
                                  double *out, int *n_out, void *stream);
 /* Op-level BoostTrack filter (device arrays, async on `stream`), the frame kernel's octet code.
  * x [n][8], P [n][8][8] row-major, z [n][4] = convert_bbox_to_z (x, y, h, w/(h+1e-6)).

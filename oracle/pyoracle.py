@@ -438,11 +438,16 @@ class OracleTracker:
         return self._update_one(dets, embs, warp)
 
     def _update_per_class(self, dets, embs, warp):
+        """``warp``: None, one 2x3 warp for every class call, or [NR_CLASSES, 2, 3] — one per
+        class call, as the reference calls cmc.apply in each (botsort.py:218,
+        boosttrack.py:243-246)."""
         L = lib()
         dets = np.asarray(dets, np.float64).reshape(-1, 6)
         fc = self._frame
         outs = []
+        wall = None if warp is None else np.asarray(warp, np.float64)
         for c in range(NR_CLASSES):
+            warp = None if wall is None else (wall[c] if wall.ndim == 3 else wall)
             idx = np.flatnonzero(dets[:, 5].astype(np.float32) == c)
             cd = dets[idx]
             ce = None if embs is None else np.asarray(embs)[idx]

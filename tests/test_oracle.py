@@ -137,6 +137,16 @@ def test_lapx_lapjv_ties_optimal():
             assert got == best, (trial, got, best)
 
 
+def test_linear_assignment_tie_order_is_lapx():
+    """lapx's _ccrrt_dense claims columns from j = n-1 down, so of two equal detections the
+    higher index wins (the cost_limit extension, matching.py:54-61); a cost exactly at the limit
+    ties matching with not matching and lapx keeps the pair (cost <= thresh)."""
+    m, ua, ub = po.linear_assignment(np.array([[0.3, 0.3]]), 0.8)
+    assert m.tolist() == [[0, 1]] and list(ub) == [0]
+    m, ua, ub = po.linear_assignment(np.array([[0.3], [0.3]]), 0.8)
+    assert m.shape == (1, 2)
+
+
 def test_linear_assignment_empty():
     m, ua, ub = po.linear_assignment(np.zeros((0, 3)), 0.5)
     assert m.shape == (0, 2) and ua.size == 0 and list(ub) == [0, 1, 2]
@@ -152,11 +162,15 @@ def test_linear_assignment_empty():
 def test_tracker_fixture(path):
     fx = np.load(path)
     kind, args = fixture_tracker_args(fx)
-    if kind not in ("ocsort", "boosttrack"):
+    if kind not in ("ocsort", "boosttrack") and "tie_order" not in fx.files:
         assert int(fx["lap_degenerate"]) == 0
+    if "tie_order" in fx.files:  # duplicate-detection captures: ties by design
+        assert int(fx["lap_degenerate"]) > 0
     # (OCSort's and BoostTrack's full-matching LAP (extend_cost, no cost_limit) can tie on
-    # zero-cost pairs; their fixtures were captured with the restated lapx JV resolving ties —
-    # make_golden.use_restated_lapx_jv)
+    # zero-cost pairs, and the ByteTrack / BoT-SORT duplicate-detection captures tie their
+    # cost_limit LAP; those fixtures were captured with the restated lapx JV resolving ties —
+    # make_golden.use_restated_lapx_jv — so their tie order is lapx's published algorithm as
+    # restated, parity with a lapx binary unpinned)
     tr = po.OracleTracker(kind, **args)
     rows = []
     for f, d, e in fixture_frames(fx):
