@@ -73,12 +73,22 @@ CONFIGS = {
         min_conf=0.1, max_cos_dist=0.15, max_iou_dist=0.7, max_age=50, n_init=2, nn_budget=150,
         mc_lambda=0.995, ema_alpha=0.9, conf_thresh_high=0.7, conf_thresh_low=0.3,
         id_preservation_weight=0.1, crowd_detection=True, born_confirmed=True)),
+    # C5 (BASELINE.json configs[4]): BoostTrack++ on 8 MOT17-ablation-like sequences sharded
+    # over the ranks (strong scaling of a fixed set): MOT17-02 / MOT17-04 public detections with
+    # identity-linked synthetic ReID + 6 synthetic 60-object sequences (SURVEY §8(d) stand-in)
+    "boosttrack_mot8": ("boosttrack", 60, 512, dict(
+        max_age=60, min_hits=3, det_thresh=0.6, iou_threshold=0.3, use_ecc=True,
+        min_box_area=10, aspect_ratio_thresh=1.6, lambda_iou=0.5, lambda_mhd=0.25,
+        lambda_shape=0.25, use_dlo_boost=True, use_duo_boost=True, dlo_boost_coef=0.65,
+        s_sim_corr=False, use_rich_s=True, use_sb=True, use_vt=True, with_reid=True)),
     "strongsort_c4": ("strongsort", 1024, 2048, dict(
         min_conf=0.1, max_cos_dist=0.15, max_iou_dist=0.7, max_age=50, n_init=2, nn_budget=150,
         mc_lambda=0.995, ema_alpha=0.9, conf_thresh_high=0.7, conf_thresh_low=0.3,
         id_preservation_weight=0.1, crowd_detection=True, born_confirmed=True)),
 }
 DEFAULT_SEQS = {"strongsort": 256, "strongsort_c4": 1}
+MOT_DETS = ROOT / "tests" / "golden" / "mot17_public_dets.npz"  # C5's real-data sequences
+C5_TOTAL = 8
 # StrongSort engine capacities (track slots, detections per frame, pool vectors per slot); the C4
 # ones are shared with tests/test_gpu_parity.py::test_strongsort_c4_size_vs_oracle
 SS_C4_CAPS = dict(track_cap=1024, det_cap=1024, vec_cap=64)
@@ -179,8 +189,27 @@ REFERENCE_CPU_FPS = {
 }
 
 
+def cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max / v1 cfs quota), or
+    None when unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return float(q) / float(per)
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return q / per if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def host_cpu():
-    """CPU model, logical CPUs of the machine and CPUs this process may run on."""
+    """CPU model, logical CPUs of the machine, CPUs this process may run on, and the cgroup's
+    CPU quota (the cores the baseline can actually use at once)."""
     model = "unknown"
     try:
         for ln in open("/proc/cpuinfo"):
@@ -193,7 +222,16 @@ def host_cpu():
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count() or 1
-    return {"model": model, "logical_cpus": os.cpu_count(), "usable_cpus": usable}
+    quota = cpu_quota()
+    cores = usable if quota is None else max(1, min(usable, int(quota)))
+    # the GPU pool grants each 1-GPU job a CPU share and exports it as OMP_NUM_THREADS (16);
+    # its rules ask worker pools to stay within that share, so the baseline does too
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        cores = min(cores, int(share))
+    return {"model": model, "logical_cpus": os.cpu_count(), "usable_cpus": usable,
+            "cgroup_cpu_quota": quota, "job_cpu_share": int(share) if share.isdigit() else None,
+            "cores": cores}
 
 
 def cpu_worker(spec):
@@ -204,11 +242,17 @@ def cpu_worker(spec):
 
     kind, n_obj, emb_dim, params = spec["kind"], spec["n_obj"], spec["emb_dim"], spec["params"]
     po.set_threads(spec.get("threads", 1))
-    extra = dict(conf_lo=OCS_CONF_LO) if kind in ("ocsort", "boosttrack", "strongsort") else {}
-    if kind in ("boosttrack", "strongsort"):
-        extra["emb_dtype"] = np.float64
-    sc = SyntheticScene(n_obj=n_obj, seed=spec["seed"], emb_dim=emb_dim,
-                        layout=spec.get("layout", "grid"), **extra)
+    if "c5" in spec:  # one of C5's eight sequences, played to its end at most
+        from boxmot_amd.synth import c5_sequences
+
+        _, sc, nf = c5_sequences(MOT_DETS, emb_dim)[spec["c5"]]
+        spec["max_frames"] = min(spec.get("max_frames", 1 << 30), nf - spec["warm"])
+    else:
+        extra = dict(conf_lo=OCS_CONF_LO) if kind in ("ocsort", "boosttrack", "strongsort") else {}
+        if kind in ("boosttrack", "strongsort"):
+            extra["emb_dtype"] = np.float64
+        sc = SyntheticScene(n_obj=n_obj, seed=spec["seed"], emb_dim=emb_dim,
+                            layout=spec.get("layout", "grid"), **extra)
     tr = po.OracleTracker(kind, **params)
     t = 0
     for _ in range(spec["warm"]):
@@ -249,20 +293,31 @@ def cpu_baseline(config, kind, n_obj, emb_dim, params, seconds=15.0):
     one thread, and one process per sequence on all usable cores (val.py:389's model; C4 is one
     sequence, so its all-cores variant is one process whose NN rows run on all cores)."""
     host = host_cpu()
-    P = max(1, min(16, host["usable_cpus"]))
+    P = host["cores"]  # every core the process may use at once (affinity, capped by the cgroup)
     c4 = config == "strongsort_c4"
     warm = 8 if c4 else 40
     base = dict(kind=kind, n_obj=n_obj, emb_dim=emb_dim, params=params, warm=warm,
                 layout="crowded" if config.endswith("_crowded") else "grid",
                 seconds=seconds, max_frames=6 if c4 else 1 << 30)
-    one = run_cpu_workers([dict(base, seed=12345, threads=1)])[0]
-    if c4:
+    c5 = config == "boosttrack_mot8"
+    if c5:  # the workload's own eight sequences, one process each (MOT17-04 for one thread)
+        one = run_cpu_workers([dict(base, seed=0, c5=1, threads=1)])[0]
+        many = run_cpu_workers([dict(base, seed=0, c5=k, threads=1) for k in range(C5_TOTAL)])
+    elif c4:
+        one = run_cpu_workers([dict(base, seed=12345, threads=1)])[0]
         many = run_cpu_workers([dict(base, seed=12345, threads=P)])
     else:
+        one = run_cpu_workers([dict(base, seed=12345, threads=1)])[0]
         many = run_cpu_workers([dict(base, seed=12345 + k, threads=1) for k in range(P)])
     fps1 = one["frames"] / one["busy"]
     fpsP = sum(r["frames"] / r["busy"] for r in many)
+    # sequences are independent and the oracle is single-threaded per sequence, so the whole
+    # machine's rate is the per-core rate times its usable CPUs (a projection, not a measurement)
+    proj = None if (c4 or c5) else round(fpsP / P * host["usable_cpus"], 1)
     what = (f"{n_obj} objects (~{n_obj // 2} dets/frame)" + (f" x {emb_dim}-d" if emb_dim else ""))
+    if c5:
+        P = min(P, C5_TOTAL)
+        what = "C5's 8 sequences (MOT17-02/04 public dets + 6 synthetic) x 512-d"
     ref = REFERENCE_CPU_FPS.get(config)
     return {
         "value": round(fpsP, 2), "unit": "frames/s", "cores": P, "kind": "port",
@@ -270,6 +325,9 @@ def cpu_baseline(config, kind, n_obj, emb_dim, params, seconds=15.0):
                    f" {P} cores; {what}; frames {warm + 1}..{many[0]['last']} per sequence, "
                    f"~{seconds:.0f}s busy each; oracle/ C fp64 port"),
         "host": host,
+        "projected_all_usable_cpus": None if proj is None else {
+            "value": proj, "cores": host["usable_cpus"],
+            "note": "measured per-core rate x usable CPUs (linear: one process per sequence)"},
         "single_thread": {"value": round(fps1, 2), "cores": 1,
                           "sample": f"1 sequence, frames {one['first']}..{one['last']} "
                                     f"({one['frames']} timed, {one['busy']:.1f}s)"},
@@ -389,6 +447,15 @@ def main():
 
     kind, n_obj, F, params = CONFIGS[args.config]
     S = args.seqs if args.seqs is not None else DEFAULT_SEQS.get(args.config, 1024)
+    c5 = args.config == "boosttrack_mot8"
+    if c5:  # a fixed set of 8 sequences, LPT-sharded by frame count (strong scaling)
+        from boxmot_amd.synth import c5_sequences
+
+        if world > C5_TOTAL:
+            raise SystemExit(f"boosttrack_mot8 has {C5_TOTAL} sequences: at most {C5_TOTAL} ranks")
+        c5seqs = c5_sequences(MOT_DETS, F)
+        c5_mine = shard_sequences([nf for _, _, nf in c5seqs], world, rank)
+        S = len(c5_mine)
     ocs = kind == "ocsort"
     bst = kind == "boosttrack"
     sss = kind == "strongsort"
@@ -415,14 +482,30 @@ def main():
                   if F or s not in ("det_features", "gate", "cosine", "features")]
     # this rank's shard: global sequences [rank*S, (rank+1)*S) — weak scaling, no exchange
     layout = "crowded" if args.config.endswith("_crowded") else "grid"
-    gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev, layout=layout,
-                          **(dict(conf_lo=OCS_CONF_LO) if ocs or bst or sss else {}))
     # W warm-up steps, then one untimed probe step per pipeline stage (each stage timed once
     # whatever W is), then the K timed steps
     n_probe = len(stages)
     t_first = args.warmup + n_probe
     total = t_first + args.steps
-    frames = [gen.frame(t) for t in range(1, total + 1)]  # resident in HBM before timing
+    if c5:
+        if total > min(c5seqs[g][2] for g in c5_mine):
+            raise SystemExit("boosttrack_mot8: warmup + probes + steps exceed the shortest "
+                             "sequence (600 frames)")
+
+        def c5_frame(t):
+            fr = [c5seqs[g][1].frame(t) for g in c5_mine]
+            off = np.zeros(S + 1, np.int32)
+            off[1:] = np.cumsum([f[0].shape[0] for f in fr])
+            d = np.concatenate([f[0] for f in fr], 0).astype(np.float32)
+            e = np.concatenate([f[1] for f in fr], 0).astype(np.float64)
+            return (torch.from_numpy(d).to(dev), torch.from_numpy(off).to(dev),
+                    torch.from_numpy(e).to(dev))
+        frames = [c5_frame(t) for t in range(1, total + 1)]  # resident in HBM before timing
+        layout = "MOT17-02/04 public dets + synthetic"
+    else:
+        gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev, layout=layout,
+                              **(dict(conf_lo=OCS_CONF_LO) if ocs or bst or sss else {}))
+        frames = [gen.frame(t) for t in range(1, total + 1)]  # resident in HBM before timing
     if bst:  # BoostTrack consumes float64 embeddings (the dtype `boxmot eval` loads)
         frames = [(d, o, e.double()) for d, o, e in frames]
     if sss:  # StrongSort: float64 detections (no setup_decorator rounding) and embeddings
@@ -495,7 +578,7 @@ def main():
     dets_seq = np.sum([np.diff(o) for o in off_h], 0)
     last_off, cnt_h, out_h = off_h[-1], cnt.cpu().numpy(), out.cpu().numpy()
     recs = np.zeros((S, 7))
-    for i, g in enumerate(shard_sequences(S * world, world, rank)):
+    for i, g in enumerate(c5_mine if c5 else shard_sequences(S * world, world, rank)):
         rows_i = out_h[last_off[i]: last_off[i] + cnt_h[i]]
         recs[i] = [g, args.steps, dets_seq[i], cnt_h[i], output_checksum(rows_i), wall, dom_ms]
     # RCCL over xGMI only to gather these KB-scale records once, never per frame
@@ -504,7 +587,8 @@ def main():
     total_frames = float(allrec[:, 1].sum())
     value = total_frames / t_max
     if rank == 0:
-        assert np.array_equal(np.sort(allrec[:, 0]), np.arange(S * world)), "shard gather"
+        n_all = C5_TOTAL if c5 else S * world
+        assert np.array_equal(np.sort(allrec[:, 0]), np.arange(n_all)), "shard gather"
         mean_d = float(allrec[:, 2].sum() / allrec[:, 1].sum())
         if ocs:
             per_launch = (units["tracks"] * OCS_TRACK_BYTES + units["dets"] * 24 +
@@ -531,10 +615,16 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_max / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": f"synthetic (GPU-generated {layout} scenes, resident in HBM before timing)",
-            "config": {"workload": f"{args.config}: {S} sequences/GPU x {n_obj} tracks x "
-                                   f"~{mean_d:.0f} dets" + (f" x {F}-d ReID" if F else ""),
+            "scaling": "strong" if c5 else "weak", "vs_baseline": None, "dtype": "f64",
+            "data": ("MOT17-02/04 public detections (tests/golden/mot17_public_dets.npz) with "
+                     "identity-linked synthetic ReID + 6 synthetic sequences, resident in HBM "
+                     "before timing" if c5 else
+                     f"synthetic (GPU-generated {layout} scenes, resident in HBM before timing)"),
+            "config": {"workload": (f"{args.config}: 8 sequences (MOT17-02, MOT17-04, 6 synthetic"
+                                    f" 60-object) sharded over {world} GPU(s), {S} on rank 0, "
+                                    f"~{mean_d:.0f} dets x {F}-d ReID" if c5 else
+                                    f"{args.config}: {S} sequences/GPU x {n_obj} tracks x "
+                                    f"~{mean_d:.0f} dets" + (f" x {F}-d ReID" if F else "")),
                        "tracker": kind, "n_seq_per_gpu": S, "n_tracks": n_obj,
                        "n_dets_mean": round(mean_d, 1), "feat_dim": F,
                        "emb_dtype": "f64" if emb_bytes == 8 else "f32",

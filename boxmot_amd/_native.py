@@ -119,6 +119,8 @@ EXPORTS = [
     "bx_iou_batch", "bx_pairwise_cost", "bx_aw_max_metric", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
     "bx_kf_multi_predict", "bx_kf_update", "bx_kf_gating_distance", "bx_linear_assignment", "bx_lapjv",
     "bx_linear_assignment_ex", "bx_engine_lap_ties_host", "bx_engine_inputs_released",
+    "bx_engine_copy_state", "bx_engine_slots_used_host", "bx_ocsort_copy_state",
+    "bx_boost_copy_state", "bx_ss_copy_state",
     "bx_nn_cosine_distance", "bx_ocsort_create", "bx_ocsort_destroy", "bx_ocsort_reset", "bx_ocsort_step",
     "bx_ocsort_update_host", "bx_ocsort_status", "bx_ocsort_counters_host",
     "bx_ocsort_set_id_count", "bx_ocsort_set_frame_size", "bx_ocsort_tracks_host", "bx_ocsort_probe", "bx_ocsort_probe_read",
@@ -173,6 +175,11 @@ _SIGS = {
     "bx_linear_assignment_ex": ([_vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp, _vp], C.c_int),
     "bx_engine_lap_ties_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_engine_inputs_released": ([_vp, _vp], C.c_int),
+    "bx_engine_copy_state": ([_vp, _vp], C.c_int),
+    "bx_ocsort_copy_state": ([_vp, _vp], C.c_int),
+    "bx_boost_copy_state": ([_vp, _vp], C.c_int),
+    "bx_ss_copy_state": ([_vp, _vp], C.c_int),
+    "bx_engine_slots_used_host": ([_vp, C.c_int, _ip], C.c_int),
     "bx_lapjv": ([_vp, C.c_int, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp], C.c_int),
     "bx_nn_cosine_distance": ([_vp, C.c_int, _vp, C.c_int, _vp, C.c_int, C.c_int, C.c_int, _vp,
                                _vp], C.c_int),

@@ -1276,6 +1276,29 @@ int bx_boost_create(const bx_boost_config* c, bx_boost** out) {
   return BX_OK;
 }
 
+int bx_boost_copy_state(bx_boost* dst, bx_boost* src) {
+  if (!dst || !src) return bx_record_error(BX_ERR_INVALID, "null engine");
+  const BstDev &a = src->dev, &b = dst->dev;
+  if (a.S != b.S || a.reid != b.reid || a.F != b.F || b.T < a.T || b.D < a.D)
+    return bx_record_error(BX_ERR_INVALID, "bx_boost_copy_state: destination must match the "
+                                           "source's sequences and ReID and have at least its "
+                                           "capacities");
+  BCHK(hipDeviceSynchronize());
+  const size_t S = a.S, Ta = a.T, Tb = b.T, F = a.F;
+  BCHK(hipMemcpy2D(b.trk, Tb * sizeof(BstTrk), a.trk, Ta * sizeof(BstTrk), Ta * sizeof(BstTrk), S,
+                   hipMemcpyDeviceToDevice));
+  BCHK(hipMemcpy2D(b.order, Tb * sizeof(int), a.order, Ta * sizeof(int), Ta * sizeof(int), S,
+                   hipMemcpyDeviceToDevice));
+  if (a.reid && F)
+    BCHK(hipMemcpy2D(b.emb, Tb * F * sizeof(double), a.emb, Ta * F * sizeof(double),
+                     Ta * F * sizeof(double), S, hipMemcpyDeviceToDevice));
+  BCHK(hipMemcpy(b.seqst, a.seqst, S * SQB * sizeof(int), hipMemcpyDeviceToDevice));
+  BCHK(hipMemcpy(b.status, a.status, 4 * sizeof(int), hipMemcpyDeviceToDevice));
+  dst->cache_seq = -1;
+  BCHK(hipDeviceSynchronize());
+  return BX_OK;
+}
+
 int bx_boost_destroy(bx_boost* e) {
   if (!e) return BX_OK;
   for (auto& p : e->ev) {

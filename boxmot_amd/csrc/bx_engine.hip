@@ -2479,6 +2479,92 @@ int bx_engine_set_overlap(bx_engine* e, int on) {
   return BX_OK;
 }
 
+// copy S rows of `row_bytes` (src pitch sp, dst pitch dp) — a per-slot array [S][T][...] into a
+// larger [S][T'][...]
+static int copy_rows(void* dst, size_t dp, const void* src, size_t sp, size_t row_bytes, int S) {
+  if (!row_bytes || !S) return BX_OK;
+  HIPCHK(hipMemcpy2D(dst, dp, src, sp, row_bytes, S, hipMemcpyDeviceToDevice));
+  return BX_OK;
+}
+
+int bx_engine_copy_state(bx_engine* dst, bx_engine* src) {
+  if (!dst || !src) return set_err(BX_ERR_INVALID, "null engine");
+  if (int rc = settle(src)) return rc;
+  if (int rc = settle(dst)) return rc;
+  const Dev &a = src->dev, &b = dst->dev;
+  if (a.S != b.S || a.kind != b.kind || a.F != b.F || a.emb_f64 != b.emb_f64 ||
+      a.with_reid != b.with_reid || b.T < a.T || b.D < a.D)
+    return set_err(BX_ERR_INVALID,
+                   "bx_engine_copy_state: destination must match the source's sequences, kind and "
+                   "features and have at least its capacities");
+  std::lock_guard<std::recursive_mutex> l1(src->mu), l2(dst->mu);
+  HIPCHK(hipDeviceSynchronize());
+  const int S = a.S;
+  const size_t Ta = a.T, Tb = b.T, fs = a.emb_f64 ? 8 : 4;
+  auto rows = [&](void* d, const void* s_, size_t per_slot) {
+    return copy_rows(d, Tb * per_slot, s_, Ta * per_slot, Ta * per_slot, S);
+  };
+  int rc = BX_OK;
+  const std::pair<std::pair<void*, const void*>, size_t> slot_arrays[] = {
+      {{b.act, a.act}, 2}, {{b.lost, a.lost}, 2}, {{b.act2, a.act2}, 2},
+      {{b.lost2, a.lost2}, 2}, {{b.flags, a.flags}, 4}, {{b.frame_id, a.frame_id}, 4},
+      {{b.start, a.start}, 4}, {{b.id, a.id}, 4}, {{b.tlen, a.tlen}, 4},
+      {{b.detind, a.detind}, 4}, {{b.conf, a.conf}, 8}, {{b.cls, a.cls}, 8},
+      {{b.kf, a.kf}, 8 * KF_STRIDE}, {{b.clsh, a.clsh}, 8 * CLS_HIST * 2}, {{b.ncls, a.ncls}, 4},
+  };
+  for (auto& x : slot_arrays)
+    if ((rc = rows(x.first.first, x.first.second, x.second))) return rc;
+  if (a.with_reid) {
+    if ((rc = rows(b.feat, a.feat, fs * a.F))) return rc;
+    if ((rc = rows(b.tdn, a.tdn, 4))) return rc;
+  }
+  HIPCHK(hipMemcpy(b.seq, a.seq, sizeof(int) * SQ_STRIDE * S, hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(b.npair, a.npair, sizeof(int) * S, hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(b.status, a.status, sizeof(int) * 16, hipMemcpyDeviceToDevice));
+  dst->overlap = src->overlap;
+  dst->cache_seq = -1;
+  // per_class state: parked class lists [C][T] (+ their lengths and the held frame counter)
+  if (src->n_classes) {
+    const int C = src->n_classes;
+    if (dst->n_classes && dst->n_classes != C)
+      return set_err(BX_ERR_INVALID, "bx_engine_copy_state: n_classes differs");
+    if (!dst->n_classes) {
+      dst->n_classes = C;
+      dst->park.assign(S, nullptr);
+      dst->cur_cls.assign(S, 0);
+      HIPCHK(hipMalloc(&dst->h_coff, sizeof(int) * 2 * C));
+      HIPCHK(hipMalloc(&dst->h_ccnt, sizeof(int) * C));
+      HIPCHK(hipMalloc(&dst->h_cwarp, sizeof(double) * 6 * C));
+    }
+    for (int q = 0; q < S; q++) {
+      dst->cur_cls[q] = src->cur_cls[q];
+      if (!src->park[q]) continue;
+      if (!dst->park[q]) {
+        const size_t bytes = park_npark_off(dst) + sizeof(int) * (C + 1);
+        HIPCHK(hipMalloc(&dst->park[q], bytes));
+        HIPCHK(hipMemset(dst->park[q], 0, bytes));
+      }
+      if ((rc = copy_rows(dst->park[q], Tb * 2, src->park[q], Ta * 2, Ta * 2, C))) return rc;
+      HIPCHK(hipMemcpy(dst->park[q] + park_npark_off(dst), src->park[q] + park_npark_off(src),
+                       sizeof(int) * (C + 1), hipMemcpyDeviceToDevice));
+    }
+  }
+  HIPCHK(hipDeviceSynchronize());
+  return BX_OK;
+}
+
+int bx_engine_slots_used_host(bx_engine* e, int seq, int* used) {
+  if (int rc = settle(e)) return rc;
+  if (!e || !used || seq < 0 || seq >= e->dev.S) return set_err(BX_ERR_INVALID, "bad sequence");
+  std::vector<uint32_t> f(e->dev.T);
+  HIPCHK(hipMemcpy(f.data(), e->dev.flags + (size_t)seq * e->dev.T, sizeof(uint32_t) * f.size(),
+                   hipMemcpyDeviceToHost));
+  int n = 0;
+  for (uint32_t x : f) n += (x & F_INUSE) != 0;
+  *used = n;
+  return BX_OK;
+}
+
 int bx_engine_inputs_released(bx_engine* e, void* stream) {
   if (!e) return set_err(BX_ERR_INVALID, "null engine");
   std::lock_guard<std::recursive_mutex> lk(e->mu);

@@ -1122,6 +1122,29 @@ int bx_ocsort_create(const bx_ocsort_config* c, bx_ocsort** out) {
   return BX_OK;
 }
 
+int bx_ocsort_copy_state(bx_ocsort* dst, bx_ocsort* src) {
+  if (!dst || !src) return bx_record_error(BX_ERR_INVALID, "null engine");
+  const OcsDev &a = src->dev, &b = dst->dev;
+  if (a.S != b.S || b.T < a.T || b.D < a.D)
+    return bx_record_error(BX_ERR_INVALID, "bx_ocsort_copy_state: destination must have the "
+                                           "source's sequences and at least its capacities");
+  OCHK(hipDeviceSynchronize());
+  const size_t S = a.S, Ta = a.T, Tb = b.T;
+  // per-slot records [S][T] and the list order [S][T]; per-sequence scalars and frame sizes
+  OCHK(hipMemcpy2D(b.trk, Tb * sizeof(OcsTrk), a.trk, Ta * sizeof(OcsTrk), Ta * sizeof(OcsTrk), S,
+                   hipMemcpyDeviceToDevice));
+  OCHK(hipMemcpy2D(b.order, Tb * sizeof(int), a.order, Ta * sizeof(int), Ta * sizeof(int), S,
+                   hipMemcpyDeviceToDevice));
+  OCHK(hipMemcpy(b.seqst, a.seqst, S * SQO * sizeof(int), hipMemcpyDeviceToDevice));
+  OCHK(hipMemcpy(b.fsz, a.fsz, S * 2 * sizeof(double), hipMemcpyDeviceToDevice));
+  OCHK(hipMemcpy(b.status, a.status, 4 * sizeof(int), hipMemcpyDeviceToDevice));
+  dst->gid = src->gid;
+  dst->lids = src->lids;
+  dst->cache_seq = -1;
+  OCHK(hipDeviceSynchronize());
+  return BX_OK;
+}
+
 int bx_ocsort_destroy(bx_ocsort* e) {
   if (!e) return BX_OK;
   for (auto& p : e->ev) {

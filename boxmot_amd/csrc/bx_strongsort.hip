@@ -2840,6 +2840,41 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   return BX_OK;
 }
 
+int bx_ss_copy_state(bx_ss* dst, bx_ss* src) {
+  if (!dst || !src) return bx_record_error(BX_ERR_INVALID, "null engine");
+  const SsDev &a = src->dev, &b = dst->dev;
+  if (a.S != b.S || a.F != b.F || a.VP != b.VP || a.GB != b.GB || b.T < a.T || b.D < a.D)
+    return bx_record_error(BX_ERR_INVALID, "bx_ss_copy_state: destination must match the "
+                                           "source's sequences, features, vector pool and budget "
+                                           "and have at least its capacities");
+  SCHK(hipDeviceSynchronize());
+  const size_t S = a.S, Ta = a.T, Tb = b.T, F = a.F, VP = a.VP, GB = a.GB;
+  auto rows = [&](void* d, const void* s_, size_t per_slot) -> hipError_t {
+    return hipMemcpy2D(d, Tb * per_slot, s_, Ta * per_slot, Ta * per_slot, S,
+                       hipMemcpyDeviceToDevice);
+  };
+  // per-slot state: track records, galleries (entries, qualities, times), the vector pools and
+  // their norms, the list order and the next frame's query list
+  SCHK(rows(b.trk, a.trk, sizeof(SsTrk)));
+  SCHK(rows(b.gal_v, a.gal_v, GB * sizeof(int)));
+  SCHK(rows(b.gal_q, a.gal_q, GB * sizeof(double)));
+  SCHK(rows(b.gal_t, a.gal_t, GB * sizeof(int)));
+  SCHK(rows(b.vec, a.vec, VP * F * sizeof(double)));
+  SCHK(rows(b.vecn, a.vecn, VP * F * sizeof(double)));
+  SCHK(rows(b.vden, a.vden, VP * sizeof(double)));
+  SCHK(rows(b.vwn, a.vwn, VP * sizeof(double)));
+  SCHK(rows(b.order, a.order, sizeof(int)));
+  SCHK(rows(b.nnl, a.nnl, sizeof(int)));
+  // per-sequence scalars (+ the defaults row S), the lost buffer (slot ids), status
+  SCHK(hipMemcpy(b.sq, a.sq, (S + 1) * SQS * sizeof(int), hipMemcpyDeviceToDevice));
+  SCHK(hipMemcpy(b.sqd, a.sqd, (S + 1) * 2 * sizeof(double), hipMemcpyDeviceToDevice));
+  SCHK(hipMemcpy(b.lost, a.lost, S * LOSTN * sizeof(int), hipMemcpyDeviceToDevice));
+  SCHK(hipMemcpy(b.status, a.status, 4 * sizeof(int), hipMemcpyDeviceToDevice));
+  dst->cache_seq = -1;
+  SCHK(hipDeviceSynchronize());
+  return BX_OK;
+}
+
 int bx_ss_destroy(bx_ss* e) {
   if (!e) return BX_OK;
   if (e->side) (void)hipStreamDestroy(e->side);

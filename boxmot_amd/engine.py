@@ -98,6 +98,22 @@ class Engine:
         # so the caching allocator cannot hand their memory out before the next step
         self._inflight = (dets, det_off, embs) if self._overlap else None
 
+    def slots_used(self, seq: int = 0) -> int:
+        """Track slots of sequence ``seq`` in use (bx_engine_slots_used_host)."""
+        u = C.c_int(0)
+        N.check(self._L.bx_engine_slots_used_host(self._h, seq, C.byref(u)), "slots_used")
+        return u.value
+
+    def grown(self, track_cap: int, det_cap: int) -> "Engine":
+        """A new engine with larger capacities holding this one's tracker state
+        (bx_engine_copy_state): the reference's lists are unbounded."""
+        e = Engine(self.kind, self.n_seq, track_cap, det_cap, self.emb_dim, self.emb_f64,
+                   self.params)
+        N.check(self._L.bx_engine_copy_state(e._h, self._h), "bx_engine_copy_state")
+        if self._overlap:
+            e.set_overlap(True)
+        return e
+
     def inputs_released(self, stream=None) -> None:
         """Overlap mode: order ``stream`` after the last step's last read of its inputs
         (bx_engine_inputs_released) — before refilling a reused input buffer in place."""
@@ -304,6 +320,15 @@ class OcsortEngine:
         N.check(self._L.bx_ocsort_create(C.byref(cfg), C.byref(h)), "bx_ocsort_create")
         self._h = h
 
+    def slots_used(self, seq: int = 0) -> int:
+        return self.counters(seq)["n_tracks"]
+
+    def grown(self, track_cap: int, det_cap: int) -> "OcsortEngine":
+        """A new engine with larger capacities holding this one's state (bx_ocsort_copy_state)."""
+        e = OcsortEngine(self.n_seq, track_cap, det_cap, self.params)
+        N.check(self._L.bx_ocsort_copy_state(e._h, self._h), "bx_ocsort_copy_state")
+        return e
+
     def close(self):
         h = getattr(self, "_h", None)
         if h:
@@ -454,6 +479,15 @@ class BoostEngine:
         h = C.c_void_p()
         N.check(self._L.bx_boost_create(C.byref(cfg), C.byref(h)), "bx_boost_create")
         self._h = h
+
+    def slots_used(self, seq: int = 0) -> int:
+        return self.counters(seq)["n_tracks"]
+
+    def grown(self, track_cap: int, det_cap: int) -> "BoostEngine":
+        """A new engine with larger capacities holding this one's state (bx_boost_copy_state)."""
+        e = BoostEngine(self.n_seq, track_cap, det_cap, self.emb_dim or 0, self.params)
+        N.check(self._L.bx_boost_copy_state(e._h, self._h), "bx_boost_copy_state")
+        return e
 
     def close(self):
         h = getattr(self, "_h", None)
@@ -627,6 +661,18 @@ class SsEngine:
         h = C.c_void_p()
         N.check(self._L.bx_ss_create(C.byref(cfg), C.byref(h)), "bx_ss_create")
         self._h = h
+        self.vec_cap = vec_cap
+
+    def slots_used(self, seq: int = 0) -> int:
+        """Listed tracks plus the lost buffer's (their galleries keep their slots)."""
+        c = self.counters(seq)
+        return c["n_tracks"] + c["n_lost"]
+
+    def grown(self, track_cap: int, det_cap: int) -> "SsEngine":
+        """A new engine with larger capacities holding this one's state (bx_ss_copy_state)."""
+        e = SsEngine(self.n_seq, track_cap, det_cap, self.emb_dim, self.vec_cap, self.params)
+        N.check(self._L.bx_ss_copy_state(e._h, self._h), "bx_ss_copy_state")
+        return e
 
     def close(self):
         h = getattr(self, "_h", None)

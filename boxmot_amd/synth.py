@@ -24,8 +24,8 @@ from dataclasses import dataclass
 
 import numpy as np
 
-__all__ = ["SyntheticScene", "SyntheticCMC", "StatefulCMC", "TorchSceneBatch", "load_mot_dets",
-           "synth_warp"]
+__all__ = ["SyntheticScene", "SyntheticCMC", "StatefulCMC", "TorchSceneBatch", "MotSequence",
+           "c5_sequences", "load_mot_dets", "synth_warp"]
 
 
 @dataclass
@@ -240,6 +240,89 @@ class TorchSceneBatch:
                 m, self.emb_dim, generator=g, device=dev) / math.sqrt(self.emb_dim)
             embs = (e / e.norm(dim=-1, keepdim=True)).contiguous()
         return dets, off, embs
+
+
+def _iou_matrix(a, b):
+    lt = np.maximum(a[:, None, :2], b[None, :, :2])
+    rb = np.minimum(a[:, None, 2:4], b[None, :, 2:4])
+    wh = np.clip(rb - lt, 0, None)
+    inter = wh[..., 0] * wh[..., 1]
+    area = lambda x: (x[:, 2] - x[:, 0]) * (x[:, 3] - x[:, 1])  # noqa: E731
+    return inter / (area(a)[:, None] + area(b)[None, :] - inter)
+
+
+class MotSequence:
+    """A real detection stream (MOT17 public detections, packed [frame, x1, y1, x2, y2, conf])
+    with synthetic ReID embeddings that follow object identity: consecutive frames' detections
+    are linked greedily by IoU (>= 0.5, best pair first), a linked detection inherits its
+    predecessor's identity, and each identity owns a random unit base vector; a detection's
+    embedding is its identity's vector plus 10% noise, normalised.  Frames are renumbered
+    1..n_frames (val.py feeds every frame that has detections).  ``frame(t)`` has
+    SyntheticScene's contract."""
+
+    def __init__(self, packed, emb_dim=0, seed=0, emb_dtype=np.float64):
+        packed = np.asarray(packed, np.float64)
+        fnos = np.unique(packed[:, 0]).astype(int)
+        self.n_frames = len(fnos)
+        self.dets, self.ids = [], []
+        prev, prev_id, next_id = None, None, 0
+        for f in fnos:
+            r = packed[packed[:, 0] == f]
+            d = np.zeros((r.shape[0], 6), np.float64)
+            d[:, :5] = r[:, 1:6]
+            ids = np.full(d.shape[0], -1, np.int64)
+            if prev is not None and prev.shape[0] and d.shape[0]:
+                iou = _iou_matrix(d, prev)
+                order = np.argsort(-iou, axis=None, kind="stable")
+                used_a, used_b = set(), set()
+                for k in order:
+                    i, j = divmod(int(k), prev.shape[0])
+                    if iou[i, j] < 0.5:
+                        break
+                    if i in used_a or j in used_b:
+                        continue
+                    used_a.add(i)
+                    used_b.add(j)
+                    ids[i] = prev_id[j]
+            for i in np.flatnonzero(ids < 0):
+                ids[i] = next_id
+                next_id += 1
+            self.dets.append(d)
+            self.ids.append(ids)
+            prev, prev_id = d, ids
+        self.emb_dim, self.seed, self.emb_dtype = emb_dim, seed, emb_dtype
+        if emb_dim:
+            rng = np.random.default_rng([seed, 0x307])
+            base = rng.standard_normal((next_id, emb_dim))
+            self.base_emb = base / np.linalg.norm(base, axis=1, keepdims=True)
+
+    def frame(self, t: int):
+        d, ids = self.dets[t - 1], self.ids[t - 1]
+        embs = None
+        if self.emb_dim:
+            rng = np.random.default_rng([self.seed, int(t)])
+            e = self.base_emb[ids] + 0.1 * rng.standard_normal((ids.size, self.emb_dim)) / \
+                math.sqrt(self.emb_dim)
+            e /= np.linalg.norm(e, axis=1, keepdims=True)
+            embs = e.astype(self.emb_dtype)
+        return d.copy(), embs, ids
+
+
+def c5_sequences(mot_npz, emb_dim=512, n_synth=6, seed=0):
+    """SURVEY §8(d)'s C5 stand-in (MOT17-ablation is a network download): MOT17-02 and MOT17-04
+    public detections + ``n_synth`` synthetic MOT-sized sequences (60 objects detected w.p. 0.5:
+    ~30 dets/frame, confidences U(0.3, 1)), float64 ReID embeddings.  Returns [(name, seq,
+    n_frames)]."""
+    z = np.load(mot_npz)
+    out = []
+    for k, name in enumerate(["MOT17-02-FRCNN", "MOT17-04-FRCNN"]):
+        sq = MotSequence(z[name], emb_dim=emb_dim, seed=seed + k)
+        out.append((name, sq, sq.n_frames))
+    for k in range(n_synth):
+        sq = SyntheticScene(n_obj=60, seed=seed + 100 + k, emb_dim=emb_dim, conf_lo=0.3,
+                            emb_dtype=np.float64, layout="crowded" if k % 2 else "grid")
+        out.append((f"synthetic-{k}", sq, 600 + 90 * k))
+    return out
 
 
 def load_mot_dets(path):

@@ -36,6 +36,47 @@ def class_warps(cmc, img, dets: np.ndarray, nr_classes: int, conv=_reshape_warp)
     return out
 
 
+def _pow2(n: int) -> int:
+    return 1 << max(0, int(n) - 1).bit_length()
+
+
+class CapacityGuard:
+    """Grows a drop-in's engine before a frame could overflow it.  The reference's track and
+    detection lists are unbounded (bytetrack.py:272-346, sort/tracker.py:118-181); the engines
+    have fixed slot arenas, so before each frame the drop-in checks that every sequence's slots
+    in use plus the frame's detections (an upper bound on its births) fit, and otherwise moves
+    the tracker state into an engine with twice the capacity (``engine.grown``, a device copy).
+    The slots in use are tracked as an upper bound (+ detections per frame) and re-read from
+    the engine only when that bound reaches the capacity."""
+
+    def __init__(self):
+        self.ub = {}
+        self.t_max = None  # track_cap the engine could not grow past (its LDS / solver limit)
+
+    def fit(self, eng, dets_per_seq: dict, n_frame: int):
+        T, D = eng.track_cap, eng.det_cap
+        need = T
+        for q, n in dets_per_seq.items():
+            if self.ub.get(q) is None or self.ub[q] + n > T:
+                self.ub[q] = eng.slots_used(q)
+            need = max(need, self.ub[q] + n)
+        t2 = T if need <= T else max(2 * T, _pow2(need))
+        if self.t_max is not None:
+            t2 = min(t2, self.t_max)
+        d2 = D if n_frame <= D else max(2 * D, _pow2(n_frame))
+        while (t2, d2) != (T, D):
+            try:
+                eng = eng.grown(t2, d2)
+                break
+            except ValueError:  # past the engine's limits: the births bound is loose, so go on
+                if t2 <= T:      # at the current slots (the engine still raises on a real overflow)
+                    raise
+                self.t_max = t2 = max(T, t2 // 2)
+        for q, n in dets_per_seq.items():
+            self.ub[q] += n
+        return eng
+
+
 class TrackView:
     """Read-only host view of one engine track (what ``active_tracks`` entries expose)."""
 

@@ -20,7 +20,7 @@ from __future__ import annotations
 import numpy as np
 
 from ..engine import BoostEngine, BoostParams
-from .basetracker import BaseTracker, _with_index, class_warps
+from .basetracker import BaseTracker, CapacityGuard, _with_index, class_warps
 
 
 def _boost_warp(w) -> np.ndarray:
@@ -85,6 +85,7 @@ class BoostTrack(BaseTracker):
             lambda_mhd=lambda_mhd, lambda_shape=lambda_shape, use_dlo_boost=use_dlo_boost,
             use_duo_boost=use_duo_boost, dlo_boost_coef=dlo_boost_coef, s_sim_corr=s_sim_corr,
             use_rich_s=use_rich_s, use_sb=use_sb, use_vt=use_vt, with_reid=with_reid)
+        self._cap = CapacityGuard()
         self._caps = (track_cap, det_cap)
         self.engine = None if with_reid else self._make_engine(0)
         self._engine_ids = 0
@@ -116,6 +117,8 @@ class BoostTrack(BaseTracker):
             for _ in range(getattr(self, "_pending_frames", 0)):
                 self.engine.update_host(0, np.empty((0, 6), np.float32),
                                         np.empty((0, self.engine.emb_dim)))
+        n = int(np.asarray(dets).reshape(-1, 6).shape[0])
+        self.engine = self._cap.fit(self.engine, {0: n}, n)
         if self._engine_ids != BoostTrack._id_count:
             self.engine.set_id_count(0, BoostTrack._id_count)
         self.frame_count += 1

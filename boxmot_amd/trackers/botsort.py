@@ -13,7 +13,7 @@ from __future__ import annotations
 import numpy as np
 
 from ..engine import Engine, EngineParams
-from .basetracker import BaseTracker, _with_index, class_warps
+from .basetracker import BaseTracker, CapacityGuard, _with_index, class_warps
 
 
 class IdentityCMC:
@@ -54,6 +54,7 @@ class BotSort(BaseTracker):
             appearance_thresh=appearance_thresh, frame_rate=frame_rate,
             fuse_first_associate=fuse_first_associate, with_reid=with_reid)
         self._caps = (track_cap, det_cap)
+        self._cap = CapacityGuard()
         self.engine = None if with_reid else self._make_engine(0, False)
 
     def _make_engine(self, emb_dim: int, emb_f64: bool) -> Engine:
@@ -76,6 +77,8 @@ class BotSort(BaseTracker):
             else:
                 self.engine = self._make_engine(embs.shape[1], embs.dtype == np.float64)
         self.frame_count += 1
+        n = int(np.asarray(dets).reshape(-1, 6).shape[0])
+        self.engine = self._cap.fit(self.engine, {0: n}, n)
         if self.per_class:  # one update per class id, lost list shared (basetracker.py:155-201)
             # the reference's cmc.apply runs once per class call (botsort.py:218) on the class's
             # detections: a stateful CMC (ECC keeps the previous frame) gives class 0 the frame's

@@ -8,7 +8,7 @@ from __future__ import annotations
 import numpy as np
 
 from ..engine import Engine, EngineParams
-from .basetracker import BaseTracker
+from .basetracker import BaseTracker, CapacityGuard
 
 
 def _xyah_box(mean):
@@ -40,6 +40,7 @@ class ByteTrack(BaseTracker):
                                                  track_buffer=track_buffer,
                                                  frame_rate=frame_rate))
         self._engine_ids = 0
+        self._cap = CapacityGuard()
 
     @staticmethod
     def clear_count():
@@ -52,6 +53,8 @@ class ByteTrack(BaseTracker):
         if self._engine_ids != ByteTrack._id_count:
             self.engine.set_id_count(0, ByteTrack._id_count)
         self.frame_count += 1
+        n = int(np.asarray(dets).reshape(-1, 6).shape[0])
+        self.engine = self._cap.fit(self.engine, {0: n}, n)
         if self.per_class:  # one update per class id, lost list shared (basetracker.py:155-201)
             out = self.engine.update_classes_host(0, dets, n_classes=self.nr_classes)
         else:

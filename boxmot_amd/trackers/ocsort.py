@@ -12,7 +12,7 @@ import numpy as np
 
 from ..engine import OcsortEngine, OcsortParams
 from ..iou import KINDS
-from .basetracker import BaseTracker
+from .basetracker import BaseTracker, CapacityGuard
 
 
 class OcSort(BaseTracker):
@@ -49,6 +49,7 @@ class OcSort(BaseTracker):
                                 asso_func=asso_func if asso_func in KINDS else "iou"))
         self._engine_ids = 0
         self._frame_latched = False
+        self._cap = CapacityGuard()
 
     @BaseTracker.setup_decorator
     @BaseTracker.per_class_decorator
@@ -60,6 +61,15 @@ class OcSort(BaseTracker):
                 self.engine.set_frame_size(q, self.w, self.h)
             self._frame_latched = True
         self.frame_count += 1
+        d = np.asarray(dets).reshape(-1, 6)
+        if self.per_class:  # class c runs as sequence c: its births are at most its detections
+            cls = d[:, 5].astype(np.float32)
+            ok = (cls >= 0) & (cls < self.nr_classes) & (cls == np.floor(cls))
+            per = np.bincount(cls[ok].astype(np.int64), minlength=self.nr_classes)
+            self.engine = self._cap.fit(self.engine, {c: int(k) for c, k in enumerate(per) if k},
+                                        d.shape[0])
+        else:
+            self.engine = self._cap.fit(self.engine, {0: d.shape[0]}, d.shape[0])
         if self.per_class:  # one launch over the class sequences, ids renumbered class-globally
             out, OcSort._id_count = self.engine.update_classes_host(0, self.nr_classes, dets,
                                                                     OcSort._id_count)

@@ -26,7 +26,7 @@ import numpy as np
 
 from ..engine import SsEngine, SsParams
 from ..occlusion import OcclusionHandler
-from .basetracker import BaseTracker
+from .basetracker import BaseTracker, CapacityGuard
 from .boosttrack import IdentityCMC
 
 
@@ -69,6 +69,7 @@ class StrongSort:
             ema_alpha=ema_alpha, conf_thresh_high=conf_thresh_high,
             conf_thresh_low=conf_thresh_low, id_preservation_weight=id_preservation_weight,
             crowd_detection=crowd_detection, born_confirmed=_born_confirmed())
+        self._cap = CapacityGuard()
         self._caps = (track_cap, det_cap, vec_cap)
         self.engine = None
         self._pending = 0
@@ -100,6 +101,11 @@ class StrongSort:
                 self.engine.update_host(0, np.empty((0, 6)), np.empty((0, self.engine.emb_dim)))
             if self.handle_occlusions:
                 self.occlusion_tracker = OcclusionHandler(self.engine, 0, self.occlusion_threshold)
+        eng = self._cap.fit(self.engine, {0: dets.shape[0]}, dets.shape[0])
+        if eng is not self.engine:  # grown: the occlusion handler reads the new engine
+            self.engine = eng
+            if self.occlusion_tracker is not None:
+                self.occlusion_tracker.engine = eng
         warp = None
         if self.cmc is not None:
             warp = np.asarray(self.cmc.apply(img, dets[:, :4]), np.float64)
@@ -116,6 +122,7 @@ class StrongSort:
         if self.engine is not None:
             self.engine.reset()
         self.frame_count = 0
+        self._cap = CapacityGuard()
 
     @property
     def tracks(self):

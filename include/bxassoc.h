@@ -150,6 +150,13 @@ int bx_engine_probe_read(bx_engine *e, double *total_ms, int *count);
  * re-solved by lapx's own lapjv (see bx_linear_assignment), summed since creation / reset. */
 int bx_engine_lap_ties_host(bx_engine *e, int seq0, int nseq, int64_t *total);
 
+/* Capacity growth (the reference's track lists are unbounded: bytetrack.py:272-346): copy every
+ * sequence's tracker state of `src` into `dst`, a fresh engine with the same kind, sequences and
+ * features and track_cap / det_cap at least src's (slot ids stay valid; per_class parked lists
+ * included).  Synchronous.  The drop-ins grow this way before a frame could overflow. */
+int bx_engine_copy_state(bx_engine *dst, bx_engine *src);
+/* Track slots of sequence `seq` in use (live tracks), host, synchronous. */
+int bx_engine_slots_used_host(bx_engine *e, int seq, int *used);
 /* Latched device-side status of the whole engine (BX_OK or BX_ERR_TRACK_OVERFLOW). */
 int bx_engine_status(bx_engine *e, int *status);
 /* Per-sequence counters (host copies): frame_count, id_count, live tracks. */

@@ -97,6 +97,10 @@ int bx_kf_boost_predict(int n, double *x, double *P, void *stream);
 int bx_kf_boost_update(int n, double *x, double *P, const double *z, void *stream);
 int bx_kf_boost_mh_dist(int nd, const double *dets, int nt, const double *x, const double *P,
                         double *out, void *stream);
+/* Capacity growth (the reference's track list is unbounded: boosttrack.py:221-341 (self.trackers)): copy every
+ * sequence's tracker state of `src` into `dst`, a fresh engine with the same configuration and
+ * sequences and track_cap / det_cap at least src's (slot ids stay valid).  Synchronous. */
+int bx_boost_copy_state(bx_boost *dst, bx_boost *src);
 int bx_boost_status(bx_boost *e, int *status);
 int bx_boost_counters_host(bx_boost *e, int seq, int *frame_count, int *id_count, int *n_tracks);
 /* KalmanBoxTracker.count is class-global in the reference (boosttrack.py:50,53-56, never reset

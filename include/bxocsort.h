@@ -88,6 +88,10 @@ int bx_kf_xysr_predict(int n, double *x, double *P, double q_xy_scaling, double 
                        void *stream);
 int bx_kf_xysr_update(int n, double *x, double *P, const double *z, void *stream);
 /* Latched device status (BX_OK, BX_ERR_TRACK_OVERFLOW or BX_ERR_CAPACITY). */
+/* Capacity growth (the reference's track list is unbounded: ocsort.py:246-439 (self.active_tracks / KalmanBoxTracker list)): copy every
+ * sequence's tracker state of `src` into `dst`, a fresh engine with the same configuration and
+ * sequences and track_cap / det_cap at least src's (slot ids stay valid).  Synchronous. */
+int bx_ocsort_copy_state(bx_ocsort *dst, bx_ocsort *src);
 int bx_ocsort_status(bx_ocsort *e, int *status);
 int bx_ocsort_counters_host(bx_ocsort *e, int seq, int *frame_count, int *id_count,
                             int *n_tracks);

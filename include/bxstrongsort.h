@@ -85,6 +85,10 @@ int bx_ss_update_host(bx_ss *e, int seq, const double *dets, int n, const double
                       const double *warp, double *out, int *n_out, void *stream);
 /* Latched device status (BX_OK, BX_ERR_TRACK_OVERFLOW — track slots or a slot's vector pool
  * exhausted — or BX_ERR_CAPACITY). */
+/* Capacity growth (the reference's track list is unbounded: sort/tracker.py:118-181 (self.tracks), sort/track.py:98-105): copy every
+ * sequence's tracker state of `src` into `dst`, a fresh engine with the same configuration and
+ * sequences and track_cap / det_cap at least src's (slot ids stay valid).  Synchronous. */
+int bx_ss_copy_state(bx_ss *dst, bx_ss *src);
 int bx_ss_status(bx_ss *e, int *status);
 /* Per-sequence counters (host): frame count, next id, live tracks, lost-buffer tracks. */
 int bx_ss_counters_host(bx_ss *e, int seq, int *frame_count, int *next_id, int *n_tracks,

@@ -420,11 +420,9 @@ def make_dropin(kind, args):
 def test_tracker_fixture_parity(torch_cuda, path):
     fx = np.load(path)
     kind, args = fixture_tracker_args(fx)
-    large = "large" in fx.files  # C4 size: drop-in capacities for 1024 objects; no oracle replay
-    if large:
-        import bench
-
-        args = dict(args, **bench.SS_C4_CAPS)
+    # C4 size ("large"): the drop-in starts at its default capacities and grows to 1024 objects
+    # (CapacityGuard); no oracle replay
+    large = "large" in fx.files
     tr = make_dropin(kind, args)
     orc = None if large else po.OracleTracker(
         kind, **(dict(args, born_confirmed=True) if kind == "strongsort" else args))

@@ -73,61 +73,97 @@ def test_shard_sequences_partition():
 
 
 # ---------------------------------------------------------------------------------------------
-# The same sharded run with the HIP engine on every rank (GPU box: both ranks share cuda:0 and
+# The same sharded run with the HIP engines on every rank (GPU box: both ranks share cuda:0 and
 # gather over gloo; on a multi-GPU node bench.py runs this code path one rank per GPU over RCCL).
-# Each rank steps its shard of sequences through ONE batched engine launch per frame and the
-# gathered per-sequence checksums must equal the single-process oracle's.
-GPU_KINDS = ("bytetrack", "botsort")
+# Each rank steps its shard of sequences through ONE batched engine launch per frame; every
+# output row is gathered ([sequence, frame, row...]) and must equal the single-process oracle's.
+GPU_KINDS = ("bytetrack", "botsort", "ocsort", "boosttrack", "strongsort")
+NCOL = {"strongsort": 10}
+BOOST_ARGS = dict(max_age=60, min_hits=3, det_thresh=0.6, iou_threshold=0.3, use_ecc=True,
+                  min_box_area=10, aspect_ratio_thresh=1.6, lambda_iou=0.5, lambda_mhd=0.25,
+                  lambda_shape=0.25, use_dlo_boost=True, use_duo_boost=True, dlo_boost_coef=0.65,
+                  s_sim_corr=False, use_rich_s=True, use_sb=True, use_vt=True, with_reid=True)
+SS_ARGS = dict(min_conf=0.1, max_cos_dist=0.15, max_iou_dist=0.7, max_age=50, n_init=2,
+               nn_budget=150, mc_lambda=0.995, ema_alpha=0.9, conf_thresh_high=0.7,
+               conf_thresh_low=0.3, id_preservation_weight=0.1, crowd_detection=True,
+               born_confirmed=True)
+OCS_ARGS = dict(min_conf=0.1, det_thresh=0.6, max_age=30, min_hits=3, asso_threshold=0.3,
+                delta_t=3, inertia=0.1, use_byte=False, Q_xy_scaling=0.01, Q_s_scaling=0.0001)
+EMB = {"botsort": 64, "boosttrack": 32, "strongsort": 32}
 
 
 def gpu_sequences(kind, g):
     from boxmot_amd.synth import SyntheticScene
 
-    emb = 64 if kind == "botsort" else 0
-    return SyntheticScene(n_obj=20 + 3 * g, seed=70 + g, emb_dim=emb,
-                          layout="crowded" if g % 2 else "grid")
+    kw = {}
+    if kind in ("boosttrack", "strongsort"):
+        kw = dict(emb_dtype=np.float64, conf_lo=0.3)
+    if kind == "ocsort":
+        kw = dict(conf_lo=0.3)
+    return SyntheticScene(n_obj=20 + 3 * g, seed=70 + g, emb_dim=EMB.get(kind, 0),
+                          layout="crowded" if g % 2 else "grid", **kw)
 
 
 def gpu_args(kind):
-    return (dict(min_conf=0.1, track_thresh=0.6, match_thresh=0.9, track_buffer=30)
-            if kind == "bytetrack" else dict(track_high_thresh=0.6, new_track_thresh=0.7,
-                                             match_thresh=0.8))
+    return {"bytetrack": dict(min_conf=0.1, track_thresh=0.6, match_thresh=0.9, track_buffer=30),
+            "botsort": dict(track_high_thresh=0.6, new_track_thresh=0.7, match_thresh=0.8),
+            "ocsort": OCS_ARGS, "boosttrack": BOOST_ARGS, "strongsort": SS_ARGS}[kind]
+
+
+def make_engine(kind, n):
+    from boxmot_amd import engine as E
+
+    a = gpu_args(kind)
+    if kind == "ocsort":
+        return E.OcsortEngine(n_seq=n, track_cap=128, det_cap=128, params=E.OcsortParams(**a))
+    if kind == "boosttrack":
+        return E.BoostEngine(n_seq=n, track_cap=128, det_cap=128, emb_dim=EMB[kind],
+                             params=E.BoostParams(**a))
+    if kind == "strongsort":
+        return E.SsEngine(n_seq=n, track_cap=256, det_cap=128, emb_dim=EMB[kind], vec_cap=32,
+                          params=E.SsParams(**a))
+    return E.Engine(kind, n_seq=n, track_cap=256, det_cap=128, emb_dim=EMB.get(kind, 0),
+                    params=E.EngineParams(**a))
 
 
 def _gpu_worker(rank, world, port, path, kind):
     import torch
     import torch.distributed as dist
 
-    from boxmot_amd.engine import Engine, EngineParams
-
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     mine = shard_sequences([N_FRAMES + g for g in range(N_SEQ)], world, rank)
     scenes = [gpu_sequences(kind, g) for g in mine]
-    emb = 64 if kind == "botsort" else 0
-    eng = Engine(kind, n_seq=len(mine), track_cap=256, det_cap=128, emb_dim=emb,
-                 params=EngineParams(**gpu_args(kind)))
-    outs = [[] for _ in mine]
+    eng = make_engine(kind, len(mine))
+    ncol = NCOL.get(kind, 8)
+    f64 = kind == "strongsort"  # StrongSort takes float64 detections (no setup_decorator)
+    rows = []
     for t in range(1, N_FRAMES + 1):
         fr = [sc.frame(t) for sc in scenes]
         off = np.zeros(len(mine) + 1, np.int32)
         off[1:] = np.cumsum([f[0].shape[0] for f in fr])
-        d = torch.from_numpy(np.concatenate([f[0] for f in fr]).astype(np.float32)).cuda()
-        e = torch.from_numpy(np.concatenate([f[1] for f in fr])).cuda() if emb else None
-        o = torch.empty((max(int(off[-1]), 1), 8), dtype=torch.float64, device="cuda")
+        d = torch.from_numpy(np.concatenate([f[0] for f in fr]).astype(
+            np.float64 if f64 else np.float32)).cuda()
+        e = (torch.from_numpy(np.concatenate([f[1] for f in fr])).cuda()
+             if EMB.get(kind) else None)
+        o = torch.empty((max(int(off[-1]), 1), ncol), dtype=torch.float64, device="cuda")
         c = torch.empty(len(mine), dtype=torch.int32, device="cuda")
-        eng.step(d, torch.from_numpy(off).cuda(), e, None, o, c)
+        do = torch.from_numpy(off).cuda()
+        if kind == "ocsort":
+            eng.step(d, do, o, c)
+        else:
+            eng.step(d, do, e, None, o, c)
         o, c = o.cpu().numpy(), c.cpu().numpy()
-        for k in range(len(mine)):
-            outs[k].append(o[off[k]: off[k] + c[k]])
+        for k, g in enumerate(mine):
+            r = o[off[k]: off[k] + c[k]]
+            rows.append(np.concatenate([np.full((r.shape[0], 1), g), np.full((r.shape[0], 1), t),
+                                        r], 1))
     assert eng.status() == 0
-    recs = np.array([[g, N_FRAMES, output_checksum(np.concatenate(outs[k], 0))]
-                     for k, g in enumerate(mine)]).reshape(-1, 3)
-    allrec = gather_records(recs, dist, "cpu")
+    recs = np.concatenate(rows, 0) if rows else np.zeros((0, ncol + 2))
+    allrec = gather_records(recs.reshape(-1, ncol + 2), dist, "cpu")
     if rank == 0:
-        with open(path, "w") as f:
-            json.dump(allrec.tolist(), f)
+        np.save(path, allrec)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -135,17 +171,21 @@ def _gpu_worker(rank, world, port, path, kind):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", GPU_KINDS)
 def test_sharded_engine_run_equals_oracle(kind):
+    """All five trackers: world-size-2 sequence sharding with the HIP engine per rank; the
+    gathered output rows of every sequence equal the oracle's, bit for bit."""
     from oracle import pyoracle as po
 
     with tempfile.TemporaryDirectory() as d:
-        path = os.path.join(d, "rec.json")
+        path = os.path.join(d, "rows.npy")
         mp.spawn(_gpu_worker, args=(2, free_port(), path, kind), nprocs=2, join=True)
-        got = np.array(json.load(open(path)))
-    got = got[np.argsort(got[:, 0])]
-    assert list(got[:, 0]) == list(range(N_SEQ))
-    ref = []
+        got = np.load(path)
+    assert sorted(set(got[:, 0].astype(int))) == list(range(N_SEQ))
     for g in range(N_SEQ):
         sc, tr = gpu_sequences(kind, g), po.OracleTracker(kind, **gpu_args(kind))
-        ref.append(output_checksum(np.concatenate(
-            [tr.update(*sc.frame(t)[:2]) for t in range(1, N_FRAMES + 1)], 0)))
-    np.testing.assert_array_equal(got[:, 2], np.array(ref))
+        ref = []
+        for t in range(1, N_FRAMES + 1):
+            dets, embs, _ = sc.frame(t)
+            o = tr.update(dets, embs) if EMB.get(kind) else tr.update(dets)
+            ref.append(np.concatenate([np.full((o.shape[0], 1), t), o], 1))
+        mine = got[got[:, 0] == g][:, 1:]
+        np.testing.assert_array_equal(mine, np.concatenate(ref, 0), err_msg=f"{kind} seq {g}")
