@@ -112,7 +112,7 @@ class BxSsConfig(C.Structure):
 EXPORTS = [
     "bx_last_error", "bx_device_count", "bx_engine_create", "bx_engine_destroy",
     "bx_engine_reset", "bx_engine_step", "bx_engine_update_host", "bx_engine_status",
-    "bx_engine_counters_host", "bx_engine_set_id_count", "bx_engine_tracks_host",
+    "bx_engine_counters_host", "bx_engine_set_id_count", "bx_engine_tracks_host", "bx_engine_class_tracks_host",
     "bx_engine_state_set_host", "bx_ocsort_state_set_host", "bx_boost_state_set_host",
     "bx_ss_state_set_host",
     "bx_engine_probe", "bx_engine_probe_read", "bx_engine_set_overlap", "bx_engine_frame_stats_host",
@@ -157,6 +157,8 @@ _SIGS = {
     "bx_engine_set_id_count": ([_vp, C.c_int, C.c_int, _vp], C.c_int),
     "bx_engine_tracks_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip,
                                _ip], C.c_int),
+    "bx_engine_class_tracks_host": ([_vp, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp,
+                                     _vp, _vp, _vp], C.c_int),
     "bx_iou_batch": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp], C.c_int),
     "bx_pairwise_cost": ([C.c_int, _vp, C.c_int, C.c_int, _vp, C.c_int, C.c_int, C.c_double,
                           C.c_double, _vp, _vp], C.c_int),

@@ -2376,19 +2376,13 @@ int bx_engine_set_id_count(bx_engine* e, int seq, int id_count, void* stream) {
   return BX_OK;
 }
 
-int bx_engine_tracks_host(bx_engine* e, int seq, int cap, int32_t* ids, int32_t* state,
-                          int32_t* is_activated, int32_t* frame_id, int32_t* start_frame,
-                          double* mean, double* cov, int* n_active, int* n_lost) {
-  if (int rc = settle(e)) return rc;
-  if (!e || seq < 0 || seq >= e->dev.S) return set_err(BX_ERR_INVALID, "bad sequence");
-  HIPCHK(hipDeviceSynchronize());
+namespace {
+// host copy of the listed slots' track fields (bx_engine_tracks_host / _class_tracks_host);
+// pending covariance predicts are materialised first
+int snapshot_slots(bx_engine* e, int seq, const std::vector<int>& slots, int32_t* ids,
+                   int32_t* state, int32_t* is_activated, int32_t* frame_id, int32_t* start_frame,
+                   double* mean, double* cov) {
   const int T = e->dev.T;
-  int v[SQ_STRIDE];
-  HIPCHK(hipMemcpy(v, e->dev.seq + (size_t)seq * SQ_STRIDE, sizeof(v), hipMemcpyDeviceToHost));
-  const int na = v[SQ_NA], nl = v[SQ_NL];
-  if (n_active) *n_active = na;
-  if (n_lost) *n_lost = nl;
-  if (na + nl > cap) return set_err(BX_ERR_CAPACITY, "cap too small for the live tracks");
   if (cov) {  // the covariance of tracks without an update since their last predicts
     if (e->cfg.kind == BX_BYTETRACK)
       hipLaunchKernelGGL(materialize_kernel<KIND_BYTE>, dim3((T + WG - 1) / WG), dim3(WG), 0, 0,
@@ -2399,21 +2393,18 @@ int bx_engine_tracks_host(bx_engine* e, int seq, int cap, int32_t* ids, int32_t*
     HIPCHK(hipGetLastError());
     HIPCHK(hipDeviceSynchronize());
   }
-  std::vector<uint16_t> act(T), lost(T);
   std::vector<uint32_t> fl(T);
   std::vector<int> id(T), fid(T), st(T);
   std::vector<double> kf((size_t)KF_STRIDE * T);
   const size_t sT = (size_t)seq * T;
-  HIPCHK(hipMemcpy(act.data(), e->dev.act + sT, 2 * T, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(lost.data(), e->dev.lost + sT, 2 * T, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(fl.data(), e->dev.flags + sT, 4 * T, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(id.data(), e->dev.id + sT, 4 * T, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(fid.data(), e->dev.frame_id + sT, 4 * T, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(st.data(), e->dev.start + sT, 4 * T, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(kf.data(), e->dev.kf + sT * KF_STRIDE, 8 * KF_STRIDE * (size_t)T,
                    hipMemcpyDeviceToHost));
-  for (int k = 0; k < na + nl; k++) {
-    const int slot = k < na ? act[k] : lost[k - na];
+  for (size_t k = 0; k < slots.size(); k++) {
+    const int slot = slots[k];
     if (ids) ids[k] = id[slot];
     if (state) state[k] = (int)(fl[slot] & F_STATE);
     if (is_activated) is_activated[k] = (fl[slot] & F_ACT) ? 1 : 0;
@@ -2423,6 +2414,64 @@ int bx_engine_tracks_host(bx_engine* e, int seq, int cap, int32_t* ids, int32_t*
     for (int q = 0; q < 64 && cov; q++) cov[64 * k + q] = kf[(size_t)slot * KF_STRIDE + 8 + q];
   }
   return BX_OK;
+}
+}  // namespace
+
+int bx_engine_tracks_host(bx_engine* e, int seq, int cap, int32_t* ids, int32_t* state,
+                          int32_t* is_activated, int32_t* frame_id, int32_t* start_frame,
+                          double* mean, double* cov, int* n_active, int* n_lost) {
+  if (int rc = settle(e)) return rc;
+  if (!e || seq < 0 || seq >= e->dev.S) return set_err(BX_ERR_INVALID, "bad sequence");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(hipDeviceSynchronize());
+  const int T = e->dev.T;
+  int v[SQ_STRIDE];
+  HIPCHK(hipMemcpy(v, e->dev.seq + (size_t)seq * SQ_STRIDE, sizeof(v), hipMemcpyDeviceToHost));
+  const int na = v[SQ_NA], nl = v[SQ_NL];
+  if (n_active) *n_active = na;
+  if (n_lost) *n_lost = nl;
+  if (na + nl > cap) return set_err(BX_ERR_CAPACITY, "cap too small for the live tracks");
+  std::vector<uint16_t> act(T), lost(T);
+  const size_t sT = (size_t)seq * T;
+  HIPCHK(hipMemcpy(act.data(), e->dev.act + sT, 2 * T, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(lost.data(), e->dev.lost + sT, 2 * T, hipMemcpyDeviceToHost));
+  std::vector<int> slots(na + nl);
+  for (int k = 0; k < na + nl; k++) slots[k] = k < na ? act[k] : lost[k - na];
+  return snapshot_slots(e, seq, slots, ids, state, is_activated, frame_id, start_frame, mean, cov);
+}
+
+int bx_engine_class_tracks_host(bx_engine* e, int seq, int n_classes, int cap, int32_t* cls_off,
+                                int32_t* ids, int32_t* state, int32_t* is_activated,
+                                int32_t* frame_id, int32_t* start_frame, double* mean,
+                                double* cov) {
+  if (int rc = settle(e)) return rc;
+  if (!e || seq < 0 || seq >= e->dev.S || n_classes <= 0 || !cls_off)
+    return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_class_tracks_host");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  if (e->n_classes && e->n_classes != n_classes)
+    return set_err(BX_ERR_INVALID, "n_classes differs from the engine's per-class calls");
+  const int T = e->dev.T, C = n_classes;
+  std::vector<int> slots;
+  for (int c = 0; c <= C; c++) cls_off[c] = 0;
+  if (!e->n_classes || !e->park[seq]) return BX_OK;  // no per-class call yet: every list empty
+  HIPCHK(hipDeviceSynchronize());
+  int v[SQ_STRIDE];
+  HIPCHK(hipMemcpy(v, e->dev.seq + (size_t)seq * SQ_STRIDE, sizeof(v), hipMemcpyDeviceToHost));
+  std::vector<uint16_t> act(T), park((size_t)C * T);
+  std::vector<int> npark(C);
+  HIPCHK(hipMemcpy(act.data(), e->dev.act + (size_t)seq * T, 2 * T, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(park.data(), e->park[seq], 2 * (size_t)C * T, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(npark.data(), e->park[seq] + park_npark_off(e), sizeof(int) * C,
+                   hipMemcpyDeviceToHost));
+  // the class that ran last holds the engine's active list, every other class its parked one
+  const int cur = e->cur_cls[seq];
+  for (int c = 0; c < C; c++) {
+    const int n = c == cur ? v[SQ_NA] : npark[c];
+    for (int k = 0; k < n; k++) slots.push_back(c == cur ? act[k] : park[(size_t)c * T + k]);
+    cls_off[c + 1] = (int)slots.size();
+  }
+  if ((int)slots.size() > cap) return set_err(BX_ERR_CAPACITY, "cap too small for the class lists");
+  return snapshot_slots(e, seq, slots, ids, state, is_activated, frame_id, start_frame, mean, cov);
 }
 
 int bx_engine_state_set_host(bx_engine* e, int seq, int n, const int32_t* ids, const double* mean,

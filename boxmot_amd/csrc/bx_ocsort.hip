@@ -1377,7 +1377,9 @@ int bx_ocsort_tracks_host(bx_ocsort* e, int seq, int cap, int32_t* ids, double* 
     OcsTrk t;
     OCHK(hipMemcpy(&t, e->dev.trk + (size_t)seq * e->dev.T + ord[k], sizeof(OcsTrk),
                    hipMemcpyDeviceToHost));
-    if (ids) ids[k] = t.id;
+    // a per-class sequence reports the class-global id its rows carry (minus one)
+    const bool g = seq < (int)e->gid.size() && t.id >= 0 && t.id < (int)e->gid[seq].size();
+    if (ids) ids[k] = g ? e->gid[seq][t.id] : t.id;
     if (x) memcpy(x + 7 * k, t.x, sizeof(t.x));
     if (p) memcpy(p + 49 * k, t.P, sizeof(t.P));
   }

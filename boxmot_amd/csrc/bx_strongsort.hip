@@ -1018,7 +1018,8 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
   const int seq = x.seq;
   SCOUNT(7, R);
   SCOUNT(8, CC);
-  unsigned long long t_slow = 0, t_s0 = 0, t_all = SS_NOW();
+  unsigned long long t_slow = 0, t_s0 = 0, t_all = SS_NOW(), t_wait = 0, t_bfly = 0, t_ballot = 0,
+                     t_sink = 0;
 #endif
   const double clampv = max_d + 1e-5;
   for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
@@ -1047,6 +1048,9 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
   int off1 = R > 1 ? roff[1] : 0;
   if (PF && R > 0) load_row(roff[0], nx);
   for (int cur = 0; cur < R; cur++) {
+#ifdef BX_PHASE_TIMING
+    unsigned long long t_r0 = SS_NOW();
+#endif
     if (!PF) load_row(roff[cur], nx);
     // scipy's minVal + cost - u[cur] - v[j] with minVal = u[cur] = 0 (up to the sign of a zero,
     // which no comparison and no later sum can tell).  A NaN cost stays NaN here and loses every
@@ -1057,11 +1061,27 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     double lmin = rv[0];
 #pragma unroll
     for (int q = 1; q < LQ; q++) lmin = fmin(lmin, rv[q]);
+#ifdef BX_PHASE_TIMING
+    asm volatile("" ::"v"(lmin));
+    {
+      const unsigned long long t = SS_NOW();
+      t_wait += t - t_r0;
+      t_r0 = t;
+    }
+#endif
     if (PF && cur + 1 < R) {  // the next row in flight during this one's reductions
       load_row(off1, nx);
       off1 = cur + 2 < R ? roff[cur + 2] : 0;
     }
     const double m0 = wave_min_bfly(lmin);
+#ifdef BX_PHASE_TIMING
+    asm volatile("" ::"v"(m0));
+    {
+      const unsigned long long t = SS_NOW();
+      t_bfly += t - t_r0;
+      t_r0 = t;
+    }
+#endif
     if (!(m0 < INF)) {  // infeasible (cannot happen with finite costs)
       if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
       return 0;
@@ -1075,6 +1095,14 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       cnt += __popcll(e);
       if (e) q0 = q, e0 = e;
     }
+#ifdef BX_PHASE_TIMING
+    asm volatile("" ::"s"(cnt));
+    {
+      const unsigned long long t = SS_NOW();
+      t_ballot += t - t_r0;
+      t_r0 = t;
+    }
+#endif
     int j0;
     bool sink;
     if (cnt == 1) {  // a unique minimum (the usual case)
@@ -1100,6 +1128,9 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
         w.row4col[j0] = cur;
         w.col4row[cur] = j0;
       }
+#ifdef BX_PHASE_TIMING
+      t_sink += SS_NOW() - t_r0;
+#endif
       continue;
     }
 #ifdef BX_PHASE_TIMING
@@ -1244,6 +1275,10 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
   __syncthreads();
 #ifdef BX_PHASE_TIMING
   SCOUNT(10, t_slow);
+  SCOUNT(12, t_wait);
+  SCOUNT(13, t_bfly);
+  SCOUNT(14, t_ballot);
+  SCOUNT(15, t_sink);
   SCOUNT(11, SS_NOW() - t_all);
 #endif
   if (tr) {  // argsort(col4row): pairs ordered by the original row

@@ -242,6 +242,30 @@ class Engine:
                 "is_activated": act[:n].astype(bool), "frame_id": fid[:n],
                 "start_frame": sf[:n], "mean": mean[:n], "covariance": cov[:n]}
 
+    def class_tracks(self, seq: int, n_classes: int) -> list:
+        """per_class mode: each class's active list (``per_class_active_tracks``), as
+        ``tracks``-style dicts in class order."""
+        cap = self.track_cap
+        off = np.zeros(n_classes + 1, np.int32)
+        ids = np.zeros(cap, np.int32)
+        st = np.zeros(cap, np.int32)
+        act = np.zeros(cap, np.int32)
+        fid = np.zeros(cap, np.int32)
+        sf = np.zeros(cap, np.int32)
+        mean = np.zeros((cap, 8))
+        cov = np.zeros((cap, 8, 8))
+        N.check(self._L.bx_engine_class_tracks_host(
+            self._h, seq, n_classes, cap, off.ctypes.data, ids.ctypes.data, st.ctypes.data,
+            act.ctypes.data, fid.ctypes.data, sf.ctypes.data, mean.ctypes.data, cov.ctypes.data),
+            "class_tracks")
+        out = []
+        for c in range(n_classes):
+            a, b = int(off[c]), int(off[c + 1])
+            out.append({"n_active": b - a, "n_lost": 0, "id": ids[a:b], "state": st[a:b],
+                        "is_activated": act[a:b].astype(bool), "frame_id": fid[a:b],
+                        "start_frame": sf[a:b], "mean": mean[a:b], "covariance": cov[a:b]})
+        return out
+
     def state_set(self, seq: int, ids, mean=None, covariance=None) -> None:
         """Write the Kalman mean [n,8] / covariance [n,8,8] of live tracks by id (host code
         editing STrack.mean / .covariance in the reference)."""

@@ -115,11 +115,21 @@ class BaseTracker:
         self.asso_func_name = asso_func + "_obb" if is_obb else asso_func
         self.is_obb = is_obb
         self.frame_count = 0
-        self.per_class_active_tracks = None
         self._first_frame_processed = False
         self._first_dets_processed = False
         if self.max_age >= self.max_obs:
             self.max_obs = self.max_age + 5
+
+    @property
+    def per_class_active_tracks(self):
+        """basetracker.py:52-60,181-192: with per_class, {class id: the active list that class's
+        last update left}; None otherwise.  Read from the engine (``_class_active_lists``)."""
+        if not self.per_class:
+            return None
+        return dict(enumerate(self._class_active_lists()))
+
+    def _class_active_lists(self) -> list:
+        return [[] for _ in range(self.nr_classes)]
 
     # -------------------------------------------------------------------- reference decorators
     @staticmethod
@@ -191,10 +201,20 @@ class BaseTracker:
         raise NotImplementedError
 
     # ------------------------------------------------------------------------ engine helpers
+    @staticmethod
+    def _views(snap, box_fn):
+        return [TrackView(snap["id"][k], snap["state"][k], snap["is_activated"][k],
+                          snap["frame_id"][k], snap["start_frame"][k], snap["mean"][k],
+                          snap["covariance"][k], box_fn)
+                for k in range(snap["id"].shape[0])]
+
     def _track_views(self, engine, box_fn):
         snap = engine.tracks(0)
-        views = [TrackView(snap["id"][k], snap["state"][k], snap["is_activated"][k],
-                           snap["frame_id"][k], snap["start_frame"][k], snap["mean"][k],
-                           snap["covariance"][k], box_fn)
-                 for k in range(snap["id"].shape[0])]
+        views = self._views(snap, box_fn)
         return views[: snap["n_active"]], views[snap["n_active"]:]
+
+    def _class_track_views(self, engine, box_fn):
+        """ByteTrack / BoT-SORT per_class: every class's active list (parked or current)."""
+        if engine is None:
+            return [[] for _ in range(self.nr_classes)]
+        return [self._views(snap, box_fn) for snap in engine.class_tracks(0, self.nr_classes)]

@@ -56,7 +56,7 @@ class BoostTrack(BaseTracker):
                  with_reid: bool = False, per_class: bool = False, track_cap: int = 256,
                  det_cap: int = 256):
         super().__init__(per_class=per_class)
-        self.active_tracks = []
+        self._out_ids = {}  # class call -> ids of the trackers it output (its active_tracks)
         self.frame_count = 0
         self.max_age = max_age
         self.min_hits = min_hits
@@ -135,7 +135,32 @@ class BoostTrack(BaseTracker):
                 warp = _boost_warp(self.cmc.apply(img, _with_index(dets)))
             out = self.engine.update_host(0, dets, embs if self.with_reid else None, warp)
         self._engine_ids = BoostTrack._id_count = self.engine.counters(0)["id_count"]
+        # active_tracks = the trackers a call output (boosttrack.py:320-329); an output row's
+        # class is its call's class (only trackers updated or born in the call are output)
+        if self.per_class:
+            self._out_ids = {c: out[out[:, 6] == c, 4].astype(np.int64) for c in
+                             np.unique(out[:, 6]).astype(np.int64)}
+        else:
+            self._out_ids = {0: out[:, 4].astype(np.int64)}
         return out if out.shape[0] else np.empty((0, 8))
+
+    def _output_trackers(self, c):
+        ids = self._out_ids.get(c)
+        if ids is None or not len(ids):
+            return []
+        # the reference keeps the tracker objects a class call output even when a later class
+        # call of the same frame drops them (D10: every call predicts every tracker, so a tracker
+        # unmatched for max_age calls dies mid-frame); those come back with no live state
+        by_id = {int(t["id"]): t for t in self.trackers}
+        return [by_id.get(int(i), {"id": np.int32(i), "x": None, "P": None}) for i in ids]
+
+    @property
+    def active_tracks(self):
+        """The trackers the last update output (per_class: the last class call's)."""
+        return self._output_trackers(self.nr_classes - 1 if self.per_class else 0)
+
+    def _class_active_lists(self):
+        return [self._output_trackers(c) for c in range(self.nr_classes)]
 
     @property
     def trackers(self):

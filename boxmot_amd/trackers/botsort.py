@@ -95,6 +95,9 @@ class BotSort(BaseTracker):
     def active_tracks(self):
         return [] if self.engine is None else self._track_views(self.engine, _xywh_box)[0]
 
+    def _class_active_lists(self):
+        return self._class_track_views(self.engine, _xywh_box)
+
     @property
     def lost_stracks(self):
         return [] if self.engine is None else self._track_views(self.engine, _xywh_box)[1]

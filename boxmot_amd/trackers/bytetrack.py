@@ -69,6 +69,9 @@ class ByteTrack(BaseTracker):
     def active_tracks(self):
         return self._track_views(self.engine, _xyah_box)[0]
 
+    def _class_active_lists(self):
+        return self._class_track_views(self.engine, _xyah_box)
+
     @property
     def lost_stracks(self):
         return self._track_views(self.engine, _xyah_box)[1]

@@ -82,6 +82,14 @@ class OcSort(BaseTracker):
 
     @property
     def active_tracks(self):
-        """Track list snapshot: ids and XYSR Kalman state (x [7], P [7, 7]) per track."""
-        snap = self.engine.tracks(0)
+        """Track list snapshot: ids and XYSR Kalman state (x [7], P [7, 7]) per track (per_class:
+        the list of the class that ran last, as the reference's swap leaves it)."""
+        return self._seq_tracks(self.nr_classes - 1 if self.per_class else 0)
+
+    def _seq_tracks(self, q):
+        snap = self.engine.tracks(q)
         return [{"id": int(i), "x": x, "P": p} for i, x, p in zip(snap["id"], snap["x"], snap["P"])]
+
+    def _class_active_lists(self):
+        # class c is engine sequence c
+        return [self._seq_tracks(c) for c in range(self.nr_classes)]

@@ -171,6 +171,14 @@ int bx_engine_set_id_count(bx_engine *e, int seq, int id_count, void *stream);
 int bx_engine_tracks_host(bx_engine *e, int seq, int cap, int32_t *ids, int32_t *state,
                           int32_t *is_activated, int32_t *frame_id, int32_t *start_frame,
                           double *mean, double *cov, int *n_active, int *n_lost);
+/* per_class mode: the active list of every class (basetracker.py:52-60,181-192
+ * `per_class_active_tracks`), concatenated in class order; cls_off [n_classes+1] receives the
+ * list offsets, the other arrays as in bx_engine_tracks_host (cap rows each).  All lists are empty
+ * before the first bx_engine_update_classes_host of the sequence. */
+int bx_engine_class_tracks_host(bx_engine *e, int seq, int n_classes, int cap, int32_t *cls_off,
+                                int32_t *ids, int32_t *state, int32_t *is_activated,
+                                int32_t *frame_id, int32_t *start_frame, double *mean,
+                                double *cov);
 /* Write the Kalman state of live tracks (host, synchronous), addressed by track id: mean [n][8],
  * cov [n][64] (either may be NULL).  What host code does to `STrack.mean` / `.covariance` in
  * the reference (the objects are plain attributes: bytetrack.py:40-53 / botsort_track.py:75-104

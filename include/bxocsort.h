@@ -99,7 +99,8 @@ int bx_ocsort_counters_host(bx_ocsort *e, int seq, int *frame_count, int *id_cou
  * Python drop-in mirrors it through this. */
 int bx_ocsort_set_id_count(bx_ocsort *e, int seq, int id_count, void *stream);
 /* Track list of a sequence in list order (host, synchronous): ids [cap], Kalman means x
- * [cap][7] and covariances p [cap][49] (any may be NULL); *n = number of tracks. */
+ * [cap][7] and covariances p [cap][49] (any may be NULL); *n = number of tracks.  A sequence
+ * driven by bx_ocsort_update_classes_host reports class-global ids (output id - 1). */
 /* Frame size (w, h) of a sequence — BaseTracker latches img.shape on the first frame. */
 int bx_ocsort_set_frame_size(bx_ocsort *e, int seq, double w, double h, void *stream);
 int bx_ocsort_tracks_host(bx_ocsort *e, int seq, int cap, int32_t *ids, double *x, double *p,

@@ -11,8 +11,8 @@ import numpy as np
 import pytest
 
 from oracle import pyoracle as po
-from tests.golden_util import (compare_outputs, fixture_crash, fixture_frames, fixture_tracker_args,
-                               fixture_warp)
+from tests.golden_util import (compare_outputs, fixture_crash, fixture_frames, fixture_id,
+                               fixture_tracker_args, fixture_warp)
 
 pytestmark = pytest.mark.gpu
 
@@ -416,8 +416,11 @@ def make_dropin(kind, args):
     return BotSort(reid_weights=None, device="cuda", half=False, **args)
 
 
-@pytest.mark.parametrize("path", TRK_FIXTURES, ids=lambda p: Path(p).stem[4:])
+@pytest.mark.parametrize("path", TRK_FIXTURES, ids=fixture_id)
 def test_tracker_fixture_parity(torch_cuda, path):
+    """Every tracker fixture through the drop-in: bitwise vs the oracle each frame, and vs the
+    reference capture (ids/det_ind/cls exact, boxes 1e-9).  Ids ending "parity-unpinned-ties<N>"
+    are fixtures whose tie order comes from the restated lapjv (golden_util.fixture_id)."""
     fx = np.load(path)
     kind, args = fixture_tracker_args(fx)
     # C4 size ("large"): the drop-in starts at its default capacities and grows to 1024 objects

@@ -9,8 +9,8 @@ import numpy as np
 import pytest
 
 from oracle import pyoracle as po
-from tests.golden_util import (compare_outputs, fixture_crash, fixture_frames, fixture_tracker_args,
-                               fixture_warp)
+from tests.golden_util import (compare_outputs, fixture_crash, fixture_frames, fixture_id,
+                               fixture_tracker_args, fixture_warp)
 
 GOLDEN = __import__("pathlib").Path(__file__).parent / "golden"
 
@@ -158,8 +158,10 @@ def test_linear_assignment_empty():
 
 @pytest.mark.parametrize(
     "path", sorted(glob.glob(str(__import__("pathlib").Path(__file__).parent / "golden" / "trk_*.npz"))),
-    ids=lambda p: p.rsplit("/", 1)[-1][4:-4])
+    ids=fixture_id)
 def test_tracker_fixture(path):
+    """Oracle vs reference capture.  Ids ending "parity-unpinned-ties<N>": N tie-sensitive LAP
+    calls resolved by the restated lapjv (tie order unpinned against a lapx binary)."""
     fx = np.load(path)
     kind, args = fixture_tracker_args(fx)
     if kind not in ("ocsort", "boosttrack") and "tie_order" not in fx.files:

@@ -23,7 +23,8 @@ PHASES = ["setup", "crowd", "camera+quality+sort+predict", "lists", "stage1 casc
           "partial_fit", "masks+outputs"]
 COUNTERS = ["cost build cyc", "lsap cyc", "lsap calls", "sum rows (tracks)", "sum cols (dets)",
             "dijkstra steps", "matches", "solver rows R", "solver cols CC", "slow rows",
-            "slow-row cyc", "lsap loop cyc"]
+            "slow-row cyc", "lsap loop cyc", "fast: wait+relax cyc",
+            "fast: wave min cyc", "fast: ballots cyc", "fast: tie/sink to next row cyc"]
 
 
 def build():
