@@ -362,14 +362,16 @@ __device__ __forceinline__ void det_measurement(const float* r, double* meas) {
 #define BX_K1_DETS 8
 #endif
 constexpr int K1_DETS = BX_K1_DETS;  // detections per K1 block (2 per wave)
-template <typename FT, bool NPF>
+// FC: the feature width when it is a compile-time constant (REG_F: bounds tests and per-element
+// addressing fold away, measured ~1/3 of the row's VALU instructions), else 0 (P.F).
+template <typename FT, bool NPF, int FC>
 __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
                                                          const float* __restrict__ dets,
                                                          const int* __restrict__ det_off,
                                                          const FT* __restrict__ embs) {
   __shared__ __align__(16) float s_w[NWAVE * REG_FP];
   const int b = blockIdx.x, s = seq0 + b, w = wave_id(), lane = lane_id();
-  const int F = P.F, D = P.D;
+  const int F = FC ? FC : P.F, D = P.D;
   const int d0 = det_off[b], N = min(det_off[b + 1] - d0, D);
   const int k0 = blockIdx.y * K1_DETS, k1 = min(k0 + K1_DETS, N);
   if (k0 >= N) return;  // block-uniform
@@ -512,13 +514,13 @@ __device__ __forceinline__ void load4(const FT* p, FT* v) {
     v[0] = t0.x; v[1] = t0.y; v[2] = t1.x; v[3] = t1.y;
   }
 }
-template <typename FT>
+template <typename FT, int FC>
 __global__ __launch_bounds__(WG) void cosine_kernel(Dev P, int seq0, const int* __restrict__ det_off,
                                                     const FT* __restrict__ embs) {
   constexpr int KR = COS_P / 8;  // row pieces per lane on each side (A: tracks, B: detections)
   // row stride COS_CH + 2: the 32 chain lanes (pair p, parity) read banks 2p + parity
   __shared__ float s_a[NWAVE][COS_P][COS_CH + 2], s_b[NWAVE][COS_P][COS_CH + 2];
-  const int b = blockIdx.x, s = seq0 + b, T = P.T, D = P.D, F = P.F, w = wave_id(),
+  const int b = blockIdx.x, s = seq0 + b, T = P.T, D = P.D, F = FC ? FC : P.F, w = wave_id(),
             lane = lane_id();
   const int np = P.npair[s], d0 = det_off[b];
   const uint32_t* pairs = P.pairs + (size_t)s * T * D;
@@ -1477,12 +1479,12 @@ __global__ __launch_bounds__(WG) void update_kernel(Dev P, int seq0, const float
 #define BX_FEAT_BLOCKS 16
 #endif
 constexpr int FEAT_BLOCKS = BX_FEAT_BLOCKS;
-template <typename FT, bool NPF>
+template <typename FT, bool NPF, int FC>
 __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
                                                      const int* __restrict__ det_off,
                                                      const FT* __restrict__ embs) {
   __shared__ __align__(16) float s_w[NWAVE * REG_FP];
-  const int b = blockIdx.x, s = seq0 + b, F = P.F, D = P.D, T = P.T, lane = lane_id();
+  const int b = blockIdx.x, s = seq0 + b, F = FC ? FC : P.F, D = P.D, T = P.T, lane = lane_id();
   const int nrec = P.seq[(size_t)s * SQ_STRIDE + SQ_NREC];
   const FT a = (FT)0.9, bb = (FT)(1.0 - 0.9);
   float* wb = s_w + wave_id() * REG_FP;
@@ -1863,10 +1865,25 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
   const bool gmc = KIND == KIND_BOT && warps;
   // K1 on the side stream, submitted first (measured: 0.644 ms/step; submitted after K2/K1b
   // 0.647; serial on the main stream 0.661)
-  if (reid)
+  // the common width (512, the bench's and osnet's) as a compile-time constant
+// Compile-time feature width (REG_F) per kernel, bit 0 K1, bit 1 K5, bit 2 K1c.  K1 only: at C3
+// K1 0.124 -> 0.104 ms and the step 0.602 -> 0.593; a faster K5 (0.226 -> 0.18) took the GPU from
+// K4 / K6 beside it and the step went to 0.633 (K5 submitted after K4, capped by LDS reservation,
+// or on a lower-priority stream: no better); K1c unchanged (its loops were already fixed-stride).
+#ifndef BX_FC_MASK
+#define BX_FC_MASK 1
+#endif
+  const bool fc = NPF && d.F == REG_F && (BX_FC_MASK & 1);
+  const bool fc5 = NPF && d.F == REG_F && (BX_FC_MASK & 2);
+  if (reid && fc)
     BX_PROBED_ON(BX_STAGE_DET_FEATURES, side,
-                 hipLaunchKernelGGL((det_feature_kernel<FT, NPF>), dim3(nseq, gy_det64), dim3(WG),
-                                    0, side, d, seq0, dets, det_off, (const FT*)embs));
+                 hipLaunchKernelGGL((det_feature_kernel<FT, NPF, (NPF ? REG_F : 0)>),
+                                    dim3(nseq, gy_det64), dim3(WG), 0, side, d, seq0, dets,
+                                    det_off, (const FT*)embs));
+  else if (reid)
+    BX_PROBED_ON(BX_STAGE_DET_FEATURES, side,
+                 hipLaunchKernelGGL((det_feature_kernel<FT, NPF, 0>), dim3(nseq, gy_det64),
+                                    dim3(WG), 0, side, d, seq0, dets, det_off, (const FT*)embs));
   if (gmc)
     BX_PROBED(BX_STAGE_PREDICT,
               hipLaunchKernelGGL((predict_kernel<KIND, true>), dim3(nseq, gy_slot), dim3(WG), 0,
@@ -1881,10 +1898,14 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
               hipLaunchKernelGGL(gate_kernel<KIND>, dim3(nseq, GATE_BLOCKS), dim3(WG), glds, st,
                                  d, seq0, dets, det_off));
     if (int rc = join(0)) return rc;
-    if (d.F % COS_CH == 0)
+    if (d.F == REG_F && (BX_FC_MASK & 4))
       BX_PROBED(BX_STAGE_COSINE,
-                hipLaunchKernelGGL(cosine_kernel<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st, d,
-                                   seq0, det_off, (const FT*)embs));
+                hipLaunchKernelGGL((cosine_kernel<FT, REG_F>), dim3(nseq, COS_BLOCKS), dim3(WG), 0,
+                                   st, d, seq0, det_off, (const FT*)embs));
+    else if (d.F % COS_CH == 0)
+      BX_PROBED(BX_STAGE_COSINE,
+                hipLaunchKernelGGL((cosine_kernel<FT, 0>), dim3(nseq, COS_BLOCKS), dim3(WG), 0, st,
+                                   d, seq0, det_off, (const FT*)embs));
     else
       BX_PROBED(BX_STAGE_COSINE,
                 hipLaunchKernelGGL(cosine_kernel_any<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st,
@@ -1894,12 +1915,22 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
   if (int rc = lds_attr((const void*)assoc, e->lds_assoc)) return rc;
   BX_PROBED(BX_STAGE_ASSOC, hipLaunchKernelGGL(assoc, dim3(nseq), dim3(WG), e->lds_assoc, st, d,
                                                seq0, dets, det_off));
+  auto launch_k5 = [&]() -> int {
+    if (fc5)
+      BX_PROBED_ON(BX_STAGE_FEATURES, side,
+                   hipLaunchKernelGGL((feature_kernel<FT, NPF, (NPF ? REG_F : 0)>),
+                                      dim3(nseq, FEAT_BLOCKS), dim3(WG), 0, side, d, seq0,
+                                      det_off, (const FT*)embs));
+    else
+      BX_PROBED_ON(BX_STAGE_FEATURES, side,
+                   hipLaunchKernelGGL((feature_kernel<FT, NPF, 0>), dim3(nseq, FEAT_BLOCKS),
+                                      dim3(WG), 0, side, d, seq0, det_off, (const FT*)embs));
+    e->side_pending = true;  // until joined below (or, in overlap mode, by the next frame)
+    return BX_OK;
+  };
   if (reid) {
     if (int rc = fork(1)) return rc;
-    BX_PROBED_ON(BX_STAGE_FEATURES, side,
-                 hipLaunchKernelGGL((feature_kernel<FT, NPF>), dim3(nseq, FEAT_BLOCKS), dim3(WG),
-                                    0, side, d, seq0, det_off, (const FT*)embs));
-    e->side_pending = true;  // until joined below (or, in overlap mode, by the next frame)
+    if (int rc = launch_k5()) return rc;
   }
   BX_PROBED(BX_STAGE_UPDATE,
             hipLaunchKernelGGL(update_kernel<KIND>,
