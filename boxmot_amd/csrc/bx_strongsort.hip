@@ -574,14 +574,31 @@ __device__ void stable_sort_desc(int* idx, int n, K key, int* tmp, double* ks) {
     ks[i] = key(idx[i]);
   }
   __syncthreads();
-  for (int i = lane; i < n; i += 64) {
-    const double ki = ks[i];
-    int r = 0;
+  // rank of element i = #{j : key j before key i}; a lane ranks up to PB of its elements
+  // (i = i0 + lane + 64 q) against each broadcast key j, so the key list is read once per pass
+  // rather than once per element (C4: 514 keys, the sort was ~0.2 ms of one wave's loads)
+  constexpr int PB = 16;
+  for (int i0 = 0; i0 < n; i0 += 64 * PB) {
+    const int nq = (n - i0 + 63) / 64;  // wave-uniform
+    double ki[PB];
+    int r[PB];
+#pragma unroll
+    for (int q = 0; q < PB; q++) {
+      const int i = i0 + lane + 64 * q;
+      ki[q] = q < nq && i < n ? ks[i] : 0.0;
+      r[q] = 0;
+    }
     for (int j = 0; j < n; j++) {
       const double kj = ks[j];
-      r += (kj > ki) || (kj == ki && j < i);
+#pragma unroll
+      for (int q = 0; q < PB; q++)
+        if (q < nq) r[q] += (kj > ki[q]) || (kj == ki[q] && j < i0 + lane + 64 * q);
     }
-    idx[r] = tmp[i];
+#pragma unroll
+    for (int q = 0; q < PB; q++) {
+      const int i = i0 + lane + 64 * q;
+      if (q < nq && i < n) idx[r[q]] = tmp[i];
+    }
   }
   __syncthreads();
 }
@@ -906,7 +923,9 @@ __global__ void __launch_bounds__(64)
       using I2 = std::integral_constant<int, 2>;
       using I3 = std::integral_constant<int, 3>;
       using I4 = std::integral_constant<int, 4>;
-      if (ndt == NDT) {
+      // a partial last block runs one tile when that covers it (NDT = 2), else all NDT tiles
+      // (columns past n read row 0 and are not stored)
+      if (ndt == NDT || (NDT > 2 && ndt > 1)) {
         if (ntile == 4) run(I4{}, std::integral_constant<int, NDT>{});
         else if (ntile == 3) run(I3{}, std::integral_constant<int, NDT>{});
         else if (ntile == 2) run(I2{}, std::integral_constant<int, NDT>{});
@@ -2668,10 +2687,17 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   // packs per sequence <= listed tracks; a wave per (pack, detection-block split), waves looping
   // over packs past the grid; the detection blocks split over waves for ~4k waves in all
   const int gx = d.T < 4 ? d.T : (d.T + 3) / 4;
-  const int nblk = (d.D + 31) / 32;
+  // detection tiles per wave: 4 when the detection capacity is large (C4: 1024 slots, ~510
+  // dets; 0.68 -> 0.64 ms and fewer waves beside ss_pre_kernel on the side stream, step 2.44 ->
+  // 2.38 ms), 2 otherwise (256 x ~24 dets: 4 tiles pad 0.19 -> 0.25 ms)
+  const int ndt = d.D >= 256 ? 4 : 2;
+  const int nblk = (d.D + 16 * ndt - 1) / (16 * ndt);
   int zb = (int)((4096 + (long)gx * nseq - 1) / ((long)gx * nseq));
   zb = zb < 1 ? 1 : (zb > nblk ? nblk : zb);
-  hipLaunchKernelGGL((ss_nn_kernel<2>), dim3(gx, nseq, zb), dim3(64), 0, st, d, seq0, off);
+  if (ndt == 4)
+    hipLaunchKernelGGL((ss_nn_kernel<4>), dim3(gx, nseq, zb), dim3(64), 0, st, d, seq0, off);
+  else
+    hipLaunchKernelGGL((ss_nn_kernel<2>), dim3(gx, nseq, zb), dim3(64), 0, st, d, seq0, off);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 1, st))) return rc;
   if ((rc = ss_probe_begin(e, 2, st))) return rc;
