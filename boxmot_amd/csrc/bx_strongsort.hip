@@ -2690,12 +2690,17 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   // detection tiles per wave: 4 when the detection capacity is large (C4: 1024 slots, ~510
   // dets; 0.68 -> 0.64 ms and fewer waves beside ss_pre_kernel on the side stream, step 2.44 ->
   // 2.38 ms), 2 otherwise (256 x ~24 dets: 4 tiles pad 0.19 -> 0.25 ms)
-  const int ndt = d.D >= 256 ? 4 : 2;
+#ifndef BX_SS_NDT
+#define BX_SS_NDT 4
+#endif
+  const int ndt = d.D >= 256 ? BX_SS_NDT : 2;
   const int nblk = (d.D + 16 * ndt - 1) / (16 * ndt);
   int zb = (int)((4096 + (long)gx * nseq - 1) / ((long)gx * nseq));
   zb = zb < 1 ? 1 : (zb > nblk ? nblk : zb);
   if (ndt == 4)
     hipLaunchKernelGGL((ss_nn_kernel<4>), dim3(gx, nseq, zb), dim3(64), 0, st, d, seq0, off);
+  else if (ndt == 3)
+    hipLaunchKernelGGL((ss_nn_kernel<3>), dim3(gx, nseq, zb), dim3(64), 0, st, d, seq0, off);
   else
     hipLaunchKernelGGL((ss_nn_kernel<2>), dim3(gx, nseq, zb), dim3(64), 0, st, d, seq0, off);
   SCHK(hipGetLastError());
