@@ -41,13 +41,16 @@ def output_checksum(rows: np.ndarray) -> float:
     return float((r[:, 4] * w).sum() + (r[:, 7] * 0.5 * w).sum() + r[:, :4].sum() * 1e-3)
 
 
-def gather_records(records: np.ndarray, dist=None, device=None) -> np.ndarray:
+def gather_records(records: np.ndarray, dist=None, device=None, collective: bool = False
+                   ) -> np.ndarray:
     """All-gather per-sequence float64 records [n_local, k] of every rank (variable n_local):
-    sizes first, then padded payloads.  Returns the concatenation in rank order."""
+    sizes first, then padded payloads.  Returns the concatenation in rank order.  A single rank
+    returns its records without a collective unless `collective` (the one-GPU test of the RCCL
+    path)."""
     import torch
 
     rec = np.ascontiguousarray(records, np.float64)
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if dist is None or not dist.is_initialized() or (dist.get_world_size() == 1 and not collective):
         return rec
     world = dist.get_world_size()
     k = rec.shape[1]

@@ -189,3 +189,26 @@ def test_sharded_engine_run_equals_oracle(kind):
             ref.append(np.concatenate([np.full((o.shape[0], 1), t), o], 1))
         mine = got[got[:, 0] == g][:, 1:]
         np.testing.assert_array_equal(mine, np.concatenate(ref, 0), err_msg=f"{kind} seq {g}")
+
+
+@pytest.mark.gpu
+def test_gather_records_over_rccl_single_gpu():
+    """The RCCL ("nccl" backend) branch of gather_records, on the one GPU a box has: a world of
+    one rank still runs both all_gathers (sizes, then the padded payload) on the device."""
+    import torch
+    import torch.distributed as dist
+
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test collected without a HIP device")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0,
+                            world_size=1)
+    try:
+        rng = np.random.default_rng(7)
+        for n in (0, 1, 37):
+            recs = rng.standard_normal((n, 3))
+            got = gather_records(recs, dist, torch.device("cuda", 0), collective=True)
+            np.testing.assert_array_equal(got, recs)
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
