@@ -409,6 +409,10 @@ def main():
                     help="sequences per GPU (default 1024; strongsort 256, strongsort_c4 1)")
     ap.add_argument("--chunk", type=int, default=0,
                     help="sequences per pipeline launch (0 = all; BoT-SORT/ByteTrack)")
+    ap.add_argument("--track-cap", type=int, default=512,
+                    help="BoT-SORT/ByteTrack engine track slots per sequence")
+    ap.add_argument("--det-cap", type=int, default=256,
+                    help="BoT-SORT/ByteTrack engine detection slots per sequence")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
                     help="join each step's feature EMA before it returns (bx_engine_set_overlap off)")
@@ -473,7 +477,7 @@ def main():
                            params=OcsortParams(**params))
         stages = []
     else:
-        eng = Engine(kind, n_seq=S, track_cap=512, det_cap=256, emb_dim=F,
+        eng = Engine(kind, n_seq=S, track_cap=args.track_cap, det_cap=args.det_cap, emb_dim=F,
                      params=EngineParams(**params))
         # every step's inputs are their own resident tensors, so the feature EMA may stay
         # unjoined into the next step (bx_engine_set_overlap)
