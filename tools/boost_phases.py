@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--seqs", type=int, default=1024)
     ap.add_argument("--frames", type=int, default=60)
     ap.add_argument("--no-build", action="store_true")
+    ap.add_argument("--c5", action="store_true", help="the boosttrack_mot8 sequences (MOT dets)")
     a = ap.parse_args()
     if not a.no_build:
         build()
@@ -48,15 +49,39 @@ def main():
     from boxmot_amd.engine import BoostEngine, BoostParams
     from boxmot_amd.synth import TorchSceneBatch
 
-    kind, n_obj, F, params = CONFIGS["boosttrack"]
-    eng = BoostEngine(n_seq=a.seqs, track_cap=128, det_cap=max(64, n_obj), emb_dim=F,
-                      params=BoostParams(**params))
-    gen = TorchSceneBatch(a.seqs, n_obj, emb_dim=F, seed=7, device="cuda", conf_lo=OCS_CONF_LO)
+    kind, n_obj, F, params = CONFIGS["boosttrack_mot8" if a.c5 else "boosttrack"]
+    if a.c5:  # bench.py's C5 frames: MOT17-02/04 public detections + 6 synthetic sequences
+        from bench import MOT_DETS
+        from boxmot_amd.synth import c5_sequences
+
+        seqs = c5_sequences(MOT_DETS, F)
+        a.seqs = len(seqs)
+        a.frames = min(a.frames, min(nf for _, _, nf in seqs))
+
+        def c5_frame(t):
+            fr = [sc.frame(t) for _, sc, _ in seqs]
+            off = np.zeros(a.seqs + 1, np.int32)
+            off[1:] = np.cumsum([f[0].shape[0] for f in fr])
+            d = np.concatenate([f[0] for f in fr], 0).astype(np.float32)
+            e = np.concatenate([f[1] for f in fr], 0).astype(np.float64)
+            return (torch.from_numpy(d).cuda(), torch.from_numpy(off).cuda(),
+                    torch.from_numpy(e).cuda())
+
+        frames = [c5_frame(t) for t in range(1, a.frames + 1)]
+        dmax = max(int((f[1][1:] - f[1][:-1]).max().item()) for f in frames)
+        eng = BoostEngine(n_seq=a.seqs, track_cap=256, det_cap=max(64, dmax), emb_dim=F,
+                          params=BoostParams(**params))
+        n_obj = dmax
+    else:
+        eng = BoostEngine(n_seq=a.seqs, track_cap=128, det_cap=max(64, n_obj), emb_dim=F,
+                          params=BoostParams(**params))
+        gen = TorchSceneBatch(a.seqs, n_obj, emb_dim=F, seed=7, device="cuda",
+                              conf_lo=OCS_CONF_LO)
+        frames = [(d, o, e.double()) for d, o, e in (gen.frame(t) for t in range(1, a.frames + 1))]
     L = N.load()
     L.bx_boost_debug_host.argtypes = [C.c_void_p, C.c_void_p]
     out = torch.empty((a.seqs * n_obj, 8), dtype=torch.float64, device="cuda")
     cnt = torch.empty(a.seqs, dtype=torch.int32, device="cuda")
-    frames = [(d, o, e.double()) for d, o, e in (gen.frame(t) for t in range(1, a.frames + 1))]
     torch.cuda.synchronize()
     for d, off, e in frames:
         eng.step(d, off, e, None, out, cnt)
