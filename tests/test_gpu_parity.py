@@ -1137,10 +1137,10 @@ def test_strongsort_c4_size_vs_oracle(torch_cuda):
     every frame and the final Kalman state bitwise against the oracle (sort/tracker.py:183-281)."""
     from boxmot_amd.synth import SyntheticScene
 
-    import bench
+    from boxmot_amd.workloads import CONFIGS, SS_C4_CAPS
 
-    _, n_obj, F, params = bench.CONFIGS["strongsort_c4"]
-    caps = bench.SS_C4_CAPS
+    _, n_obj, F, params = CONFIGS["strongsort_c4"]
+    caps = SS_C4_CAPS
     sc = SyntheticScene(n_obj=n_obj, seed=41, emb_dim=F, emb_dtype=np.float64, conf_lo=0.3)
     eng = run_ss_batched(torch_cuda, [sc], 16, dict(params), F, track_cap=caps["track_cap"],
                          det_cap=caps["det_cap"], vec_cap=caps["vec_cap"])
