@@ -430,8 +430,11 @@ def main():
     n_probe = len(stages)
     t_first = args.warmup + n_probe
     total = t_first + args.steps
+    # after the timed steps, one more probe step per stage: the stages at the timed frames' state
+    # (StrongSort's galleries, for one, are still filling during the early probes)
+    n_frames = total + n_probe
     if c5:
-        if total > min(c5seqs[g][2] for g in c5_mine):
+        if n_frames > min(c5seqs[g][2] for g in c5_mine):
             raise SystemExit("boosttrack_mot8: warmup + probes + steps exceed the shortest "
                              "sequence (600 frames)")
 
@@ -443,12 +446,12 @@ def main():
             e = np.concatenate([f[1] for f in fr], 0).astype(np.float64)
             return (torch.from_numpy(d).to(dev), torch.from_numpy(off).to(dev),
                     torch.from_numpy(e).to(dev))
-        frames = [c5_frame(t) for t in range(1, total + 1)]  # resident in HBM before timing
+        frames = [c5_frame(t) for t in range(1, n_frames + 1)]  # resident in HBM before timing
         layout = "MOT17-02/04 public dets + synthetic"
     else:
         gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev, layout=layout,
                               **(dict(conf_lo=OCS_CONF_LO) if ocs or bst or sss else {}))
-        frames = [gen.frame(t) for t in range(1, total + 1)]  # resident in HBM before timing
+        frames = [gen.frame(t) for t in range(1, n_frames + 1)]  # resident in HBM before timing
     if bst:  # BoostTrack consumes float64 embeddings (the dtype `boxmot eval` loads)
         frames = [(d, o, e.double()) for d, o, e in frames]
     if sss:  # StrongSort: float64 detections (no setup_decorator rounding) and embeddings
@@ -520,6 +523,15 @@ def main():
     off_h = [frames[k][1].cpu().numpy() for k in range(t_first, total)]
     dets_seq = np.sum([np.diff(o) for o in off_h], 0)
     last_off, cnt_h, out_h = off_h[-1], cnt.cpu().numpy(), out.cpu().numpy()
+    # untimed, after the timed region and its outputs: one probe step per stage at the timed
+    # frames' state (StrongSort's galleries, for one, are still filling during the early probes)
+    stage_ms_late = {}
+    for j in range(n_probe):
+        eng.probe(stages[j])
+        step(total + j)
+        stage_ms_late[stages[j]] = eng.probe_read()[0]
+        eng.probe(None)
+    torch.cuda.synchronize()
     recs = np.zeros((S, 7))
     for i, g in enumerate(c5_mine if c5 else shard_sequences(S * world, world, rank)):
         rows_i = out_h[last_off[i]: last_off[i] + cnt_h[i]]
@@ -579,7 +591,9 @@ def main():
                          "launches_per_step": len(bounds),
                          "algorithmic_bytes_per_launch": int(per_launch),
                          "units_last_frame": units,
-                         "stage_ms_probe": {k: round(v, 4) for k, v in stage_ms.items()}},
+                         "stage_ms_probe": {k: round(v, 4) for k, v in stage_ms.items()},
+                         "stage_ms_after_timed": {k: round(v, 4)
+                                                  for k, v in stage_ms_late.items()}},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
