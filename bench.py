@@ -355,6 +355,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
                     help="join each step's feature EMA before it returns (bx_engine_set_overlap off)")
+    ap.add_argument("--start-frame", type=int, default=0,
+                    help="first timed frame (raises the warm-up so the timed frames start there: "
+                         "StrongSort C4 at gallery steady state)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--dropin", action="store_true",
@@ -383,79 +386,37 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from boxmot_amd.engine import (BoostEngine, BoostParams, Engine, EngineParams, OcsortEngine,
-                                   OcsortParams, SsEngine, SsParams)
     from boxmot_amd.shard import gather_records, output_checksum, shard_sequences
-    from boxmot_amd.synth import TorchSceneBatch
+    from boxmot_amd.workloads import BenchFrames, bench_engine
 
     kind, n_obj, F, params = CONFIGS[args.config]
     S = args.seqs if args.seqs is not None else DEFAULT_SEQS.get(args.config, 1024)
     c5 = args.config == "boosttrack_mot8"
-    if c5:  # a fixed set of 8 sequences, LPT-sharded by frame count (strong scaling)
-        from boxmot_amd.synth import c5_sequences
-
-        if world > C5_TOTAL:
-            raise SystemExit(f"boosttrack_mot8 has {C5_TOTAL} sequences: at most {C5_TOTAL} ranks")
-        c5seqs = c5_sequences(MOT_DETS, F)
-        c5_mine = shard_sequences([nf for _, _, nf in c5seqs], world, rank)
-        S = len(c5_mine)
+    # the input stream and the engine (shared with tests/test_bench_workload.py, which checks
+    # this exact workload against the oracle); C5: this rank's LPT shard of its 8 sequences
+    src = BenchFrames(args.config, S, dev, rank, world)
+    S = src.n_seq
+    c5_mine = src.mine
     ocs = kind == "ocsort"
     bst = kind == "boosttrack"
     sss = kind == "strongsort"
-    if sss:
-        eng = SsEngine(n_seq=S, emb_dim=F, params=SsParams(**params),
-                       **ss_caps(args.config, n_obj))
-        stages = list(SsEngine.STAGES)
-    elif bst:
-        eng = BoostEngine(n_seq=S, track_cap=128, det_cap=max(64, n_obj), emb_dim=F,
-                          params=BoostParams(**params))
-        stages = list(BoostEngine.STAGES)
-    elif ocs:
-        tcap = int(os.environ.get("BX_OCS_TRACK_CAP", max(64, 2 * n_obj)))
-        eng = OcsortEngine(n_seq=S, track_cap=tcap, det_cap=max(64, n_obj),
-                           params=OcsortParams(**params))
-        stages = []
-    else:
-        eng = Engine(kind, n_seq=S, track_cap=args.track_cap, det_cap=args.det_cap, emb_dim=F,
-                     params=EngineParams(**params))
-        # every step's inputs are their own resident tensors, so the feature EMA may stay
-        # unjoined into the next step (bx_engine_set_overlap)
-        eng.set_overlap(not args.no_overlap)
-        stages = [s for s in Engine.STAGES
-                  if F or s not in ("det_features", "gate", "cosine", "features")]
-    # this rank's shard: global sequences [rank*S, (rank+1)*S) — weak scaling, no exchange
-    layout = "crowded" if args.config.endswith("_crowded") else "grid"
-    # W warm-up steps, then one untimed probe step per pipeline stage (each stage timed once
-    # whatever W is), then the K timed steps
+    eng, stages = bench_engine(args.config, S, args.track_cap, args.det_cap,
+                               overlap=not args.no_overlap)
+    layout = src.layout
+    # W warm-up steps (at least start_frame - 1 - probes: the first timed frame), then one
+    # untimed probe step per pipeline stage (each stage timed once whatever W is), then the K
+    # timed steps
     n_probe = len(stages)
-    t_first = args.warmup + n_probe
+    warmup = max(args.warmup, args.start_frame - 1 - n_probe)
+    t_first = warmup + n_probe
     total = t_first + args.steps
     # after the timed steps, one more probe step per stage: the stages at the timed frames' state
     # (StrongSort's galleries, for one, are still filling during the early probes)
     n_frames = total + n_probe
-    if c5:
-        if n_frames > min(c5seqs[g][2] for g in c5_mine):
-            raise SystemExit("boosttrack_mot8: warmup + probes + steps exceed the shortest "
-                             "sequence (600 frames)")
-
-        def c5_frame(t):
-            fr = [c5seqs[g][1].frame(t) for g in c5_mine]
-            off = np.zeros(S + 1, np.int32)
-            off[1:] = np.cumsum([f[0].shape[0] for f in fr])
-            d = np.concatenate([f[0] for f in fr], 0).astype(np.float32)
-            e = np.concatenate([f[1] for f in fr], 0).astype(np.float64)
-            return (torch.from_numpy(d).to(dev), torch.from_numpy(off).to(dev),
-                    torch.from_numpy(e).to(dev))
-        frames = [c5_frame(t) for t in range(1, n_frames + 1)]  # resident in HBM before timing
-        layout = "MOT17-02/04 public dets + synthetic"
-    else:
-        gen = TorchSceneBatch(S, n_obj, emb_dim=F, seed=1000 + rank, device=dev, layout=layout,
-                              **(dict(conf_lo=OCS_CONF_LO) if ocs or bst or sss else {}))
-        frames = [gen.frame(t) for t in range(1, n_frames + 1)]  # resident in HBM before timing
-    if bst:  # BoostTrack consumes float64 embeddings (the dtype `boxmot eval` loads)
-        frames = [(d, o, e.double()) for d, o, e in frames]
-    if sss:  # StrongSort: float64 detections (no setup_decorator rounding) and embeddings
-        frames = [(d.double(), o, e.double()) for d, o, e in frames]
+    if c5 and n_frames > src.n_frames_max:
+        raise SystemExit("boosttrack_mot8: warmup + probes + steps exceed the shortest "
+                         "sequence (600 frames)")
+    frames = [src.frame(t) for t in range(1, n_frames + 1)]  # resident in HBM before timing
     max_n = max(int(f[1][-1].item()) for f in frames)
     out = torch.empty((max_n, 10 if kind == "strongsort" else 8), dtype=torch.float64, device=dev)
     cnt = torch.empty(S, dtype=torch.int32, device=dev)
@@ -482,7 +443,7 @@ def main():
     # warm-up, then the probe steps: each times one stage to find the dominant kernel
     stage_ms = {}
     for k in range(t_first):
-        j = k - args.warmup
+        j = k - warmup
         if j >= 0:
             eng.probe(stages[j])
         step(k)
@@ -517,6 +478,12 @@ def main():
     emb_bytes = 8 if bst or sss else 4
     if sss:
         units["seqs"] = S
+        # distinct gallery samples compared per queried track at the last timed frame
+        units["rows_per_queried_track"] = round(units["rows"] / max(units["queried"], 1), 2)
+    if kind in ("bytetrack", "botsort"):
+        # associations whose optimum was tied, re-solved in lapx's JV order, summed
+        # over all frames of this rank
+        units["lap_ties_all_frames"] = eng.lap_ties()
 
     # per-sequence records of this rank's shard: [global seq id, frames timed, dets timed,
     # rows of the last frame, checksum of the last frame, rank wall s, dominant-stage ms]
@@ -568,7 +535,7 @@ def main():
                     "traffic": traffic, "algorithmic_flops_per_launch": int(flops)}
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
+            "steps": args.steps, "warmup": warmup,
             "ms_per_step": round(t_max / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "strong" if c5 else "weak", "vs_baseline": None, "dtype": "f64",
             "data": ("MOT17-02/04 public detections (tests/golden/mot17_public_dets.npz) with "
@@ -584,6 +551,7 @@ def main():
                        "n_dets_mean": round(mean_d, 1), "feat_dim": F,
                        "emb_dtype": "f64" if emb_bytes == 8 else "f32",
                        "parallelism": f"seq-sharded x{world}",
+                       "timed_frames": [t_first + 1, total],
                        **({"feature_overlap": not args.no_overlap}
                           if kind == "botsort" and F else {})},
             "roofline": {**roof, "kernel": dominant,

@@ -426,9 +426,12 @@ __device__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync) {
   }
 }
 
-__device__ void jv_wave(const double* C, int nr, int nc, JvLds& w) {
-  jv_wave_t([&](int i, int j) { return cget(C, nr, nc, i, j); }, nr > nc ? nr : nc, w,
-            SyncBlock{});
+// sync: SyncBlock when `w` is in LDS (or the workgroup is this one wave and the state is in
+// LDS); SyncWaveG when the state is in global memory (its atomics' results are read back
+// through an invalidated L1)
+template <class SY = SyncBlock>
+__device__ void jv_wave(const double* C, int nr, int nc, JvLds& w, SY sync = SY{}) {
+  jv_wave_t([&](int i, int j) { return cget(C, nr, nc, i, j); }, nr > nc ? nr : nc, w, sync);
 }
 
 // ------------------------------------------------------------------------------------------

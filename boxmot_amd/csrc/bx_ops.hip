@@ -266,18 +266,26 @@ __global__ __launch_bounds__(OW) void lapjv_kernel(const double* cost, int nr, i
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = mode == 2 ? nr + nc : (nr > nc ? nr : nc);
   JvLds w = jv_bind(gst ? gst : smem, n);
-  if (mode == 2) {
-    const double half = lim / 2.;
-    jv_wave_t([&](int i, int j) {
-                return (i < nr && j < nc) ? cost[(size_t)i * nc + j]
-                                          : (i >= nr && j >= nc) ? 0.0 : half;
-              },
-              n, w, SyncBlock{});
-  } else if (n <= OW) {
-    jv_wave64(cost, nr, nc, w);
-  } else {
-    jv_wave(cost, nr, nc, w);
-  }
+  // state past the LDS lives in global memory: the solver's atomics (column ownership) run in
+  // L2, so their results are read back through an invalidated L1 (SyncWaveG)
+  auto solve = [&](auto sync) {
+    if (mode == 2) {
+      const double half = lim / 2.;
+      jv_wave_t([&](int i, int j) {
+                  return (i < nr && j < nc) ? cost[(size_t)i * nc + j]
+                                            : (i >= nr && j >= nc) ? 0.0 : half;
+                },
+                n, w, sync);
+    } else if (n <= OW) {
+      jv_wave64(cost, nr, nc, w);
+    } else {
+      jv_wave(cost, nr, nc, w, sync);
+    }
+  };
+  if (gst)
+    solve(SyncWaveG{});
+  else
+    solve(SyncBlock{});
   const bool cut = mode != 0;  // lapx: x >= n_cols -> -1, y >= n_rows -> -1, then [:nr] / [:nc]
   for (int i = threadIdx.x; i < nr; i += OW) x[i] = (cut && w.x[i] >= nc) ? -1 : w.x[i];
   for (int j = threadIdx.x; j < nc; j += OW) y[j] = (cut && w.y[j] >= nr) ? -1 : w.y[j];

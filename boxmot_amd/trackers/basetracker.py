@@ -15,7 +15,9 @@ import numpy as np
 def _with_index(dets: np.ndarray) -> np.ndarray:
     """dets with the detection-index column the reference appends before its CMC call
     (botsort.py:169, boosttrack.py:239)."""
-    d = np.asarray(dets).reshape(-1, np.asarray(dets).shape[-1] if np.asarray(dets).ndim else 6)
+    d = np.asarray(dets)
+    # an empty frame may arrive 1-D (np.array([])); normalised like class_warps does
+    d = d.reshape(-1, d.shape[-1]) if d.size and d.ndim else np.empty((0, 6))
     return np.hstack([d, np.arange(len(d)).reshape(-1, 1)])
 
 

@@ -72,3 +72,96 @@ def ss_caps(config, n_obj):
 
 
 OCS_CONF_LO = 0.3  # OCSort / BoostTrack scenes: confidences U(0.3, 1) -> ~40% below det_thresh
+
+
+def bench_engine(config, n_seq, track_cap=512, det_cap=256, overlap=True):
+    """The engine bench.py times for ``config`` with ``n_seq`` sequences per launch, and its
+    pipeline stages (the probe targets).  BoT-SORT / ByteTrack: ``track_cap`` / ``det_cap`` slots
+    and overlap mode (each step's feature EMA left unjoined: the caller keeps a step's inputs
+    alive until the next step is enqueued)."""
+    import os
+
+    from .engine import (BoostEngine, BoostParams, Engine, EngineParams, OcsortEngine,
+                         OcsortParams, SsEngine, SsParams)
+
+    kind, n_obj, F, params = CONFIGS[config]
+    if kind == "strongsort":
+        return (SsEngine(n_seq=n_seq, emb_dim=F, params=SsParams(**params),
+                         **ss_caps(config, n_obj)), list(SsEngine.STAGES))
+    if kind == "boosttrack":
+        return (BoostEngine(n_seq=n_seq, track_cap=128, det_cap=max(64, n_obj), emb_dim=F,
+                            params=BoostParams(**params)), list(BoostEngine.STAGES))
+    if kind == "ocsort":
+        tcap = int(os.environ.get("BX_OCS_TRACK_CAP", max(64, 2 * n_obj)))
+        return (OcsortEngine(n_seq=n_seq, track_cap=tcap, det_cap=max(64, n_obj),
+                             params=OcsortParams(**params)), [])
+    eng = Engine(kind, n_seq=n_seq, track_cap=track_cap, det_cap=det_cap, emb_dim=F,
+                 params=EngineParams(**params))
+    eng.set_overlap(overlap)
+    return eng, [s for s in Engine.STAGES
+                 if F or s not in ("det_features", "gate", "cosine", "features")]
+
+
+class BenchFrames:
+    """bench.py's input stream for ``config`` on ``device``: ``frame(t)`` (t = 1, 2, ... in order:
+    the GPU generator draws frames sequentially) -> ``(dets, det_off, embs)`` device tensors in
+    the dtypes the engine consumes (BoT-SORT / ByteTrack / OCSort: float32 detections, float32
+    embeddings; BoostTrack: float64 embeddings; StrongSort: float64 detections and embeddings).
+
+    Synthetic configs draw ``n_seq`` sequences from ``TorchSceneBatch(seed=1000 + rank)``; C5
+    (``boosttrack_mot8``) plays this rank's LPT shard of its eight sequences (``self.mine``, global
+    indices into ``self.c5``), so ``self.n_seq`` is that shard's size."""
+
+    def __init__(self, config, n_seq, device, rank=0, world=1):
+        import numpy as np
+
+        self.config, self.device = config, device
+        kind, n_obj, F, _ = CONFIGS[config]
+        self.kind, self.emb_dim = kind, F
+        self.c5 = self.mine = None
+        if config == "boosttrack_mot8":
+            from .shard import shard_sequences
+            from .synth import c5_sequences
+
+            if world > C5_TOTAL:
+                raise SystemExit(f"boosttrack_mot8 has {C5_TOTAL} sequences: at most {C5_TOTAL} "
+                                 "ranks")
+            self.c5 = c5_sequences(MOT_DETS, F)
+            self.mine = shard_sequences([nf for _, _, nf in self.c5], world, rank)
+            self.n_seq = len(self.mine)
+            self.n_frames_max = min(self.c5[g][2] for g in self.mine)
+            self.layout = "MOT17-02/04 public dets + synthetic"
+            self._np = np
+        else:
+            from .synth import TorchSceneBatch
+
+            self.n_seq = n_seq
+            self.n_frames_max = None
+            self.layout = "crowded" if config.endswith("_crowded") else "grid"
+            lo = kind in ("ocsort", "boosttrack", "strongsort")
+            self.gen = TorchSceneBatch(n_seq, n_obj, emb_dim=F, seed=1000 + rank, device=device,
+                                       layout=self.layout,
+                                       **(dict(conf_lo=OCS_CONF_LO) if lo else {}))
+        self._next = 1
+
+    def frame(self, t):
+        if t != self._next:
+            raise ValueError(f"frames are drawn in order: expected frame {self._next}, got {t}")
+        self._next += 1
+        if self.c5 is not None:
+            import torch
+
+            np = self._np
+            fr = [self.c5[g][1].frame(t) for g in self.mine]
+            off = np.zeros(self.n_seq + 1, np.int32)
+            off[1:] = np.cumsum([f[0].shape[0] for f in fr])
+            d = np.concatenate([f[0] for f in fr], 0).astype(np.float32)
+            e = np.concatenate([f[1] for f in fr], 0).astype(np.float64)
+            return (torch.from_numpy(d).to(self.device), torch.from_numpy(off).to(self.device),
+                    torch.from_numpy(e).to(self.device))
+        d, o, e = self.gen.frame(t)
+        if self.kind == "boosttrack":
+            e = e.double()
+        elif self.kind == "strongsort":
+            d, e = d.double(), e.double()
+        return d, o, e

@@ -589,6 +589,3 @@ class OracleTracker:
             free.get(self.kind, lib().bxo_free)(h)
             self.h = None
 
-
-def set_threads(n: int = 1):
-    os.environ.setdefault("OMP_NUM_THREADS", str(n))

@@ -1,0 +1,173 @@
+"""The workloads bench.py times, at their bench shape, checked against the oracle.
+
+Every other parity test drives the engines with `SyntheticScene` streams of a few sequences at
+test capacities.  These drive exactly what `bench.py` times — `workloads.BenchFrames` (the GPU
+`TorchSceneBatch` generator, or C5's eight MOT17 / synthetic sequences) into
+`workloads.bench_engine` (bench capacities, BoT-SORT overlap mode), with the bench's probe
+schedule (W warm-up steps, one probe step per stage, the dominant stage probed on every later
+step) and no host synchronisation between steps — and compare sampled sequences, spread over
+the batch, every frame bitwise with the C oracle fed the same device-generated inputs, then
+their Kalman state at the end.
+
+* C3 `botsort` (the driver-timed line): 1024 sequences, track_cap 512 / det_cap 256, overlap
+  mode, 60 frames (`trackers/botsort/botsort.py:94-166`).
+* C4 `strongsort_c4`: 1 sequence x 1024 objects x 2048-d at `SS_C4_CAPS`, 64 frames — past the
+  frame where the galleries' distinct samples per track stop growing
+  (`sort/linear_assignment.py:555-600`, `sort/tracker.py:166-178`).
+* C5 `boosttrack_mot8`: the 8 sequences on one GPU, 100 frames (`boosttrack.py:221-336`).
+"""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test collected without a HIP device")
+    from boxmot_amd import _native
+
+    _native.load()  # the in-tree HIP library, never a fallback
+    return torch
+
+
+def drive_bench(torch, config, n_seq, n_frames, warmup=10, track_cap=512, det_cap=256):
+    """Run `n_frames` steps of bench.py's workload for `config` the way bench.py runs them (probe
+    schedule included, one launch per frame over every sequence, no host sync in between).
+    Returns (engine, frames on device, per-frame (out, cnt) on device)."""
+    from boxmot_amd.workloads import CONFIGS, BenchFrames, bench_engine
+
+    kind = CONFIGS[config][0]
+    dev = torch.device("cuda", 0)
+    src = BenchFrames(config, n_seq, dev)
+    eng, stages = bench_engine(config, src.n_seq, track_cap, det_cap, overlap=True)
+    S = src.n_seq
+    stream = torch.cuda.current_stream()
+    width = 10 if kind == "strongsort" else 8
+    frames, outs = [], []
+    dominant = stages[-1] if stages else None
+    for t in range(1, n_frames + 1):
+        d, off, e = src.frame(t)
+        frames.append((d, off, e))
+        j = t - 1 - warmup
+        probed = None
+        if stages and 0 <= j < len(stages):
+            probed = stages[j]
+        elif stages and j == len(stages):
+            probed = dominant
+        if probed is not None:
+            eng.probe(probed)
+        out = torch.empty((max(int(d.shape[0]), 1), width), dtype=torch.float64, device=dev)
+        cnt = torch.empty(S, dtype=torch.int32, device=dev)
+        if kind == "ocsort":
+            eng.step(d, off, out, cnt, stream=stream.cuda_stream)
+        elif kind in ("boosttrack", "strongsort"):
+            eng.step(d, off, e, None, out, cnt, stream=stream.cuda_stream)
+        else:
+            eng.step(d, off, e, None, out, cnt, seq0=0, nseq=S, stream=stream.cuda_stream)
+        outs.append((out, cnt))
+        if probed is not None and j < len(stages):
+            eng.probe_read()
+            eng.probe(None)
+    torch.cuda.synchronize()
+    assert eng.status() == 0
+    return eng, frames, outs
+
+
+def host_rows(frames, outs, s, t):
+    """(dets, embs, engine rows) of sequence s at frame t (1-based), on the host."""
+    d, off, e = frames[t - 1]
+    out, cnt = outs[t - 1]
+    o = off.cpu().numpy()
+    a, b = int(o[s]), int(o[s + 1])
+    dets = d[a:b].cpu().numpy().astype(np.float64)
+    embs = None if e is None else e[a:b].cpu().numpy()
+    rows = out[a: a + int(cnt[s].item())].cpu().numpy()
+    return dets, embs, rows
+
+
+def test_botsort_c3_bench_workload_vs_oracle(torch_cuda):
+    """The driver-timed line (BASELINE configs[2]): 1024 sequences in one launch per frame at
+    bench capacities in overlap mode; 8 sequences spread over the batch (first, last, both
+    halves' edges) bitwise against the oracle every frame, and their Kalman state at the end."""
+    from boxmot_amd.workloads import CONFIGS
+
+    _, _, F, params = CONFIGS["botsort"]
+    n_frames = 60
+    eng, frames, outs = drive_bench(torch_cuda, "botsort", 1024, n_frames)
+    st = eng.frame_stats()
+    assert st["dets"] > 1024 * 100 and st["active"] > 1024 * 100, st  # the C3 shape, really
+    for s in (0, 1, 255, 511, 512, 700, 1022, 1023):
+        orc = po.OracleTracker("botsort", **params)
+        for t in range(1, n_frames + 1):
+            dets, embs, rows = host_rows(frames, outs, s, t)
+            assert embs.dtype == np.float32 and embs.shape[1] == F
+            np.testing.assert_array_equal(rows, orc.update(dets, embs),
+                                          err_msg=f"seq {s} frame {t}")
+        g, r = eng.tracks(s), orc.tracks()
+        for k in ("id", "state", "mean", "covariance"):
+            np.testing.assert_array_equal(g[k], r[k], err_msg=f"seq {s} {k}")
+
+
+@pytest.mark.timeout(600)
+def test_strongsort_c4_bench_workload_vs_oracle(torch_cuda):
+    """BASELINE configs[3] as bench.py times it (TorchSceneBatch seed 1000, 1024 objects, 2048-d,
+    SS_C4_CAPS) for 64 frames — past the frame where the distinct gallery samples per track
+    level off — every frame's rows and the final Kalman state bitwise against the oracle."""
+    from boxmot_amd.workloads import CONFIGS
+
+    _, _, F, params = CONFIGS["strongsort_c4"]
+    n_frames = 64
+    eng, frames, outs = drive_bench(torch_cuda, "strongsort_c4", 1, n_frames)
+    st = eng.frame_stats()
+    assert st["dets"] > 450 and st["tracks"] > 900, st
+    orc = po.OracleTracker("strongsort", **params)
+    for t in range(1, n_frames + 1):
+        dets, embs, rows = host_rows(frames, outs, 0, t)
+        assert dets.shape[1] == 6 and embs.shape[1] == F
+        np.testing.assert_array_equal(rows, orc.update(dets, embs), err_msg=f"frame {t}")
+    L = po.lib()
+    g = eng.tracks(0)
+    n = L.bxo_ss_tracks(orc.h, 0, None, None, None, None)
+    ids = np.zeros(max(n, 1), np.int32)
+    state = np.zeros(max(n, 1), np.int32)
+    mean = np.zeros((max(n, 1), 8))
+    cov = np.zeros((max(n, 1), 8, 8))
+    L.bxo_ss_tracks(orc.h, n, ids.ctypes.data, state.ctypes.data, mean.ctypes.data,
+                    cov.ctypes.data)
+    np.testing.assert_array_equal(g["id"], ids[:n])
+    np.testing.assert_array_equal(g["state"], state[:n])
+    np.testing.assert_array_equal(g["mean"], mean[:n])
+    np.testing.assert_array_equal(g["covariance"], cov[:n])
+
+
+def test_boosttrack_c5_bench_workload_vs_oracle(torch_cuda):
+    """BASELINE configs[4] (`boosttrack_mot8`) on one GPU: its 8 sequences (MOT17-02/04 public
+    detections + 6 synthetic) in one launch per frame, 100 frames, all 8 bitwise against the
+    oracle every frame and their Kalman state at the end."""
+    from boxmot_amd.workloads import CONFIGS
+
+    _, _, F, params = CONFIGS["boosttrack_mot8"]
+    n_frames = 100
+    eng, frames, outs = drive_bench(torch_cuda, "boosttrack_mot8", 8, n_frames)
+    L = po.lib()
+    for s in range(8):
+        orc = po.OracleTracker("boosttrack", **params)
+        for t in range(1, n_frames + 1):
+            dets, embs, rows = host_rows(frames, outs, s, t)
+            assert embs.dtype == np.float64 and embs.shape[1] == F
+            np.testing.assert_array_equal(rows, orc.update(dets, embs),
+                                          err_msg=f"seq {s} frame {t}")
+        g = eng.tracks(s)
+        n = L.bxo_boost_tracks(orc.h, 0, None, None, None)
+        ids = np.zeros(max(n, 1), np.int32)
+        x = np.zeros((max(n, 1), 8))
+        P = np.zeros((max(n, 1), 8, 8))
+        L.bxo_boost_tracks(orc.h, n, ids.ctypes.data, x.ctypes.data, P.ctypes.data)
+        np.testing.assert_array_equal(g["id"], ids[:n], err_msg=f"seq {s}")
+        np.testing.assert_array_equal(g["x"], x[:n], err_msg=f"seq {s}")
+        np.testing.assert_array_equal(g["P"], P[:n], err_msg=f"seq {s}")

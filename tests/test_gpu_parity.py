@@ -380,6 +380,24 @@ def test_lapjv_ties_vs_oracle(torch_cuda, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape,kw", [((4400, 4000), dict(extend_cost=True)),
+                                      ((2300, 2100), dict(extend_cost=True, cost_limit=4.0)),
+                                      ((4200, 4200), {})])
+def test_lapjv_global_state_vs_oracle(torch_cuda, shape, kw):
+    """bx_lapjv past the LDS (n > 4096: the solver state in HBM, its column-ownership atomics read
+    back through an invalidated L1) on tie-heavy integer costs with a planted cheap matching."""
+    rng = np.random.default_rng(7)
+    nr, nc = shape
+    c = rng.integers(5, 9, (nr, nc)).astype(np.float64)
+    k = min(nr, nc)
+    c[np.arange(k), rng.permutation(nc)[:k]] = rng.integers(0, 3, k)
+    ox, oy = po.lapjv(c, **kw)
+    gx, gy = gpu_lapjv(torch_cuda, c, **kw)
+    np.testing.assert_array_equal(gx, ox)
+    np.testing.assert_array_equal(gy, oy)
+
+
+@pytest.mark.gpu
 def test_lapjv_errors(torch_cuda):
     with pytest.raises(ValueError, match="Square cost array expected"):
         gpu_lapjv(torch_cuda, np.zeros((2, 3)))

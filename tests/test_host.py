@@ -91,3 +91,14 @@ def test_oracle_multi_sequence_is_independent():
     for t in range(1, 20):
         d, _, _ = sc.frame(t)
         np.testing.assert_array_equal(t1.update(d), t2.update(d))
+
+
+def test_with_index_empty_inputs():
+    """The detection-index column appended before a CMC call, on empty frames in every shape
+    the trackers can pass (a 1-D np.array([]) included)."""
+    from boxmot_amd.trackers.basetracker import _with_index
+
+    assert _with_index(np.array([])).shape == (0, 7)
+    assert _with_index(np.zeros((0, 6))).shape == (0, 7)
+    d = _with_index(np.ones((3, 6)))
+    assert d.shape == (3, 7) and list(d[:, 6]) == [0, 1, 2]
