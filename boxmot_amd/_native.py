@@ -38,23 +38,66 @@ class NativeUnavailable(RuntimeError):
     pass
 
 
+def _deps(src: Path, seen=None) -> list:
+    """src and the in-tree headers it includes (transitively)."""
+    import re
+
+    seen = set() if seen is None else seen
+    if src in seen or not src.exists():
+        return []
+    seen.add(src)
+    out = [src]
+    for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', src.read_text(), re.M):
+        for d in (src.parent, REPO / "include"):
+            if (d / inc).exists():
+                out += _deps((d / inc).resolve(), seen)
+                break
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile the HIP extension for gfx950 in-tree (boxmot_amd/lib/libbxassoc.so)."""
-    srcs = [CSRC / s for s in SOURCES] + [CSRC / "bx_device.h", CSRC / "bx_jv.h", HEADER,
-                                          HEADER_OCS, HEADER_BOOST, HEADER_SS, HEADER_IO]
-    if not force and LIB_PATH.exists():
-        t = LIB_PATH.stat().st_mtime
-        if all(s.stat().st_mtime <= t for s in srcs):
-            return LIB_PATH
-    LIB_DIR.mkdir(exist_ok=True)
+    """Compile the HIP extension for gfx950 in-tree (boxmot_amd/lib/libbxassoc.so): one object per
+    translation unit (compiled in parallel, and only when it or a header it includes changed),
+    then one link."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    objdir = LIB_DIR / "obj"
+    objdir.mkdir(parents=True, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    flags = [f for f in HIPCC_FLAGS if f != "-shared"]
+    stale = []
+    objs = []
+    for s in SOURCES:
+        src = CSRC / s
+        obj = objdir / (s + ".o")
+        objs.append(obj)
+        if force or not obj.exists() or any(d.stat().st_mtime > obj.stat().st_mtime
+                                            for d in _deps(src)):
+            stale.append((src, obj))
+
+    def compile_one(so):
+        src, obj = so
+        tmp = obj.with_suffix(".o.tmp")
+        r = subprocess.run([hipcc, *flags, "-c", "-o", str(tmp), str(src)], capture_output=True,
+                           text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src.name}:\n{r.stderr}")
+        if verbose and r.stderr:
+            print(r.stderr)
+        os.replace(tmp, obj)
+
+    if stale:
+        with ThreadPoolExecutor(max_workers=min(len(stale), os.cpu_count() or 1)) as ex:
+            list(ex.map(compile_one, stale))
+    if not stale and LIB_PATH.exists() and all(
+            o.stat().st_mtime <= LIB_PATH.stat().st_mtime for o in objs):
+        return LIB_PATH
+    LIB_DIR.mkdir(exist_ok=True)
     tmp = LIB_PATH.with_suffix(".so.tmp")
-    cmd = [hipcc, *HIPCC_FLAGS, "-o", str(tmp), *[str(CSRC / s) for s in SOURCES]]
-    r = subprocess.run(cmd, capture_output=True, text=True)
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(tmp),
+                        *[str(o) for o in objs]], capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed:\n{r.stderr}")
-    if verbose and r.stderr:
-        print(r.stderr)
+        raise RuntimeError(f"hipcc link failed:\n{r.stderr}")
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
 

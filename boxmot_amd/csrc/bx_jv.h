@@ -89,7 +89,7 @@ struct SyncWaveG {
 // Wave-order-preserving compaction: emit(k, pos) for k < n with pred(k); returns the count.
 template <class P, class E, class SY>
 __device__ int wave_compact_s(int n, P pred, E emit, SY sync) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   int base = 0;
   for (int c = 0; c < n; c += OW) {
     const int k = c + lane;

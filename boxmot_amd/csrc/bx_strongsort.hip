@@ -129,12 +129,13 @@ struct SsDev {
 
 // Diagnostic phase stamps and counters (build with -DBX_PHASE_TIMING; never shipped): per
 // sequence, cycles accumulated per phase [0, 16), sub-phase cycles / counters [16, 32).
-constexpr int SS_DBG = 32;
+constexpr int SS_DBG = 48;
 #ifdef BX_PHASE_TIMING
 #define SSTAMP(k)                                                                    \
   do {                                                                               \
-    __syncthreads();                                                                 \
-    if (threadIdx.x == 0 && g.dbg) {                                                 \
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");                           \
+    __builtin_amdgcn_wave_barrier();                                                 \
+    if ((threadIdx.x & 63) == 0 && g.dbg) {                                          \
       const unsigned long long _now = __builtin_amdgcn_s_memtime();                  \
       g.dbg[(size_t)seq * SS_DBG + (k)] += _now - t_last;                            \
       t_last = _now;                                                                 \
@@ -142,7 +143,7 @@ constexpr int SS_DBG = 32;
   } while (0)
 #define SCOUNT(k, v)                                                                 \
   do {                                                                               \
-    if (threadIdx.x == 0 && g.dbg) g.dbg[(size_t)seq * SS_DBG + 16 + (k)] += (v);    \
+    if ((threadIdx.x & 63) == 0 && g.dbg) g.dbg[(size_t)seq * SS_DBG + 16 + (k)] += (v);    \
   } while (0)
 #define SS_NOW() __builtin_amdgcn_s_memtime()
 #else
@@ -157,6 +158,15 @@ constexpr int SS_DBG = 32;
 
 __device__ __forceinline__ double* vecp(const SsDev& g, int seq, int slot, int v) {
   return g.vec + ((((size_t)seq * g.T + slot) * g.VP + v) * (size_t)g.F);
+}
+// Where element q of a stored NN operand row (a gallery vector's vecn row, a detection's dn row)
+// lives: within each whole 8-element block (F even; the rest in order) the order is
+// [0 4 1 5 2 6 3 7], so lane group m's 16-byte load of positions (2m, 2m + 1) holds exactly the
+// k-slots the fp64 MFMA takes from it in its two k-steps (k0 + m, k0 + 4 + m): ss_nn_kernel feeds
+// its loads to the matrix cores as they arrive, and each output's chain stays ascending in k.
+__device__ __forceinline__ int nn_pos(int q, int F) {
+  const int FB = (F & 1) ? 0 : F - F % 8;
+  return q < FB ? (q & ~7) | ((q & 3) << 1) | ((q >> 2) & 1) : q;
 }
 __device__ __forceinline__ double* vecnp(const SsDev& g, int seq, int slot, int v) {
   return g.vecn + ((((size_t)seq * g.T + slot) * g.VP + v) * (size_t)g.F);
@@ -493,6 +503,12 @@ __device__ int pool_alloc(SsTrk& t, int VP) {
 }
 
 // ---- the match kernel's code generation ---------------------------------------------------
+#ifndef SS_TAB_HELPERS  // the match kernel's two helper waves work on the first-step tables
+#define SS_TAB_HELPERS 1
+#endif
+#ifndef SS_TAB_RATIO  // the LSAP's first-step table when R * SS_TAB_RATIO >= CC (0: never)
+#define SS_TAB_RATIO 0
+#endif
 #ifndef SS_MATCH_ATTR  // everything inlined: a call left by the inliner keeps its frame in scratch
 #define SS_MATCH_ATTR __attribute__((flatten))
 #endif
@@ -564,6 +580,19 @@ __device__ void ws_carve(const SsDev& g, int seq, SsWs& w, char* lds) {
 __device__ __forceinline__ int bcast(int v) { return __shfl(v, 0); }
 __device__ __forceinline__ double bcastd(double v) { return __shfl(v, 0); }
 
+// The cross-lane hand-off of ONE wave (LDS / global stores complete and visible to its later
+// loads): what __syncthreads() is in a one-wave workgroup, without waiting for other waves — the
+// match kernel runs its cascade and its solver as two waves of one workgroup, each synchronising
+// only itself.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+template <class P, class E>
+__device__ __forceinline__ int wcompact(int n, P pred, E emit) {
+  return wave_compact_s(n, pred, emit, SyncWaveG{});
+}
+
 // stable sort of idx[0..n) by key descending (ties keep order): rank placement, lane-parallel,
 // the keys staged in ks (LDS, n entries)
 template <class K>
@@ -606,7 +635,7 @@ __device__ void stable_sort_desc(int* idx, int n, K key, int* tmp, double* ks) {
 // keep a[k] unless it appears in column `col` of matches [m0, m1): in place via tmp
 __device__ int filter_matched(int* a, int na, const int* mt, int m0, int m1, int col, int* tmp) {
   const int lane = threadIdx.x & 63;
-  const int n = wave_compact(
+  const int n = wcompact(
       na,
       [&](int k) {
         for (int q = m0; q < m1; q++)
@@ -615,7 +644,7 @@ __device__ int filter_matched(int* a, int na, const int* mt, int m0, int m1, int
       },
       [&](int k, int p) { tmp[p] = a[k]; });
   for (int k = lane; k < n; k += 64) a[k] = tmp[k];
-  __syncthreads();
+  wsync();
   return n;
 }
 
@@ -624,12 +653,12 @@ __device__ int filter_matched_fl(int* a, int na, const int* mt, int m0, int m1, 
                                  int* fl, int nu) {
   const int lane = threadIdx.x & 63;
   for (int k = lane; k < nu; k += 64) fl[k] = 0;
-  __syncthreads();
+  wsync();
   for (int q = m0 + lane; q < m1; q += 64) fl[mt[2 * q + col]] = 1;
-  __syncthreads();
-  const int n = wave_compact(na, [&](int k) { return fl[a[k]] == 0; }, [&](int k, int p) { tmp[p] = a[k]; });
+  wsync();
+  const int n = wcompact(na, [&](int k) { return fl[a[k]] == 0; }, [&](int k, int p) { tmp[p] = a[k]; });
   for (int k = lane; k < n; k += 64) a[k] = tmp[k];
-  __syncthreads();
+  wsync();
   return n;
 }
 
@@ -725,7 +754,7 @@ __global__ void __launch_bounds__(64)
 #pragma unroll
     for (int r = 0; r < PQ; r++) {
       const int q = lane + 64 * r;
-      if (q < F) dn[q] = rx[r] / dd;
+      if (q < F) dn[nn_pos(q, F)] = rx[r] / dd;
       rx[r] = rx[r] / dw;
       if (q < F) nf[q] = rx[r];
     }
@@ -745,7 +774,7 @@ __global__ void __launch_bounds__(64)
   const double pwn = wpw_norm(x, F, lo, ln, leaf);
   const double dd = pwn + 1e-8, dw = fn + 1e-8;
   for (int q = lane; q < F; q += 64) {
-    dn[q] = x[q] / dd;
+    dn[nn_pos(q, F)] = x[q] / dd;
     nf[q] = x[q] / dw;
   }
   __syncthreads();
@@ -762,25 +791,9 @@ __global__ void __launch_bounds__(64)
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// Operands of two k-steps from one 16-byte load per lane: lane group m (lanes 16m..16m+15) loaded
-// elements (k0 + 2m, k0 + 2m + 1) of its row; the MFMA wants k0 + m for the first step and
-// k0 + 4 + m for the second (each step's k-slots ascending, so the accumulation stays the oracle's
-// ascending fma chain).  Two gfx950 row swaps transpose the 4 x 2 blocks:
-// swap16 -> [x0 y0 x2 y2] / [x1 y1 x3 y3], swap32 -> [x0 y0 x1 y1] / [x2 y2 x3 y3] (rows of 16 lanes).
-__device__ __forceinline__ void kpair(const double2 v, double& s0, double& s1) {
-  const long long a = __double_as_longlong(v.x), b = __double_as_longlong(v.y);
-  const auto l16 = __builtin_amdgcn_permlane16_swap((unsigned)a, (unsigned)b, false, false);
-  const auto h16 = __builtin_amdgcn_permlane16_swap((unsigned)(a >> 32), (unsigned)(b >> 32),
-                                                    false, false);
-  const auto l32 = __builtin_amdgcn_permlane32_swap(l16[0], l16[1], false, false);
-  const auto h32 = __builtin_amdgcn_permlane32_swap(h16[0], h16[1], false, false);
-  s0 = __longlong_as_double(((long long)h32[0] << 32) | l32[0]);
-  s1 = __longlong_as_double(((long long)h32[1] << 32) | l32[1]);
-}
-
 // The NN contraction's k loop for RT row tiles x NDT detection tiles (ap / bp: the lane's row
-// bases): blocks of 8 k, one 16-byte load per tile and lane transposed into two MFMA k-steps
-// (kpair), the next block's loads in flight during this block's MFMAs; padded rows (past a
+// bases): blocks of 8 k, one 16-byte load per tile and lane holding its two MFMA k-steps' operands
+// (rows stored in MFMA order, nn_pos), the next block's loads in flight during this block's MFMAs; padded rows (past a
 // track's samples) read valid rows and are discarded by the caller, so no branch splits the chains.
 template <int RT, int NDT, int NA>
 __device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT],
@@ -800,21 +813,17 @@ __device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT],
       for (int rt = 0; rt < RT; rt++) na[rt] = *(const double2*)(ap[rt] + kn + 2 * kl);
 #pragma unroll
       for (int dt = 0; dt < NDT; dt++) nb[dt] = *(const double2*)(bp[dt] + kn + 2 * kl);
-      double a0[RT], a1[RT], b0[NDT], b1[NDT];
-#pragma unroll
-      for (int rt = 0; rt < RT; rt++) kpair(a[rt], a0[rt], a1[rt]);
-#pragma unroll
-      for (int dt = 0; dt < NDT; dt++) kpair(bb[dt], b0[dt], b1[dt]);
+      // (rows stored in MFMA order, nn_pos: .x is k-slot k + kl, .y is k + 4 + kl)
 #pragma unroll
       for (int rt = 0; rt < RT; rt++)
 #pragma unroll
         for (int dt = 0; dt < NDT; dt++)
-          acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[rt], b0[dt], acc[rt][dt], 0, 0, 0);
+          acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[rt].x, bb[dt].x, acc[rt][dt], 0, 0, 0);
 #pragma unroll
       for (int rt = 0; rt < RT; rt++)
 #pragma unroll
         for (int dt = 0; dt < NDT; dt++)
-          acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[rt], b1[dt], acc[rt][dt], 0, 0, 0);
+          acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[rt].y, bb[dt].y, acc[rt][dt], 0, 0, 0);
 #pragma unroll
       for (int rt = 0; rt < RT; rt++) a[rt] = na[rt];
 #pragma unroll
@@ -991,6 +1000,29 @@ __global__ void __launch_bounds__(256)
 
 // ------------------------------------------------------------------------------------------
 // The frame kernel: one wave64 per sequence.
+// An LSAP handed by the match kernel's cascade wave to its solver wave (LDS): the matrix P and
+// its transpose PT, the clamp, the shape (the rows' offsets and the columns' indices are the
+// kernel's LDS arrays, passed to both waves as such so their accesses compile to LDS
+// instructions); np is the solver's answer.  flag: 0 idle (or done), 1 posted, -1 exit.
+struct LsapJob {
+  const double* P;
+  const double* PT;
+  double max_d;
+  int R, CC, tr, ld, ldT, np;
+  int flag;
+};
+// The first-step table of an LSAP (see lsap_wave), computed by the solver wave and the match
+// kernel's two helper waves in 64-row groups: tickets from ctr = epoch << 48 | groups << 32 |
+// next group (a ticket at or past the group count is void; a valid ticket's job cannot change
+// before its group is done, so its parameters are read after taking it); a finished group stamps
+// its job's epoch into gdone (one writer per group: no count to get wrong).  Epoch 0xffff: exit.
+struct TabJob {
+  const double* PT;
+  double max_d;
+  int R, CC, ld, ldT;
+  unsigned long long ctr;
+  int gdone[16];  // group g of the job with epoch e is done when gdone[g] == e
+};
 struct SsCtx {
   const SsDev& g;
   SsWs& w;
@@ -1009,9 +1041,91 @@ struct SsCtx {
   int* flt;     // match kernel: scratch table (LDS, 1024 ints)
   double* ks;   // match kernel: sort-key scratch (LDS)
   int* cidx;    // match kernel: the solver's column indices (LDS, 2048 ints)
+  struct LsapJob* job;  // match kernel: the hand-off to its solver wave
+  TabJob* tab;          // match kernel: the first-step table's work queue (solver + helpers)
+  unsigned tep;         // match kernel, solver wave: the last table epoch posted
   __device__ const double* det(int i) const { return w.dt + (size_t)w.dord[i] * DTW; }
   __device__ int det_in(int i) const { return (int)det(i)[6]; }
 };
+
+// One 64-row group of an LSAP's first-step table, lane per row (see lsap_wave): the minimum of
+// the row's unclamped entries and the column at it when it is the only one and at most max_d
+// (clamping then changes neither; above max_d every entry clamps to one value: a tie), else -2.
+// A NaN entry is never the minimum nor equal to it, as in the solver's first step.  Four
+// independent chains over the columns (u mod 4), merged at the end; 32 loads in flight.
+__device__ __forceinline__ void tab_group(SsWs& w, const TabJob* tj, const int* roff,
+                                          const int* cidx, int grp, int lane) {
+  const double* PT = tj->PT;
+  const int R = tj->R, CC = tj->CC, ld = tj->ld, ldT = tj->ldT;
+  const double max_d = tj->max_d;
+  const int r = 64 * grp + lane;
+  const double* base = PT + (r < R ? roff[r] / ld : 0);
+  double m[4] = {INF, INF, INF, INF};
+  int a[4] = {-1, -1, -1, -1};
+  bool tie[4] = {false, false, false, false};
+  for (int j0 = 0; j0 < CC; j0 += 32) {
+    double e[32];
+#pragma unroll
+    for (int u = 0; u < 32; u++) {
+      const int j = j0 + u < CC ? j0 + u : CC - 1;
+      e[u] = base[(size_t)cidx[j] * ldT];
+    }
+#pragma unroll
+    for (int u = 0; u < 32; u++) {
+      if (j0 + u >= CC) break;
+      const int c = u & 3;
+      if (e[u] < m[c]) m[c] = e[u], a[c] = j0 + u, tie[c] = false;
+      else if (e[u] == m[c]) tie[c] = true;
+    }
+  }
+  double mm = m[0];
+  int aa = a[0];
+  bool tt = tie[0];
+#pragma unroll
+  for (int c = 1; c < 4; c++) {
+    if (m[c] < mm) mm = m[c], aa = a[c], tt = tie[c];
+    else if (m[c] == mm) tt = true;
+  }
+  if (r < R) {
+    w.u[r] = mm;
+    w.col4row[r] = (!tt && mm <= max_d && mm < INF) ? aa : -2;
+  }
+}
+
+// take table tickets until a void one; returns.  The ticket is made wave-uniform by readfirstlane
+// (lane 0 took it; every lane is active here), so the exit test is a scalar branch.
+__device__ __forceinline__ void tab_work(SsWs& w, TabJob* tj, const int* roff, const int* cidx,
+                                         int lane) {
+  for (;;) {
+    unsigned long long t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(&tj->ctr, 1ull, __ATOMIC_ACQ_REL,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(t >> 32));
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(t & 0xffffffffull));
+    const int ng = (int)(hi & 0xffffu), gi = (int)lo;
+    if (gi >= ng) return;
+    tab_group(w, tj, roff, cidx, gi, lane);
+    wsync();
+    if (lane == 0)
+      __hip_atomic_store(&tj->gdone[gi], (int)(hi >> 16), __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+// the match kernel's helper waves: table groups of every posted LSAP until the exit epoch
+__device__ __forceinline__ void tab_server(SsWs& w, TabJob* tj, const int* roff, const int* cidx,
+                                           int lane) {
+  unsigned seen = 0;
+  for (;;) {
+    unsigned ep;
+    while ((ep = __builtin_amdgcn_readfirstlane((unsigned)(__hip_atomic_load(
+                &tj->ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 48))) == seen)
+      __builtin_amdgcn_s_sleep(2);
+    seen = ep;
+    if (seen == 0xffffu) return;
+    tab_work(w, tj, roff, cidx, lane);
+  }
+}
 
 // scipy.optimize.linear_sum_assignment (Crouse's shortest augmenting path, rectangular),
 // wave-parallel, in the solver's orientation: R x CC, R <= CC (`tr`: the caller's matrix was
@@ -1027,9 +1141,21 @@ struct SsCtx {
 // Only a row whose minimum lands on an assigned column writes the search state out (rem / pos /
 // SC / spc / path in LDS) and continues Crouse's search as scipy does; u[cur] is 0 before row cur
 // (only rows already assigned are ever on a path).  Pairs sorted by row into w.rows / w.cols.
+//
+// First steps from a table (when the rows are many for their width): every row's first Dijkstra
+// step at v = 0 is computed up front, one lane per row over the transposed matrix PT (the rows
+// of a level are consecutive ranks / list positions, so a load is coalesced) — its minimum, and
+// the column at it when that column is the only one and the row has no NaN.  v only ever
+// decreases, on the SC columns of rows whose search goes on (`chg`), which only raises other
+// entries of a later row's first step: so unless its column's v changed, a row's first step at
+// the current v is its table entry, and when that column is unassigned the row is assigned
+// without loading its costs.  Any other row loads its costs and takes the step below.  Table
+// entries park in u (scipy's u[cur] = minVal for a row that ends on its first step; a row's u is
+// never read before the row is reached) and col4row (never read before the row is assigned).
 template <int LQ, bool IDX>
 __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P, const int* roff,
-                                         const int* cidx, double max_d, int R, int CC, bool tr) {
+                                         const int* cidx, double max_d, int R, int CC, bool tr,
+                                         const double* __restrict__ PT, int ld, int ldT) {
   SsWs& w = x.w;
   const int lane = x.lane;
 #ifdef BX_PHASE_TIMING
@@ -1041,7 +1167,60 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
                      t_sink = 0;
 #endif
   const double clampv = max_d + 1e-5;
-  for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
+  // the table pays when a row's full first step (~1.8 k cycles) outweighs its share of the
+  // table's CC-column sweep per 64 rows
+  const bool TB = SS_TAB_RATIO > 0 && IDX && LQ <= 16 && R >= 2 && R * SS_TAB_RATIO >= CC;
+  if (TB) {  // posted to the helper waves, worked on here too, waited for
+    TabJob* tj = x.tab;
+    const int ng = (R + 63) / 64;
+    const unsigned ep = ++x.tep;
+    if (lane == 0) {
+      tj->PT = PT;
+      tj->max_d = max_d;
+      tj->R = R;
+      tj->CC = CC;
+      tj->ld = ld;
+      tj->ldT = ldT;
+    }
+    wsync();
+    if (lane == 0)
+      __hip_atomic_store(&tj->ctr, (unsigned long long)ep << 48 | (unsigned long long)ng << 32,
+                         __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    tab_work(w, tj, roff, cidx, lane);
+    // every group stamped with this epoch (lane g checks group g; ng <= 16)
+    while (__ballot(lane < ng && __hip_atomic_load(&tj->gdone[lane < 16 ? lane : 0],
+                                                   __ATOMIC_ACQUIRE,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP) != (int)ep))
+      __builtin_amdgcn_s_sleep(1);
+#ifdef SS_TAB_VERIFY  // diagnostic builds: the table re-derived here, row by row, must agree
+    for (int r0 = 0; r0 < R; r0 += 64) {
+      const int r = r0 + lane;
+      if (r >= R) continue;
+      const double* base = PT + roff[r] / ld;
+      double mm = INF;
+      int aa = -1;
+      bool tt = false;
+      for (int j = 0; j < CC; j++) {
+        const double e = base[(size_t)cidx[j] * ldT];
+        if (e < mm) mm = e, aa = j, tt = false;
+        else if (e == mm) tt = true;
+      }
+      const int code = (!tt && mm <= max_d && mm < INF) ? aa : -2;
+      const double um = w.u[r];
+      const int uc = w.col4row[r];
+      if (!(um == mm || (um != um && mm != mm)) || uc != code) {
+        atomicExch(x.g.status, 9000 + (uc == code ? 1 : 2));
+        if (atomicAdd(&x.g.status[1], 1) < 24)
+          printf("TABV seq %d ep %u R %d CC %d ld %d ldT %d r %d roff %d: table (%g, %d) "
+                 "recomputed (%g, %d) tj(R %d CC %d ld %d ldT %d PT %p/%p)\n",
+                 x.seq, ep, R, CC, ld, ldT, r, roff[r], um, uc, mm, code, tj->R, tj->CC,
+                 tj->ld, tj->ldT, (const void*)tj->PT, (const void*)PT);
+      }
+    }
+#endif
+  } else {
+    for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
+  }
   for (int j = lane; j < CC; j += 64) w.path[j] = -1, w.row4col[j] = -1;
   unsigned cb[LQ];  // byte offset of the lane's column q in a row (column 0's past CC)
   double vr[LQ];    // v[j]; -INF past CC, so those columns relax to +INF
@@ -1052,7 +1231,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     cb[q] = 8u * (unsigned)(j < CC ? (IDX ? cidx[j] : j) : 0);
     vr[q] = j < CC ? 0.0 : -INF;
   }
-  __syncthreads();
+  wsync();
   // raw loads, unconditional (in-row offsets): clamped where used, so a load is waited for only
   // when its value is needed
   auto load_row = [&](int off, double* dst) {
@@ -1062,15 +1241,35 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
   };
   // the next row's loads are issued during this one's reductions, except at LQ = 32 (IoU stage of
   // more than 1024 candidates, rare) where the registers would not hold both rows
-  constexpr bool PF = LQ <= 16;
+  // (with a table only the rows it cannot settle load their costs, on demand)
+  const bool PF = LQ <= 16 && !TB;
   double nx[LQ];
   int off1 = R > 1 ? roff[1] : 0;
   if (PF && R > 0) load_row(roff[0], nx);
+  unsigned chg = 0;  // columns whose v changed: the SC bits of every search that went on
+  int tcode = -2;    // the table's column codes of the current 64 rows, lane l row 64k + l
   for (int cur = 0; cur < R; cur++) {
 #ifdef BX_PHASE_TIMING
     unsigned long long t_r0 = SS_NOW();
 #endif
-    if (!PF) load_row(roff[cur], nx);
+    if (TB) {
+      if ((cur & 63) == 0) tcode = cur + lane < R ? w.col4row[cur + lane] : -2;
+      const int jt = rl_i(tcode, cur & 63);
+      if (jt >= 0 && !((rl_i((int)(asg | chg), jt & 63) >> (jt >> 6)) & 1u)) {
+        if (lane == (jt & 63)) asg |= 1u << (jt >> 6);
+        if (lane == 0) {  // u[cur] holds the table's minimum already
+          w.row4col[jt] = cur;
+          w.col4row[cur] = jt;
+        }
+#ifdef BX_PHASE_TIMING
+        SCOUNT(16, 1);
+#endif
+        continue;
+      }
+      load_row(roff[cur], nx);
+    } else if (!PF) {
+      load_row(roff[cur], nx);
+    }
     // scipy's minVal + cost - u[cur] - v[j] with minVal = u[cur] = 0 (up to the sign of a zero,
     // which no comparison and no later sum can tell).  A NaN cost stays NaN here and loses every
     // comparison below, as the INF that scipy's `r < INF` test would make of it.
@@ -1103,6 +1302,10 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
 #endif
     if (!(m0 < INF)) {  // infeasible (cannot happen with finite costs)
       if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
+#ifdef SS_TAB_VERIFY
+      if (lane == 0 && atomicAdd(&x.g.status[1], 1) < 24)
+        printf("INFEAS seq %d R %d CC %d TB %d cur %d m0 %g\n", x.seq, R, CC, (int)TB, cur, m0);
+#endif
       return 0;
     }
     // the columns at the minimum, one wave mask per q
@@ -1174,7 +1377,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
         if (ok) w.path[j] = cur;
       }
     }
-    __syncthreads();
+    wsync();
     if (lane == 0) {
       const int jl = w.rem[nrem - 1];
       w.rem[index0] = jl;
@@ -1259,10 +1462,10 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       }
       nrem--;
 #ifdef BX_PHASE_TIMING
-      if (threadIdx.x == 0 && x.g.dbg) x.g.dbg[(size_t)x.seq * SS_DBG + 16 + 5] += 1;
+      if ((threadIdx.x & 63) == 0 && x.g.dbg) x.g.dbg[(size_t)x.seq * SS_DBG + 16 + 5] += 1;
 #endif
     }
-    __syncthreads();
+    wsync();
     // duals: u[cur] = minVal (it was 0), u[i] += minVal - spc[col4row[i]] for the visited rows,
     // v[j] -= minVal - spc[j] for the SC columns; then the augmentation along path
     for (int k = lane; k < nvis; k += 64) {
@@ -1273,7 +1476,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
 #pragma unroll
     for (int q = 0; q < LQ; q++)
       if ((sc >> q) & 1u) vr[q] -= minVal - rv[q];
-    __syncthreads();
+    wsync();
     if (lane == 0) {
       int jj = sk;
       for (;;) {
@@ -1286,12 +1489,13 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       }
     }
     if (lane == (sk & 63)) asg |= 1u << (sk >> 6);
+    chg |= sc;
 #ifdef BX_PHASE_TIMING
     t_slow += SS_NOW() - t_s0;
 #endif
-    __syncthreads();
+    wsync();
   }
-  __syncthreads();
+  wsync();
 #ifdef BX_PHASE_TIMING
   SCOUNT(10, t_slow);
   SCOUNT(12, t_wait);
@@ -1300,6 +1504,21 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
   SCOUNT(15, t_sink);
   SCOUNT(11, SS_NOW() - t_all);
 #endif
+  // every row is assigned a column in [0, CC) by now; a value outside it would be an engine
+  // fault: latched as an error instead of indexing with it
+  for (int q = lane; q < R; q += 64) {
+    const int c = w.col4row[q];
+    if (c < 0 || c >= CC) {
+      atomicExch(x.g.status, (int)BX_ERR_INVALID);
+#ifdef SS_TAB_VERIFY
+      if (atomicAdd(&x.g.status[1], 1) < 24)
+        printf("GUARD seq %d R %d CC %d tr %d TB %d row %d col4row %d\n", x.seq, R, CC, (int)tr,
+               (int)TB, q, c);
+#endif
+      w.col4row[q] = 0;
+    }
+  }
+  wsync();
   if (tr) {  // argsort(col4row): pairs ordered by the original row
     for (int q = lane; q < R; q += 64) {
       const int orow = w.col4row[q];
@@ -1314,7 +1533,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       w.cols[q] = w.col4row[q];
     }
   }
-  __syncthreads();
+  wsync();
   return R;
 }
 
@@ -1479,6 +1698,33 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
   }
 }
 
+// The match kernel's solver wave: runs each posted LSAP (column slots per lane sized to CC: every
+// slot past CC is a relaxation, a minimum and a ballot per row for nothing — measured at C4: 16 ->
+// 8 slots for CC <= 512, match 1.63 -> 1.52 ms), answers with the pair count, until told to exit.
+// Its own wave, so the solver's registers are not live across the cascade's bookkeeping.
+__device__ __forceinline__ void lsap_server(SsCtx& x, LsapJob* jb, const int* roff,
+                                            const int* cidx) {
+  for (;;) {
+    int f;
+    while ((f = (int)__builtin_amdgcn_readfirstlane((unsigned)__hip_atomic_load(
+                &jb->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))) == 0)
+      __builtin_amdgcn_s_sleep(1);
+    if (f < 0) return;
+    const double* P = jb->P;
+    const double* PT = jb->PT;
+    const double mx = jb->max_d;
+    const int R = jb->R, CC = jb->CC, ld = jb->ld, ldT = jb->ldT;
+    const bool tr = jb->tr != 0;
+    const int np = CC <= 256    ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT)
+                   : CC <= 512  ? lsap_wave<8, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT)
+                   : CC <= 1024 ? lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT)
+                                : lsap_wave<32, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT);
+    if (x.lane == 0) jb->np = np;
+    wsync();
+    if (x.lane == 0) __hip_atomic_store(&jb->flag, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
 // min_cost_matching (linear_assignment.py:14-93) of track positions ti x sorted detections di:
 // matches appended to w.mt at x.nm; unmatched tracks to ut_out (if non-null), detections to
 // ud_out.  Cost rows lane per track (gated_metric + gate_cost_matrix + id preservation, or
@@ -1495,7 +1741,7 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
     for (int k = lane; k < nd; k += 64) ud_out[k] = di[k];
     nut = nt;
     nud = nd;
-    __syncthreads();
+    wsync();
     return;
   }
   // the solver's orientation: R x CC with R <= CC, transposed (tr) when detections are fewer
@@ -1509,10 +1755,12 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
   int* roff = x.flt;   // the solver rows' element offsets into P (LDS)
   int* cidx = x.cidx;  // the solver columns' element indices (LDS)
   const double* P;
+  const double* PT;  // the same matrix transposed: entry (r, j) at PT[cidx[j] * ldT + roff[r] / ld]
+  int ld, ldT;
   double mx;
 #ifdef BX_PHASE_TIMING
   const int seq = x.seq;
-  __syncthreads();
+  wsync();
   unsigned long long t0 = SS_NOW();
 #endif
   if (kind == M_GATED) {
@@ -1523,7 +1771,9 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
     const int* oi = tr ? di : ti;  // rows
     const int* rk = x.rank;        // track list position -> cascade rank
     P = tr ? g.cfullT + (size_t)x.seq * g.D * g.T : g.cfull + (size_t)x.seq * g.T * g.D;
-    const int ld = tr ? g.T : g.D;
+    PT = tr ? g.cfull + (size_t)x.seq * g.T * g.D : g.cfullT + (size_t)x.seq * g.D * g.T;
+    ld = tr ? g.T : g.D;
+    ldT = tr ? g.D : g.T;
     for (int o = lane; o < R; o += 64) roff[o] = (tr ? oi[o] : rk[oi[o]]) * ld;
     for (int c = lane; c < CC; c += 64) cidx[c] = tr ? rk[li[c]] : li[c];
     mx = max_d;
@@ -1532,14 +1782,16 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
     // read in place; the clamp at max_iou_distance here
     const double* io = g.cost + (size_t)x.seq * 4 * g.T * g.D;
     P = tr ? io + (size_t)g.T * g.D : io;
-    const int ld = tr ? g.T : g.D;
+    PT = tr ? io : io + (size_t)g.T * g.D;
+    ld = tr ? g.T : g.D;
+    ldT = tr ? g.D : g.T;
     const int* li = tr ? ti : di;  // columns
     const int* oi = tr ? di : ti;  // rows
     for (int o = lane; o < R; o += 64) roff[o] = oi[o] * ld;
     for (int c = lane; c < CC; c += 64) cidx[c] = li[c];
     mx = max_d;
   }
-  __syncthreads();
+  wsync();
 #ifdef BX_PHASE_TIMING
   unsigned long long t1 = SS_NOW();
   SCOUNT(0, t1 - t0);
@@ -1553,22 +1805,39 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
   // ballot per row for nothing — measured at C4: 16 -> 8 slots for CC <= 512, match 1.63 -> 1.52
   // ms; more instantiations (1, 2, 10, 12 slots) measured slower, 1.83 ms: the kernel's code and
   // register allocation grow with every inlined copy)
-  const int np_ = CC <= 256    ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr)
-                  : CC <= 512  ? lsap_wave<8, true>(x, P, roff, cidx, mx, R, CC, tr)
-                  : CC <= 1024 ? lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr)
-                               : lsap_wave<32, true>(x, P, roff, cidx, mx, R, CC, tr);
+  // the LSAP runs on the solver wave (lsap_server): posted, then waited for
+  int np_;
+  {
+    LsapJob* jb = x.job;
+    if (lane == 0) {
+      jb->P = P;
+      jb->PT = PT;
+      jb->max_d = mx;
+      jb->R = R;
+      jb->CC = CC;
+      jb->tr = tr;
+      jb->ld = ld;
+      jb->ldT = ldT;
+    }
+    wsync();
+    if (lane == 0) __hip_atomic_store(&jb->flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__builtin_amdgcn_readfirstlane((unsigned)__hip_atomic_load(
+               &jb->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0)
+      __builtin_amdgcn_s_sleep(1);
+    np_ = jb->np;
+  }
 #ifdef BX_PHASE_TIMING
-  __syncthreads();
+  wsync();
   SCOUNT(1, SS_NOW() - t1);
 #endif
   // assigned flags (w.SR rows, w.SC columns), unmatched in index order, then the rejected pairs
   for (int r = lane; r < nt; r += 64) w.SR[r] = 0;
   for (int c = lane; c < nd; c += 64) w.SC[c] = 0;
-  __syncthreads();
+  wsync();
   for (int q = lane; q < np_; q += 64) w.SR[w.rows[q]] = 1, w.SC[w.cols[q]] = 1;
-  __syncthreads();
-  nud = wave_compact(nd, [&](int c) { return w.SC[c] == 0; }, [&](int c, int p) { ud_out[p] = di[c]; });
-  nut = wave_compact(nt, [&](int r) { return w.SR[r] == 0; },
+  wsync();
+  nud = wcompact(nd, [&](int c) { return w.SC[c] == 0; }, [&](int c, int p) { ud_out[p] = di[c]; });
+  nut = wcompact(nt, [&](int r) { return w.SR[r] == 0; },
                      [&](int r, int p) { if (ut_out) ut_out[p] = ti[r]; });
   for (int c0 = 0; c0 < np_; c0 += 64) {
     const int q = c0 + lane;
@@ -1596,71 +1865,85 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
     nut += __popcll(mr);
     nud += __popcll(mr);
   }
-  __syncthreads();
+  wsync();
 }
 
-// matching_cascade (linear_assignment.py:96-171): levels by time_since_update ascending (up to
-// tracker.max_age), each level's tracks ordered by -(quality + stability), stable
-__device__ __forceinline__ void matching_cascade(SsCtx& x, double max_d, const int* ti, int nt, const int* di,
-                                 int nd) {
+// One matching stage of Tracker._enhanced_match with a single solver call site (the solver is
+// inlined once per column-slot width, not once per stage: every inlined copy grows the kernel's
+// register allocation).  M_GATED = matching_cascade (linear_assignment.py:96-171): levels by
+// time_since_update ascending (up to tracker.max_age), each level's tracks ordered by
+// -(quality + stability), stable; the unmatched detections end in w.ud.  M_IOU = one
+// min_cost_matching of every track in ti (stage 3): unmatched tracks to ut_out, detections to w.ud.
+__device__ void match_stage(SsCtx& x, int kind, double max_d, const int* ti, int nt, const int* di,
+                            int nd, int* ut_out, int& nut) {
   SsWs& w = x.w;
   const int lane = x.lane;
   int nud = nd;
   for (int k = lane; k < nd; k += 64) w.ud[k] = di[k];
-  // the distinct time_since_update values, ascending (only levels <= max_age are matched)
+  int na = 1;
   const int max_age = x.sq[Q_MAXAGE];
-  int* pres = x.flt;  // presence table over ages 0..max_age (LDS, 1024 entries)
-  const int amax = max_age < 1023 ? max_age : 1023;
-  for (int a = lane; a <= amax; a += 64) pres[a] = 0;
-  __syncthreads();
-  int over = 0;
-  for (int k = lane; k < nt; k += 64) {
-    const int a = x.tsu[ti[k]];
-    if (a <= amax)
-      pres[a] = 1;
-    else if (a <= max_age)
-      over = 1;
-  }
-  over = __any(over);
-  __syncthreads();
-  int na = wave_compact(amax + 1, [&](int a) { return pres[a] != 0; },
-                        [&](int a, int p) { w.ages[p] = a; });
-  if (over) {  // ages beyond the table (max_age >= 1024): the levels up to max_age, serially
-    if (lane == 0) {
-      for (int k = 0; k < nt; k++) {
-        const int a = x.tsu[ti[k]];
-        if (a <= amax || a > max_age) continue;
-        bool seen = false;
-        for (int q = 0; q < na && !seen; q++) seen = w.ages[q] == a;
-        if (!seen) w.ages[na++] = a;
-      }
-      for (int p = 1; p < na; p++)
-        for (int y = p; y > 0 && w.ages[y - 1] > w.ages[y]; y--) {
-          const int tmp = w.ages[y];
-          w.ages[y] = w.ages[y - 1];
-          w.ages[y - 1] = tmp;
-        }
+  if (kind == M_GATED) {
+    // the distinct time_since_update values, ascending (only levels <= max_age are matched)
+    int* pres = x.flt;  // presence table over ages 0..max_age (LDS, 1024 entries)
+    const int amax = max_age < 1023 ? max_age : 1023;
+    for (int a = lane; a <= amax; a += 64) pres[a] = 0;
+    wsync();
+    int over = 0;
+    for (int k = lane; k < nt; k += 64) {
+      const int a = x.tsu[ti[k]];
+      if (a <= amax)
+        pres[a] = 1;
+      else if (a <= max_age)
+        over = 1;
     }
-    na = bcast(na);
+    over = __any(over);
+    wsync();
+    na = wcompact(amax + 1, [&](int a) { return pres[a] != 0; },
+                      [&](int a, int p) { w.ages[p] = a; });
+    if (over) {  // ages beyond the table (max_age >= 1024): the levels up to max_age, serially
+      if (lane == 0) {
+        for (int k = 0; k < nt; k++) {
+          const int a = x.tsu[ti[k]];
+          if (a <= amax || a > max_age) continue;
+          bool seen = false;
+          for (int q = 0; q < na && !seen; q++) seen = w.ages[q] == a;
+          if (!seen) w.ages[na++] = a;
+        }
+        for (int p = 1; p < na; p++)
+          for (int y = p; y > 0 && w.ages[y - 1] > w.ages[y]; y--) {
+            const int tmp = w.ages[y];
+            w.ages[y] = w.ages[y - 1];
+            w.ages[y - 1] = tmp;
+          }
+      }
+      na = bcast(na);
+    }
+    wsync();
+    // members of ti by list position
+    for (int p = lane; p < x.ntr; p += 64) x.inset[p] = 0;
+    wsync();
+    for (int k = lane; k < nt; k += 64) x.inset[ti[k]] = 1;
+    wsync();
   }
-  __syncthreads();
-  // members of ti by list position
-  for (int p = lane; p < x.ntr; p += 64) x.inset[p] = 0;
-  __syncthreads();
-  for (int k = lane; k < nt; k += 64) x.inset[ti[k]] = 1;
-  __syncthreads();
   for (int q = 0; q < na; q++) {
-    const int age = w.ages[q];
-    if (age > max_age) break;
-    // the level's tracks in cascade order (its run of ranks, restricted to ti)
-    const int nl = wave_compact(
-        x.ncf, [&](int r) { const int p = x.gpos[r]; return x.inset[p] && x.tsu[p] == age; },
-        [&](int r, int p) { w.lvl[p] = x.gpos[r]; });
-    int nut_dummy = 0, nud2 = 0;
-    min_cost_matching(x, M_GATED, max_d, w.lvl, nl, w.ud, nud, nullptr, nut_dummy, w.ud2, nud2);
+    const int* lt = ti;
+    int nl = nt;
+    if (kind == M_GATED) {
+      const int age = w.ages[q];
+      if (age > max_age) break;
+      // the level's tracks in cascade order (its run of ranks, restricted to ti)
+      nl = wcompact(
+          x.ncf, [&](int r) { const int p = x.gpos[r]; return x.inset[p] && x.tsu[p] == age; },
+          [&](int r, int p) { w.lvl[p] = x.gpos[r]; });
+      lt = w.lvl;
+    }
+    int nud2 = 0, nut_l = 0;
+    min_cost_matching(x, kind, max_d, lt, nl, w.ud, nud, kind == M_IOU ? ut_out : nullptr, nut_l,
+                      w.ud2, nud2);
+    if (kind == M_IOU) nut = nut_l;
     for (int k = lane; k < nud2; k += 64) w.ud[k] = w.ud2[k];
     nud = nud2;
-    __syncthreads();
+    wsync();
   }
 }
 
@@ -1777,7 +2060,7 @@ __device__ void track_update(SsCtx& x, int slot, int di) {
 #pragma unroll
       for (int r = 0; r < UQ; r++) {
         const int q = lane + 64 * r;
-        if (q < F) dstn[q] = rl[r] / pn;
+        if (q < F) dstn[nn_pos(q, F)] = rl[r] / pn;
       }
       if (lane == 0) {
         t.app_cons = 0.9 * t.app_cons + 0.1 * sim;
@@ -1800,7 +2083,7 @@ __device__ void track_update(SsCtx& x, int slot, int di) {
       const double wn = sqrt(wdot(dst, dst, F));
       const double pn = wpw_norm(dst, F, x.w.pwlo, x.w.pwln, x.w.pwleaf) + 1e-8;
       double* dstn = vecnp(g, x.seq, slot, v);
-      for (int q = lane; q < F; q += 64) dstn[q] = dst[q] / pn;
+      for (int q = lane; q < F; q += 64) dstn[nn_pos(q, F)] = dst[q] / pn;
       if (lane == 0) {
         t.app_cons = 0.9 * t.app_cons + 0.1 * sim;
         g.vwn[vi] = wn;
@@ -1811,7 +2094,7 @@ __device__ void track_update(SsCtx& x, int slot, int di) {
       const double pn = pr[3];
       for (int q = lane; q < F; q += 64) {
         dst[q] = nf[q];
-        dstn[q] = nf[q] / pn;
+        dstn[nn_pos(q, F)] = nf[q] / pn;
       }
       if (lane == 0) {
         g.vwn[vi] = pr[2];
@@ -2070,15 +2353,44 @@ __global__ void __launch_bounds__(64)
 // ss_match_kernel (one wave per sequence): the three matching stages of Tracker._enhanced_match
 // (stage 1/2 costs gathered from ss_cost_kernel's matrix).  Hands the matches (fmt), the unmatched
 // tracks (ffut) and detections (faud) to the next launches.
-__global__ void __launch_bounds__(64) SS_MATCH_ATTR
+__global__ void __launch_bounds__(256) SS_MATCH_ATTR
     ss_match_kernel(SsDev g, int seq0) {
   extern __shared__ __align__(16) char ss_lds[];
   __shared__ int srank[1024], sgpos[1024], sinset[1024];
   __shared__ int flt[2048], fld[1024];  // solver column indices; sorted-detection membership
   __shared__ int stsu[1024], sage[1024];
-  const int lane = threadIdx.x, b = blockIdx.x, seq = seq0 + b;
+  __shared__ LsapJob job;
+  __shared__ TabJob tab;
+  const int lane = threadIdx.x & 63, b = blockIdx.x, seq = seq0 + b;
   SsWs w;
   ws_carve(g, seq, w, ss_lds);
+  if (threadIdx.x == 0) {
+    job.flag = 0;
+    tab.ctr = 0;
+    for (int k = 0; k < 16; k++) tab.gdone[k] = 0;
+  }
+  __syncthreads();  // the only barrier of all four waves; from here each synchronises itself
+  // the LSAP's rows' offsets and columns' indices (written by the cascade wave, read by the
+  // solver and helper waves): sage and flt
+  // the wave's role, wave-uniform (readfirstlane: scalar branches, no divergent-region masks)
+  const int wid = (int)__builtin_amdgcn_readfirstlane((unsigned)(threadIdx.x >> 6));
+  if (wid >= 2) {  // the helper waves: first-step tables
+#if SS_TAB_HELPERS
+    tab_server(w, &tab, sage, flt, lane);
+#endif
+    return;
+  }
+  if (wid == 1) {  // the solver wave
+    SsCtx xs{g, w, seq, lane, g.trk + (size_t)seq * g.T, g.sq + (size_t)seq * SQS,
+             g.sqd + (size_t)seq * 2, g.lost + (size_t)seq * LOSTN, 0, 0, 0, 0};
+    xs.tab = &tab;
+    xs.tep = 0;
+    lsap_server(xs, &job, sage, flt);
+    // the helpers' exit
+    if (lane == 0)
+      __hip_atomic_store(&tab.ctr, 0xffffull << 48, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+  }
 #ifdef BX_PHASE_TIMING
   unsigned long long t_last = SS_NOW();
 #endif
@@ -2107,79 +2419,84 @@ __global__ void __launch_bounds__(64) SS_MATCH_ATTR
   x.rank = srank;
   x.gpos = sgpos;
   x.inset = sinset;
-  __syncthreads();
+  x.job = &job;
+  wsync();
 
   // ---- Tracker._enhanced_match (tracker.py:183-281, P6) --------------------------------------
   x.nm = 0;
-  const int ncf = wave_compact(x.ntr, [&](int p) { return x.trk[w.lst[p]].state == 2; },
+  const int ncf = wcompact(x.ntr, [&](int p) { return x.trk[w.lst[p]].state == 2; },
                                [&](int p, int q) { w.conf_t[q] = p; });
-  const int nun = wave_compact(x.ntr, [&](int p) { return x.trk[w.lst[p]].state != 1; },
+  const int nun = wcompact(x.ntr, [&](int p) { return x.trk[w.lst[p]].state != 1; },
                                [&](int p, int q) { w.unconf_t[q] = p; });
-  const int nhi = wave_compact(x.nk, [&](int i) { return x.det(i)[4] >= g.thi; },
+  const int nhi = wcompact(x.nk, [&](int i) { return x.det(i)[4] >= g.thi; },
                                [&](int i, int q) { w.hi[q] = i; });
-  const int nmed = wave_compact(
+  const int nmed = wcompact(
       x.nk, [&](int i) { const double c = x.det(i)[4]; return g.tlo <= c && c < g.thi; },
       [&](int i, int q) { w.med[q] = i; });
-  const int nlo = wave_compact(x.nk, [&](int i) { return x.det(i)[4] < g.tlo; },
+  const int nlo = wcompact(x.nk, [&](int i) { return x.det(i)[4] < g.tlo; },
                                [&](int i, int q) { w.lo[q] = i; });
   int naut = ncf, naud = x.nk;
   for (int k = lane; k < ncf; k += 64) w.aut[k] = w.conf_t[k];
   for (int k = lane; k < x.nk; k += 64) w.aud[k] = k;
-  __syncthreads();
+  wsync();
   const double thr = x.sqd[0];
   SSTAMP(3);
   const int NT = x.ntr, NK = x.nk;
-  if (nhi && ncf) {  // stage 1: high-confidence detections, confirmed tracks
-    const int m0 = x.nm;
-    matching_cascade(x, thr * 0.8, w.conf_t, ncf, w.hi, nhi);
-    naut = filter_matched_fl(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp, flt, NT);
-    naud = filter_matched_fl(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp, fld, NK);
-  }
-  SSTAMP(4);
-  {  // stage 2: medium-confidence detections, remaining confirmed tracks
-    // the unmatched tracks are all confirmed (a subset of conf_t)
-    const int nrt = naut;
-    for (int k = lane; k < naut; k += 64) w.ti2[k] = w.aut[k];
-    for (int k = lane; k < NK; k += 64) fld[k] = 0;
-    __syncthreads();
-    for (int k = lane; k < naud; k += 64) fld[w.aud[k]] = 1;
-    __syncthreads();
-    const int nrm = wave_compact(nmed, [&](int k) { return fld[w.med[k]] != 0; },
-                                 [&](int k, int q) { w.rd[q] = w.med[k]; });
-    if (nrm && nrt) {
-      const int m0 = x.nm;
-      matching_cascade(x, thr, w.ti2, nrt, w.rd, nrm);
-      naut = filter_matched_fl(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp, flt, NT);
-      naud = filter_matched_fl(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp, fld, NK);
+  // stage 1: high-confidence detections x confirmed tracks (cascade); stage 2: medium-confidence
+  // detections x the remaining confirmed tracks (cascade); stage 3: IoU on unconfirmed
+  // (= non-tentative) + unmatched with time_since_update == 1 — one loop, one solver call site
+  int ncand = 0, nut3 = 0;
+  for (int st = 0; st < 3; st++) {
+    if (st == 1) SSTAMP(4);
+    if (st == 2) SSTAMP(5);
+    const int* ti = w.conf_t;
+    const int* di = w.hi;
+    int nt = ncf, nd = nhi;
+    double md = thr * 0.8;
+    int kind = M_GATED;
+    if (st == 1) {
+      // the unmatched tracks are all confirmed (a subset of conf_t)
+      for (int k = lane; k < naut; k += 64) w.ti2[k] = w.aut[k];
+      for (int k = lane; k < NK; k += 64) fld[k] = 0;
+      wsync();
+      for (int k = lane; k < naud; k += 64) fld[w.aud[k]] = 1;
+      wsync();
+      nd = wcompact(nmed, [&](int k) { return fld[w.med[k]] != 0; },
+                        [&](int k, int q) { w.rd[q] = w.med[k]; });
+      ti = w.ti2;
+      nt = naut;
+      di = w.rd;
+      md = thr;
+    } else if (st == 2) {
+      ncand = nun;
+      for (int k = lane; k < nun; k += 64) w.cand[k] = w.unconf_t[k];
+      wsync();
+      ncand += wcompact(naut, [&](int k) { return stsu[w.aut[k]] == 1; },
+                            [&](int k, int q) { w.cand[nun + q] = w.aut[k]; });
+      nd = wcompact(naud, [&](int k) { return !(x.det(w.aud[k])[4] < g.tlo); },
+                        [&](int k, int q) { w.rd[q] = w.aud[k]; });
+      ti = w.cand;
+      nt = ncand;
+      di = w.rd;
+      md = g.max_iou;
+      kind = M_IOU;
     }
-  }
-  SSTAMP(5);
-  // stage 3: IoU on unconfirmed (= non-tentative) + unmatched with time_since_update == 1
-  int ncand = nun;
-  for (int k = lane; k < nun; k += 64) w.cand[k] = w.unconf_t[k];
-  __syncthreads();
-  ncand += wave_compact(naut, [&](int k) { return stsu[w.aut[k]] == 1; },
-                        [&](int k, int q) { w.cand[nun + q] = w.aut[k]; });
-  (void)nlo;
-  const int nrd = wave_compact(naud, [&](int k) { return !(x.det(w.aud[k])[4] < g.tlo); },
-                               [&](int k, int q) { w.rd[q] = w.aud[k]; });
-  int nut3 = 0;
-  if (nrd && ncand) {
+    if (!(nd && nt)) continue;
     const int m0 = x.nm;
-    int nud3 = 0;
-    min_cost_matching(x, M_IOU, g.max_iou, w.cand, ncand, w.rd, nrd, w.ut3, nut3, w.ud, nud3);
+    match_stage(x, kind, md, ti, nt, di, nd, w.ut3, nut3);
     naut = filter_matched_fl(w.aut, naut, w.mt, m0, x.nm, 0, w.tmp, flt, NT);
     naud = filter_matched_fl(w.aud, naud, w.mt, m0, x.nm, 1, w.tmp, fld, NK);
   }
+  (void)nlo;
   for (int k = lane; k < NT; k += 64) flt[k] = 0;
-  __syncthreads();
+  wsync();
   for (int k = lane; k < ncand; k += 64) flt[w.cand[k]] = 1;
-  __syncthreads();
-  int nfut = wave_compact(naut, [&](int k) { return flt[w.aut[k]] == 0; },
+  wsync();
+  int nfut = wcompact(naut, [&](int k) { return flt[w.aut[k]] == 0; },
                           [&](int k, int q) { w.fut[q] = w.aut[k]; });
   for (int k = lane; k < nut3; k += 64) w.fut[nfut + k] = w.ut3[k];
   nfut += nut3;
-  __syncthreads();
+  wsync();
   SSTAMP(6);
 
   // the matched tracks' updates are ss_update_kernel's, the misses follow them (ss_post_kernel):
@@ -2189,7 +2506,7 @@ __global__ void __launch_bounds__(64) SS_MATCH_ATTR
   // updates it twice, in match order.  Later occurrences are flagged (negative position) and
   // listed after the matches; ss_update_kernel does the first ones, ss_post_kernel these in order.
   int* dupl = w.mt + 2 * (g.D + 2);
-  const int ndup = wave_compact(
+  const int ndup = wcompact(
       x.nm,
       [&](int q) {
         for (int j = 0; j < q; j++)
@@ -2207,6 +2524,8 @@ __global__ void __launch_bounds__(64) SS_MATCH_ATTR
 
   SCOUNT(6, x.nm);
   SSTAMP(7);
+  wsync();
+  if (lane == 0) __hip_atomic_store(&job.flag, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Track.update for every match of the three stages (tracker.py:139-141): wave per match.
@@ -2453,7 +2772,7 @@ __global__ void __launch_bounds__(64) ss_fit_kernel(SsDev g, int seq0) {
     const double pn = g.dprep[((size_t)seq * g.D + bdk) * 4 + 3];
     for (int q = lane; q < F; q += 64) {
       dst[q] = nf[q];
-      dstn[q] = nf[q] / pn;
+      dstn[nn_pos(q, F)] = nf[q] / pn;
     }
   }
   int* gv = g.gal_v + ((size_t)seq * g.T + slot) * g.GB;
@@ -2576,7 +2895,7 @@ __global__ void __launch_bounds__(64) ss_feat_set_kernel(SsDev g, int seq, const
   const double wn = sqrt(wdot(dst, dst, F));
   const double pn = wpw_norm(dst, F, lo, ln, leaf) + 1e-8;
   double* dstn = vecnp(g, seq, slot, v);
-  for (int q = lane; q < F; q += 64) dstn[q] = dst[q] / pn;
+  for (int q = lane; q < F; q += 64) dstn[nn_pos(q, F)] = dst[q] / pn;
   if (lane == 0) {
     const size_t vi = vidx(g, seq, slot, v);
     g.vwn[vi] = wn;
@@ -2715,7 +3034,7 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 4, st))) return rc;
   if ((rc = ss_probe_begin(e, 5, st))) return rc;
-  hipLaunchKernelGGL(ss_match_kernel, dim3(nseq), dim3(64), lds, st, d, seq0);
+  hipLaunchKernelGGL(ss_match_kernel, dim3(nseq), dim3(256), lds, st, d, seq0);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 5, st))) return rc;
   if ((rc = ss_probe_begin(e, 6, st))) return rc;

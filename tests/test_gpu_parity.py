@@ -1166,10 +1166,12 @@ def test_strongsort_c4_size_vs_oracle(torch_cuda):
     assert st["dets"] > 450 and st["tracks"] > 900, st  # the C4 geometry was really exercised
 
 
-@pytest.mark.parametrize("emb_dim", [128, 1024, 2048, 640])
+@pytest.mark.parametrize("emb_dim", [128, 1024, 2048, 640, 100, 37])
 def test_strongsort_feature_widths_vs_oracle(torch_cuda, emb_dim):
     """Feature widths around the NN kernel's k-blocks and the pairwise norm's leaf tree: one
-    leaf (128), 8 and 16 leaves (1024, 2048: the shuffle fold), 640 (the generic split tree)."""
+    leaf (128), 8 and 16 leaves (1024, 2048: the shuffle fold), 640 (the generic split tree);
+    100 (whole 8-element MFMA-order blocks then a 4-element tail in order), 37 (odd: no 16-byte
+    loads, every element in order)."""
     from boxmot_amd.synth import SyntheticScene
 
     scenes = [SyntheticScene(n_obj=20 + 10 * s, seed=900 + s, emb_dim=emb_dim,

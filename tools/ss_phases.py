@@ -24,7 +24,8 @@ PHASES = ["setup", "crowd", "camera+quality+sort+predict", "lists", "stage1 casc
 COUNTERS = ["cost build cyc", "lsap cyc", "lsap calls", "sum rows (tracks)", "sum cols (dets)",
             "dijkstra steps", "matches", "solver rows R", "solver cols CC", "slow rows",
             "slow-row cyc", "lsap loop cyc", "fast: wait+relax cyc",
-            "fast: wave min cyc", "fast: ballots cyc", "fast: tie/sink to next row cyc"]
+            "fast: wave min cyc", "fast: ballots cyc", "fast: tie/sink to next row cyc",
+            "table-settled rows"]
 
 
 def build():
@@ -67,7 +68,7 @@ def main():
         d, off, e = gen.frame(t)
         eng.step(d.double(), off, e.double(), None, out, cnt)
         torch.cuda.synchronize()
-    dbg = np.zeros((S, 32), np.uint64)
+    dbg = np.zeros((S, 48), np.uint64)
     N.check(L.bx_ss_debug_host(eng._h, dbg.ctypes.data), "debug")
     per = dbg.astype(np.float64) / a.frames
     tot = per[:, :len(PHASES)].sum(1)
