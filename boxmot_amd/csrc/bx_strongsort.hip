@@ -504,7 +504,7 @@ __device__ int pool_alloc(SsTrk& t, int VP) {
 
 // ---- the match kernel's code generation ---------------------------------------------------
 #ifndef SS_TAB_HELPERS  // the match kernel's two helper waves work on the first-step tables
-#define SS_TAB_HELPERS 1
+#define SS_TAB_HELPERS 0
 #endif
 #ifndef SS_TAB_RATIO  // the LSAP's first-step table when R * SS_TAB_RATIO >= CC (0: never)
 #define SS_TAB_RATIO 0
@@ -1000,15 +1000,13 @@ __global__ void __launch_bounds__(256)
 
 // ------------------------------------------------------------------------------------------
 // The frame kernel: one wave64 per sequence.
-// An LSAP handed by the match kernel's cascade wave to its solver wave (LDS): the matrix P and
-// its transpose PT, the clamp, the shape (the rows' offsets and the columns' indices are the
-// kernel's LDS arrays, passed to both waves as such so their accesses compile to LDS
+// An LSAP handed by the match kernel's cascade wave to its solver wave (LDS): the matrix kind and
+// orientation (lsap_mats), the clamp, the shape (the rows' offsets and the columns' indices are
+// the kernel's LDS arrays, passed to every wave as such so their accesses compile to LDS
 // instructions); np is the solver's answer.  flag: 0 idle (or done), 1 posted, -1 exit.
 struct LsapJob {
-  const double* P;
-  const double* PT;
   double max_d;
-  int R, CC, tr, ld, ldT, np;
+  int R, CC, tr, kind, np;
   int flag;
 };
 // The first-step table of an LSAP (see lsap_wave), computed by the solver wave and the match
@@ -1017,9 +1015,8 @@ struct LsapJob {
 // before its group is done, so its parameters are read after taking it); a finished group stamps
 // its job's epoch into gdone (one writer per group: no count to get wrong).  Epoch 0xffff: exit.
 struct TabJob {
-  const double* PT;
   double max_d;
-  int R, CC, ld, ldT;
+  int R, CC, kind, tr;
   unsigned long long ctr;
   int gdone[16];  // group g of the job with epoch e is done when gdone[g] == e
 };
@@ -1048,21 +1045,41 @@ struct SsCtx {
   __device__ int det_in(int i) const { return (int)det(i)[6]; }
 };
 
+// The matrices of an LSAP (min_cost_matching): P in the solver's orientation and its transpose
+// PT, with their leading dimensions — derived from the kernel argument in the wave that reads
+// them, so the loads compile to global (not flat) memory instructions, whose waits do not also
+// wait for LDS.  kind 0: the gated cost by cascade rank (ss_cost_kernel's cfull / cfullT); 1: the
+// IoU cost by list position (cost / its transpose).
+__device__ __forceinline__ void lsap_mats(const SsDev& g, int seq, int kind, bool tr,
+                                          const double*& P, const double*& PT, int& ld, int& ldT) {
+  if (kind == 0) {
+    const double* a = g.cfull + (size_t)seq * g.T * g.D;
+    const double* b = g.cfullT + (size_t)seq * g.D * g.T;
+    P = tr ? b : a;
+    PT = tr ? a : b;
+  } else {
+    const double* io = g.cost + (size_t)seq * 4 * g.T * g.D;
+    P = tr ? io + (size_t)g.T * g.D : io;
+    PT = tr ? io : io + (size_t)g.T * g.D;
+  }
+  ld = tr ? g.T : g.D;
+  ldT = tr ? g.D : g.T;
+}
+
 // One 64-row group of an LSAP's first-step table, lane per row (see lsap_wave): the minimum of
 // the row's unclamped entries and the column at it when it is the only one and at most max_d
 // (clamping then changes neither; above max_d every entry clamps to one value: a tie), else -2.
 // A NaN entry is never the minimum nor equal to it, as in the solver's first step.  Four
 // independent chains over the columns (u mod 4), merged at the end; 32 loads in flight.
-__device__ __forceinline__ void tab_group(SsWs& w, const TabJob* tj, const int* roff,
-                                          const int* cidx, int grp, int lane) {
-  const double* PT = tj->PT;
-  const int R = tj->R, CC = tj->CC, ld = tj->ld, ldT = tj->ldT;
-  const double max_d = tj->max_d;
+__device__ __forceinline__ void tab_rows(SsWs& w, const double* __restrict__ PT,
+                                         const int* roff, const int* cidx, int R, int CC, int ld,
+                                         int ldT, double max_d, int grp, int lane) {
   const int r = 64 * grp + lane;
   const double* base = PT + (r < R ? roff[r] / ld : 0);
   double m[4] = {INF, INF, INF, INF};
   int a[4] = {-1, -1, -1, -1};
   bool tie[4] = {false, false, false, false};
+  bool big = true;  // every entry above max_d (a NaN is not): all clamp to one value
   for (int j0 = 0; j0 < CC; j0 += 32) {
     double e[32];
 #pragma unroll
@@ -1074,6 +1091,7 @@ __device__ __forceinline__ void tab_group(SsWs& w, const TabJob* tj, const int* 
     for (int u = 0; u < 32; u++) {
       if (j0 + u >= CC) break;
       const int c = u & 3;
+      big &= e[u] > max_d;
       if (e[u] < m[c]) m[c] = e[u], a[c] = j0 + u, tie[c] = false;
       else if (e[u] == m[c]) tie[c] = true;
     }
@@ -1088,33 +1106,40 @@ __device__ __forceinline__ void tab_group(SsWs& w, const TabJob* tj, const int* 
   }
   if (r < R) {
     w.u[r] = mm;
-    w.col4row[r] = (!tt && mm <= max_d && mm < INF) ? aa : -2;
+    w.col4row[r] = (!tt && mm <= max_d && mm < INF) ? aa : (big ? -3 : -2);
   }
 }
 
 // take table tickets until a void one; returns.  The ticket is made wave-uniform by readfirstlane
 // (lane 0 took it; every lane is active here), so the exit test is a scalar branch.
-__device__ __forceinline__ void tab_work(SsWs& w, TabJob* tj, const int* roff, const int* cidx,
-                                         int lane) {
+__device__ __forceinline__ void tab_work(const SsDev& g, int seq, SsWs& w, TabJob* tj,
+                                         const int* roff, const int* cidx, int lane) {
   for (;;) {
-    unsigned long long t = 0;
-    if (lane == 0) t = __hip_atomic_fetch_add(&tj->ctr, 1ull, __ATOMIC_ACQ_REL,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(t >> 32));
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(t & 0xffffffffull));
+    // every lane takes part (lane 0 adds 1, the rest 0): no lane-dependent branch around the
+    // atomic, so the compiler keeps the loop uniform; lane 0's value is the ticket
+    const unsigned long long t = __hip_atomic_fetch_add(&tj->ctr, lane == 0 ? 1ull : 0ull,
+                                                        __ATOMIC_ACQ_REL,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(t >> 32), 0);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)(t & 0xffffffffull), 0);
     const int ng = (int)(hi & 0xffffu), gi = (int)lo;
     if (gi >= ng) return;
-    tab_group(w, tj, roff, cidx, gi, lane);
+    const double* P;
+    const double* PT;
+    int ld, ldT;
+    const int R = tj->R, CC = tj->CC;
+    const double max_d = tj->max_d;
+    lsap_mats(g, seq, tj->kind, tj->tr != 0, P, PT, ld, ldT);
+    tab_rows(w, PT, roff, cidx, R, CC, ld, ldT, max_d, gi, lane);
     wsync();
-    if (lane == 0)
-      __hip_atomic_store(&tj->gdone[gi], (int)(hi >> 16), __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&tj->gdone[gi], (int)(hi >> 16), __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
 
 // the match kernel's helper waves: table groups of every posted LSAP until the exit epoch
-__device__ __forceinline__ void tab_server(SsWs& w, TabJob* tj, const int* roff, const int* cidx,
-                                           int lane) {
+__device__ __forceinline__ void tab_server(const SsDev& g, int seq, SsWs& w, TabJob* tj,
+                                           const int* roff, const int* cidx, int lane) {
   unsigned seen = 0;
   for (;;) {
     unsigned ep;
@@ -1123,7 +1148,7 @@ __device__ __forceinline__ void tab_server(SsWs& w, TabJob* tj, const int* roff,
       __builtin_amdgcn_s_sleep(2);
     seen = ep;
     if (seen == 0xffffu) return;
-    tab_work(w, tj, roff, cidx, lane);
+    tab_work(g, seq, w, tj, roff, cidx, lane);
   }
 }
 
@@ -1155,7 +1180,8 @@ __device__ __forceinline__ void tab_server(SsWs& w, TabJob* tj, const int* roff,
 template <int LQ, bool IDX>
 __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P, const int* roff,
                                          const int* cidx, double max_d, int R, int CC, bool tr,
-                                         const double* __restrict__ PT, int ld, int ldT) {
+                                         const double* __restrict__ PT, int ld, int ldT,
+                                         int kind) {
   SsWs& w = x.w;
   const int lane = x.lane;
 #ifdef BX_PHASE_TIMING
@@ -1170,28 +1196,36 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
   // the table pays when a row's full first step (~1.8 k cycles) outweighs its share of the
   // table's CC-column sweep per 64 rows
   const bool TB = SS_TAB_RATIO > 0 && IDX && LQ <= 16 && R >= 2 && R * SS_TAB_RATIO >= CC;
-  if (TB) {  // posted to the helper waves, worked on here too, waited for
+  if (TB && !SS_TAB_HELPERS) {  // the solver wave alone, 64 rows at a time
+    for (int grp = 0; grp * 64 < R; grp++)
+      tab_rows(w, PT, roff, cidx, R, CC, ld, ldT, max_d, grp, lane);
+    wsync();
+  } else if (TB) {  // posted to the helper waves, worked on here too, waited for
     TabJob* tj = x.tab;
     const int ng = (R + 63) / 64;
     const unsigned ep = ++x.tep;
     if (lane == 0) {
-      tj->PT = PT;
       tj->max_d = max_d;
       tj->R = R;
       tj->CC = CC;
-      tj->ld = ld;
-      tj->ldT = ldT;
+      tj->kind = kind;
+      tj->tr = tr;
     }
     wsync();
     if (lane == 0)
       __hip_atomic_store(&tj->ctr, (unsigned long long)ep << 48 | (unsigned long long)ng << 32,
                          __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    tab_work(w, tj, roff, cidx, lane);
+    tab_work(x.g, x.seq, w, tj, roff, cidx, lane);
     // every group stamped with this epoch (lane g checks group g; ng <= 16)
     while (__ballot(lane < ng && __hip_atomic_load(&tj->gdone[lane < 16 ? lane : 0],
                                                    __ATOMIC_ACQUIRE,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP) != (int)ep))
       __builtin_amdgcn_s_sleep(1);
+
+  } else {
+    for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
+  }
+  if (TB) {
 #ifdef SS_TAB_VERIFY  // diagnostic builds: the table re-derived here, row by row, must agree
     for (int r0 = 0; r0 < R; r0 += 64) {
       const int r = r0 + lane;
@@ -1200,26 +1234,26 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       double mm = INF;
       int aa = -1;
       bool tt = false;
+      bool big = true;
       for (int j = 0; j < CC; j++) {
         const double e = base[(size_t)cidx[j] * ldT];
+        big &= e > max_d;
         if (e < mm) mm = e, aa = j, tt = false;
         else if (e == mm) tt = true;
       }
-      const int code = (!tt && mm <= max_d && mm < INF) ? aa : -2;
+      const int code = (!tt && mm <= max_d && mm < INF) ? aa : (big ? -3 : -2);
       const double um = w.u[r];
       const int uc = w.col4row[r];
       if (!(um == mm || (um != um && mm != mm)) || uc != code) {
         atomicExch(x.g.status, 9000 + (uc == code ? 1 : 2));
         if (atomicAdd(&x.g.status[1], 1) < 24)
-          printf("TABV seq %d ep %u R %d CC %d ld %d ldT %d r %d roff %d: table (%g, %d) "
-                 "recomputed (%g, %d) tj(R %d CC %d ld %d ldT %d PT %p/%p)\n",
-                 x.seq, ep, R, CC, ld, ldT, r, roff[r], um, uc, mm, code, tj->R, tj->CC,
-                 tj->ld, tj->ldT, (const void*)tj->PT, (const void*)PT);
+          printf("TABV seq %d R %d CC %d ld %d ldT %d r %d roff %d: table (%g, %d) "
+                 "recomputed (%g, %d)\n",
+                 x.seq, R, CC, ld, ldT, r, roff[r], um, uc, mm, code);
       }
     }
 #endif
-  } else {
-    for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
+    wsync();
   }
   for (int j = lane; j < CC; j += 64) w.path[j] = -1, w.row4col[j] = -1;
   unsigned cb[LQ];  // byte offset of the lane's column q in a row (column 0's past CC)
@@ -1247,17 +1281,52 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
   int off1 = R > 1 ? roff[1] : 0;
   if (PF && R > 0) load_row(roff[0], nx);
   unsigned chg = 0;  // columns whose v changed: the SC bits of every search that went on
-  int tcode = -2;    // the table's column codes of the current 64 rows, lane l row 64k + l
+  // v decreases in exact arithmetic, but a rounded reduced cost can make a search's last minimum
+  // fall below an earlier one and raise a v[j] by an ulp: from then on a later row's other
+  // entries may drop, so the table's first steps are not trusted for the rest of this LSAP
+  bool vpos = false;
+  int tcode = -4;    // the table's column codes of the current 64 rows, lane l row 64k + l
+  // with a table: the rows it cannot settle (code -2) are known ahead, so the next such row of
+  // the current 64 has its costs in flight in nx meanwhile (pf_row; -1: none)
+  int pf_row = -1;
+  auto prefetch_from = [&](int from) {
+    const unsigned long long m =
+        __ballot(tcode == -2) & (((from & 63) == 0) ? ~0ull : (~0ull << (from & 63)));
+    const int r = m ? (from & ~63) + (__ffsll((long long)m) - 1) : R;
+    if (r < R) {  // (lanes past R hold -4, never -2: r < R by construction)
+      pf_row = r;
+      load_row(roff[pf_row], nx);
+    }
+  };
   for (int cur = 0; cur < R; cur++) {
 #ifdef BX_PHASE_TIMING
     unsigned long long t_r0 = SS_NOW();
 #endif
     if (TB) {
-      if ((cur & 63) == 0) tcode = cur + lane < R ? w.col4row[cur + lane] : -2;
-      const int jt = rl_i(tcode, cur & 63);
-      if (jt >= 0 && !((rl_i((int)(asg | chg), jt & 63) >> (jt >> 6)) & 1u)) {
+      if ((cur & 63) == 0) {
+        tcode = cur + lane < R ? w.col4row[cur + lane] : -4;  // -4: past the last row
+        if (pf_row < cur) prefetch_from(cur);
+      }
+      int jt = vpos ? -2 : rl_i(tcode, cur & 63);
+      if (jt == -3) {
+        // every entry clamps to clampv: the first step's minimum set is the columns whose
+        // clampv - v[j] rounds to clampv (v only decreases, so no entry is below it), and scipy
+        // takes the smallest unassigned one among them (the last in its fresh `remaining`
+        // order), when there is one (columns past CC have v = -INF)
+        jt = -2;
+#pragma unroll
+        for (int q = LQ - 1; q >= 0; q--) {
+          const unsigned long long fr =
+              __ballot(!((asg >> q) & 1u) && clampv - vr[q] == clampv);
+          if (fr) jt = 64 * q + (__ffsll((long long)fr) - 1);
+        }
+        if (jt >= 0 && lane == 0) w.u[cur] = clampv;
+      } else if (jt >= 0 && ((rl_i((int)(asg | chg), jt & 63) >> (jt >> 6)) & 1u)) {
+        jt = -2;
+      }
+      if (jt >= 0) {
         if (lane == (jt & 63)) asg |= 1u << (jt >> 6);
-        if (lane == 0) {  // u[cur] holds the table's minimum already
+        if (lane == 0) {  // u[cur]: the table's minimum (or clampv)
           w.row4col[jt] = cur;
           w.col4row[cur] = jt;
         }
@@ -1266,7 +1335,8 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
 #endif
         continue;
       }
-      load_row(roff[cur], nx);
+      if (pf_row != cur) load_row(roff[cur], nx);
+      pf_row = -1;
     } else if (!PF) {
       load_row(roff[cur], nx);
     }
@@ -1291,6 +1361,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       load_row(off1, nx);
       off1 = cur + 2 < R ? roff[cur + 2] : 0;
     }
+    if (TB && ((cur + 1) & 63) != 0) prefetch_from(cur + 1);
     const double m0 = wave_min_bfly(lmin);
 #ifdef BX_PHASE_TIMING
     asm volatile("" ::"v"(m0));
@@ -1475,7 +1546,13 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     if (lane == 0) w.u[cur] = 0.0 + minVal;
 #pragma unroll
     for (int q = 0; q < LQ; q++)
-      if ((sc >> q) & 1u) vr[q] -= minVal - rv[q];
+      if ((sc >> q) & 1u) {
+        const double dv = minVal - rv[q];
+        vr[q] -= dv;
+        if (dv != 0.0) chg |= 1u << q;  // v[j] changed (a zero step leaves it as it was)
+        vpos |= vr[q] > 0.0;
+      }
+    vpos = __any(vpos);
     wsync();
     if (lane == 0) {
       int jj = sk;
@@ -1489,7 +1566,6 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       }
     }
     if (lane == (sk & 63)) asg |= 1u << (sk >> 6);
-    chg |= sc;
 #ifdef BX_PHASE_TIMING
     t_slow += SS_NOW() - t_s0;
 #endif
@@ -1710,15 +1786,18 @@ __device__ __forceinline__ void lsap_server(SsCtx& x, LsapJob* jb, const int* ro
                 &jb->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))) == 0)
       __builtin_amdgcn_s_sleep(1);
     if (f < 0) return;
-    const double* P = jb->P;
-    const double* PT = jb->PT;
     const double mx = jb->max_d;
-    const int R = jb->R, CC = jb->CC, ld = jb->ld, ldT = jb->ldT;
+    const int R = jb->R, CC = jb->CC, kind = jb->kind;
     const bool tr = jb->tr != 0;
-    const int np = CC <= 256    ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT)
-                   : CC <= 512  ? lsap_wave<8, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT)
-                   : CC <= 1024 ? lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT)
-                                : lsap_wave<32, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT);
+    const double* P;
+    const double* PT;
+    int ld, ldT;
+    lsap_mats(x.g, x.seq, kind, tr, P, PT, ld, ldT);
+    const int np =
+        CC <= 256    ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT, kind)
+        : CC <= 512  ? lsap_wave<8, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT, kind)
+        : CC <= 1024 ? lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT, kind)
+                     : lsap_wave<32, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT, kind);
     if (x.lane == 0) jb->np = np;
     wsync();
     if (x.lane == 0) __hip_atomic_store(&jb->flag, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1810,14 +1889,11 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
   {
     LsapJob* jb = x.job;
     if (lane == 0) {
-      jb->P = P;
-      jb->PT = PT;
       jb->max_d = mx;
       jb->R = R;
       jb->CC = CC;
       jb->tr = tr;
-      jb->ld = ld;
-      jb->ldT = ldT;
+      jb->kind = kind;
     }
     wsync();
     if (lane == 0) __hip_atomic_store(&jb->flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2376,7 +2452,7 @@ __global__ void __launch_bounds__(256) SS_MATCH_ATTR
   const int wid = (int)__builtin_amdgcn_readfirstlane((unsigned)(threadIdx.x >> 6));
   if (wid >= 2) {  // the helper waves: first-step tables
 #if SS_TAB_HELPERS
-    tab_server(w, &tab, sage, flt, lane);
+    tab_server(g, seq, w, &tab, sage, flt, lane);
 #endif
     return;
   }
