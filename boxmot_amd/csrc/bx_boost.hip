@@ -478,28 +478,42 @@ __global__ void __launch_bounds__(OW)
       L.colsum[t] = cs;
     }
     __syncthreads();
-    // S = ((MhSim + shape) + soft-BIoU) / 3 row by row (lanes over tracks): each detection's
-    // max over tracks (the reference's np.max: NaN-propagating, otherwise order-free) and the
-    // VT test by wave reductions; E stays intact for the association cost
-    for (int d = 0; d < n; d++) {
-      const double* a = L.dd + DDW * d;
+    // S = ((MhSim + shape) + soft-BIoU) / 3 for every (detection, track): G lanes per
+    // detection (G = the largest power of two with n * G <= 64, at most 16), each over the tracks
+    // t = sub (mod G); each detection's max over tracks (the reference's np.max: NaN-propagating,
+    // otherwise order-free) and the VT test combined within the lane group by shuffles.  The
+    // detections are independent, so all of them are scored at once instead of one wave
+    // reduction after another.  E stays intact for the association cost.
+    int G = 1;
+    while (G < 16 && n * G * 2 <= OW) G *= 2;
+    const int sub = lane & (G - 1);
+    for (int d0 = 0; d0 < n * G; d0 += OW) {
+      const int d = (d0 + lane) / G;
+      const bool live = d < n;
+      const double* a = L.dd + DDW * (live ? d : 0);
       double mx = -INF;
       bool nan = false, vt = false;
-      for (int t = lane; t < nt; t += OW) {
-        const double* rw = tb + (size_t)t * TBB;
-        const double ev = E[d * nt + t];
-        const double mhs = ev < 0 ? 0.0 : ev / L.colsum[t];
-        const double S = ((mhs + shape_sim(a, rw, g.s_sim_corr)) + soft_biou(a, rw, rw[4])) / 3;
-        if (S != S)
-          nan = true;
-        else
-          mx = mx > S ? mx : S;
-        if (g.use_vt && S > nmax(0.95 - (rw[5] - 1.0), 0.8)) vt = true;
+      if (live) {
+        for (int t = sub; t < nt; t += G) {
+          const double* rw = tb + (size_t)t * TBB;
+          const double ev = E[d * nt + t];
+          const double mhs = ev < 0 ? 0.0 : ev / L.colsum[t];
+          const double S = ((mhs + shape_sim(a, rw, g.s_sim_corr)) + soft_biou(a, rw, rw[4])) / 3;
+          if (S != S)
+            nan = true;
+          else
+            mx = mx > S ? mx : S;
+          if (g.use_vt && S > nmax(0.95 - (rw[5] - 1.0), 0.8)) vt = true;
+        }
       }
-      nan = __any(nan);
-      vt = __any(vt);
-      const double max_s = nan ? __builtin_nan("") : -wave_min_dpp(-mx);
-      if (lane == 0) {
+      for (int o = 1; o < G; o <<= 1) {  // within the lane group (xor stays inside it)
+        const double om = __shfl_xor(mx, o);
+        mx = om > mx ? om : mx;
+        nan = (__shfl_xor((int)nan, o) != 0) || nan;
+        vt = (__shfl_xor((int)vt, o) != 0) || vt;
+      }
+      if (live && sub == 0) {
+        const double max_s = nan ? __builtin_nan("") : mx;
         double c = a[4];
         if (!g.use_sb && !g.use_vt) {
           c = nmax(c, max_s * g.dlo_coef);

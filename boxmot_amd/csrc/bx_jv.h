@@ -690,6 +690,23 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
     if (lane == a) col = cb, y = yb, pred = pb, v = vb, d = db;
     if (lane == b) col = ca, y = ya, pred = pa, v = va, d = da;
   };
+  // A run of swaps replayed on one index register (perm: the lane whose registers end at this
+  // position) and applied once, by one gather per register, when it is long: a swap then costs
+  // two readlanes instead of fourteen.  (The runs below only swap a position k with one at or
+  // before it, so a later position still holds its own registers while the run is replayed.)
+  auto swap_perm = [&](int& perm, int a, int b) {
+    if (a == b) return;
+    const int pa = rl_i(perm, a), pb = rl_i(perm, b);
+    perm = lane == a ? pb : (lane == b ? pa : perm);
+  };
+  auto apply_perm = [&](int perm) {
+    col = __shfl(col, perm);
+    y = __shfl(y, perm);
+    pred = __shfl(pred, perm);
+    v = __shfl(v, perm);
+    d = __shfl(d, perm);
+  };
+  constexpr int PERM_RUN = 3;  // swaps in a run from which the gather pays
   // ---- _ca_dense
   for (int f = 0; f < nfree; f++) {
     const int start = rl_i(fr, f);
@@ -739,16 +756,32 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
             double ex = __shfl_up(pm, 1);
             if (lane == 0) ex = INF;
             unsigned long long ev = __ballot(own && lane > low && d <= ex);
-            while (ev) {
-              const int k = __ffsll((long long)ev) - 1;
-              ev &= ev - 1;
-              const double h = rl_d(d, k);
-              if (h < mn) {
-                up = low;
-                mn = h;
+            if (__popcll(ev) >= PERM_RUN) {
+              int perm = lane;
+              while (ev) {
+                const int k = __ffsll((long long)ev) - 1;
+                ev &= ev - 1;
+                const double h = rl_d(d, k);  // position k is still untouched
+                if (h < mn) {
+                  up = low;
+                  mn = h;
+                }
+                swap_perm(perm, k, up);
+                up++;
               }
-              swap_pos(k, up);
-              up++;
+              apply_perm(perm);
+            } else {
+              while (ev) {
+                const int k = __ffsll((long long)ev) - 1;
+                ev &= ev - 1;
+                const double h = rl_d(d, k);
+                if (h < mn) {
+                  up = low;
+                  mn = h;
+                }
+                swap_pos(k, up);
+                up++;
+              }
             }
           } else {
             for (int k = up; k < n; k++) {
@@ -800,11 +833,22 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
         }
         // columns lowered to the minimum join the SCAN set, in position order (all before pe)
         unsigned long long bits = __ballot(act && B && lane < pe);
-        while (bits) {
-          const int k = __ffsll((long long)bits) - 1;
-          bits &= bits - 1;
-          swap_pos(k, up);
-          up++;
+        if (__popcll(bits) >= PERM_RUN) {
+          int perm = lane;
+          while (bits) {
+            const int k = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            swap_perm(perm, k, up);
+            up++;
+          }
+          apply_perm(perm);
+        } else {
+          while (bits) {
+            const int k = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            swap_pos(k, up);
+            up++;
+          }
         }
       }
       JVT(6);

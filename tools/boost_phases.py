@@ -38,10 +38,11 @@ def main():
     ap.add_argument("--frames", type=int, default=60)
     ap.add_argument("--no-build", action="store_true")
     ap.add_argument("--c5", action="store_true", help="the boosttrack_mot8 sequences (MOT dets)")
+    ap.add_argument("--lib", default=None, help="a timing build of tools/build_variant.py")
     a = ap.parse_args()
     if not a.no_build:
         build()
-    os.environ["BX_LIB_PATH"] = str(LIB)
+    os.environ["BX_LIB_PATH"] = a.lib or str(LIB)
     import torch
 
     from bench import CONFIGS, OCS_CONF_LO
