@@ -10,11 +10,12 @@
 //                         every sequence: fp64 MFMA (v_mfma_f64_16x16x4_f64), K staged through
 //                         LDS, one 4-wave workgroup per sequence; the MFMA accumulates each entry
 //                         as an ascending-k fma chain = oracle/bxo_boost.c emb_dot
-//   boost_frame_kernel    one wave64 per sequence: CMC warp + Kalman predict (an octet of lanes
-//                         per track, lane r owns row r), DLO/DUO boosts, the detection filter,
-//                         the association cost (lane per track, detections broadcast from LDS),
-//                         one-to-one fast path or lapx's JV (bx_jv.h), validation, Kalman updates
-//                         (octets), births, outputs, deaths; emits embedding-update records
+//   boost_frame_kernel    one four-wave workgroup per sequence: CMC warp + Kalman predict (an
+//                         octet of lanes per track, lane r owns row r), DLO/DUO boosts (thread
+//                         per pair / lane groups per detection), the detection filter, the
+//                         association cost (thread per entry), one-to-one fast path or lapx's JV
+//                         (bx_jv.h, wave 0), validation, Kalman updates (octets), births,
+//                         outputs, deaths; emits embedding-update records
 //   boost_feature_kernel  (with_reid) wave per record: emb = a*emb + (1-a)*det, emb /= ||emb||
 //                         (wave-order norm), or the newborn track's copy of its detection's
 // Every floating-point expression restates oracle/bxo_boost.c operation for operation (built
@@ -61,6 +62,7 @@ struct BstDev {
   int* order;             // [S][T] slot ids in the reference's list order
   double* tb;             // [S][T][TBB]
   double* cost_g;         // [S][D*T] or null
+  double* e_g;            // [S][D*T] DLO MhDist numerators when they do not fit LDS, or null
   double* ec;             // [S][D][T] emb cost by (detection, list position)  (reid)
   double* emb;            // [S][T][F] track embeddings by slot                 (reid)
   int* rec;               // [S][D][2] (slot, global detection row)            (reid)
@@ -316,6 +318,7 @@ struct BstLds {
   int *mi, *mm;    // [2N] candidate / validated (kept det, list position) pairs
   int *ud, *ut;    // [D+T] unmatched lists
   int *rowcnt, *colcnt, *rowcol, *fl;  // [N] each
+  int* u;          // [8] values one wave derives for all
   JvLds jv;
 };
 
@@ -349,29 +352,44 @@ __device__ void carve(const BstDev& g, char* base, BstLds& L) {
   L.jv.pred = takeI(N);
   L.jv.col = takeI(N);
   L.jv.sc = takeI(8);
+  L.u = takeI(8);
   L.jv.dc = nullptr;
 }
 
 size_t lds_bytes(int D, int T, int N, int cost_lds) {
   auto dI = [](size_t n) { return ((n * 4 + 7) / 8) * 8; };
   return (size_t)D * DDW * 8 + (size_t)cost_lds * 8 + (size_t)T * 8 + 2 * (size_t)N * 8 + 2 * 8 +
-         2 * dI(D) + 2 * dI(T) + 2 * dI(2 * N) + 2 * dI(D + T) + 4 * dI(N) + 6 * dI(N) + dI(8);
+         2 * dI(D) + 2 * dI(T) + 2 * dI(2 * N) + 2 * dI(D + T) + 4 * dI(N) + 6 * dI(N) + dI(8) +
+         dI(8);
 }
 
-__global__ void __launch_bounds__(OW)
+// One workgroup of 1-4 waves per sequence (frame_threads: about one wave per SIMD over the
+// launch — four for up to 256 sequences, one from 1024 on).  Work over pairs, detections or tracks
+// is spread over all the waves; the order-dependent steps (compactions, the validation's ballots)
+// run in every wave at once on the same LDS data — each wave derives the same counts and writes the
+// same values — except the JV, which wave 0 solves alone (SyncWaveL) while the others wait at the
+// barrier after it.
+constexpr int BW = 256;  // the most threads per sequence
+__host__ __device__ constexpr int frame_threads(int nseq) {
+  return nseq >= 1024 ? 64 : nseq >= 512 ? 128 : nseq > 256 ? 192 : 256;
+}
+constexpr int COST_KR = 4;  // cost entries per thread per chunk (registers held across a barrier)
+
+__global__ void __launch_bounds__(BW)
     boost_frame_kernel(BstDev g, int seq0, const float* __restrict__ dets,
                        const int* __restrict__ det_off, const double* __restrict__ warps,
                        double* __restrict__ out, int* __restrict__ out_count) {
   extern __shared__ __align__(16) char lds_raw[];
   BstLds L;
   carve(g, lds_raw, L);
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, nth = blockDim.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x, seq = seq0 + b;
   L.jv.dc = g.dbg ? g.dbg + (size_t)seq * BST_DBG + 24 : nullptr;
   const int r0 = det_off[b];
   int n = det_off[b + 1] - r0;
   if (n > g.D) {  // the host checks det_cap; a device-side overflow is latched, never run past
-    if (lane == 0) atomicExch(g.status, (int)BX_ERR_CAPACITY);
+    if (tid == 0) atomicExch(g.status, (int)BX_ERR_CAPACITY);
     n = g.D;
   }
   int* sq = g.seqst + (size_t)seq * SQB;
@@ -379,6 +397,7 @@ __global__ void __launch_bounds__(OW)
   int* order = g.order + (size_t)seq * g.T;
   double* tb = g.tb + (size_t)seq * g.T * TBB;
   double* costg = g.cost_g ? g.cost_g + (size_t)seq * g.D * g.T : nullptr;
+  double* eg = g.e_g ? g.e_g + (size_t)seq * g.D * g.T : nullptr;
   const double* ec = g.reid ? g.ec + (size_t)seq * g.D * g.T : nullptr;
   const int frame = sq[SB_FRAME] + 1;
   const int id0 = sq[SB_IDS];
@@ -390,23 +409,23 @@ __global__ void __launch_bounds__(OW)
 #endif
 
   // detections (x1,y1,x2,y2,conf,cls, det_ind = input row) and the track list
-  for (int q = lane; q < n * 6; q += OW) L.dd[(q / 6) * DDW + q % 6] = (double)dets[(size_t)r0 * 6 + q];
+  for (int q = tid; q < n * 6; q += nth) L.dd[(q / 6) * DDW + q % 6] = (double)dets[(size_t)r0 * 6 + q];
   __syncthreads();
-  for (int i = lane; i < n; i += OW) {
+  for (int i = tid; i < n; i += nth) {
     L.dd[DDW * i + 6] = (double)i;
     bbox_to_z(L.dd + DDW * i, L.dd + DDW * i + 7);
   }
-  for (int p = lane; p < nt; p += OW) L.lst[p] = order[p];
+  for (int p = tid; p < nt; p += nth) L.lst[p] = order[p];
   __syncthreads();
   BSTAMP(0);
 
   // ---- CMC warp (camera_update, boosttrack.py:81-103) + predict (:105-111), octet per track;
   // tb row: box[4], get_confidence, time_since_update, x[0..3], 1/diag(P)[0..3]
-  const int oct = lane >> 3, r = lane & 7;
+  const int oct = tid >> 3, r = tid & 7;
   double w6[6] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0};
   if (warps)
     for (int q = 0; q < 6; q++) w6[q] = warps[(size_t)b * 6 + q];
-  for (int c = 0; c < nt; c += 8) {
+  for (int c = 0; c < nt; c += nth / 8) {
     const int p = c + oct;
     if (p < nt) {
       BstTrk& t = trk[L.lst[p]];
@@ -455,40 +474,41 @@ __global__ void __launch_bounds__(OW)
   BSTAMP(1);
 
   // ---- DLO confidence boost (boosttrack.py:413-456) ----------------------------------------
-  bool have_e = false;  // L.cost holds MhDist numerators E[d][t] (sign = clipped) of all dets
-  if (g.use_dlo && n > 0 && nt > 0 && g.rich_s && n * nt <= g.cost_lds) {
-    // the (detection, track) similarity terms lane per PAIR, staged in the (not yet used) cost
-    // matrix's LDS: E = MhDist numerator (negated where MhDist clipped, exp() > 0), then the
-    // column sums in detection order, then S = ((MhSim + shape) + soft-BIoU) / 3 in place, then
-    // each detection's max over tracks in track order (the reference's reduction order)
-    double* E = L.cost;
-    for (int p = lane; p < n * nt; p += OW) {
-      const int d = p / nt, t = p - d * nt;
-      bool m;
-      const double e = mh_num(mh_dist(L.dd + DDW * d, tb + (size_t)t * TBB), m);
-      E[p] = m ? -e : e;
-    }
-    __syncthreads();
-    for (int t = lane; t < nt; t += OW) {
-      double cs = 0.0;
-      for (int d = 0; d < n; d++) {
-        const double e = fabs(E[d * nt + t]);
-        cs = d == 0 ? e : cs + e;
+  // With rich_s: E[d][t] = the MhDist numerator of every (detection, track) pair, negated where
+  // MhDist clipped (exp() > 0), thread per pair, staged in the cost matrix's LDS (not used yet)
+  // or the sequence's global scratch; then the column sums in detection order (thread per track).
+  // E stays intact for the association cost.
+  const double* E = nullptr;
+  if (g.use_dlo && n > 0 && nt > 0) {
+    if (g.rich_s) {
+      double* Ew = (n * nt <= g.cost_lds) ? L.cost : eg;
+      for (int p = tid; p < n * nt; p += nth) {
+        const int d = p / nt, t = p - d * nt;
+        bool m;
+        const double e = mh_num(mh_dist(L.dd + DDW * d, tb + (size_t)t * TBB), m);
+        Ew[p] = m ? -e : e;
       }
-      L.colsum[t] = cs;
+      __syncthreads();
+      for (int t = tid; t < nt; t += nth) {
+        double cs = 0.0;
+        for (int d = 0; d < n; d++) {
+          const double e = fabs(Ew[d * nt + t]);
+          cs = d == 0 ? e : cs + e;
+        }
+        L.colsum[t] = cs;
+      }
+      __syncthreads();
+      E = Ew;
     }
-    __syncthreads();
-    // S = ((MhSim + shape) + soft-BIoU) / 3 for every (detection, track): G lanes per
-    // detection (G = the largest power of two with n * G <= 64, at most 16), each over the tracks
-    // t = sub (mod G); each detection's max over tracks (the reference's np.max: NaN-propagating,
-    // otherwise order-free) and the VT test combined within the lane group by shuffles.  The
-    // detections are independent, so all of them are scored at once instead of one wave
-    // reduction after another.  E stays intact for the association cost.
+    // S[d][t] = ((MhSim + shape) + soft-BIoU) / 3 (rich_s) or IoU: G threads per detection (G =
+    // the largest power of two with n * G <= nth, at most 16), each over the tracks t = sub
+    // (mod G); each detection's max over tracks (np.max: NaN-propagating, otherwise order-free)
+    // and the VT test combined within the thread group by shuffles (the group stays in a wave)
     int G = 1;
-    while (G < 16 && n * G * 2 <= OW) G *= 2;
-    const int sub = lane & (G - 1);
-    for (int d0 = 0; d0 < n * G; d0 += OW) {
-      const int d = (d0 + lane) / G;
+    while (G < 16 && n * G * 2 <= nth) G *= 2;
+    const int sub = tid & (G - 1);
+    for (int d0 = 0; d0 < n * G; d0 += nth) {
+      const int d = (d0 + tid) / G;
       const bool live = d < n;
       const double* a = L.dd + DDW * (live ? d : 0);
       double mx = -INF;
@@ -496,9 +516,14 @@ __global__ void __launch_bounds__(OW)
       if (live) {
         for (int t = sub; t < nt; t += G) {
           const double* rw = tb + (size_t)t * TBB;
-          const double ev = E[d * nt + t];
-          const double mhs = ev < 0 ? 0.0 : ev / L.colsum[t];
-          const double S = ((mhs + shape_sim(a, rw, g.s_sim_corr)) + soft_biou(a, rw, rw[4])) / 3;
+          double S;
+          if (E) {
+            const double ev = E[d * nt + t];
+            const double mhs = ev < 0 ? 0.0 : ev / L.colsum[t];
+            S = ((mhs + shape_sim(a, rw, g.s_sim_corr)) + soft_biou(a, rw, rw[4])) / 3;
+          } else {
+            S = iou_b(a, rw);
+          }
           if (S != S)
             nan = true;
           else
@@ -506,7 +531,7 @@ __global__ void __launch_bounds__(OW)
           if (g.use_vt && S > nmax(0.95 - (rw[5] - 1.0), 0.8)) vt = true;
         }
       }
-      for (int o = 1; o < G; o <<= 1) {  // within the lane group (xor stays inside it)
+      for (int o = 1; o < G; o <<= 1) {  // within the thread group (xor stays inside it)
         const double om = __shfl_xor(mx, o);
         mx = om > mx ? om : mx;
         nan = (__shfl_xor((int)nan, o) != 0) || nan;
@@ -514,60 +539,6 @@ __global__ void __launch_bounds__(OW)
       }
       if (live && sub == 0) {
         const double max_s = nan ? __builtin_nan("") : mx;
-        double c = a[4];
-        if (!g.use_sb && !g.use_vt) {
-          c = nmax(c, max_s * g.dlo_coef);
-        } else {
-          if (g.use_sb) {
-            const double alpha = 0.65;
-            c = nmax(c, alpha * c + (1 - alpha) * bst_pow15(max_s));
-          }
-          if (g.use_vt && vt) c = nmax(c, det_thresh + 1e-5);
-        }
-        L.dd[DDW * d + 4] = c;
-      }
-    }
-    have_e = true;
-    __syncthreads();
-  } else if (g.use_dlo && n > 0 && nt > 0) {
-    if (g.rich_s) {  // MhDist_similarity column sums over all detections, lane per track
-      for (int t0 = 0; t0 < nt; t0 += OW) {
-        const int t = t0 + lane;
-        if (t < nt) {
-          const double* rw = tb + (size_t)t * TBB;
-          double cs = 0.0;
-          for (int d = 0; d < n; d++) {
-            bool m;
-            const double e = mh_num(mh_dist(L.dd + DDW * d, rw), m);
-            cs = d == 0 ? e : cs + e;
-          }
-          L.colsum[t] = cs;
-        }
-      }
-      __syncthreads();
-    }
-    for (int d0 = 0; d0 < n; d0 += OW) {  // lane per detection
-      const int d = d0 + lane;
-      if (d < n) {
-        const double* a = L.dd + DDW * d;
-        double max_s = 0.0;
-        bool vt = false;
-        for (int t = 0; t < nt; t++) {
-          const double* rw = tb + (size_t)t * TBB;
-          double S;
-          if (g.rich_s) {
-            bool m;
-            const double e = mh_num(mh_dist(a, rw), m);
-            const double mhs = m ? 0.0 : e / L.colsum[t];
-            const double sh = shape_sim(a, rw, g.s_sim_corr);
-            const double sb = soft_biou(a, rw, rw[4]);
-            S = ((mhs + sh) + sb) / 3;
-          } else {
-            S = iou_b(a, rw);
-          }
-          max_s = t == 0 ? S : nmax(max_s, S);
-          if (g.use_vt && !vt) vt = S > nmax(0.95 - (rw[5] - 1.0), 0.8);
-        }
         double c = a[4];
         if (!g.use_sb && !g.use_vt) {
           c = nmax(c, max_s * g.dlo_coef);
@@ -601,7 +572,7 @@ __global__ void __launch_bounds__(OW)
         [&](int d, int p) { L.bi[p] = d; });
     if (nb > 0) {
       // bdiou = iou(boost, boost) - eye: row maxima -> remaining (<= .3) / args (> .3)
-      for (int i = lane; i < nb; i += OW) {
+      for (int i = tid; i < nb; i += nth) {
         const double* a = L.dd + DDW * L.bi[i];
         double m = 0.0;
         for (int j = 0; j < nb; j++) {
@@ -612,7 +583,7 @@ __global__ void __launch_bounds__(OW)
       }
       __syncthreads();
       // an overlapping candidate stays if it holds the maximum confidence of its overlaps
-      for (int i = lane; i < nb; i += OW) {
+      for (int i = tid; i < nb; i += nth) {
         if (!(L.fl[i] & 2)) continue;
         const double* a = L.dd + DDW * L.bi[i];
         double cm = a[4];
@@ -624,7 +595,7 @@ __global__ void __launch_bounds__(OW)
         if (a[4] == cm) L.fl[i] |= 4;
       }
       __syncthreads();
-      for (int i = lane; i < nb; i += OW)
+      for (int i = tid; i < nb; i += nth)
         if (L.fl[i] & 5) L.dd[DDW * L.bi[i] + 4] = det_thresh + 1e-4;
       __syncthreads();
     }
@@ -638,45 +609,49 @@ __global__ void __launch_bounds__(OW)
   // ---- associate (assoc.py:156-200) ---------------------------------------------------------
   int nm = 0, nud = 0, nut = 0;
   if (nt == 0) {
-    for (int k = lane; k < nk; k += OW) L.ud[k] = k;
+    for (int k = tid; k < nk; k += nth) L.ud[k] = k;
     nud = nk;
+    __syncthreads();
   } else {
     int nmi = 0;
     const double lambda_emb = (((1 + g.l_iou) + g.l_shape) + g.l_mhd) * 1.5;
     double* C = (nk * nt <= g.cost_lds) ? L.cost : costg;
     if (nk > 0) {
-      // MhDist_similarity over the kept detections: column sums, lane per track (from the DLO
-      // boost's E when it staged one: the boosts change confidences, never boxes).  The cost
-      // below is written over E in place: row i <= kd[i] <= the rows still to be read.
-      for (int t0 = 0; t0 < nt; t0 += OW) {
-        const int t = t0 + lane;
-        if (t < nt) {
-          const double* rw = tb + (size_t)t * TBB;
-          double cs = 0.0;
-          for (int i = 0; i < nk; i++) {
-            double e;
-            if (have_e) {
-              e = fabs(L.cost[L.kd[i] * nt + t]);
-            } else {
-              bool m;
-              e = mh_num(mh_dist(L.dd + DDW * L.kd[i], rw), m);
-            }
-            cs = i == 0 ? e : cs + e;
+      // MhDist_similarity over the kept detections: column sums, thread per track (from the DLO
+      // boost's E when it staged one: the boosts change confidences, never boxes)
+      for (int t = tid; t < nt; t += nth) {
+        const double* rw = tb + (size_t)t * TBB;
+        double cs = 0.0;
+        for (int i = 0; i < nk; i++) {
+          double e;
+          if (E) {
+            e = fabs(E[L.kd[i] * nt + t]);
+          } else {
+            bool m;
+            e = mh_num(mh_dist(L.dd + DDW * L.kd[i], rw), m);
           }
-          L.colsum[t] = cs;
+          cs = i == 0 ? e : cs + e;
         }
+        L.colsum[t] = cs;
       }
-      for (int k = lane; k < nk; k += OW) L.rowcnt[k] = 0;
+      for (int k = tid; k < nk; k += nth) L.rowcnt[k] = 0;
+      for (int k = tid; k < nt; k += nth) L.colcnt[k] = 0;
       __syncthreads();
       BSTAMP(4);
-      // the cost matrix (stored negated for lapjv(-cost)), lane per track; counts of entries
-      // above the threshold per row/column for match()'s one-to-one test
-      for (int t0 = 0; t0 < nt; t0 += OW) {
-        const int t = t0 + lane;
-        if (t < nt) {
-          const double* rw = tb + (size_t)t * TBB;
-          int cc = 0;
-          for (int i = 0; i < nk; i++) {
+      // the cost matrix (stored negated for lapjv(-cost)), thread per entry p = i * nt + t; counts
+      // of entries above the threshold per row/column for match()'s one-to-one test.  C may be E's
+      // storage: entry p reads E at kd[i] * nt + t >= p, so a chunk's entries are all computed
+      // before any is stored and no later chunk reads below its own first entry.
+      const int np = nk * nt;
+      for (int c0 = 0; c0 < np; c0 += nth * COST_KR) {
+        double cv[COST_KR];
+#pragma unroll
+        for (int k = 0; k < COST_KR; k++) {
+          const int p = c0 + k * nth + tid;
+          cv[k] = 0.0;
+          if (p < np) {
+            const int i = p / nt, t = p - i * nt;
+            const double* rw = tb + (size_t)t * TBB;
             const int d = L.kd[i];
             const double* a = L.dd + DDW * d;
             const double o = iou_b(a, rw);
@@ -686,8 +661,8 @@ __global__ void __launch_bounds__(OW)
             cst += g.l_iou * cf * o;
             bool m;
             double e;
-            if (have_e) {
-              const double ev = L.cost[d * nt + t];
+            if (E) {
+              const double ev = E[d * nt + t];
               m = ev < 0;
               e = fabs(ev);
             } else {
@@ -696,14 +671,22 @@ __global__ void __launch_bounds__(OW)
             cst += g.l_mhd * (m ? 0.0 : e / L.colsum[t]);
             cst += g.l_shape * cf * shape_sim(a, rw, g.s_sim_corr);
             if (ec) cst += lambda_emb * ec[(size_t)d * g.T + t];
-            C[i * nt + t] = -cst;
-            if (cst > thr) {
+            cv[k] = cst;
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < COST_KR; k++) {
+          const int p = c0 + k * nth + tid;
+          if (p < np) {
+            const int i = p / nt, t = p - i * nt;
+            C[p] = -cv[k];
+            if (cv[k] > thr) {
               atomicAdd(&L.rowcnt[i], 1);
-              L.rowcol[i] = t;
-              cc++;
+              L.rowcol[i] = t;  // read only where the row's count is 1
+              atomicAdd(&L.colcnt[t], 1);
             }
           }
-          L.colcnt[t] = cc;
         }
       }
       __syncthreads();
@@ -723,7 +706,12 @@ __global__ void __launch_bounds__(OW)
               L.mi[2 * p + 1] = L.rowcol[i];
             });
       } else {  // lap.lapjv(-cost, extend_cost=True) -> [[y[i], i] for i in x if i >= 0]
-        nmi = legacy_lap(C, nk, nt, L.jv, L.mi);
+        if (wid == 0) {
+          nmi = legacy_lap(C, nk, nt, L.jv, L.mi, SyncWaveL{});
+          if (lane == 0) L.u[0] = nmi;
+        }
+        __syncthreads();
+        nmi = L.u[0];
         BCOUNT(0, 1);
         BCOUNT(1, nk > nt ? nk : nt);
       }
@@ -731,9 +719,9 @@ __global__ void __launch_bounds__(OW)
     }
     // linear_assignment (assoc.py:117-153): unmatched = absent from the pairs, ascending; then
     // the validation, rejected pairs appended in pair order
-    for (int k = lane; k < g.N; k += OW) L.rowcnt[k] = L.colcnt[k] = 0;
+    for (int k = tid; k < g.N; k += nth) L.rowcnt[k] = L.colcnt[k] = 0;
     __syncthreads();
-    for (int q = lane; q < nmi; q += OW) {
+    for (int q = tid; q < nmi; q += nth) {
       L.rowcnt[L.mi[2 * q]] = 1;
       L.colcnt[L.mi[2 * q + 1]] = 1;
     }
@@ -778,7 +766,7 @@ __global__ void __launch_bounds__(OW)
   // ---- matched updates (boosttrack.py:297-306), octet per pair ------------------------------
   int* rec = g.reid ? g.rec + (size_t)seq * g.D * 2 : nullptr;
   double* rec_a = g.reid ? g.rec_a + (size_t)seq * g.D : nullptr;
-  for (int c = 0; c < nm; c += 8) {
+  for (int c = 0; c < nm; c += nth / 8) {
     const int q = c + oct;
     if (q < nm) {
       const int d = L.kd[L.mm[2 * q]];
@@ -814,17 +802,17 @@ __global__ void __launch_bounds__(OW)
 
   BSTAMP(8);
   // ---- births for the unmatched detections (boosttrack.py:308-312), free slots ascending ----
-  for (int s2 = lane; s2 < g.T; s2 += OW) L.fl[s2] = 0;
+  for (int s2 = tid; s2 < g.T; s2 += nth) L.fl[s2] = 0;
   __syncthreads();
-  for (int p = lane; p < nt; p += OW) L.fl[L.lst[p]] = 1;
+  for (int p = tid; p < nt; p += nth) L.fl[L.lst[p]] = 1;
   __syncthreads();
   const int nfree = wave_compact(g.T, [&](int s2) { return L.fl[s2] == 0; }, [&](int s2, int p) { L.lst2[p] = s2; });
   int nnew = nud;  // every kept detection satisfies dets[i, 4] >= det_thresh
   if (nnew > nfree) {
-    if (lane == 0) atomicExch(g.status, (int)BX_ERR_TRACK_OVERFLOW);
+    if (tid == 0) atomicExch(g.status, (int)BX_ERR_TRACK_OVERFLOW);
     nnew = nfree;
   }
-  for (int c = 0; c < nnew; c += 8) {
+  for (int c = 0; c < nnew; c += nth / 8) {
     const int k = c + oct;
     if (k < nnew) {
       const int slot = L.lst2[k];
@@ -855,7 +843,8 @@ __global__ void __launch_bounds__(OW)
   const int ntr = nt + nnew;
   BSTAMP(9);
 
-  // ---- outputs in list order + filter_outputs (boosttrack.py:314-341), then deaths ----------
+  // ---- outputs in list order + filter_outputs (boosttrack.py:314-341), then deaths; every wave
+  // counts, wave 0 writes ----------------------------------------------------------------------
   double* orow = out + (size_t)r0 * 8;
   auto out_box = [&](const BstTrk& t, double* bx) { x_to_bbox(t.x[0], t.x[1], t.x[2], t.x[3], bx); };
   const int nout = wave_compact(
@@ -869,23 +858,24 @@ __global__ void __launch_bounds__(OW)
         return (w / h <= g.ar_thresh) && (w * h > g.min_box_area);
       },
       [&](int k, int p) {
+        if (wid != 0 || p >= n) return;
         const BstTrk& t = trk[L.lst[k]];
         double bx[4];
         out_box(t, bx);
-        if (p < n) {
-          double* o = orow + (size_t)p * 8;
-          o[0] = bx[0]; o[1] = bx[1]; o[2] = bx[2]; o[3] = bx[3];
-          o[4] = (double)t.id;
-          o[5] = t.conf;
-          o[6] = t.cls;
-          o[7] = t.det_ind;
-        }
+        double* o = orow + (size_t)p * 8;
+        o[0] = bx[0]; o[1] = bx[1]; o[2] = bx[2]; o[3] = bx[3];
+        o[4] = (double)t.id;
+        o[5] = t.conf;
+        o[6] = t.cls;
+        o[7] = t.det_ind;
       });
   const int nkeep = wave_compact(
       ntr, [&](int k) { return trk[L.lst[k]].tsu <= g.max_age; },
-      [&](int k, int p) { order[p] = L.lst[k]; });
+      [&](int k, int p) {
+        if (wid == 0) order[p] = L.lst[k];
+      });
   BSTAMP(10);
-  if (lane == 0) {
+  if (tid == 0) {
     out_count[b] = nout < n ? nout : n;
     sq[SB_FRAME] = frame;
     sq[SB_IDS] = id0 + nnew;
@@ -1162,7 +1152,7 @@ static int launch(bx_boost* e, int seq0, int nseq, const float* dets, const int*
     if ((rc = probe_end(e, 0, st))) return rc;
   }
   if ((rc = probe_begin(e, 1, st))) return rc;
-  hipLaunchKernelGGL(boost_frame_kernel, dim3(nseq), dim3(OW), e->lds, st, d, seq0, dets, off,
+  hipLaunchKernelGGL(boost_frame_kernel, dim3(nseq), dim3(frame_threads(nseq)), e->lds, st, d, seq0, dets, off,
                      d.use_ecc ? warps : nullptr, out, cnt);
   BCHK(hipGetLastError());
   if ((rc = probe_end(e, 1, st))) return rc;
@@ -1214,9 +1204,13 @@ int bx_boost_create(const bx_boost_config* c, bx_boost** out) {
   d.rich_s = c->use_rich_s != 0;
   d.use_sb = c->use_sb != 0;
   d.use_vt = c->use_vt != 0;
-  // LDS: the fixed part plus as much cost matrix as keeps ~4 workgroups per CU resident
+  // LDS: the fixed part plus as much cost matrix as keeps every sequence's workgroup resident
+  // at once (256 CUs; at least 40 KB, i.e. 4 workgroups per CU, at most 152 KB)
   const size_t fixed = lds_bytes(d.D, d.T, d.N, 0);
-  long budget = 40 * 1024 - (long)fixed;
+  long cap = 160L * 1024 / ((d.S + 255) / 256);
+  if (cap > 152L * 1024) cap = 152L * 1024;
+  if (cap < 40L * 1024) cap = 40L * 1024;
+  long budget = cap - (long)fixed;
   int cl = budget > 0 ? (int)(budget / 8) : 0;
   if (cl > d.D * d.T) cl = d.D * d.T;
   if (cl < 64) cl = 64;
@@ -1240,6 +1234,7 @@ int bx_boost_create(const bx_boost_config* c, bx_boost** out) {
   const size_t o_ord = carve_b(S * T * sizeof(int));
   const size_t o_tb = carve_b(S * T * TBB * sizeof(double));
   const size_t o_cg = need_g ? carve_b(S * D * T * sizeof(double)) : 0;
+  const size_t o_eg = need_g ? carve_b(S * D * T * sizeof(double)) : 0;
   const size_t o_ec = d.reid ? carve_b(S * D * T * sizeof(double)) : 0;
   const size_t o_emb = d.reid ? carve_b(S * T * F * sizeof(double)) : 0;
   const size_t o_rec = d.reid ? carve_b(S * D * 2 * sizeof(int)) : 0;
@@ -1260,6 +1255,7 @@ int bx_boost_create(const bx_boost_config* c, bx_boost** out) {
   d.order = (int*)(base + o_ord);
   d.tb = (double*)(base + o_tb);
   d.cost_g = need_g ? (double*)(base + o_cg) : nullptr;
+  d.e_g = need_g ? (double*)(base + o_eg) : nullptr;
   d.ec = d.reid ? (double*)(base + o_ec) : nullptr;
   d.emb = d.reid ? (double*)(base + o_emb) : nullptr;
   d.rec = d.reid ? (int*)(base + o_rec) : nullptr;

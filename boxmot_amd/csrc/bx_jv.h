@@ -75,6 +75,15 @@ struct SyncBlock {
   __device__ void operator()() const { __syncthreads(); }
   __device__ void after_atomics() const {}
 };
+// Only the calling wave of a larger workgroup, its state in LDS (LDS atomics are performed in
+// the LDS itself: the workgroup-scope fence, i.e. the wait for the wave's LDS operations, is all).
+struct SyncWaveL {
+  __device__ void operator()() const {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ void after_atomics() const { (*this)(); }
+};
 struct SyncWaveG {
   __device__ void operator()() const {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -114,7 +123,7 @@ constexpr int JV_CH = 8;  // 64-position chunks of one relaxation loaded togethe
 // the calling wave only).
 template <class CF, class SY>
 __device__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   // ---- _ccrrt_dense.  Column minima from LARGE, first row on ties (lane per column) ...
   for (int j = lane; j < n; j += OW) {
     double mn = LAPX_LARGE;
@@ -536,9 +545,10 @@ __device__ __forceinline__ double wave_min_bfly(double r) {
   return rl_d(r, 0);
 }
 
-__device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
+template <class SY = SyncBlock>
+__device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = SY{}) {
   const int n = nr > nc ? nr : nc;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const bool own = lane < n;
 #ifdef BX_PHASE_TIMING
   unsigned long long jt0 = __builtin_amdgcn_s_memtime(), jt1 = 0, jacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -564,13 +574,14 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
     w.x[lane] = -1;
     w.matches[lane] = 0;
   }
-  __syncthreads();
+  sync();
   // ... each row keeps the largest column whose minimum it holds (the j = n-1..0 sweep's first)
   if (own) {
     atomicMax(&w.x[y], lane);
     atomicAdd(&w.matches[y], 1);
   }
-  __syncthreads();
+  sync();
+  sync.after_atomics();
   bool uniq = false;
   if (own) {
     xr = w.x[lane];
@@ -599,7 +610,7 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
     const unsigned long long fm = __ballot(own && xr < 0);
     nfree = __popcll(fm);
     if (own && xr < 0) w.freer[__popcll(fm & ((1ull << lane) - 1ull))] = lane;
-    __syncthreads();
+    sync();
     if (lane < nfree) fr = w.freer[lane];
   }
   // ---- _carr_dense, at most two passes
@@ -869,7 +880,7 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
     w.y[col] = y;
     w.v[col] = v;
   }
-  __syncthreads();
+  sync();
   JVT(7);
 #undef JVT
 #ifdef BX_PHASE_TIMING
@@ -879,16 +890,19 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w) {
 }
 
 // legacy linear_assignment of the nr x nc matrix C: pairs (row, col) in row order into out
-// (interleaved), returns the count (uniform)
-__device__ int legacy_lap(const double* C, int nr, int nc, JvLds& jv, int* out) {
+// (interleaved), returns the count (uniform).  SY: the whole one-wave workgroup, or SyncWaveL
+// when one wave of a larger workgroup solves alone.
+template <class SY = SyncBlock>
+__device__ int legacy_lap(const double* C, int nr, int nc, JvLds& jv, int* out, SY sync = SY{}) {
   if ((nr > nc ? nr : nc) <= OW)
-    jv_wave64(C, nr, nc, jv);
+    jv_wave64(C, nr, nc, jv, sync);
   else
-    jv_wave(C, nr, nc, jv);
-  return wave_compact(
+    jv_wave(C, nr, nc, jv, sync);
+  return wave_compact_s(
       nr, [&](int i) { return jv.x[i] < nc; },
       [&](int i, int p) {
         out[2 * p] = i;
         out[2 * p + 1] = jv.x[i];
-      });
+      },
+      sync);
 }

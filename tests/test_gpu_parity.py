@@ -997,6 +997,28 @@ def test_boosttrack_batched_vs_oracle(torch_cuda, variant):
     run_boost_batched(torch_cuda, scenes, 60, args, emb)
 
 
+class _EmptyScene:
+    def __init__(self, emb_dim):
+        self.emb_dim = emb_dim
+
+    def frame(self, t):
+        return np.zeros((0, 6)), np.zeros((0, self.emb_dim))
+
+
+@pytest.mark.parametrize("n_seq", [384, 600, 1024])
+def test_boosttrack_wide_launch_vs_oracle(torch_cuda, n_seq):
+    """Launch widths with fewer threads per sequence (three, two and one wave: `frame_threads`):
+    three busy sequences (first, middle, last) among empty ones, bitwise against the oracle."""
+    from boxmot_amd.synth import SyntheticScene
+
+    busy = {0: 0, n_seq // 2: 1, n_seq - 1: 2}
+    scenes = [SyntheticScene(n_obj=30 + 12 * busy[s], seed=900 + s, emb_dim=32,
+                             emb_dtype=np.float64, layout="crowded" if busy[s] != 1 else "grid",
+                             p_det=0.5, conf_lo=0.3)
+              if s in busy else _EmptyScene(32) for s in range(n_seq)]
+    run_boost_batched(torch_cuda, scenes, 30, dict(BOOST_ARGS), 32, track_cap=128, det_cap=64)
+
+
 def test_boosttrack_large_scene_vs_oracle(torch_cuda):
     """A crowded 160-object sequence with 512-d ReID: cost matrices past the LDS budget (HBM
     path), several MFMA output tiles per sequence, LAP solves."""
