@@ -73,8 +73,9 @@ struct BstDev {
 };
 
 // Diagnostic phase stamps and counters (build with -DBX_PHASE_TIMING; never shipped): per
-// sequence, cycles accumulated per phase over all frames [0, 16) and event counters [16, 32).
-constexpr int BST_DBG = 32;
+// sequence, cycles accumulated per phase over all frames [0, 16), event counters [16, 24) and
+// the JV's counters [24, 40).
+constexpr int BST_DBG = 40;
 #ifdef BX_PHASE_TIMING
 #define BSTAMP(k)                                                                    \
   do {                                                                               \
@@ -707,6 +708,8 @@ __global__ void __launch_bounds__(BW)
             });
       } else {  // lap.lapjv(-cost, extend_cost=True) -> [[y[i], i] for i in x if i >= 0]
         if (wid == 0) {
+          // (generic cost loads: LDS-typed ones, legacy_lap's cas = 3, measured slower at C5,
+          // frame kernel 0.413 vs 0.393 ms)
           nmi = legacy_lap(C, nk, nt, L.jv, L.mi, SyncWaveL{});
           if (lane == 0) L.u[0] = nmi;
         }

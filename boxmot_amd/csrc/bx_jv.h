@@ -545,10 +545,24 @@ __device__ __forceinline__ double wave_min_bfly(double r) {
   return rl_d(r, 0);
 }
 
-template <class SY = SyncBlock>
+// Cost loads of the register-resident solver from address space AS (0: generic, 1: global,
+// 3: LDS — a generic pointer into LDS would be read by flat loads, which wait on both counters).
+template <int AS>
+__device__ __forceinline__ double cget_as(const double* C, int nr, int nc, int i, int j) {
+  if (!(i < nr && j < nc)) return 0.0;
+  if constexpr (AS == 3)
+    return ((const __attribute__((address_space(3))) double*)C)[i * nc + j];
+  else if constexpr (AS == 1)
+    return ((const __attribute__((address_space(1))) double*)C)[i * nc + j];
+  else
+    return C[i * nc + j];
+}
+
+template <class SY = SyncBlock, int AS = 0>
 __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = SY{}) {
   const int n = nr > nc ? nr : nc;
   const int lane = threadIdx.x & 63;
+  auto cget = [&](const double*, int, int, int i, int j) { return cget_as<AS>(C, nr, nc, i, j); };
   const bool own = lane < n;
 #ifdef BX_PHASE_TIMING
   unsigned long long jt0 = __builtin_amdgcn_s_memtime(), jt1 = 0, jacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -684,6 +698,9 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
       if (lane == fi) xr = j1;
       if (lane == j1) y = fi;
     }
+#ifdef BX_PHASE_TIMING
+    if (lane == 0 && w.dc) w.dc[11] += rr_cnt;
+#endif
     nfree = nnew;
   }
 #ifdef BX_PHASE_TIMING
@@ -767,6 +784,9 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
             double ex = __shfl_up(pm, 1);
             if (lane == 0) ex = INF;
             unsigned long long ev = __ballot(own && lane > low && d <= ex);
+#ifdef BX_PHASE_TIMING
+            if (lane == 0 && w.dc) w.dc[8] += __popcll(ev);
+#endif
             if (__popcll(ev) >= PERM_RUN) {
               int perm = lane;
               while (ev) {
@@ -844,6 +864,9 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
         }
         // columns lowered to the minimum join the SCAN set, in position order (all before pe)
         unsigned long long bits = __ballot(act && B && lane < pe);
+#ifdef BX_PHASE_TIMING
+        if (lane == 0 && w.dc) w.dc[9] += __popcll(bits);
+#endif
         if (__popcll(bits) >= PERM_RUN) {
           int perm = lane;
           while (bits) {
@@ -873,6 +896,9 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
       const int j1 = endofpath;
       endofpath = rl_i(xr, i);
       if (lane == i) xr = j1;
+#ifdef BX_PHASE_TIMING
+      if (lane == 0 && w.dc) w.dc[10] += 1;
+#endif
     } while (i != start);
   }
   if (own) {
@@ -892,11 +918,18 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
 // legacy linear_assignment of the nr x nc matrix C: pairs (row, col) in row order into out
 // (interleaved), returns the count (uniform).  SY: the whole one-wave workgroup, or SyncWaveL
 // when one wave of a larger workgroup solves alone.
+// cas: the address space C is known to be in (3: LDS, 1: global, 0: either), for n <= 64.
 template <class SY = SyncBlock>
-__device__ int legacy_lap(const double* C, int nr, int nc, JvLds& jv, int* out, SY sync = SY{}) {
-  if ((nr > nc ? nr : nc) <= OW)
-    jv_wave64(C, nr, nc, jv, sync);
-  else
+__device__ int legacy_lap(const double* C, int nr, int nc, JvLds& jv, int* out, SY sync = SY{},
+                          int cas = 0) {
+  if ((nr > nc ? nr : nc) <= OW) {
+    if (cas == 3)
+      jv_wave64<SY, 3>(C, nr, nc, jv, sync);
+    else if (cas == 1)
+      jv_wave64<SY, 1>(C, nr, nc, jv, sync);
+    else
+      jv_wave64<SY, 0>(C, nr, nc, jv, sync);
+  } else
     jv_wave(C, nr, nc, jv, sync);
   return wave_compact_s(
       nr, [&](int i) { return jv.x[i] < nc; },

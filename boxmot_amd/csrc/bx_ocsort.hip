@@ -69,8 +69,9 @@ struct OcsDev {
 };
 
 // Diagnostic phase stamps and counters (build with -DBX_PHASE_TIMING; never shipped): per
-// sequence, cycles accumulated per phase over all frames [0, 16) and event counters [16, 32).
-constexpr int OCS_DBG = 32;
+// sequence, cycles accumulated per phase over all frames [0, 16), event counters [16, 24) and
+// the JV's counters [24, 40).
+constexpr int OCS_DBG = 40;
 #ifdef BX_PHASE_TIMING
 #define OSTAMP(k)                                                                    \
   do {                                                                               \

@@ -21,7 +21,8 @@ PHASES = ["load", "warp+predict", "DLO", "DUO", "keep+colsum", "cost", "fastpath
           "validate", "updates", "births", "outputs+deaths"]
 COUNTERS = ["LAP calls", "LAP n", "kept dets", "tracks", "frames", "-", "-", "-",
             "JV free rows", "JV scans", "JV relax steps", "JV sequential scans",
-            "JV64 setup cyc", "JV64 scan cyc", "JV64 relax cyc", "JV64 init+path cyc"]
+            "JV64 setup cyc", "JV64 scan cyc", "JV64 relax cyc", "JV64 init+path cyc",
+            "JV64 find events", "JV64 scan events", "JV64 path steps", "JV64 ARR iterations"]
 
 
 def build():
@@ -87,7 +88,7 @@ def main():
     for d, off, e in frames:
         eng.step(d, off, e, None, out, cnt)
     torch.cuda.synchronize()
-    dbg = np.zeros((a.seqs, 32), np.uint64)
+    dbg = np.zeros((a.seqs, 40), np.uint64)
     N.check(L.bx_boost_debug_host(eng._h, dbg.ctypes.data), "debug")
     per = dbg.astype(np.float64) / a.frames
     tot = per[:, :len(PHASES)].sum(1)

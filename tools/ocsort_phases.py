@@ -66,7 +66,7 @@ def main():
     torch.cuda.synchronize()
     print(f"kernel time per frame (all sequences, timing build): "
           f"{ev0.elapsed_time(ev1) / a.frames:.3f} ms")
-    dbg = np.zeros((a.seqs, 32), np.uint64)
+    dbg = np.zeros((a.seqs, 40), np.uint64)
     N.check(L.bx_ocsort_debug_host(eng._h, dbg.ctypes.data), "debug")
     per = dbg.astype(np.float64) / a.frames
     tot = per[:, :len(PHASES)].sum(1)
