@@ -893,13 +893,22 @@ __global__ void __launch_bounds__(BW)
 
 // ------------------------------------------------------------------------------------------
 // dets_embs @ trk_embs.T (boosttrack.py:274-281) for every detection x live track of a
-// sequence, on the fp64 matrix cores.  Workgroup = 4 waves per sequence; output tiles of
-// 32 detections x 64 tracks (wave (wr, wc): rows 16 wr, columns 32 wc + {0, 16}); K advances in
-// chunks of 16 through LDS stored k-major, the next chunk's global loads issued before the
-// current chunk's MFMAs.  Entry (d, p) = ascending-k fma chain over F (oracle emb_dot).
+// sequence, on the fp64 matrix cores.  One workgroup of 4 waves per output tile of 32 detections x
+// 64 tracks (grid (sequences, tiles); wave (wr, wc): rows 16 wr, columns 32 wc + {0, 16}); K
+// advances in chunks of 16 through LDS stored k-major, with EC_PF chunks' global loads in flight
+// (a chunk's MFMAs take ~50 ns, a load round trip ~1 us: the loop is bound by how many round
+// trips it waits for).  Entry (d, p) = ascending-k fma chain over F (oracle emb_dot).
 constexpr int EC_BM = 32, EC_BN = 64, EC_KC = 16, EC_LDA = EC_BM + 16, EC_LDB = EC_BN + 16;
 constexpr int EC_STAGE = EC_KC * (EC_LDA + EC_LDB);
+#ifndef BX_EC_PF
+#define BX_EC_PF 4
+#endif
+constexpr int EC_PF = BX_EC_PF;  // chunks in flight
 typedef double d4 __attribute__((ext_vector_type(4)));
+__host__ __device__ constexpr int ec_tiles_t(int T) { return (T + EC_BN - 1) / EC_BN; }
+__host__ __device__ constexpr int ec_tiles(int D, int T) {
+  return (D + EC_BM - 1) / EC_BM * ec_tiles_t(T);
+}
 
 __global__ void __launch_bounds__(256)
     boost_embcost_kernel(BstDev g, int seq0, const int* __restrict__ det_off,
@@ -910,7 +919,9 @@ __global__ void __launch_bounds__(256)
   int nd = det_off[b + 1] - r0;
   if (nd > g.D) nd = g.D;
   const int nt = g.seqst[(size_t)seq * SQB + SB_NTR];
-  if (nd <= 0 || nt <= 0) return;
+  const int d0 = (int)blockIdx.y / ec_tiles_t(g.T) * EC_BM;
+  const int t0 = (int)blockIdx.y % ec_tiles_t(g.T) * EC_BN;
+  if (d0 >= nd || t0 >= nt) return;  // workgroup-uniform
   const int F = g.F;
   const int* order = g.order + (size_t)seq * g.T;
   const double* temb = g.emb + (size_t)seq * g.T * F;
@@ -920,34 +931,40 @@ __global__ void __launch_bounds__(256)
   // staging: A 32 rows x 16 k (8 threads x 2 per row), B 64 rows x 16 k (4 threads x 4)
   const int ar = tid >> 3, aq = (tid & 7) * 2, br = tid >> 2, bq = (tid & 3) * 4;
   const int nk = (F + EC_KC - 1) / EC_KC;
-  for (int d0 = 0; d0 < nd; d0 += EC_BM)
-    for (int t0 = 0; t0 < nt; t0 += EC_BN) {
-      const bool a_ok = d0 + ar < nd, b_ok = t0 + br < nt;
-      const double* ap = embs + (size_t)(r0 + (a_ok ? d0 + ar : 0)) * F + aq;
-      const double* bp = temb + (size_t)(b_ok ? order[t0 + br] : 0) * F + bq;
-      double ra[2], rb[4];
-      auto load = [&](int k0) {
+  const bool a_ok = d0 + ar < nd, b_ok = t0 + br < nt;
+  const double* ap = embs + (size_t)(r0 + (a_ok ? d0 + ar : 0)) * F + aq;
+  const double* bp = temb + (size_t)(b_ok ? order[t0 + br] : 0) * F + bq;
+  double ra[EC_PF][2], rb[EC_PF][4];
+  auto load = [&](int sl, int kc) {
+    const int k0 = kc * EC_KC;
 #pragma unroll
-        for (int j = 0; j < 2; j++) ra[j] = (a_ok && k0 + aq + j < F) ? ap[k0 + j] : 0.0;
+    for (int j = 0; j < 2; j++) ra[sl][j] = (a_ok && k0 + aq + j < F) ? ap[k0 + j] : 0.0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) rb[j] = (b_ok && k0 + bq + j < F) ? bp[k0 + j] : 0.0;
-      };
-      auto store = [&](double* buf) {
+    for (int j = 0; j < 4; j++) rb[sl][j] = (b_ok && k0 + bq + j < F) ? bp[k0 + j] : 0.0;
+  };
+  auto store = [&](int sl, double* buf) {
 #pragma unroll
-        for (int j = 0; j < 2; j++) buf[(aq + j) * EC_LDA + ar] = ra[j];
+    for (int j = 0; j < 2; j++) buf[(aq + j) * EC_LDA + ar] = ra[sl][j];
 #pragma unroll
-        for (int j = 0; j < 4; j++) buf[EC_KC * EC_LDA + (bq + j) * EC_LDB + br] = rb[j];
-      };
-      d4 acc[2];
-      acc[0] = (d4){0.0, 0.0, 0.0, 0.0};
-      acc[1] = (d4){0.0, 0.0, 0.0, 0.0};
-      load(0);
-      __syncthreads();  // the previous tile's readers are done with buffer 0
-      store(lds);
-      __syncthreads();
-      for (int kc = 0; kc < nk; kc++) {
+    for (int j = 0; j < 4; j++) buf[EC_KC * EC_LDA + (bq + j) * EC_LDB + br] = rb[sl][j];
+  };
+  d4 acc[2];
+  acc[0] = (d4){0.0, 0.0, 0.0, 0.0};
+  acc[1] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int p = 0; p < EC_PF; p++)
+    if (p < nk) load(p, p);
+  store(0, lds);
+  __syncthreads();
+  // chunk kc sits in LDS stage kc & 1 and register slot kc % EC_PF (free once stored); the loop
+  // is unrolled by EC_PF so the slots are static
+  for (int kb = 0; kb < nk; kb += EC_PF) {
+#pragma unroll
+    for (int u = 0; u < EC_PF; u++) {
+      const int kc = kb + u;
+      if (kc < nk) {
+        if (kc + EC_PF < nk) load(u, kc + EC_PF);
         const double* cur = lds + (kc & 1) * EC_STAGE;
-        if (kc + 1 < nk) load((kc + 1) * EC_KC);
 #pragma unroll
         for (int ks = 0; ks < EC_KC / 4; ks++) {
           const int kr = ks * 4 + (lane >> 4);
@@ -958,19 +975,20 @@ __global__ void __launch_bounds__(256)
             acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc[j], 0, 0, 0);
           }
         }
-        if (kc + 1 < nk) store(lds + ((kc + 1) & 1) * EC_STAGE);
+        if (kc + 1 < nk) store((u + 1) % EC_PF, lds + ((kc + 1) & 1) * EC_STAGE);
         __syncthreads();
       }
-#pragma unroll
-      for (int j = 0; j < 2; j++) {
-        const int col = t0 + wc * 32 + j * 16 + (lane & 15);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int row = d0 + wr * 16 + (lane >> 4) + 4 * q;
-          if (row < nd && col < nt) ec[(size_t)row * g.T + col] = acc[j][q];
-        }
-      }
     }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const int col = t0 + wc * 32 + j * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int row = d0 + wr * 16 + (lane >> 4) + 4 * q;
+      if (row < nd && col < nt) ec[(size_t)row * g.T + col] = acc[j][q];
+    }
+  }
 }
 
 // update_emb (boosttrack.py:117-119) / the newborn's emb = its detection's row; wave per record
@@ -1150,7 +1168,8 @@ static int launch(bx_boost* e, int seq0, int nseq, const float* dets, const int*
   if (d.reid) {
     if (!embs) return bx_record_error(BX_ERR_SHAPE, "with_reid BoostTrack needs embeddings");
     if ((rc = probe_begin(e, 0, st))) return rc;
-    hipLaunchKernelGGL(boost_embcost_kernel, dim3(nseq), dim3(256), 0, st, d, seq0, off, embs);
+    hipLaunchKernelGGL(boost_embcost_kernel, dim3(nseq, ec_tiles(d.D, d.T)), dim3(256), 0, st, d,
+                       seq0, off, embs);
     BCHK(hipGetLastError());
     if ((rc = probe_end(e, 0, st))) return rc;
   }

@@ -430,7 +430,14 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
 // conservative reject); one thread per track, detections walked in order from LDS (broadcast).
 // (Fusing K2's predict into this kernel and overlapping it with K1 measured slower: the two
 // VALU-bound kernels slowed each other down.)
-constexpr int GATE_BLOCKS = 2;
+#ifndef BX_GATE_BLOCKS
+#define BX_GATE_BLOCKS 4
+#endif
+#ifndef BX_GATE_SPLIT
+#define BX_GATE_SPLIT 4
+#endif
+constexpr int GATE_BLOCKS = BX_GATE_BLOCKS;
+constexpr int GATE_SPLIT = BX_GATE_SPLIT;  // threads per track, each over every SPLIT-th detection
 template <int KIND>
 __global__ __launch_bounds__(WG) void gate_kernel(Dev P, int seq0, const float* __restrict__ dets,
                                                   const int* __restrict__ det_off) {
@@ -457,13 +464,15 @@ __global__ __launch_bounds__(WG) void gate_kernel(Dev P, int seq0, const float* 
   const double* g_kf = P.kf + (size_t)s * T * KF_STRIDE;
   uint32_t* pairs = P.pairs + (size_t)s * T * D;
   const bool prefilter = P.prox < 1.0;  // gating needs IoU > 0, i.e. intersecting boxes
-  for (int p = blockIdx.y * WG + threadIdx.x; p < na + nl; p += GATE_BLOCKS * WG) {
+  const int part = threadIdx.x % GATE_SPLIT;
+  for (int p = (blockIdx.y * WG + threadIdx.x) / GATE_SPLIT; p < na + nl;
+       p += GATE_BLOCKS * WG / GATE_SPLIT) {
     const int slot = p < na ? P.act[(size_t)s * T + p] : P.lost[(size_t)s * T + p - na];
     double tb[4];
     track_box<KIND>(g_kf, slot, tb);
     const float4 tf = make_float4(__double2float_rd(tb[0]), __double2float_rd(tb[1]),
                                   __double2float_ru(tb[2]), __double2float_ru(tb[3]));
-    for (int j = 0; j < N; j++) {
+    for (int j = part; j < N; j += GATE_SPLIT) {
       const float4 db = s_fb[j];
       if (__builtin_isnan(db.x)) continue;  // not a high detection
       if (prefilter &&
