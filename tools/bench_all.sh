@@ -1,0 +1,11 @@
+#!/bin/bash
+# Every bench config once (GPU box, repo root) into gpurun_out/bench_all/<config>.json; the
+# default C3 line and C5 with their CPU baselines.
+set -euo pipefail
+mkdir -p gpurun_out/bench_all
+timeout -k 10 300 python bench.py > gpurun_out/bench_all/botsort.json 2> gpurun_out/bench_all/botsort.err
+timeout -k 10 300 python bench.py --config boosttrack_mot8 > gpurun_out/bench_all/boosttrack_mot8.json 2> gpurun_out/bench_all/boosttrack_mot8.err
+for c in botsort_crowded bytetrack ocsort boosttrack strongsort strongsort_c4; do
+  timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > gpurun_out/bench_all/$c.json 2> gpurun_out/bench_all/$c.err
+done
+timeout -k 10 300 python bench.py --config strongsort_c4 --start-frame 150 --no-cpu-baseline > gpurun_out/bench_all/strongsort_c4_steady.json 2> gpurun_out/bench_all/strongsort_c4_steady.err
