@@ -2426,9 +2426,11 @@ __global__ void __launch_bounds__(64)
   SSTAMP(2);
 }
 
-// ss_match_kernel (one wave per sequence): the three matching stages of Tracker._enhanced_match
-// (stage 1/2 costs gathered from ss_cost_kernel's matrix).  Hands the matches (fmt), the unmatched
-// tracks (ffut) and detections (faud) to the next launches.
+// ss_match_kernel (one four-wave workgroup per sequence): the three matching stages of
+// Tracker._enhanced_match (stage 1/2 costs gathered from ss_cost_kernel's matrix).  Wave 0 runs
+// the cascade and posts each LSAP (LsapJob) to wave 1, the solver, which keeps its own register
+// context; waves 2-3 serve the first-step tables when SS_TAB_HELPERS is set, else leave at once.
+// Hands the matches (fmt), the unmatched tracks (ffut) and detections (faud) to the next launches.
 __global__ void __launch_bounds__(256) SS_MATCH_ATTR
     ss_match_kernel(SsDev g, int seq0) {
   extern __shared__ __align__(16) char ss_lds[];
