@@ -565,7 +565,11 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
   auto cget = [&](const double*, int, int, int i, int j) { return cget_as<AS>(C, nr, nc, i, j); };
   const bool own = lane < n;
 #ifdef BX_PHASE_TIMING
+  // cycles per slot and event counters kept in registers, added to w.dc once at the end (a
+  // global read-modify-write per step would put its latency into the next wait it meets)
   unsigned long long jt0 = __builtin_amdgcn_s_memtime(), jt1 = 0, jacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long jcnt[16] = {0};
+#define JCNT(k, v) (jcnt[k] += (unsigned long long)(v))
 #define JVT(slot)                                                             \
   do {                                                                        \
     jt1 = __builtin_amdgcn_s_memtime();                                       \
@@ -576,6 +580,7 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
 #define JVT(slot) \
   do {            \
   } while (0)
+#define JCNT(k, v) ((void)0)
 #endif
   // ---- _ccrrt_dense.  Column minima from LARGE (first row on ties) ...
   double v = LAPX_LARGE, d = 0.0;
@@ -698,14 +703,10 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
       if (lane == fi) xr = j1;
       if (lane == j1) y = fi;
     }
-#ifdef BX_PHASE_TIMING
-    if (lane == 0 && w.dc) w.dc[11] += rr_cnt;
-#endif
+    JCNT(11, rr_cnt);
     nfree = nnew;
   }
-#ifdef BX_PHASE_TIMING
-  if (lane == 0 && w.dc) w.dc[0] += nfree;
-#endif
+  JCNT(0, nfree);
   JVT(4);
   // exchange the registers of positions a and b (cols[a] <-> cols[b])
   auto swap_pos = [&](int a, int b) {
@@ -720,8 +721,8 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
   };
   // A run of swaps replayed on one index register (perm: the lane whose registers end at this
   // position) and applied once, by one gather per register, when it is long: a swap then costs
-  // two readlanes instead of fourteen.  (The runs below only swap a position k with one at or
-  // before it, so a later position still holds its own registers while the run is replayed.)
+  // one or two readlanes instead of fourteen.  (The runs below only swap a position k with one at
+  // or before it, so a later position still holds its own registers while the run is replayed.)
   auto swap_perm = [&](int& perm, int a, int b) {
     if (a == b) return;
     const int pa = rl_i(perm, a), pb = rl_i(perm, b);
@@ -751,17 +752,23 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
     int low = 0, up = 0, last = 0, endofpath = -1;
     bool found = false;
     double mn = 0.0;
+    JVT(0);
     do {
-#ifdef BX_PHASE_TIMING
-      if (lane == 0 && w.dc) w.dc[up == low ? 1 : 2] += 1;
-#endif
-      JVT(7);
+      if (up == low)
+        JCNT(1, 1);
+      else
+        JCNT(2, 1);
+      JVT(3);
       if (up == low) {
         last = low - 1;
         const bool cand = own && lane >= low;
-        bool bad = __any(cand && isnan(d));
-        double m = bad ? INF : wave_min_dpp(cand ? d : INF);
-        bad = bad || !(m < INF);
+        const bool nanb = __any(cand && isnan(d));
+        // inclusive prefix minimum of d over the TODO positions (lanes below lo hold INF): its
+        // lane 63 is the minimum, and shifted by one lane (DPP wave_shr, lane 0 INF) the
+        // exclusive one the sequential find below compares against
+        const double pm = nanb ? INF : scan_min_d(cand ? d : INF);
+        const double m = nanb ? INF : rl_d(pm, 63);
+        const bool bad = nanb || !(m < INF);
         const int ke = bad ? -1 : last_lane(cand && d == m && y < 0);
         if (ke >= 0) {
           // _find_dense's SCAN set = the TODO columns at the minimum in position order; the path
@@ -770,34 +777,29 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
           endofpath = rl_i(col, ke);
           found = true;
         } else {
-#ifdef BX_PHASE_TIMING
-          if (lane == 0 && w.dc) w.dc[3] += 1;
-#endif
+          JCNT(3, 1);
           // _find_dense on the position lanes: mind runs from d[cols[lo]], and the positions
-          // k > lo whose d is <= the minimum of d over [lo, k) are its events (a swap only
-          // exchanges k with a position <= k, so later positions still hold their columns) —
-          // found by a prefix minimum across the lanes, then replayed in order
+          // k > lo whose d is <= the minimum of d over [lo, k) are its events — those with d
+          // strictly below it reset up to lo — found by ballots against the exclusive prefix
+          // minimum, then replayed in order (a swap only exchanges k with a position <= k, so a
+          // later position still holds its own registers: position k's own are k's at its event)
           mn = rl_d(d, low);
           up = low + 1;
-          if (!__any(own && lane >= low && isnan(d))) {
-            const double pm = scan_min_d((own && lane >= low) ? d : INF);
-            double ex = __shfl_up(pm, 1);
-            if (lane == 0) ex = INF;
-            unsigned long long ev = __ballot(own && lane > low && d <= ex);
-#ifdef BX_PHASE_TIMING
-            if (lane == 0 && w.dc) w.dc[8] += __popcll(ev);
-#endif
+          if (!nanb) {
+            const double ex = dpp_d<0x138, 0xf, 0xf>(pm, INF);  // wave_shr:1
+            const bool evk = own && lane > low && d <= ex;
+            unsigned long long ev = __ballot(evk);
+            const unsigned long long st = __ballot(evk && d < ex);
+            JCNT(8, __popcll(ev));
+            if (st) mn = rl_d(d, 63 - __clzll((long long)st));  // the last reset's d
             if (__popcll(ev) >= PERM_RUN) {
-              int perm = lane;
+              int perm = lane;  // the lane whose registers end at this position
               while (ev) {
                 const int k = __ffsll((long long)ev) - 1;
                 ev &= ev - 1;
-                const double h = rl_d(d, k);  // position k is still untouched
-                if (h < mn) {
-                  up = low;
-                  mn = h;
-                }
-                swap_perm(perm, k, up);
+                if ((st >> k) & 1ull) up = low;
+                const int pu = rl_i(perm, up);
+                perm = lane == up ? k : (lane == k ? pu : perm);
                 up++;
               }
               apply_perm(perm);
@@ -805,11 +807,7 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
               while (ev) {
                 const int k = __ffsll((long long)ev) - 1;
                 ev &= ev - 1;
-                const double h = rl_d(d, k);
-                if (h < mn) {
-                  up = low;
-                  mn = h;
-                }
+                if ((st >> k) & 1ull) up = low;
                 swap_pos(k, up);
                 up++;
               }
@@ -837,16 +835,18 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
       JVT(5);
       if (!found) {
         // _scan_dense from the SCAN column at position lo
-        const int j1 = rl_i(col, low);
+        // (the next scan's row prefetched at the end of this one measured slower: C5 scan cycles
+        // +8%, the load's wait lands at the loop head)
         const int i = rl_i(y, low);
+        const double crow = own ? cget(C, nr, nc, i, col) : 0.0;
         const double mind = rl_d(d, low);
-        const double h = cget(C, nr, nc, i, j1) - rl_d(v, low) - mind;
+        const double h = rl_d(crow, low) - rl_d(v, low) - mind;  // lane lo holds column cols[lo]
         low++;
         const bool R = own && lane >= up;
         double v2 = 0.0;
         bool A = false, B = false, E = false;
         if (R) {
-          v2 = cget(C, nr, nc, i, col) - v - h;
+          v2 = crow - v - h;
           A = v2 < d;
           B = A && v2 == mind;
           E = B && y < 0;
@@ -864,9 +864,7 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
         }
         // columns lowered to the minimum join the SCAN set, in position order (all before pe)
         unsigned long long bits = __ballot(act && B && lane < pe);
-#ifdef BX_PHASE_TIMING
-        if (lane == 0 && w.dc) w.dc[9] += __popcll(bits);
-#endif
+        JCNT(9, __popcll(bits));
         if (__popcll(bits) >= PERM_RUN) {
           int perm = lane;
           while (bits) {
@@ -888,6 +886,7 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
       JVT(6);
     } while (!found);
     if (own && lane <= last) v = v + (d - mn);  // lapx: v[j] += d[j] - mind
+    JVT(1);
     int i;
     do {
       const int le = first_lane(own && col == endofpath);
@@ -896,11 +895,11 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
       const int j1 = endofpath;
       endofpath = rl_i(xr, i);
       if (lane == i) xr = j1;
-#ifdef BX_PHASE_TIMING
-      if (lane == 0 && w.dc) w.dc[10] += 1;
-#endif
+      JCNT(10, 1);
     } while (i != start);
+    JVT(2);
   }
+  JVT(7);
   if (own) {
     w.x[lane] = xr;
     w.y[col] = y;
@@ -910,9 +909,13 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
   JVT(7);
 #undef JVT
 #ifdef BX_PHASE_TIMING
-  if (lane == 0 && w.dc)
+  if (lane == 0 && w.dc) {
+    for (int q = 0; q < 16; q++) w.dc[q] += jcnt[q];
     for (int q = 4; q < 8; q++) w.dc[q] += jacc[q];
+    for (int q = 0; q < 4; q++) w.dc[12 + q] += jacc[q];
+  }
 #endif
+#undef JCNT
 }
 
 // legacy linear_assignment of the nr x nc matrix C: pairs (row, col) in row order into out

@@ -21,8 +21,9 @@ PHASES = ["load", "warp+predict", "DLO", "DUO", "keep+colsum", "cost", "fastpath
           "validate", "updates", "births", "outputs+deaths"]
 COUNTERS = ["LAP calls", "LAP n", "kept dets", "tracks", "frames", "-", "-", "-",
             "JV free rows", "JV scans", "JV relax steps", "JV sequential scans",
-            "JV64 setup cyc", "JV64 scan cyc", "JV64 relax cyc", "JV64 init+path cyc",
-            "JV64 find events", "JV64 scan events", "JV64 path steps", "JV64 ARR iterations"]
+            "JV64 setup (ccrrt+ARR) cyc", "JV64 find cyc", "JV64 scan cyc", "JV64 writeout cyc",
+            "JV64 find events", "JV64 scan events", "JV64 path steps", "JV64 ARR iterations",
+            "JV64 row init cyc", "JV64 v update cyc", "JV64 path cyc", "JV64 loop top cyc"]
 
 
 def build():
