@@ -563,6 +563,16 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
   const int n = nr > nc ? nr : nc;
   const int lane = threadIdx.x & 63;
   auto cget = [&](const double*, int, int, int i, int j) { return cget_as<AS>(C, nr, nc, i, j); };
+  // row i (wave-uniform) at this lane's column j: a scalar branch on the row (rows past nr are
+  // zero) and a clamped, unconditional load for the column (no exec-masked region)
+  auto crow_at = [&](int i, int j) -> double {
+    double c = 0.0;
+    if (i < nr && nc > 0) {
+      const double t = cget_as<AS>(C, nr, nc, i, j < nc ? j : nc - 1);
+      c = j < nc ? t : 0.0;
+    }
+    return c;
+  };
   const bool own = lane < n;
 #ifdef BX_PHASE_TIMING
   // cycles per slot and event counters kept in registers, added to w.dc once at the end (a
@@ -640,7 +650,7 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
       rr_cnt++;
       const int fi = rl_i(fr, (int)current);
       current++;
-      const double h = own ? cget(C, nr, nc, fi, lane) - v : INF;
+      const double h = own ? crow_at(fi, lane) - v : INF;
       int j1, j2;
       double v1, v2;
       if (!__any(own && !(h < LAPX_LARGE))) {
@@ -745,8 +755,9 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
       y = perm_i(y, c0);
       col = lane;
     }
+    const double cs = crow_at(start, lane);
     if (own) {
-      d = cget(C, nr, nc, start, lane) - v;
+      d = cs - v;
       pred = start;
     }
     int low = 0, up = 0, last = 0, endofpath = -1;
@@ -838,19 +849,15 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
         // (the next scan's row prefetched at the end of this one measured slower: C5 scan cycles
         // +8%, the load's wait lands at the loop head)
         const int i = rl_i(y, low);
-        const double crow = own ? cget(C, nr, nc, i, col) : 0.0;
+        const double crow = crow_at(i, col);  // lanes past n: column >= nc, 0
         const double mind = rl_d(d, low);
         const double h = rl_d(crow, low) - rl_d(v, low) - mind;  // lane lo holds column cols[lo]
         low++;
         const bool R = own && lane >= up;
-        double v2 = 0.0;
-        bool A = false, B = false, E = false;
-        if (R) {
-          v2 = crow - v - h;
-          A = v2 < d;
-          B = A && v2 == mind;
-          E = B && y < 0;
-        }
+        const double v2 = crow - v - h;  // every lane (no masked region); used where R
+        const bool A = R && v2 < d;
+        const bool B = A && v2 == mind;
+        const bool E = B && y < 0;
         int pe = first_lane(E);  // _scan_dense's early return
         if (pe < 0) pe = OW;
         const bool act = R && lane <= pe;
@@ -865,7 +872,8 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
         // columns lowered to the minimum join the SCAN set, in position order (all before pe)
         unsigned long long bits = __ballot(act && B && lane < pe);
         JCNT(9, __popcll(bits));
-        if (__popcll(bits) >= PERM_RUN) {
+        if (!bits) {
+        } else if (__popcll(bits) >= PERM_RUN) {
           int perm = lane;
           while (bits) {
             const int k = __ffsll((long long)bits) - 1;
