@@ -99,6 +99,11 @@ def main():
         col = per[:, k]
         print(f"  {name:16s} mean {col.mean():10.0f} max {col.max():10.0f} "
               f"share {100 * col.mean() / tot.mean():5.1f}%")
+    lap = PHASES.index("fastpath/LAP")
+    for q in range(a.seqs):
+        calls = max(dbg[q, 16], 1)
+        print(f"  seq {q}: cycles/frame {tot[q]:9.0f}  LAP {per[q, lap]:9.0f}  LAP calls {dbg[q, 16]:5d} "
+              f"mean n {dbg[q, 17] / calls:6.1f}  JV64 scans+relax {dbg[q, 25] + dbg[q, 26]:7d}")
     cs = dbg[:, 16:16 + len(COUNTERS)].astype(np.float64).sum(0)
     for k, name in enumerate(COUNTERS):
         if name != "-":
