@@ -57,6 +57,7 @@ struct BstDev {
   double det_thresh, iou_thr, min_box_area, ar_thresh, l_iou, l_mhd, l_shape, dlo_coef;
   int max_age, min_hits, use_ecc, use_dlo, use_duo, s_sim_corr, rich_s, use_sb, use_vt, reid;
   int cost_lds, ntab;
+  int tb_lds;             // the per-frame track rows staged in LDS (launches of <= 512 sequences)
   BstTrk* trk;            // [S][T]
   int* seqst;             // [S][SQB]
   int* order;             // [S][T] slot ids in the reference's list order
@@ -314,6 +315,7 @@ struct BstLds {
                  // det_ind, convert_bbox_to_z)
   double* cost;  // [cost_lds]
   double* colsum;  // [T]
+  double* tbl;     // [T][TBB] the frame's track rows (tb_lds) or null
   int *kd, *bi;    // [D] kept detections, DUO boost candidates
   int *lst, *lst2; // [T]
   int *mi, *mm;    // [2N] candidate / validated (kept det, list position) pairs
@@ -331,6 +333,7 @@ __device__ void carve(const BstDev& g, char* base, BstLds& L) {
   L.dd = takeD((size_t)D * DDW);
   L.cost = takeD(g.cost_lds);
   L.colsum = takeD(T);
+  L.tbl = g.tb_lds ? takeD((size_t)T * TBB) : nullptr;
   L.jv.v = takeD(N);
   L.jv.d = takeD(N);
   L.jv.sd = takeD(2);
@@ -357,9 +360,10 @@ __device__ void carve(const BstDev& g, char* base, BstLds& L) {
   L.jv.dc = nullptr;
 }
 
-size_t lds_bytes(int D, int T, int N, int cost_lds) {
+size_t lds_bytes(int D, int T, int N, int cost_lds, int tb_lds) {
   auto dI = [](size_t n) { return ((n * 4 + 7) / 8) * 8; };
   return (size_t)D * DDW * 8 + (size_t)cost_lds * 8 + (size_t)T * 8 + 2 * (size_t)N * 8 + 2 * 8 +
+         (tb_lds ? (size_t)T * TBB * 8 : 0) +
          2 * dI(D) + 2 * dI(T) + 2 * dI(2 * N) + 2 * dI(D + T) + 4 * dI(N) + 6 * dI(N) + dI(8) +
          dI(8);
 }
@@ -396,7 +400,9 @@ __global__ void __launch_bounds__(BW)
   int* sq = g.seqst + (size_t)seq * SQB;
   BstTrk* trk = g.trk + (size_t)seq * g.T;
   int* order = g.order + (size_t)seq * g.T;
-  double* tb = g.tb + (size_t)seq * g.T * TBB;
+  // the frame's track rows: written by the predict phase, read by every later phase (per pair in
+  // DLO / DUO / the cost): in LDS when the launch leaves room, else this sequence's HBM rows
+  double* tb = g.tb_lds ? L.tbl : g.tb + (size_t)seq * g.T * TBB;
   double* costg = g.cost_g ? g.cost_g + (size_t)seq * g.D * g.T : nullptr;
   double* eg = g.e_g ? g.e_g + (size_t)seq * g.D * g.T : nullptr;
   const double* ec = g.reid ? g.ec + (size_t)seq * g.D * g.T : nullptr;
@@ -717,6 +723,7 @@ __global__ void __launch_bounds__(BW)
         nmi = L.u[0];
         BCOUNT(0, 1);
         BCOUNT(1, nk > nt ? nk : nt);
+        BCOUNT(5, (nk > nt ? nk : nt) > OW ? 1 : 0);
       }
       BSTAMP(6);
     }
@@ -1228,16 +1235,23 @@ int bx_boost_create(const bx_boost_config* c, bx_boost** out) {
   d.use_vt = c->use_vt != 0;
   // LDS: the fixed part plus as much cost matrix as keeps every sequence's workgroup resident
   // at once (256 CUs; at least 40 KB, i.e. 4 workgroups per CU, at most 152 KB)
-  const size_t fixed = lds_bytes(d.D, d.T, d.N, 0);
   long cap = 160L * 1024 / ((d.S + 255) / 256);
   if (cap > 152L * 1024) cap = 152L * 1024;
   if (cap < 40L * 1024) cap = 40L * 1024;
+  // the frame's track rows in LDS too when the cap leaves room for them beside the cost matrix
+  // (up to 512 sequences: cap >= 80 KB)
+  d.tb_lds = 0;
+  size_t fixed = lds_bytes(d.D, d.T, d.N, 0, 0);
+  if (d.S <= 512 && (long)(fixed + (size_t)d.T * TBB * 8) + 64 * 8 <= cap) {
+    d.tb_lds = 1;
+    fixed = lds_bytes(d.D, d.T, d.N, 0, 1);
+  }
   long budget = cap - (long)fixed;
   int cl = budget > 0 ? (int)(budget / 8) : 0;
   if (cl > d.D * d.T) cl = d.D * d.T;
   if (cl < 64) cl = 64;
   d.cost_lds = cl;
-  e->lds = lds_bytes(d.D, d.T, d.N, cl);
+  e->lds = lds_bytes(d.D, d.T, d.N, cl, d.tb_lds);
   if (e->lds > 160 * 1024) {
     delete e;
     return bx_record_error(BX_ERR_INVALID, "track_cap/det_cap too large for one workgroup's LDS");

@@ -19,7 +19,7 @@ sys.path.insert(0, str(ROOT))
 LIB = ROOT / "boxmot_amd" / "lib" / "libbxassoc_timing.so"
 PHASES = ["load", "warp+predict", "DLO", "DUO", "keep+colsum", "cost", "fastpath/LAP",
           "validate", "updates", "births", "outputs+deaths"]
-COUNTERS = ["LAP calls", "LAP n", "kept dets", "tracks", "frames", "-", "-", "-",
+COUNTERS = ["LAP calls", "LAP n", "kept dets", "tracks", "frames", "LAP calls n > 64", "-", "-",
             "JV free rows", "JV scans", "JV relax steps", "JV sequential scans",
             "JV64 setup (ccrrt+ARR) cyc", "JV64 find cyc", "JV64 scan cyc", "JV64 writeout cyc",
             "JV64 find events", "JV64 scan events", "JV64 path steps", "JV64 ARR iterations",
@@ -103,7 +103,7 @@ def main():
     for q in range(a.seqs):
         calls = max(dbg[q, 16], 1)
         print(f"  seq {q}: cycles/frame {tot[q]:9.0f}  LAP {per[q, lap]:9.0f}  LAP calls {dbg[q, 16]:5d} "
-              f"mean n {dbg[q, 17] / calls:6.1f}  JV64 scans+relax {dbg[q, 25] + dbg[q, 26]:7d}")
+              f"mean n {dbg[q, 17] / calls:6.1f}  n > 64: {dbg[q, 21]:4d}  JV64 scans+relax {dbg[q, 25] + dbg[q, 26]:7d}")
     cs = dbg[:, 16:16 + len(COUNTERS)].astype(np.float64).sum(0)
     for k, name in enumerate(COUNTERS):
         if name != "-":
