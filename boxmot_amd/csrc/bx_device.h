@@ -708,36 +708,64 @@ __device__ __forceinline__ void lap_augment(const LapWS& w, int root, int sink, 
 }
 
 // One SSP root on ONE lane (the lane's component only touches its own rows/columns).  Touched
-// columns and visited rows are kept as linked lists through touched[] / srlist[].
-__device__ __forceinline__ int lap_root_lane(int root, double L, const LapWS& w) {
+// columns are appended to the lane's own stretch `tl` of touched[] (as long as its component has
+// columns: the stretches of the wave's lanes are disjoint), so the argmin walks an array — the
+// loads of consecutive entries are independent — instead of a linked list, whose every hop waited
+// for the previous one's LDS load; touch order is kept, so ties resolve as before.  The
+// relaxation loads the next edge's column state before storing the current one's (the columns of
+// a row's edges are distinct; batches of four measured slower: K3's register budget).  Visited
+// rows are kept as a linked list through srlist[].
+__device__ __forceinline__ int lap_root_lane(int root, double L, const LapWS& w, uint16_t* tl) {
   double minVal = 0.0;
-  int i = root, thead = -1, ttail = -1, shead = -1, stail = -1, steps = 0;
+  int i = root, nt = 0, shead = -1, stail = -1, steps = 0;
   double dummy_best = INF;
   int dummy_row = -1, sink = -1;
   while (true) {
     const double ui = w.u[i];
-    for (int e = w.row_ptr[i]; e < w.row_ptr[i + 1]; e++) {
+    const int e1 = w.row_ptr[i + 1];
+    int e = w.row_ptr[i];
+    if (e < e1) {
       int j;
       double c;
       lap_edge(w, e, j, c);
-      if (w.colflag[j] & 1) continue;
-      const double r = minVal + (c - L) - ui - w.v[j];
-      if (r < w.spc[j]) {
-        w.spc[j] = r;
-        w.path[j] = (int16_t)i;
-        if (!(w.colflag[j] & 2)) {
-          w.colflag[j] |= 2;
-          if (ttail >= 0) w.touched[ttail] = (uint16_t)j; else thead = j;
-          ttail = j;
+      uint8_t f = w.colflag[j];
+      double vj = w.v[j], sj = w.spc[j];
+      for (; e < e1; e++) {
+        int jn = j;
+        double cn = 0.0, vn = 0.0, sn = 0.0;
+        uint8_t fn = 0;
+        if (e + 1 < e1) {
+          lap_edge(w, e + 1, jn, cn);
+          fn = w.colflag[jn];
+          vn = w.v[jn];
+          sn = w.spc[jn];
         }
+        if (!(f & 1)) {
+          const double r = minVal + (c - L) - ui - vj;
+          if (r < sj) {
+            w.spc[j] = r;
+            w.path[j] = (int16_t)i;
+            if (!(f & 2)) {
+              w.colflag[j] = f | 2;
+              tl[nt++] = (uint16_t)j;
+            }
+          }
+        }
+        j = jn;
+        c = cn;
+        f = fn;
+        vj = vn;
+        sj = sn;
       }
     }
     const double dv = minVal - ui;
     if (dv < dummy_best) { dummy_best = dv; dummy_row = i; }
     double bv = INF;
     int bj = -1;
-    for (int j = thead; j >= 0; j = (j == ttail) ? -1 : (int)w.touched[j])
+    for (int k = 0; k < nt; k++) {
+      const int j = tl[k];
       if (!(w.colflag[j] & 1) && w.spc[j] < bv) { bv = w.spc[j]; bj = j; }
+    }
     if (dummy_best <= bv) { minVal = dummy_best; sink = -2; break; }
     minVal = bv;
     steps++;
@@ -751,14 +779,15 @@ __device__ __forceinline__ int lap_root_lane(int root, double L, const LapWS& w)
   w.u[root] += minVal;
   for (int r = shead; r >= 0; r = (r == stail) ? -1 : (int)w.srlist[r])
     w.u[r] += minVal - w.spc[w.col4row[r]];
-  for (int j = thead; j >= 0; j = (j == ttail) ? -1 : (int)w.touched[j])
+  for (int k = 0; k < nt; k++) {
+    const int j = tl[k];
     if (w.colflag[j] & 1) w.v[j] -= minVal - w.spc[j];
+  }
   lap_augment(w, root, sink, dummy_row);
-  for (int j = thead; j >= 0;) {
-    const int nx = (j == ttail) ? -1 : (int)w.touched[j];
+  for (int k = 0; k < nt; k++) {
+    const int j = tl[k];
     w.spc[j] = INF;
     w.colflag[j] = 0;
-    j = nx;
   }
   return steps;
 }
@@ -1134,13 +1163,16 @@ __device__ __forceinline__ int lap_prepare_block(int R, int C, double L, const L
 }
 
 // The searches, called by all 64 lanes of ONE wave after lap_prepare_block.
-__device__ __forceinline__ void lap_solve_roots_wave(int R, int nroots, double L, const LapWS& w) {
+__device__ __forceinline__ void lap_solve_roots_wave(int R, int C, int nroots, double L,
+                                                    const LapWS& w) {
   const int lane = lane_id();
   int nsteps = 0, ncomp = 0, maxrows = 0, iters = 0;
   if (w.dbg && lane == 0) w.dbg[3] = __builtin_amdgcn_s_memtime();
   if (nroots > 0) {
     // component labels by min-label propagation over the roots' finite edges (coldeg reused as
-    // the per-column label)
+    // the per-column label; columns no root reaches keep "none")
+    for (int j = lane; j < C; j += WAVE) w.coldeg[j] = 0x7fffffff;
+    wave_sync_lds();
     for (int k = lane; k < nroots; k += WAVE) {
       const int r = w.roots[k];
       w.rlab[r] = r;
@@ -1183,32 +1215,54 @@ __device__ __forceinline__ void lap_solve_roots_wave(int R, int nroots, double L
     if (w.dbg && lane == 0) w.dbg[8] = __builtin_amdgcn_s_memtime();
     // a component is headed by its smallest row (label == row); its rows are the roots carrying
     // that label, taken in ascending order.  Small components: one lane each, in parallel.
+    // The lanes take the component heads 64 at a time; a lane solving its component gets a
+    // stretch of touched[] as long as the component's column count (exclusive prefix over the
+    // wave: the components are disjoint, so the stretches fit in C).
     bool big = false;
-    for (int k = lane; k < nroots; k += WAVE) {
-      const int h = w.roots[k];
-      if (w.rlab[h] != h) continue;
-      int nrows = 0;
-      for (int q = k; q < nroots; q++) nrows += w.rlab[w.roots[q]] == h;
-      ncomp++;
-      maxrows = max(maxrows, nrows);
-      if (nrows > LAP_LANE_ROWS) { big = true; continue; }
-      if (nrows <= LAP_RM) {  // register-resident solve when it fits
-        int rr[LAP_RM];
-        int n = 0;
+    for (int k0 = 0; k0 < nroots; k0 += WAVE) {
+      const int k = k0 + lane;
+      int h = -1, nrows = 0;
+      bool mine = false;
+      if (k < nroots) {
+        h = w.roots[k];
+        if (w.rlab[h] == h) {
+          for (int q = k; q < nroots; q++) nrows += w.rlab[w.roots[q]] == h;
+          ncomp++;
+          maxrows = max(maxrows, nrows);
+          mine = true;
+          if (nrows > LAP_LANE_ROWS) {
+            big = true;
+            mine = false;
+          } else if (nrows <= LAP_RM) {  // register-resident solve when it fits
+            int rr[LAP_RM];
+            int n = 0;
 #pragma unroll
-        for (int t = 0; t < LAP_RM; t++) rr[t] = h;
-        for (int q = k; q < nroots && n < nrows; q++) {
-          const int r = w.roots[q];
-          if (w.rlab[r] == h) { rput(rr, n, r); n++; }
+            for (int t = 0; t < LAP_RM; t++) rr[t] = h;
+            for (int q = k; q < nroots && n < nrows; q++) {
+              const int r = w.roots[q];
+              if (w.rlab[r] == h) { rput(rr, n, r); n++; }
+            }
+            if (lap_component_regs(rr, nrows, L, w, nsteps)) mine = false;
+          }
         }
-        if (lap_component_regs(rr, nrows, L, w, nsteps)) continue;
       }
-      for (int q = k; q < nroots; q++) {
-        const int r = w.roots[q];
-        if (w.rlab[r] == h) nsteps += lap_root_lane(r, L, w);
+      int ncols = 0;
+      if (mine)
+        for (int j = 0; j < C; j++) ncols += w.coldeg[j] == h;
+      int off = ncols;  // inclusive prefix over the lanes, then exclusive
+#pragma unroll
+      for (int d = 1; d < WAVE; d <<= 1) {
+        const int o = __shfl_up(off, d);
+        if (lane >= d) off += o;
       }
+      off -= ncols;
+      if (mine)
+        for (int q = k; q < nroots; q++) {
+          const int r = w.roots[q];
+          if (w.rlab[r] == h) nsteps += lap_root_lane(r, L, w, w.touched + off);
+        }
+      wave_sync_lds();
     }
-    wave_sync_lds();
     if (w.dbg && lane == 0) w.dbg[9] = __builtin_amdgcn_s_memtime();
     // large components: wave-parallel, one after another (components are independent)
     if (__ballot(big) != 0ull) {
@@ -1352,7 +1406,7 @@ __device__ inline bool lap_tied_block(int R, int C, double L, const LapWS& w, in
 __device__ __forceinline__ void lap_solve_block(int R, int C, double L, const LapWS& w,
                                                 int* scan_tmp) {
   const int nroots = lap_prepare_block(R, C, L, w, scan_tmp);
-  if (wave_id() == 0) lap_solve_roots_wave(R, nroots, L, w);
+  if (wave_id() == 0) lap_solve_roots_wave(R, C, nroots, L, w);
   __syncthreads();
 }
 
