@@ -35,6 +35,7 @@
 using namespace bx;
 
 int bx_record_error(int code, const char* msg);  // bx_engine.hip (shared bx_last_error)
+hipError_t bx_lds_attr(const void* kern, size_t bytes);  // bx_engine.hip (never lowers a limit)
 
 namespace {
 
@@ -1304,8 +1305,7 @@ int bx_boost_create(const bx_boost_config* c, bx_boost** out) {
   d.dbg = nullptr;
 #endif
   BCHK(hipMemcpy(base + o_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
-  BCHK(hipFuncSetAttribute((const void*)boost_frame_kernel,
-                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->lds));
+  BCHK(bx_lds_attr((const void*)boost_frame_kernel, e->lds));
   BCHK(hipMalloc(&e->h_dets, sizeof(float) * 6 * D));
   BCHK(hipMalloc(&e->h_off, sizeof(int) * 2));
   if (d.reid) BCHK(hipMalloc(&e->h_embs, sizeof(double) * D * F));

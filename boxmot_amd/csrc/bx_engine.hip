@@ -1979,6 +1979,27 @@ static int settle(bx_engine* e) {
 
 int bx_record_error(int code, const char* msg) { return set_err(code, msg); }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) that never lowers a kernel's limit: engines of
+// different capacities share the kernels, and a later, smaller engine must not shrink the limit
+// an earlier one launches with (shared by every translation unit of the library)
+hipError_t bx_lds_attr(const void* kern, size_t bytes) {
+  static std::mutex mu;
+  static std::vector<std::pair<const void*, size_t>> done;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto& d : done)
+    if (d.first == kern) {
+      if (d.second >= bytes) return hipSuccess;
+      const hipError_t e =
+          hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+      if (e == hipSuccess) d.second = bytes;
+      return e;
+    }
+  const hipError_t e =
+      hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) done.emplace_back(kern, bytes);
+  return e;
+}
+
 extern "C" {
 
 const char* bx_last_error(void) { return g_err.c_str(); }

@@ -31,6 +31,7 @@
 using namespace bx;
 
 int bx_record_error(int code, const char* msg);  // bx_engine.hip (shared bx_last_error)
+hipError_t bx_lds_attr(const void* kern, size_t bytes);  // bx_engine.hip (never lowers a limit)
 
 namespace {
 
@@ -1109,8 +1110,7 @@ int bx_ocsort_create(const bx_ocsort_config* c, bx_ocsort** out) {
 #else
   d.dbg = nullptr;
 #endif
-  OCHK(hipFuncSetAttribute((const void*)ocsort_frame_kernel,
-                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->lds));
+  OCHK(bx_lds_attr((const void*)ocsort_frame_kernel, e->lds));
   OCHK(hipMalloc(&e->h_dets, sizeof(float) * 6 * d.D));
   OCHK(hipMalloc(&e->h_off, sizeof(int) * 2));
   OCHK(hipMalloc(&e->h_out, sizeof(double) * 8 * d.D));

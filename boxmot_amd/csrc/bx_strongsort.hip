@@ -50,6 +50,7 @@
 using namespace bx;
 
 int bx_record_error(int code, const char* msg);  // bx_engine.hip (shared bx_last_error)
+hipError_t bx_lds_attr(const void* kern, size_t bytes);  // bx_engine.hip (never lowers a limit)
 
 namespace {
 
@@ -3277,12 +3278,9 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   SCHK(hipMemcpy(d.sqd, qd.data(), qd.size() * sizeof(double), hipMemcpyHostToDevice));
   if (d.ws_lds) {
     const int lds = (int)ss_lds_bytes(d);
-    SCHK(hipFuncSetAttribute((const void*)ss_pre_kernel,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    SCHK(hipFuncSetAttribute((const void*)ss_match_kernel,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    SCHK(hipFuncSetAttribute((const void*)ss_post_kernel,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    SCHK(bx_lds_attr((const void*)ss_pre_kernel, lds));
+    SCHK(bx_lds_attr((const void*)ss_match_kernel, lds));
+    SCHK(bx_lds_attr((const void*)ss_post_kernel, lds));
   }
   SCHK(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
   SCHK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));

@@ -478,8 +478,8 @@ class BoostParams:
 
 class BoostEngine:
     """Handle over ``bx_boost_*`` (include/bxboost.h): ``n_seq`` BoostTrack sequences in HBM;
-    per frame a ReID contraction (fp64 MFMA), the frame kernel (one wave per sequence) and the
-    embedding update."""
+    per frame a ReID contraction (fp64 MFMA), the frame kernel (a 1-4 wave workgroup per
+    sequence) and the embedding update."""
 
     def __init__(self, n_seq: int = 1, track_cap: int = 256, det_cap: int = 256,
                  emb_dim: int = 0, params: BoostParams | None = None):

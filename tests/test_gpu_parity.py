@@ -1019,6 +1019,27 @@ def test_boosttrack_wide_launch_vs_oracle(torch_cuda, n_seq):
     run_boost_batched(torch_cuda, scenes, 30, dict(BOOST_ARGS), 32, track_cap=128, det_cap=64)
 
 
+def test_boosttrack_engines_of_different_lds_sizes(torch_cuda):
+    """The frame kernel's dynamic-LDS limit is shared by every engine: a later engine with a
+    smaller LDS footprint (more sequences: less LDS per workgroup) must not shrink the limit an
+    earlier one launches with.  Steps the small-launch engine after creating the large one and
+    checks it against the oracle."""
+    from boxmot_amd.engine import BoostEngine, BoostParams
+    from boxmot_amd.synth import SyntheticScene
+
+    args = dict(BOOST_ARGS)
+    big = BoostEngine(n_seq=2, track_cap=128, det_cap=64, emb_dim=32, params=BoostParams(**args))
+    BoostEngine(n_seq=1024, track_cap=128, det_cap=64, emb_dim=32, params=BoostParams(**args))
+    sc = SyntheticScene(n_obj=30, seed=31, emb_dim=32, emb_dtype=np.float64, layout="crowded",
+                        p_det=0.5, conf_lo=0.3)
+    orc = po.OracleTracker("boosttrack", **args)
+    for t in range(1, 16):
+        d, e = sc.frame(t)[:2]
+        np.testing.assert_array_equal(big.update_host(0, d, e), orc.update(d, e),
+                                      err_msg=f"frame {t}")
+    assert big.status() == 0
+
+
 def test_boosttrack_large_scene_vs_oracle(torch_cuda):
     """A crowded 160-object sequence with 512-d ReID: cost matrices past the LDS budget (HBM
     path), several MFMA output tiles per sequence, LAP solves."""
