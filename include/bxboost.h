@@ -8,8 +8,8 @@
  * (dets_embs @ trk_embs.T on the fp64 matrix cores), the one-to-one fast path or lapx JV, the
  * IoU/appearance validation, Kalman updates, embedding EMA, births, deaths and the filtered
  * output rows — runs on the GPU behind these entry points: per frame a ReID contraction kernel
- * (workgroup per sequence), the frame kernel (one wave per sequence) and an embedding-update
- * kernel (wave per updated track).
+ * (workgroup per 32x64 output tile), the frame kernel (a 1-4 wave workgroup per sequence) and an
+ * embedding-update kernel (wave per updated track).
  *
  * Reference interfaces replaced (file:line in muntherr/boxmot @ /root/reference):
  *   bx_boost_create/step/update_host  BoostTrack.__init__ / BoostTrack.update
