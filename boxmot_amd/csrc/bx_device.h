@@ -1046,7 +1046,10 @@ __device__ __forceinline__ bool lap_component_regs(const int (&rr)[LAP_RM], int 
   return true;
 }
 
-constexpr int LAP_LANE_ROWS = 16;  // components up to this many rows are solved by one lane
+#ifndef BX_LAP_LANE_ROWS
+#define BX_LAP_LANE_ROWS 24
+#endif
+constexpr int LAP_LANE_ROWS = BX_LAP_LANE_ROWS;  // components up to this many rows: one lane
 
 // Preparation, called by ALL threads of the workgroup (block-wide syncs): initialise, settle
 // single-edge and star components, and list the rows left for the searches (ascending) in
