@@ -375,9 +375,12 @@ size_t lds_bytes(int D, int T, int N, int cost_lds, int tb_lds) {
 // run in every wave at once on the same LDS data — each wave derives the same counts and writes the
 // same values — except the JV, which wave 0 solves alone (SyncWaveL) while the others wait at the
 // barrier after it.
-constexpr int BW = 256;  // the most threads per sequence
+#ifndef BX_BOOST_MAX_THREADS
+#define BX_BOOST_MAX_THREADS 256
+#endif
+constexpr int BW = BX_BOOST_MAX_THREADS > 256 ? BX_BOOST_MAX_THREADS : 256;  // the most threads per sequence
 __host__ __device__ constexpr int frame_threads(int nseq) {
-  return nseq >= 1024 ? 64 : nseq >= 512 ? 128 : nseq > 256 ? 192 : 256;
+  return nseq >= 1024 ? 64 : nseq >= 512 ? 128 : nseq > 256 ? 192 : BX_BOOST_MAX_THREADS;
 }
 constexpr int COST_KR = 4;  // cost entries per thread per chunk (registers held across a barrier)
 
