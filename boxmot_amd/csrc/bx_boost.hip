@@ -369,8 +369,9 @@ size_t lds_bytes(int D, int T, int N, int cost_lds, int tb_lds) {
          dI(8);
 }
 
-// One workgroup of 1-4 waves per sequence (frame_threads: about one wave per SIMD over the
-// launch — four for up to 256 sequences, one from 1024 on).  Work over pairs, detections or tracks
+// One workgroup of 2-4 waves per sequence (frame_threads: four for up to 256 sequences in the
+// launch, three up to 511, two from 512 on — at 1024 sequences two waves each measured 5% faster
+// than one (C2 1.39 -> 1.46 M frames/s) and four 20% slower).  Work over pairs, detections or tracks
 // is spread over all the waves; the order-dependent steps (compactions, the validation's ballots)
 // run in every wave at once on the same LDS data — each wave derives the same counts and writes the
 // same values — except the JV, which wave 0 solves alone (SyncWaveL) while the others wait at the
@@ -379,8 +380,12 @@ size_t lds_bytes(int D, int T, int N, int cost_lds, int tb_lds) {
 #define BX_BOOST_MAX_THREADS 256
 #endif
 constexpr int BW = BX_BOOST_MAX_THREADS > 256 ? BX_BOOST_MAX_THREADS : 256;  // the most threads per sequence
+#ifndef BX_BOOST_THREADS_1024
+#define BX_BOOST_THREADS_1024 128
+#endif
 __host__ __device__ constexpr int frame_threads(int nseq) {
-  return nseq >= 1024 ? 64 : nseq >= 512 ? 128 : nseq > 256 ? 192 : BX_BOOST_MAX_THREADS;
+  return nseq >= 1024 ? BX_BOOST_THREADS_1024
+                      : nseq >= 512 ? 128 : nseq > 256 ? 192 : BX_BOOST_MAX_THREADS;
 }
 constexpr int COST_KR = 4;  // cost entries per thread per chunk (registers held across a barrier)
 

@@ -1007,7 +1007,7 @@ class _EmptyScene:
 
 @pytest.mark.parametrize("n_seq", [384, 600, 1024])
 def test_boosttrack_wide_launch_vs_oracle(torch_cuda, n_seq):
-    """Launch widths with fewer threads per sequence (three, two and one wave: `frame_threads`):
+    """Launch widths with fewer threads per sequence (three and two waves: `frame_threads`):
     three busy sequences (first, middle, last) among empty ones, bitwise against the oracle."""
     from boxmot_amd.synth import SyntheticScene
 
