@@ -161,7 +161,8 @@ EXPORTS = [
     "bx_engine_probe", "bx_engine_probe_read", "bx_engine_set_overlap", "bx_engine_frame_stats_host",
     "bx_iou_batch", "bx_pairwise_cost", "bx_aw_max_metric", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
     "bx_kf_multi_predict", "bx_kf_update", "bx_kf_gating_distance", "bx_linear_assignment", "bx_lapjv",
-    "bx_linear_assignment_ex", "bx_engine_lap_ties_host", "bx_engine_inputs_released",
+    "bx_linear_assignment_ex", "bx_engine_lap_ties_host", "bx_engine_lap_components_host",
+    "bx_engine_inputs_released",
     "bx_engine_copy_state", "bx_engine_slots_used_host", "bx_ocsort_copy_state",
     "bx_boost_copy_state", "bx_ss_copy_state",
     "bx_nn_cosine_distance", "bx_ocsort_create", "bx_ocsort_destroy", "bx_ocsort_reset", "bx_ocsort_step",
@@ -219,6 +220,7 @@ _SIGS = {
     "bx_linear_assignment": ([_vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp], C.c_int),
     "bx_linear_assignment_ex": ([_vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp, _vp], C.c_int),
     "bx_engine_lap_ties_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
+    "bx_engine_lap_components_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_engine_inputs_released": ([_vp, _vp], C.c_int),
     "bx_engine_copy_state": ([_vp, _vp], C.c_int),
     "bx_ocsort_copy_state": ([_vp, _vp], C.c_int),

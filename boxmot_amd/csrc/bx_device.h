@@ -664,6 +664,8 @@ struct LapWS {
   int* rlab;              // [R] component label (smallest row index of the component)
   int* colaux;            // [C] multi-edge rows per column (star detection)
   int* colmin;            // [C] star components: winning row
+  int* comp_stats = nullptr;  // if set: [0] += components of 17..LAP_LANE_ROWS rows (lane
+                              // solver), [1] += components of more rows (wave solver)
   unsigned long long* dbg = nullptr;  // diagnostic counters (phase-timing builds only)
 };
 
@@ -1169,7 +1171,7 @@ __device__ __forceinline__ int lap_prepare_block(int R, int C, double L, const L
 __device__ __forceinline__ void lap_solve_roots_wave(int R, int C, int nroots, double L,
                                                     const LapWS& w) {
   const int lane = lane_id();
-  int nsteps = 0, ncomp = 0, maxrows = 0, iters = 0;
+  int nsteps = 0, ncomp = 0, maxrows = 0, iters = 0, nlane17 = 0, nwave = 0;
   if (w.dbg && lane == 0) w.dbg[3] = __builtin_amdgcn_s_memtime();
   if (nroots > 0) {
     // component labels by min-label propagation over the roots' finite edges (coldeg reused as
@@ -1233,6 +1235,8 @@ __device__ __forceinline__ void lap_solve_roots_wave(int R, int C, int nroots, d
           ncomp++;
           maxrows = max(maxrows, nrows);
           mine = true;
+          nlane17 += nrows > 16 && nrows <= LAP_LANE_ROWS;
+          nwave += nrows > LAP_LANE_ROWS;
           if (nrows > LAP_LANE_ROWS) {
             big = true;
             mine = false;
@@ -1286,6 +1290,17 @@ __device__ __forceinline__ void lap_solve_roots_wave(int R, int C, int nroots, d
   for (int r = lane; r < R; r += WAVE)
     if (w.col4row[r] == -2) w.col4row[r] = -1;
   wave_sync_lds();
+  if (w.comp_stats) {
+    int sa = nlane17, sb = nwave;
+    for (int d = 32; d >= 1; d >>= 1) {
+      sa += __shfl_xor(sa, d);
+      sb += __shfl_xor(sb, d);
+    }
+    if (lane == 0 && (sa | sb)) {
+      w.comp_stats[0] += sa;
+      w.comp_stats[1] += sb;
+    }
+  }
   for (int d = 32; d >= 1; d >>= 1) {
     nsteps += __shfl_xor(nsteps, d);
     ncomp += __shfl_xor(ncomp, d);

@@ -235,6 +235,7 @@ enum {
   SQ_NA = 0, SQ_NL, SQ_FC, SQ_IDC, SQ_STATUS, SQ_NA2, SQ_NL2, SQ_NREC, SQ_SKIP,
   SQ_NHIGH, SQ_NPAIR, SQ_NDET,  // last frame's high dets, gated pairs, dets (statistics)
   SQ_NTIE,                       // associations re-solved by lapx's lapjv (tied optimum), total
+  SQ_NCOMP17, SQ_NCOMPW,         // LAP components of 17..24 rows (lane SSP) / more (wave SSP)
   SQ_STRIDE = 16
 };
 // update records: x = slot | kind << 16, y = detection index within the sequence's frame
@@ -930,6 +931,7 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
   W.rlab = (int*)(smem + Lo.o_rlab);
   W.colaux = (int*)(smem + Lo.o_colaux);
   W.colmin = (int*)(smem + Lo.o_colmin);
+  W.comp_stats = seq + SQ_NCOMP17;
   uint16_t* e_gcol = P.gcol + (size_t)s * T * D;
   double* e_gcost = P.gcost + (size_t)s * T * D;
   auto put_edge = [&](int e, int col, double cost) {
@@ -2385,6 +2387,21 @@ int bx_engine_lap_ties_host(bx_engine* e, int seq0, int nseq, int64_t* total) {
   int64_t t = 0;
   for (int q = 0; q < nseq; q++) t += v[(size_t)q * SQ_STRIDE + SQ_NTIE];
   *total = t;
+  return BX_OK;
+}
+
+int bx_engine_lap_components_host(bx_engine* e, int seq0, int nseq, int64_t* sums) {
+  if (int rc = settle(e)) return rc;
+  if (!e || !sums || seq0 < 0 || nseq <= 0 || seq0 + nseq > e->dev.S)
+    return set_err(BX_ERR_INVALID, "bad arguments to bx_engine_lap_components_host");
+  std::vector<int> v((size_t)nseq * SQ_STRIDE);
+  HIPCHK(hipMemcpy(v.data(), e->dev.seq + (size_t)seq0 * SQ_STRIDE, sizeof(int) * v.size(),
+                   hipMemcpyDeviceToHost));
+  sums[0] = sums[1] = 0;
+  for (int q = 0; q < nseq; q++) {
+    sums[0] += v[(size_t)q * SQ_STRIDE + SQ_NCOMP17];
+    sums[1] += v[(size_t)q * SQ_STRIDE + SQ_NCOMPW];
+  }
   return BX_OK;
 }
 

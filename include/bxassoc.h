@@ -149,6 +149,11 @@ int bx_engine_probe_read(bx_engine *e, double *total_ms, int *count);
 /* Associations of sequences [seq0, seq0+nseq) whose optimum was tied and that were therefore
  * re-solved by lapx's own lapjv (see bx_linear_assignment), summed since creation / reset. */
 int bx_engine_lap_ties_host(bx_engine *e, int seq0, int nseq, int64_t *total);
+/* Connected components the sparse LAP solver (matching.py:30-108 restated) handed to
+ * its per-lane SSP with 17..24 rows (sums[0]) and to its wave-parallel SSP with more rows
+ * (sums[1]), over sequences [seq0, seq0+nseq), summed since creation / reset.  Diagnostic: the
+ * parity tests use it to show a workload exercised both solver paths. */
+int bx_engine_lap_components_host(bx_engine *e, int seq0, int nseq, int64_t *sums);
 
 /* Capacity growth (the reference's track lists are unbounded: bytetrack.py:272-346): copy every
  * sequence's tracker state of `src` into `dst`, a fresh engine with the same kind, sequences and
