@@ -55,16 +55,34 @@ def _deps(src: Path, seen=None) -> list:
     return out
 
 
+def _toolchain_stamp(hipcc: str, flags: list) -> str:
+    """Hash of the compile flags and the compiler's version: objects built under another stamp
+    are stale even when their sources did not change."""
+    import hashlib
+
+    try:
+        ver = subprocess.run([hipcc, "--version"], capture_output=True, text=True).stdout
+    except OSError:
+        ver = ""
+    return hashlib.sha256(("\0".join(flags) + "\0" + ver).encode()).hexdigest()[:16]
+
+
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the HIP extension for gfx950 in-tree (boxmot_amd/lib/libbxassoc.so): one object per
-    translation unit (compiled in parallel, and only when it or a header it includes changed),
-    then one link."""
+    translation unit (compiled in parallel, and only when it or a header it includes changed, or
+    the flags / compiler did), then one link.  Temporary outputs carry the process id, so two
+    processes building at once never replace each other's half-written file."""
     from concurrent.futures import ThreadPoolExecutor
 
     objdir = LIB_DIR / "obj"
     objdir.mkdir(parents=True, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = [f for f in HIPCC_FLAGS if f != "-shared"]
+    link_flags = [f for f in HIPCC_FLAGS if f.startswith("--offload-arch")] + ["-shared", "-fPIC"]
+    stamp_file = objdir / "toolchain.stamp"
+    stamp = _toolchain_stamp(hipcc, flags)
+    if not stamp_file.exists() or stamp_file.read_text().strip() != stamp:
+        force = True
     stale = []
     objs = []
     for s in SOURCES:
@@ -77,10 +95,11 @@ def build(force: bool = False, verbose: bool = False) -> Path:
 
     def compile_one(so):
         src, obj = so
-        tmp = obj.with_suffix(".o.tmp")
+        tmp = obj.with_suffix(f".o.{os.getpid()}.tmp")
         r = subprocess.run([hipcc, *flags, "-c", "-o", str(tmp), str(src)], capture_output=True,
                            text=True)
         if r.returncode != 0:
+            tmp.unlink(missing_ok=True)
             raise RuntimeError(f"hipcc failed on {src.name}:\n{r.stderr}")
         if verbose and r.stderr:
             print(r.stderr)
@@ -89,14 +108,16 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     if stale:
         with ThreadPoolExecutor(max_workers=min(len(stale), os.cpu_count() or 1)) as ex:
             list(ex.map(compile_one, stale))
+        stamp_file.write_text(stamp + "\n")
     if not stale and LIB_PATH.exists() and all(
             o.stat().st_mtime <= LIB_PATH.stat().st_mtime for o in objs):
         return LIB_PATH
     LIB_DIR.mkdir(exist_ok=True)
-    tmp = LIB_PATH.with_suffix(".so.tmp")
-    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(tmp),
-                        *[str(o) for o in objs]], capture_output=True, text=True)
+    tmp = LIB_PATH.with_suffix(f".so.{os.getpid()}.tmp")
+    r = subprocess.run([hipcc, *link_flags, "-o", str(tmp), *[str(o) for o in objs]],
+                       capture_output=True, text=True)
     if r.returncode != 0:
+        tmp.unlink(missing_ok=True)
         raise RuntimeError(f"hipcc link failed:\n{r.stderr}")
     os.replace(tmp, LIB_PATH)
     return LIB_PATH

@@ -1279,7 +1279,9 @@ int bx_boost_create(const bx_boost_config* c, bx_boost** out) {
   const size_t o_ord = carve_b(S * T * sizeof(int));
   const size_t o_tb = carve_b(S * T * TBB * sizeof(double));
   const size_t o_cg = need_g ? carve_b(S * D * T * sizeof(double)) : 0;
-  const size_t o_eg = need_g ? carve_b(S * D * T * sizeof(double)) : 0;
+  // the DLO numerators spill only with use_dlo && rich_s (boost_frame_kernel's E staging)
+  const bool need_eg = need_g && d.use_dlo && d.rich_s;
+  const size_t o_eg = need_eg ? carve_b(S * D * T * sizeof(double)) : 0;
   const size_t o_ec = d.reid ? carve_b(S * D * T * sizeof(double)) : 0;
   const size_t o_emb = d.reid ? carve_b(S * T * F * sizeof(double)) : 0;
   const size_t o_rec = d.reid ? carve_b(S * D * 2 * sizeof(int)) : 0;
@@ -1300,7 +1302,7 @@ int bx_boost_create(const bx_boost_config* c, bx_boost** out) {
   d.order = (int*)(base + o_ord);
   d.tb = (double*)(base + o_tb);
   d.cost_g = need_g ? (double*)(base + o_cg) : nullptr;
-  d.e_g = need_g ? (double*)(base + o_eg) : nullptr;
+  d.e_g = need_eg ? (double*)(base + o_eg) : nullptr;
   d.ec = d.reid ? (double*)(base + o_ec) : nullptr;
   d.emb = d.reid ? (double*)(base + o_emb) : nullptr;
   d.rec = d.reid ? (int*)(base + o_rec) : nullptr;

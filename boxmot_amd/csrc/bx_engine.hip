@@ -1983,22 +1983,30 @@ int bx_record_error(int code, const char* msg) { return set_err(code, msg); }
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) that never lowers a kernel's limit: engines of
 // different capacities share the kernels, and a later, smaller engine must not shrink the limit
-// an earlier one launches with (shared by every translation unit of the library)
+// an earlier one launches with (shared by every translation unit of the library).  The attribute
+// belongs to the current device, so the cache is keyed by (device, kernel).
 hipError_t bx_lds_attr(const void* kern, size_t bytes) {
+  struct Entry {
+    int dev;
+    const void* kern;
+    size_t bytes;
+  };
   static std::mutex mu;
-  static std::vector<std::pair<const void*, size_t>> done;
+  static std::vector<Entry> done;
+  int dev = 0;
+  if (const hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
   std::lock_guard<std::mutex> lk(mu);
   for (auto& d : done)
-    if (d.first == kern) {
-      if (d.second >= bytes) return hipSuccess;
+    if (d.dev == dev && d.kern == kern) {
+      if (d.bytes >= bytes) return hipSuccess;
       const hipError_t e =
           hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-      if (e == hipSuccess) d.second = bytes;
+      if (e == hipSuccess) d.bytes = bytes;
       return e;
     }
   const hipError_t e =
       hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  if (e == hipSuccess) done.emplace_back(kern, bytes);
+  if (e == hipSuccess) done.push_back({dev, kern, bytes});
   return e;
 }
 
