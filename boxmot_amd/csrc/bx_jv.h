@@ -541,14 +541,40 @@ __device__ __forceinline__ double swap_min(double r, bool half) {
   const double y = __longlong_as_double(((long long)h1 << 32) | a1);
   return fmin(x, y);
 }
+// a row rotation of an fp64 within rows of 16: every lane's source is valid, so no old value is
+// needed (mov_dpp: the compiler does not copy the destination first)
+template <int CTRL>
+__device__ __forceinline__ double ror_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 __device__ __forceinline__ double wave_min_bfly(double r) {
-  r = fmin(r, dpp_d<0x128, 0xf, 0xf>(r, r));
-  r = fmin(r, dpp_d<0x124, 0xf, 0xf>(r, r));
-  r = fmin(r, dpp_d<0x122, 0xf, 0xf>(r, r));
-  r = fmin(r, dpp_d<0x121, 0xf, 0xf>(r, r));
+  r = fmin(r, ror_d<0x128>(r));
+  r = fmin(r, ror_d<0x124>(r));
+  r = fmin(r, ror_d<0x122>(r));
+  r = fmin(r, ror_d<0x121>(r));
   r = swap_min(r, false);
   r = swap_min(r, true);
   return rl_d(r, 0);
+}
+// two independent wave minima, level by level (the two chains interleave)
+__device__ __forceinline__ void wave_min_bfly2(double& a, double& b) {
+  a = fmin(a, ror_d<0x128>(a));
+  b = fmin(b, ror_d<0x128>(b));
+  a = fmin(a, ror_d<0x124>(a));
+  b = fmin(b, ror_d<0x124>(b));
+  a = fmin(a, ror_d<0x122>(a));
+  b = fmin(b, ror_d<0x122>(b));
+  a = fmin(a, ror_d<0x121>(a));
+  b = fmin(b, ror_d<0x121>(b));
+  a = swap_min(a, false);
+  b = swap_min(b, false);
+  a = swap_min(a, true);
+  b = swap_min(b, true);
+  a = rl_d(a, 0);
+  b = rl_d(b, 0);
 }
 
 // Cost loads of the register-resident solver from address space AS (0: generic, 1: global,

@@ -504,12 +504,6 @@ __device__ int pool_alloc(SsTrk& t, int VP) {
 }
 
 // ---- the match kernel's code generation ---------------------------------------------------
-#ifndef SS_TAB_HELPERS  // the match kernel's two helper waves work on the first-step tables
-#define SS_TAB_HELPERS 0
-#endif
-#ifndef SS_TAB_RATIO  // the LSAP's first-step table when R * SS_TAB_RATIO >= CC (0: never)
-#define SS_TAB_RATIO 0
-#endif
 #ifndef SS_MATCH_ATTR  // everything inlined: a call left by the inliner keeps its frame in scratch
 #define SS_MATCH_ATTR __attribute__((flatten))
 #endif
@@ -1010,17 +1004,6 @@ struct LsapJob {
   int R, CC, tr, kind, np;
   int flag;
 };
-// The first-step table of an LSAP (see lsap_wave), computed by the solver wave and the match
-// kernel's two helper waves in 64-row groups: tickets from ctr = epoch << 48 | groups << 32 |
-// next group (a ticket at or past the group count is void; a valid ticket's job cannot change
-// before its group is done, so its parameters are read after taking it); a finished group stamps
-// its job's epoch into gdone (one writer per group: no count to get wrong).  Epoch 0xffff: exit.
-struct TabJob {
-  double max_d;
-  int R, CC, kind, tr;
-  unsigned long long ctr;
-  int gdone[16];  // group g of the job with epoch e is done when gdone[g] == e
-};
 struct SsCtx {
   const SsDev& g;
   SsWs& w;
@@ -1040,149 +1023,73 @@ struct SsCtx {
   double* ks;   // match kernel: sort-key scratch (LDS)
   int* cidx;    // match kernel: the solver's column indices (LDS, 2048 ints)
   struct LsapJob* job;  // match kernel: the hand-off to its solver wave
-  TabJob* tab;          // match kernel: the first-step table's work queue (solver + helpers)
-  unsigned tep;         // match kernel, solver wave: the last table epoch posted
   __device__ const double* det(int i) const { return w.dt + (size_t)w.dord[i] * DTW; }
   __device__ int det_in(int i) const { return (int)det(i)[6]; }
 };
 
-// The matrices of an LSAP (min_cost_matching): P in the solver's orientation and its transpose
-// PT, with their leading dimensions — derived from the kernel argument in the wave that reads
-// them, so the loads compile to global (not flat) memory instructions, whose waits do not also
-// wait for LDS.  kind 0: the gated cost by cascade rank (ss_cost_kernel's cfull / cfullT); 1: the
-// IoU cost by list position (cost / its transpose).
-__device__ __forceinline__ void lsap_mats(const SsDev& g, int seq, int kind, bool tr,
-                                          const double*& P, const double*& PT, int& ld, int& ldT) {
-  if (kind == 0) {
-    const double* a = g.cfull + (size_t)seq * g.T * g.D;
-    const double* b = g.cfullT + (size_t)seq * g.D * g.T;
-    P = tr ? b : a;
-    PT = tr ? a : b;
-  } else {
-    const double* io = g.cost + (size_t)seq * 4 * g.T * g.D;
-    P = tr ? io + (size_t)g.T * g.D : io;
-    PT = tr ? io : io + (size_t)g.T * g.D;
-  }
-  ld = tr ? g.T : g.D;
-  ldT = tr ? g.D : g.T;
+// The matrix of an LSAP (min_cost_matching) in the solver's orientation — derived from the kernel
+// argument in the wave that reads it, so the loads compile to global (not flat) memory
+// instructions, whose waits do not also wait for LDS.  kind 0: the gated cost by cascade rank
+// (ss_cost_kernel's cfull / cfullT); 1: the IoU cost by list position (cost / its transpose).
+__device__ __forceinline__ const double* lsap_mat(const SsDev& g, int seq, int kind, bool tr) {
+  if (kind == 0)
+    return tr ? g.cfullT + (size_t)seq * g.D * g.T : g.cfull + (size_t)seq * g.T * g.D;
+  const double* io = g.cost + (size_t)seq * 4 * g.T * g.D;
+  return tr ? io + (size_t)g.T * g.D : io;
 }
 
-// One 64-row group of an LSAP's first-step table, lane per row (see lsap_wave): the minimum of
-// the row's unclamped entries and the column at it when it is the only one and at most max_d
-// (clamping then changes neither; above max_d every entry clamps to one value: a tie), else -2.
-// A NaN entry is never the minimum nor equal to it, as in the solver's first step.  Four
-// independent chains over the columns (u mod 4), merged at the end; 32 loads in flight.
-__device__ __forceinline__ void tab_rows(SsWs& w, const double* __restrict__ PT,
-                                         const int* roff, const int* cidx, int R, int CC, int ld,
-                                         int ldT, double max_d, int grp, int lane) {
-  const int r = 64 * grp + lane;
-  const double* base = PT + (r < R ? roff[r] / ld : 0);
-  double m[4] = {INF, INF, INF, INF};
-  int a[4] = {-1, -1, -1, -1};
-  bool tie[4] = {false, false, false, false};
-  bool big = true;  // every entry above max_d (a NaN is not): all clamp to one value
-  for (int j0 = 0; j0 < CC; j0 += 32) {
-    double e[32];
-#pragma unroll
-    for (int u = 0; u < 32; u++) {
-      const int j = j0 + u < CC ? j0 + u : CC - 1;
-      e[u] = base[(size_t)cidx[j] * ldT];
-    }
-#pragma unroll
-    for (int u = 0; u < 32; u++) {
-      if (j0 + u >= CC) break;
-      const int c = u & 3;
-      big &= e[u] > max_d;
-      if (e[u] < m[c]) m[c] = e[u], a[c] = j0 + u, tie[c] = false;
-      else if (e[u] == m[c]) tie[c] = true;
-    }
-  }
-  double mm = m[0];
-  int aa = a[0];
-  bool tt = tie[0];
-#pragma unroll
-  for (int c = 1; c < 4; c++) {
-    if (m[c] < mm) mm = m[c], aa = a[c], tt = tie[c];
-    else if (m[c] == mm) tt = true;
-  }
-  if (r < R) {
-    w.u[r] = mm;
-    w.col4row[r] = (!tt && mm <= max_d && mm < INF) ? aa : (big ? -3 : -2);
-  }
-}
-
-// take table tickets until a void one; returns.  The ticket is made wave-uniform by readfirstlane
-// (lane 0 took it; every lane is active here), so the exit test is a scalar branch.
-__device__ __forceinline__ void tab_work(const SsDev& g, int seq, SsWs& w, TabJob* tj,
-                                         const int* roff, const int* cidx, int lane) {
+// The match kernel's two waves hand LSAPs over through LDS flags.  A wait that outlasts any
+// legitimate LSAP (SS_SPIN_TICKS of the 100 MHz real-time counter: 2 s) latches BX_ERR_INVALID
+// in the engine status and gives up, so a fault in either wave ends the launch with an error
+// instead of leaving the queue spinning.
+#ifndef SS_SPIN_TICKS
+#define SS_SPIN_TICKS 200000000ull
+#endif
+// wait until *flag != v (want_ne) or == v (!want_ne); returns the value seen, or v after a timeout
+__device__ __forceinline__ int lds_flag_wait(int* flag, int v, bool want_ne, int* status,
+                                             bool& timed_out) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    // every lane takes part (lane 0 adds 1, the rest 0): no lane-dependent branch around the
-    // atomic, so the compiler keeps the loop uniform; lane 0's value is the ticket
-    const unsigned long long t = __hip_atomic_fetch_add(&tj->ctr, lane == 0 ? 1ull : 0ull,
-                                                        __ATOMIC_ACQ_REL,
-                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(t >> 32), 0);
-    const unsigned lo = __builtin_amdgcn_readlane((unsigned)(t & 0xffffffffull), 0);
-    const int ng = (int)(hi & 0xffffu), gi = (int)lo;
-    if (gi >= ng) return;
-    const double* P;
-    const double* PT;
-    int ld, ldT;
-    const int R = tj->R, CC = tj->CC;
-    const double max_d = tj->max_d;
-    lsap_mats(g, seq, tj->kind, tj->tr != 0, P, PT, ld, ldT);
-    tab_rows(w, PT, roff, cidx, R, CC, ld, ldT, max_d, gi, lane);
-    wsync();
-    __hip_atomic_store(&tj->gdone[gi], (int)(hi >> 16), __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-}
-
-// the match kernel's helper waves: table groups of every posted LSAP until the exit epoch
-__device__ __forceinline__ void tab_server(const SsDev& g, int seq, SsWs& w, TabJob* tj,
-                                           const int* roff, const int* cidx, int lane) {
-  unsigned seen = 0;
-  for (;;) {
-    unsigned ep;
-    while ((ep = __builtin_amdgcn_readfirstlane((unsigned)(__hip_atomic_load(
-                &tj->ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 48))) == seen)
-      __builtin_amdgcn_s_sleep(2);
-    seen = ep;
-    if (seen == 0xffffu) return;
-    tab_work(g, seq, w, tj, roff, cidx, lane);
+    const int f = (int)__builtin_amdgcn_readfirstlane(
+        (unsigned)__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if ((f != v) == want_ne) return f;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > SS_SPIN_TICKS) {
+      if ((threadIdx.x & 63) == 0) atomicExch(status, (int)BX_ERR_INVALID);
+      timed_out = true;
+      return v;
+    }
+    __builtin_amdgcn_s_sleep(1);
   }
 }
 
 // scipy.optimize.linear_sum_assignment (Crouse's shortest augmenting path, rectangular),
 // wave-parallel, in the solver's orientation: R x CC, R <= CC (`tr`: the caller's matrix was
 // transposed to get there, so the output pairs are argsorted by the original row).  Entry (r, j)
-// is P[roff[r] + cidx[j]], clamped at max_d (min_cost_matching's clamp: above max_d ->
-// max_d + 1e-5; max_d = INF: none), read straight from the stage's matrix — no per-level copy.
+// is P[roff[r] + cidx[j]], read straight from the stage's matrix — no per-level copy — which
+// ss_cost_kernel stores with min_cost_matching's clamp already applied (above max_d -> max_d +
+// 1e-5, max_d being the stage's: every detection takes part in one stage only).  Rows are read by
+// buffer loads: the row's byte offset in a scalar register, the lane's column offsets in vector
+// registers, no per-load address arithmetic.
 //
 // Lane l owns the columns j = l + 64 q (q < LQ, CC <= 64 LQ): their matrix index (cidx, or j
-// itself when !IDX), v[j] and an assigned bit stay in registers.  Each row's first Dijkstra step — where most rows end — runs
-// from registers: relax against v, wave minimum, scipy's tie rule (the last unassigned column at
-// the minimum in `remaining` order, else the first; fresh positions are CC-1-j, so the smallest
-// unassigned j, else the largest j), assignment.  The next row's costs are loaded meanwhile.
-// Only a row whose minimum lands on an assigned column writes the search state out (rem / pos /
-// SC / spc / path in LDS) and continues Crouse's search as scipy does; u[cur] is 0 before row cur
-// (only rows already assigned are ever on a path).  Pairs sorted by row into w.rows / w.cols.
+// itself when !IDX), v[j] and an assigned bit stay in registers.  Each row's first Dijkstra step —
+// where most rows end — runs from registers: relax against v, wave minimum, scipy's tie rule (the
+// last unassigned column at the minimum in `remaining` order, else the first; fresh positions are
+// CC-1-j, so the smallest unassigned j, else the largest j), assignment.  Only a row whose minimum
+// lands on an assigned column writes the search state out (rem / pos / SC / spc / path in LDS)
+// and continues Crouse's search as scipy does; u[cur] is 0 before row cur (only rows already
+// assigned are ever on a path).  Pairs sorted by row into w.rows / w.cols.
 //
-// First steps from a table (when the rows are many for their width): every row's first Dijkstra
-// step at v = 0 is computed up front, one lane per row over the transposed matrix PT (the rows
-// of a level are consecutive ranks / list positions, so a load is coalesced) — its minimum, and
-// the column at it when that column is the only one and the row has no NaN.  v only ever
-// decreases, on the SC columns of rows whose search goes on (`chg`), which only raises other
-// entries of a later row's first step: so unless its column's v changed, a row's first step at
-// the current v is its table entry, and when that column is unassigned the row is assigned
-// without loading its costs.  Any other row loads its costs and takes the step below.  Table
-// entries park in u (scipy's u[cur] = minVal for a row that ends on its first step; a row's u is
-// never read before the row is reached) and col4row (never read before the row is assigned).
+// Rows are taken in pairs (LQ <= 16): a row's first step depends on the rows before it only
+// through v — which a row ending on its first step leaves unchanged — and through the assigned
+// bits, which only its decision (ballots, tie rule) reads.  So both rows of a pair are relaxed
+// and reduced against the same v (two independent chains for the scheduler to interleave), then
+// decided in order; when the first row's search goes on (v changes), the second is reloaded and
+// relaxed again first: every row is decided exactly as the sequential solver decides it.  The
+// next pair's costs are in flight meanwhile.
 template <int LQ, bool IDX>
 __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P, const int* roff,
-                                         const int* cidx, double max_d, int R, int CC, bool tr,
-                                         const double* __restrict__ PT, int ld, int ldT,
-                                         int kind) {
+                                         const int* cidx, double max_d, int R, int CC, bool tr) {
   SsWs& w = x.w;
   const int lane = x.lane;
 #ifdef BX_PHASE_TIMING
@@ -1190,72 +1097,9 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
   const int seq = x.seq;
   SCOUNT(7, R);
   SCOUNT(8, CC);
-  unsigned long long t_slow = 0, t_s0 = 0, t_all = SS_NOW(), t_wait = 0, t_bfly = 0, t_ballot = 0,
-                     t_sink = 0;
+  unsigned long long t_slow = 0, t_all = SS_NOW();
 #endif
-  const double clampv = max_d + 1e-5;
-  // the table pays when a row's full first step (~1.8 k cycles) outweighs its share of the
-  // table's CC-column sweep per 64 rows
-  const bool TB = SS_TAB_RATIO > 0 && IDX && LQ <= 16 && R >= 2 && R * SS_TAB_RATIO >= CC;
-  if (TB && !SS_TAB_HELPERS) {  // the solver wave alone, 64 rows at a time
-    for (int grp = 0; grp * 64 < R; grp++)
-      tab_rows(w, PT, roff, cidx, R, CC, ld, ldT, max_d, grp, lane);
-    wsync();
-  } else if (TB) {  // posted to the helper waves, worked on here too, waited for
-    TabJob* tj = x.tab;
-    const int ng = (R + 63) / 64;
-    const unsigned ep = ++x.tep;
-    if (lane == 0) {
-      tj->max_d = max_d;
-      tj->R = R;
-      tj->CC = CC;
-      tj->kind = kind;
-      tj->tr = tr;
-    }
-    wsync();
-    if (lane == 0)
-      __hip_atomic_store(&tj->ctr, (unsigned long long)ep << 48 | (unsigned long long)ng << 32,
-                         __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    tab_work(x.g, x.seq, w, tj, roff, cidx, lane);
-    // every group stamped with this epoch (lane g checks group g; ng <= 16)
-    while (__ballot(lane < ng && __hip_atomic_load(&tj->gdone[lane < 16 ? lane : 0],
-                                                   __ATOMIC_ACQUIRE,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP) != (int)ep))
-      __builtin_amdgcn_s_sleep(1);
-
-  } else {
-    for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
-  }
-  if (TB) {
-#ifdef SS_TAB_VERIFY  // diagnostic builds: the table re-derived here, row by row, must agree
-    for (int r0 = 0; r0 < R; r0 += 64) {
-      const int r = r0 + lane;
-      if (r >= R) continue;
-      const double* base = PT + roff[r] / ld;
-      double mm = INF;
-      int aa = -1;
-      bool tt = false;
-      bool big = true;
-      for (int j = 0; j < CC; j++) {
-        const double e = base[(size_t)cidx[j] * ldT];
-        big &= e > max_d;
-        if (e < mm) mm = e, aa = j, tt = false;
-        else if (e == mm) tt = true;
-      }
-      const int code = (!tt && mm <= max_d && mm < INF) ? aa : (big ? -3 : -2);
-      const double um = w.u[r];
-      const int uc = w.col4row[r];
-      if (!(um == mm || (um != um && mm != mm)) || uc != code) {
-        atomicExch(x.g.status, 9000 + (uc == code ? 1 : 2));
-        if (atomicAdd(&x.g.status[1], 1) < 24)
-          printf("TABV seq %d R %d CC %d ld %d ldT %d r %d roff %d: table (%g, %d) "
-                 "recomputed (%g, %d)\n",
-                 x.seq, R, CC, ld, ldT, r, roff[r], um, uc, mm, code);
-      }
-    }
-#endif
-    wsync();
-  }
+  for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
   for (int j = lane; j < CC; j += 64) w.path[j] = -1, w.row4col[j] = -1;
   unsigned cb[LQ];  // byte offset of the lane's column q in a row (column 0's past CC)
   double vr[LQ];    // v[j]; -INF past CC, so those columns relax to +INF
@@ -1267,140 +1111,62 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     vr[q] = j < CC ? 0.0 : -INF;
   }
   wsync();
-  // raw loads, unconditional (in-row offsets): clamped where used, so a load is waited for only
-  // when its value is needed
+  // the matrix as a buffer (its base made provably wave-uniform: no waterfall loops)
+  const unsigned long long pb = (unsigned long long)P;
+  // (each half widened from unsigned: readfirstlane returns int, which would sign-extend)
+  const unsigned long long pbu =
+      (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(pb >> 32)) << 32 |
+      (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)pb);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)pbu, (short)0, (int)__builtin_amdgcn_readfirstlane((unsigned)(8 * x.g.T * x.g.D)),
+      0x00020000);
+  auto ld_elem = [&](int roff_r, int q) {  // row element offset roff_r (wave-uniform), slot q
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                          rsrc, cb[q], __builtin_amdgcn_readfirstlane(8 * roff_r), 0));
+  };
+  // raw loads, unconditional: a load is waited for only when its value is needed
   auto load_row = [&](int off, double* dst) {
-    const char* base = (const char*)(P + off);
 #pragma unroll
-    for (int q = 0; q < LQ; q++) dst[q] = *(const double*)(base + cb[q]);
+    for (int q = 0; q < LQ; q++) dst[q] = ld_elem(off, q);
   };
-  // the next row's loads are issued during this one's reductions, except at LQ = 32 (IoU stage of
-  // more than 1024 candidates, rare) where the registers would not hold both rows
-  // (with a table only the rows it cannot settle load their costs, on demand)
-  const bool PF = LQ <= 16 && !TB;
-  double nx[LQ];
-  int off1 = R > 1 ? roff[1] : 0;
-  if (PF && R > 0) load_row(roff[0], nx);
-  unsigned chg = 0;  // columns whose v changed: the SC bits of every search that went on
-  // v decreases in exact arithmetic, but a rounded reduced cost can make a search's last minimum
-  // fall below an earlier one and raise a v[j] by an ulp: from then on a later row's other
-  // entries may drop, so the table's first steps are not trusted for the rest of this LSAP
-  bool vpos = false;
-  int tcode = -4;    // the table's column codes of the current 64 rows, lane l row 64k + l
-  // with a table: the rows it cannot settle (code -2) are known ahead, so the next such row of
-  // the current 64 has its costs in flight in nx meanwhile (pf_row; -1: none)
-  int pf_row = -1;
-  auto prefetch_from = [&](int from) {
-    const unsigned long long m =
-        __ballot(tcode == -2) & (((from & 63) == 0) ? ~0ull : (~0ull << (from & 63)));
-    const int r = m ? (from & ~63) + (__ffsll((long long)m) - 1) : R;
-    if (r < R) {  // (lanes past R hold -4, never -2: r < R by construction)
-      pf_row = r;
-      load_row(roff[pf_row], nx);
-    }
-  };
-  for (int cur = 0; cur < R; cur++) {
-#ifdef BX_PHASE_TIMING
-    unsigned long long t_r0 = SS_NOW();
-#endif
-    if (TB) {
-      if ((cur & 63) == 0) {
-        tcode = cur + lane < R ? w.col4row[cur + lane] : -4;  // -4: past the last row
-        if (pf_row < cur) prefetch_from(cur);
-      }
-      int jt = vpos ? -2 : rl_i(tcode, cur & 63);
-      if (jt == -3) {
-        // every entry clamps to clampv: the first step's minimum set is the columns whose
-        // clampv - v[j] rounds to clampv (v only decreases, so no entry is below it), and scipy
-        // takes the smallest unassigned one among them (the last in its fresh `remaining`
-        // order), when there is one (columns past CC have v = -INF)
-        jt = -2;
+  // scipy's minVal + cost - u[cur] - v[j] with minVal = u[cur] = 0 (up to the sign of a zero,
+  // which no comparison and no later sum can tell).  A NaN cost stays NaN here and loses every
+  // comparison below, as the INF that scipy's `r < INF` test would make of it.  Returns the
+  // lane's minimum.
+  auto relax = [&](const double* raw, double* rv) {
 #pragma unroll
-        for (int q = LQ - 1; q >= 0; q--) {
-          const unsigned long long fr =
-              __ballot(!((asg >> q) & 1u) && clampv - vr[q] == clampv);
-          if (fr) jt = 64 * q + (__ffsll((long long)fr) - 1);
-        }
-        if (jt >= 0 && lane == 0) w.u[cur] = clampv;
-      } else if (jt >= 0 && ((rl_i((int)(asg | chg), jt & 63) >> (jt >> 6)) & 1u)) {
-        jt = -2;
-      }
-      if (jt >= 0) {
-        if (lane == (jt & 63)) asg |= 1u << (jt >> 6);
-        if (lane == 0) {  // u[cur]: the table's minimum (or clampv)
-          w.row4col[jt] = cur;
-          w.col4row[cur] = jt;
-        }
-#ifdef BX_PHASE_TIMING
-        SCOUNT(16, 1);
-#endif
-        continue;
-      }
-      if (pf_row != cur) load_row(roff[cur], nx);
-      pf_row = -1;
-    } else if (!PF) {
-      load_row(roff[cur], nx);
-    }
-    // scipy's minVal + cost - u[cur] - v[j] with minVal = u[cur] = 0 (up to the sign of a zero,
-    // which no comparison and no later sum can tell).  A NaN cost stays NaN here and loses every
-    // comparison below, as the INF that scipy's `r < INF` test would make of it.
-    double rv[LQ];
-#pragma unroll
-    for (int q = 0; q < LQ; q++) rv[q] = (nx[q] > max_d ? clampv : nx[q]) - vr[q];
+    for (int q = 0; q < LQ; q++) rv[q] = raw[q] - vr[q];
     double lmin = rv[0];
 #pragma unroll
     for (int q = 1; q < LQ; q++) lmin = fmin(lmin, rv[q]);
-#ifdef BX_PHASE_TIMING
-    asm volatile("" ::"v"(lmin));
-    {
-      const unsigned long long t = SS_NOW();
-      t_wait += t - t_r0;
-      t_r0 = t;
-    }
-#endif
-    if (PF && cur + 1 < R) {  // the next row in flight during this one's reductions
-      load_row(off1, nx);
-      off1 = cur + 2 < R ? roff[cur + 2] : 0;
-    }
-    if (TB && ((cur + 1) & 63) != 0) prefetch_from(cur + 1);
-    const double m0 = wave_min_bfly(lmin);
-#ifdef BX_PHASE_TIMING
-    asm volatile("" ::"v"(m0));
-    {
-      const unsigned long long t = SS_NOW();
-      t_bfly += t - t_r0;
-      t_r0 = t;
-    }
-#endif
+    return lmin;
+  };
+  bool bad = false;
+  // Row cur from its first step (rv, wave minimum m0): assigned when the step ends on an
+  // unassigned column, else Crouse's search continued.  Returns true when v changed (the search
+  // went on).
+  auto finish_row = [&](int cur, double* rv, double m0) -> bool {
     if (!(m0 < INF)) {  // infeasible (cannot happen with finite costs)
-      if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
-#ifdef SS_TAB_VERIFY
-      if (lane == 0 && atomicAdd(&x.g.status[1], 1) < 24)
-        printf("INFEAS seq %d R %d CC %d TB %d cur %d m0 %g\n", x.seq, R, CC, (int)TB, cur, m0);
-#endif
-      return 0;
+      bad = true;
+      return false;
     }
-    // the columns at the minimum, one wave mask per q
-    int cnt = 0, q0 = 0;
-    unsigned long long e0 = 0;
+    // the columns at the minimum: a wave mask per q (counted), their union, and per lane the
+    // slot at the minimum (meaningful where the minimum is unique)
+    int cnt = 0, qi = 0;
+    unsigned long long un0 = 0;
 #pragma unroll
     for (int q = 0; q < LQ; q++) {
-      const unsigned long long e = __ballot(rv[q] == m0);
+      const bool eq = rv[q] == m0;
+      const unsigned long long e = __ballot(eq);
       cnt += __popcll(e);
-      if (e) q0 = q, e0 = e;
+      un0 |= e;
+      qi = eq ? q : qi;
     }
-#ifdef BX_PHASE_TIMING
-    asm volatile("" ::"s"(cnt));
-    {
-      const unsigned long long t = SS_NOW();
-      t_ballot += t - t_r0;
-      t_r0 = t;
-    }
-#endif
     int j0;
     bool sink;
     if (cnt == 1) {  // a unique minimum (the usual case)
-      const int L = __ffsll((long long)e0) - 1;
+      const int L = __ffsll((long long)un0) - 1;
+      const int q0 = rl_i(qi, L);
       j0 = L + 64 * q0;
       sink = !((rl_i((int)asg, L) >> q0) & 1);
     } else {  // scipy's tie rule over the lanes
@@ -1422,14 +1188,11 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
         w.row4col[j0] = cur;
         w.col4row[cur] = j0;
       }
-#ifdef BX_PHASE_TIMING
-      t_sink += SS_NOW() - t_r0;
-#endif
-      continue;
+      return false;
     }
 #ifdef BX_PHASE_TIMING
     SCOUNT(9, 1);
-    t_s0 = SS_NOW();
+    const unsigned long long t_s0 = SS_NOW();
 #endif
     // The search continues as scipy's does, its per-column state in registers: spc (rv, NaN as
     // INF), the SC bits, v; `remaining` (rem / pos, for the tie rule), path and the visited rows
@@ -1462,7 +1225,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     nvis = 1;
     while (sk == -1) {
       const double ui = w.u[i];
-      const char* rowi = (const char*)(P + roff[i]);
+      const int roff_i = roff[i];
       double m = INF;
       constexpr int QB = LQ < 8 ? LQ : 8;  // loads in flight per lane
 #pragma unroll
@@ -1470,8 +1233,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
         double cv[QB];
 #pragma unroll
         for (int u = 0; u < QB; u++) {
-          const double e = *(const double*)(rowi + cb[q0 + u]);
-          cv[u] = e > max_d ? clampv : e;
+          cv[u] = ld_elem(roff_i, q0 + u);  // (stored clamped)
         }
 #pragma unroll
         for (int u = 0; u < QB; u++) {
@@ -1487,8 +1249,8 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       }
       m = wave_min_bfly(m);
       if (!(m < INF)) {  // infeasible (cannot happen with finite costs)
-        if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
-        return 0;
+        bad = true;
+        return false;
       }
       int c1 = 0, qs = 0;
       unsigned long long es = 0;
@@ -1547,13 +1309,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     if (lane == 0) w.u[cur] = 0.0 + minVal;
 #pragma unroll
     for (int q = 0; q < LQ; q++)
-      if ((sc >> q) & 1u) {
-        const double dv = minVal - rv[q];
-        vr[q] -= dv;
-        if (dv != 0.0) chg |= 1u << q;  // v[j] changed (a zero step leaves it as it was)
-        vpos |= vr[q] > 0.0;
-      }
-    vpos = __any(vpos);
+      if ((sc >> q) & 1u) vr[q] -= minVal - rv[q];
     wsync();
     if (lane == 0) {
       int jj = sk;
@@ -1567,18 +1323,65 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       }
     }
     if (lane == (sk & 63)) asg |= 1u << (sk >> 6);
+    wsync();
 #ifdef BX_PHASE_TIMING
     t_slow += SS_NOW() - t_s0;
 #endif
-    wsync();
+    return true;
+  };
+  if constexpr (LQ <= 16) {
+    // Rows in pairs: the pair's two rows relaxed against the same v and their wave minima taken
+    // together (two independent chains), then decided in order — the second one after the first
+    // one's assignment, or relaxed again (its costs reloaded) when the first one's search changed
+    // v.  The next pair's costs are in flight meanwhile: two register pairs alternate (an
+    // unrolled pair of pair-steps), written only by unconditional loads (rows past the last one
+    // re-read it), so no register row is ever merged or copied at a branch.
+    double A0[LQ], A1[LQ], B0[LQ], B1[LQ];
+    const int rlast = R - 1;
+    auto roff_c = [&](int r) { return roff[r < rlast ? r : rlast]; };
+    auto pair = [&](int cur, double* r0, double* r1) {
+      double m0 = relax(r0, r0), m1 = relax(r1, r1);
+      wave_min_bfly2(m0, m1);
+      const bool chg = finish_row(cur, r0, m0);
+      if (cur + 1 < R && !bad) {
+        double m1b = m1;
+        if (chg) {  // v changed: row cur+1 again
+          load_row(roff_c(cur + 1), r1);
+          m1b = wave_min_bfly(relax(r1, r1));
+        }
+        finish_row(cur + 1, r1, m1b);
+      }
+    };
+    if (R > 0) {
+      load_row(roff_c(0), A0);
+      load_row(roff_c(1), A1);
+    }
+    for (int cur = 0; cur < R && !bad;) {
+      load_row(roff_c(cur + 2), B0);
+      load_row(roff_c(cur + 3), B1);
+      pair(cur, A0, A1);
+      cur += 2;
+      if (cur >= R || bad) break;
+      load_row(roff_c(cur + 2), A0);
+      load_row(roff_c(cur + 3), A1);
+      pair(cur, B0, B1);
+      cur += 2;
+    }
+  } else {  // LQ = 32 (IoU stage of more than 1024 candidates, rare): one row at a time
+    double A[LQ], C[LQ];
+    for (int cur = 0; cur < R && !bad; cur++) {
+      load_row(roff[cur], C);
+      const double m0 = wave_min_bfly(relax(C, A));
+      finish_row(cur, A, m0);
+    }
+  }
+  if (bad) {
+    if (lane == 0) atomicExch(x.g.status, (int)BX_ERR_INVALID);
+    return 0;
   }
   wsync();
 #ifdef BX_PHASE_TIMING
   SCOUNT(10, t_slow);
-  SCOUNT(12, t_wait);
-  SCOUNT(13, t_bfly);
-  SCOUNT(14, t_ballot);
-  SCOUNT(15, t_sink);
   SCOUNT(11, SS_NOW() - t_all);
 #endif
   // every row is assigned a column in [0, CC) by now; a value outside it would be an engine
@@ -1587,11 +1390,6 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     const int c = w.col4row[q];
     if (c < 0 || c >= CC) {
       atomicExch(x.g.status, (int)BX_ERR_INVALID);
-#ifdef SS_TAB_VERIFY
-      if (atomicAdd(&x.g.status[1], 1) < 24)
-        printf("GUARD seq %d R %d CC %d tr %d TB %d row %d col4row %d\n", x.seq, R, CC, (int)tr,
-               (int)TB, q, c);
-#endif
       w.col4row[q] = 0;
     }
   }
@@ -1676,6 +1474,9 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
         e = 1.0 - ai / ((ab + q[2] * q[3]) - ai);
       }
       e = enhance(t, q, e);
+      // stored with min_cost_matching's clamp (linear_assignment.py:67) at the IoU stage's
+      // max_iou_distance, as the solver reads it
+      if (e > g.max_iou) e = g.max_iou + 1e-5;
       io[(size_t)k * g.D + c] = e;
       ioT[(size_t)c * g.T + k] = e;
     }
@@ -1738,6 +1539,10 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
   const double* nnd = g.nnd + ((size_t)seq * g.T + slot) * g.D;
   double* out = g.cfull + ((size_t)seq * g.T + rk) * g.D;
   double* outT = g.cfullT + (size_t)seq * g.D * g.T + rk;
+  // min_cost_matching's clamp (linear_assignment.py:67) applied here, with the max_distance of the
+  // one cascade a detection takes part in: stage 1 (high confidence) thr * 0.8, stage 2 (medium)
+  // thr (tracker.py:206-233; thr after ss_pre_kernel's crowd-mode adjustment)
+  const double thr = g.sqd[(size_t)seq * 2];
   for (int c = lane; c < nk; c += 64) {
     const double* d = dt + (size_t)dord[c] * DTW;
     double z[4];
@@ -1769,7 +1574,9 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
     if (hs) v *= 0.97;
     if (ls) v *= 1.05;
     if (g.idw > 0) v *= (1.0 - pb);
-    const double e = enhance(t, d, v);
+    double e = enhance(t, d, v);
+    const double md = d[4] >= g.thi ? thr * 0.8 : thr;
+    if (e > md) e = md + 1e-5;
     out[c] = e;
     outT[(size_t)c * g.T] = e;
   }
@@ -1782,23 +1589,18 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
 __device__ __forceinline__ void lsap_server(SsCtx& x, LsapJob* jb, const int* roff,
                                             const int* cidx) {
   for (;;) {
-    int f;
-    while ((f = (int)__builtin_amdgcn_readfirstlane((unsigned)__hip_atomic_load(
-                &jb->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))) == 0)
-      __builtin_amdgcn_s_sleep(1);
-    if (f < 0) return;
+    bool to = false;
+    const int f = lds_flag_wait(&jb->flag, 0, true, x.g.status, to);
+    if (f < 0 || to) return;  // exit posted (the cascade always posts it last), or a timeout
     const double mx = jb->max_d;
     const int R = jb->R, CC = jb->CC, kind = jb->kind;
     const bool tr = jb->tr != 0;
-    const double* P;
-    const double* PT;
-    int ld, ldT;
-    lsap_mats(x.g, x.seq, kind, tr, P, PT, ld, ldT);
+    const double* P = lsap_mat(x.g, x.seq, kind, tr);
     const int np =
-        CC <= 256    ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT, kind)
-        : CC <= 512  ? lsap_wave<8, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT, kind)
-        : CC <= 1024 ? lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT, kind)
-                     : lsap_wave<32, true>(x, P, roff, cidx, mx, R, CC, tr, PT, ld, ldT, kind);
+        CC <= 256    ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr)
+        : CC <= 512  ? lsap_wave<8, true>(x, P, roff, cidx, mx, R, CC, tr)
+        : CC <= 1024 ? lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr)
+                     : lsap_wave<32, true>(x, P, roff, cidx, mx, R, CC, tr);
     if (x.lane == 0) jb->np = np;
     wsync();
     if (x.lane == 0) __hip_atomic_store(&jb->flag, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1834,9 +1636,8 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
   }
   int* roff = x.flt;   // the solver rows' element offsets into P (LDS)
   int* cidx = x.cidx;  // the solver columns' element indices (LDS)
-  const double* P;
-  const double* PT;  // the same matrix transposed: entry (r, j) at PT[cidx[j] * ldT + roff[r] / ld]
-  int ld, ldT;
+  const double* P = lsap_mat(g, x.seq, kind == M_GATED ? 0 : 1, tr);
+  const int ld = tr ? g.T : g.D;
   double mx;
 #ifdef BX_PHASE_TIMING
   const int seq = x.seq;
@@ -1850,21 +1651,12 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
     const int* li = tr ? ti : di;  // columns
     const int* oi = tr ? di : ti;  // rows
     const int* rk = x.rank;        // track list position -> cascade rank
-    P = tr ? g.cfullT + (size_t)x.seq * g.D * g.T : g.cfull + (size_t)x.seq * g.T * g.D;
-    PT = tr ? g.cfull + (size_t)x.seq * g.T * g.D : g.cfullT + (size_t)x.seq * g.D * g.T;
-    ld = tr ? g.T : g.D;
-    ldT = tr ? g.D : g.T;
     for (int o = lane; o < R; o += 64) roff[o] = (tr ? oi[o] : rk[oi[o]]) * ld;
     for (int c = lane; c < CC; c += 64) cidx[c] = tr ? rk[li[c]] : li[c];
     mx = max_d;
   } else {
     // ss_cost_kernel's iou_cost + _enhance_cost_matrix of (list position, sorted detection),
     // read in place; the clamp at max_iou_distance here
-    const double* io = g.cost + (size_t)x.seq * 4 * g.T * g.D;
-    P = tr ? io + (size_t)g.T * g.D : io;
-    PT = tr ? io : io + (size_t)g.T * g.D;
-    ld = tr ? g.T : g.D;
-    ldT = tr ? g.D : g.T;
     const int* li = tr ? ti : di;  // columns
     const int* oi = tr ? di : ti;  // rows
     for (int o = lane; o < R; o += 64) roff[o] = oi[o] * ld;
@@ -1898,10 +1690,9 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
     }
     wsync();
     if (lane == 0) __hip_atomic_store(&jb->flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (__builtin_amdgcn_readfirstlane((unsigned)__hip_atomic_load(
-               &jb->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0)
-      __builtin_amdgcn_s_sleep(1);
-    np_ = jb->np;
+    bool to = false;
+    lds_flag_wait(&jb->flag, 0, false, g.status, to);
+    np_ = to ? 0 : jb->np;  // (a timeout latched BX_ERR_INVALID: the frame is void)
   }
 #ifdef BX_PHASE_TIMING
   wsync();
@@ -2427,47 +2218,31 @@ __global__ void __launch_bounds__(64)
   SSTAMP(2);
 }
 
-// ss_match_kernel (one four-wave workgroup per sequence): the three matching stages of
+// ss_match_kernel (one two-wave workgroup per sequence): the three matching stages of
 // Tracker._enhanced_match (stage 1/2 costs gathered from ss_cost_kernel's matrix).  Wave 0 runs
 // the cascade and posts each LSAP (LsapJob) to wave 1, the solver, which keeps its own register
-// context; waves 2-3 serve the first-step tables when SS_TAB_HELPERS is set, else leave at once.
-// Hands the matches (fmt), the unmatched tracks (ffut) and detections (faud) to the next launches.
-__global__ void __launch_bounds__(256) SS_MATCH_ATTR
+// context.  Hands the matches (fmt), the unmatched tracks (ffut) and detections (faud) to the next
+// launches.
+__global__ void __launch_bounds__(128) SS_MATCH_ATTR
     ss_match_kernel(SsDev g, int seq0) {
   extern __shared__ __align__(16) char ss_lds[];
   __shared__ int srank[1024], sgpos[1024], sinset[1024];
   __shared__ int flt[2048], fld[1024];  // solver column indices; sorted-detection membership
   __shared__ int stsu[1024], sage[1024];
   __shared__ LsapJob job;
-  __shared__ TabJob tab;
   const int lane = threadIdx.x & 63, b = blockIdx.x, seq = seq0 + b;
   SsWs w;
   ws_carve(g, seq, w, ss_lds);
-  if (threadIdx.x == 0) {
-    job.flag = 0;
-    tab.ctr = 0;
-    for (int k = 0; k < 16; k++) tab.gdone[k] = 0;
-  }
-  __syncthreads();  // the only barrier of all four waves; from here each synchronises itself
+  if (threadIdx.x == 0) job.flag = 0;
+  __syncthreads();  // the only barrier of both waves; from here each synchronises itself
   // the LSAP's rows' offsets and columns' indices (written by the cascade wave, read by the
-  // solver and helper waves): sage and flt
+  // solver wave): sage and flt
   // the wave's role, wave-uniform (readfirstlane: scalar branches, no divergent-region masks)
   const int wid = (int)__builtin_amdgcn_readfirstlane((unsigned)(threadIdx.x >> 6));
-  if (wid >= 2) {  // the helper waves: first-step tables
-#if SS_TAB_HELPERS
-    tab_server(g, seq, w, &tab, sage, flt, lane);
-#endif
-    return;
-  }
   if (wid == 1) {  // the solver wave
     SsCtx xs{g, w, seq, lane, g.trk + (size_t)seq * g.T, g.sq + (size_t)seq * SQS,
              g.sqd + (size_t)seq * 2, g.lost + (size_t)seq * LOSTN, 0, 0, 0, 0};
-    xs.tab = &tab;
-    xs.tep = 0;
     lsap_server(xs, &job, sage, flt);
-    // the helpers' exit
-    if (lane == 0)
-      __hip_atomic_store(&tab.ctr, 0xffffull << 48, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     return;
   }
 #ifdef BX_PHASE_TIMING
@@ -2584,15 +2359,17 @@ __global__ void __launch_bounds__(256) SS_MATCH_ATTR
   // a track listed twice among stage 3's candidates can also be matched twice: the reference
   // updates it twice, in match order.  Later occurrences are flagged (negative position) and
   // listed after the matches; ss_update_kernel does the first ones, ss_post_kernel these in order.
+  // (a match is a repeat iff an earlier match has its track: the first match per list position
+  // by an LDS atomicMin table — the membership table is free by now — not a scan of the earlier
+  // matches per match, which at C4's ~470 matches was ~0.3 M cycles of the wave)
   int* dupl = w.mt + 2 * (g.D + 2);
+  int* first = sinset;
+  for (int p = lane; p < NT; p += 64) first[p] = 0x7fffffff;
+  wsync();
+  for (int q = lane; q < x.nm; q += 64) atomicMin(&first[w.mt[2 * q]], q);
+  wsync();
   const int ndup = wcompact(
-      x.nm,
-      [&](int q) {
-        for (int j = 0; j < q; j++)
-          if (w.mt[2 * j] == w.mt[2 * q]) return true;
-        return false;
-      },
-      [&](int q, int p) { dupl[p] = q; });
+      x.nm, [&](int q) { return first[w.mt[2 * q]] < q; }, [&](int q, int p) { dupl[p] = q; });
   for (int k = lane; k < ndup; k += 64) w.mt[2 * dupl[k]] = -1 - w.mt[2 * dupl[k]];
   if (lane == 0) {
     sq[Q_NDUP] = ndup;
@@ -2604,6 +2381,8 @@ __global__ void __launch_bounds__(256) SS_MATCH_ATTR
   SCOUNT(6, x.nm);
   SSTAMP(7);
   wsync();
+  // the solver wave's exit: the cascade must ALWAYS post it last (no early return above), or the
+  // solver waits out SS_SPIN_TICKS and latches BX_ERR_INVALID
   if (lane == 0) __hip_atomic_store(&job.flag, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -3113,7 +2892,7 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 4, st))) return rc;
   if ((rc = ss_probe_begin(e, 5, st))) return rc;
-  hipLaunchKernelGGL(ss_match_kernel, dim3(nseq), dim3(256), lds, st, d, seq0);
+  hipLaunchKernelGGL(ss_match_kernel, dim3(nseq), dim3(128), lds, st, d, seq0);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 5, st))) return rc;
   if ((rc = ss_probe_begin(e, 6, st))) return rc;
