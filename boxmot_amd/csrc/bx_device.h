@@ -643,31 +643,52 @@ __device__ inline void wave0_exclusive_scan(int* cnt, int n) {
 //   * small components run the sequential SSP on one lane each, all lanes in parallel;
 //   * large components run it wave-parallel (relaxations over a row's edges and the argmin over
 //     touched columns spread over the 64 lanes), one component after another.
+// Every workspace array lives in LDS (the engine's association kernel and the op-level LAP
+// kernel carve them from their dynamic LDS), so the pointers carry address space 3: their
+// accesses compile to ds_* instructions, whose waits do not also wait for the vector-memory
+// counter (a generic pointer is read by flat instructions, which wait on both).  Only the
+// overflow edges (gcol / gcost) are global.
+#define BX_LDS __attribute__((address_space(3)))
 struct LapWS {
-  const int* row_ptr;     // [R+1] edge offsets
-  const uint16_t* ecol;   // edge columns (first elds in LDS, the rest in gcol)
-  const double* ecost;    // edge costs  (first elds in LDS, the rest in gcost)
-  const uint16_t* gcol;   // overflow edges in global memory
+  const BX_LDS int* row_ptr;    // [R+1] edge offsets
+  const BX_LDS uint16_t* ecol;  // edge columns (first elds in LDS, the rest in gcol)
+  const BX_LDS double* ecost;   // edge costs  (first elds in LDS, the rest in gcost)
+  const uint16_t* gcol;         // overflow edges in global memory
   const double* gcost;
   int elds;
-  int16_t* col4row;       // [R] out: column or -1
-  int16_t* row4col;       // [C] out: row or -1
-  double* u;              // [R] row potentials
-  double* v;              // [C] column potentials
-  double* spc;            // [C] shortest-path costs (INF between solves)
-  int16_t* path;          // [C]
-  uint8_t* colflag;       // [C] bit0 = in SC, bit1 = touched
-  uint16_t* touched;      // [C] touched column list (wave solver) / next-touched links (lane)
-  uint16_t* srlist;       // [R] rows visited (SR) except the root / next-SR links (lane)
-  int* coldeg;            // [C] finite-edge degree per column, then component labels per column
-  uint16_t* roots;        // [R] rows left for the shortest-path phase, ascending
-  int* rlab;              // [R] component label (smallest row index of the component)
-  int* colaux;            // [C] multi-edge rows per column (star detection)
-  int* colmin;            // [C] star components: winning row
+  BX_LDS int16_t* col4row;      // [R] out: column or -1
+  BX_LDS int16_t* row4col;      // [C] out: row or -1
+  BX_LDS double* u;             // [R] row potentials
+  BX_LDS double* v;             // [C] column potentials
+  BX_LDS double* spc;           // [C] shortest-path costs (INF between solves)
+  BX_LDS int16_t* path;         // [C]
+  BX_LDS uint8_t* colflag;      // [C] bit0 = in SC, bit1 = touched
+  BX_LDS uint16_t* touched;     // [C] touched column list (wave solver) / per-lane stretches
+  BX_LDS uint16_t* srlist;      // [R] rows visited (SR) except the root / next-SR links (lane)
+  BX_LDS int* coldeg;           // [C] finite-edge degree per column, then component labels
+  BX_LDS uint16_t* roots;       // [R] rows left for the shortest-path phase, ascending
+  BX_LDS int* rlab;             // [R] component label (smallest row index of the component)
+  BX_LDS int* colaux;           // [C] multi-edge rows per column (star detection)
+  BX_LDS int* colmin;           // [C] star components: winning row
   int* comp_stats = nullptr;  // if set: [0] += components of 17..LAP_LANE_ROWS rows (lane
                               // solver), [1] += components of more rows (wave solver)
   unsigned long long* dbg = nullptr;  // diagnostic counters (phase-timing builds only)
 };
+// a generic pointer into LDS (a __shared__ array or the dynamic LDS) as an address-space-3 one
+template <typename T>
+__device__ __forceinline__ BX_LDS T* lds_ptr(void* p) {
+  return (BX_LDS T*)(p);
+}
+// LDS atomics on address-space-3 pointers
+__device__ __forceinline__ void lds_add(BX_LDS int* p, int v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_min(BX_LDS int* p, int v) {
+  __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_min(BX_LDS unsigned long long* p, unsigned long long v) {
+  __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 __device__ __forceinline__ void lap_edge(const LapWS& w, int e, int& col, double& cost) {
   if (e < w.elds) { col = w.ecol[e]; cost = w.ecost[e]; }
@@ -717,7 +738,8 @@ __device__ __forceinline__ void lap_augment(const LapWS& w, int root, int sink, 
 // relaxation loads the next edge's column state before storing the current one's (the columns of
 // a row's edges are distinct; batches of four measured slower: K3's register budget).  Visited
 // rows are kept as a linked list through srlist[].
-__device__ __forceinline__ int lap_root_lane(int root, double L, const LapWS& w, uint16_t* tl) {
+__device__ __forceinline__ int lap_root_lane(int root, double L, const LapWS& w,
+                                             BX_LDS uint16_t* tl) {
   double minVal = 0.0;
   int i = root, nt = 0, shead = -1, stail = -1, steps = 0;
   double dummy_best = INF;
@@ -1085,8 +1107,8 @@ __device__ __forceinline__ int lap_prepare_block(int R, int C, double L, const L
       double c;
       lap_edge(w, e, j, c);
       if (!(c < INF)) continue;
-      atomicAdd(&w.coldeg[j], 1);
-      if (nf >= 2) atomicAdd(&w.colaux[j], 1);
+      lds_add(&w.coldeg[j], 1);
+      if (nf >= 2) lds_add(&w.colaux[j], 1);
     }
   }
   __syncthreads();
@@ -1102,7 +1124,7 @@ __device__ __forceinline__ int lap_prepare_block(int R, int C, double L, const L
     const unsigned long long b = __builtin_bit_cast(unsigned long long, c);
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
   };
-  unsigned long long* keyslot = (unsigned long long*)w.spc;  // spc is INF outside searches
+  BX_LDS unsigned long long* keyslot = (BX_LDS unsigned long long*)w.spc;  // INF outside searches
   int nstar = 0;
   for (int r = tid; r < R; r += WG) {
     int nf, jj;
@@ -1131,13 +1153,13 @@ __device__ __forceinline__ int lap_prepare_block(int R, int C, double L, const L
     for (int r = tid; r < R; r += WG) {
       int jj;
       double cc;
-      if (star(r, jj, cc)) atomicMin(&keyslot[jj], okey(cc));
+      if (star(r, jj, cc)) lds_min(&keyslot[jj], okey(cc));
     }
     __syncthreads();
     for (int r = tid; r < R; r += WG) {
       int jj;
       double cc;
-      if (star(r, jj, cc) && okey(cc) == keyslot[jj]) atomicMin(&w.colmin[jj], r);
+      if (star(r, jj, cc) && okey(cc) == keyslot[jj]) lds_min(&w.colmin[jj], r);
     }
     __syncthreads();
     for (int r = tid; r < R; r += WG) {
@@ -1196,7 +1218,7 @@ __device__ __forceinline__ void lap_solve_roots_wave(int R, int C, int nroots, d
           int j;
           double c;
           lap_edge(w, e, j, c);
-          if (c < INF) atomicMin(&w.coldeg[j], lr);
+          if (c < INF) lds_min(&w.coldeg[j], lr);
         }
       }
       wave_sync_lds();
@@ -1358,8 +1380,8 @@ __device__ inline bool lap_tied_block(int R, int C, double L, const LapWS& w, in
   if (ntie) return true;
   if (!nextra) return false;
   // reach-T: hc[j] = column j leads to a sink, hr[r] = row r does
-  int* hr = w.rlab;
-  int* hc = w.coldeg;
+  BX_LDS int* hr = w.rlab;
+  BX_LDS int* hc = w.coldeg;
   for (int r = tid; r < R; r += WG) hr[r] = 0;
   for (int j = tid; j < C; j += WG) {
     const int r = w.row4col[j];
@@ -1392,7 +1414,7 @@ __device__ inline bool lap_tied_block(int R, int C, double L, const LapWS& w, in
   if (nst) return true;
   // cycles: peel rows without a live successor (row -> the row matched to a tight column);
   // whatever survives lies on or leads into a cycle
-  int* al = w.rlab;
+  BX_LDS int* al = w.rlab;
   for (int r = tid; r < R; r += WG) al[r] = 1;
   __syncthreads();
   while (true) {

@@ -921,16 +921,18 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
 
   // LAP workspace (rows use s_c4r/s_u/s_srl, columns s_r4c/s_v/s_spc/...)
   LapWS W;
-  W.row_ptr = s_rowptr; W.ecol = s_ecol; W.ecost = s_ecost;
+  W.row_ptr = lds_ptr<int>(s_rowptr); W.ecol = lds_ptr<uint16_t>(s_ecol);
+  W.ecost = lds_ptr<double>(s_ecost);
   W.gcol = P.gcol + (size_t)s * T * D; W.gcost = P.gcost + (size_t)s * T * D;
-  W.elds = P.elds; W.col4row = s_c4r; W.row4col = s_r4c;
-  W.u = (double*)(smem + Lo.o_u); W.v = (double*)(smem + Lo.o_v);
-  W.spc = (double*)(smem + Lo.o_spc); W.path = (int16_t*)(smem + Lo.o_path);
-  W.colflag = (uint8_t*)(smem + Lo.o_colf); W.touched = (uint16_t*)(smem + Lo.o_touch);
-  W.srlist = s_srl; W.coldeg = (int*)(smem + Lo.o_cdeg); W.roots = (uint16_t*)(smem + Lo.o_roots);
-  W.rlab = (int*)(smem + Lo.o_rlab);
-  W.colaux = (int*)(smem + Lo.o_colaux);
-  W.colmin = (int*)(smem + Lo.o_colmin);
+  W.elds = P.elds; W.col4row = lds_ptr<int16_t>(s_c4r); W.row4col = lds_ptr<int16_t>(s_r4c);
+  W.u = lds_ptr<double>(smem + Lo.o_u); W.v = lds_ptr<double>(smem + Lo.o_v);
+  W.spc = lds_ptr<double>(smem + Lo.o_spc); W.path = lds_ptr<int16_t>(smem + Lo.o_path);
+  W.colflag = lds_ptr<uint8_t>(smem + Lo.o_colf); W.touched = lds_ptr<uint16_t>(smem + Lo.o_touch);
+  W.srlist = lds_ptr<uint16_t>(s_srl); W.coldeg = lds_ptr<int>(smem + Lo.o_cdeg);
+  W.roots = lds_ptr<uint16_t>(smem + Lo.o_roots);
+  W.rlab = lds_ptr<int>(smem + Lo.o_rlab);
+  W.colaux = lds_ptr<int>(smem + Lo.o_colaux);
+  W.colmin = lds_ptr<int>(smem + Lo.o_colmin);
   W.comp_stats = seq + SQ_NCOMP17;
   uint16_t* e_gcol = P.gcol + (size_t)s * T * D;
   double* e_gcost = P.gcost + (size_t)s * T * D;
@@ -1130,14 +1132,22 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
         M[k] = pair_cost(tb, rows[i], cols[j]);
       }
       __syncthreads();
-      JvLds jw = jv_bind(P.jvs + (size_t)s * P.jvs_stride, R + C);
+      // lapx's state in this association's LAP workspace and candidate-sweep LDS, which are dead
+      // until the next association rebuilds them (three blocks: see LdsA's take order), when it
+      // fits; else in the sequence's global scratch (one wave either way)
+      const int n = R + C;
+      const bool in_lds = jv_split_d_bytes(n) <= Lo.o_flags - Lo.o_u &&
+                          jv_split_a_bytes(n) <= Lo.o_dconf - Lo.o_tboxf &&
+                          jv_split_b_bytes(n) <= Lo.o_ints - Lo.o_rowptr;
+      JvLds jw = in_lds ? jv_bind_split(smem + Lo.o_u, smem + Lo.o_tboxf, smem + Lo.o_rowptr, n)
+                        : jv_bind(P.jvs + (size_t)s * P.jvs_stride, n);
       if (wave_id() == 0) {
         const double half = L / 2.;
         jv_wave_t([&](int i, int j) {
                     return (i < R && j < C) ? M[(size_t)i * C + j]
                                             : (i >= R && j >= C) ? 0.0 : half;
                   },
-                  R + C, jw, SyncWaveG{});
+                  n, jw, SyncWaveLG{!in_lds});
       }
       __syncthreads();
       // x >= C: unmatched (-1); a real partner above L is neither matched nor listed (-3)

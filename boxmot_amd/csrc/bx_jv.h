@@ -43,6 +43,31 @@ __device__ inline JvLds jv_bind(unsigned char* p, int n) {
   return w;
 }
 
+// The same state split over three buffers (the doubles v, d, sd in pd: 16 n + 16 bytes; x, y,
+// matches, freer in pa: 4 jv_ints_bytes(n); pred, col, sc in pb: 2 jv_ints_bytes(n) + 32) — for
+// a caller whose free LDS is not one contiguous block.
+__host__ __device__ constexpr size_t jv_split_d_bytes(int n) { return 16 * (size_t)n + 16; }
+__host__ __device__ constexpr size_t jv_split_a_bytes(int n) { return 4 * jv_ints_bytes(n); }
+__host__ __device__ constexpr size_t jv_split_b_bytes(int n) { return 2 * jv_ints_bytes(n) + 32; }
+__device__ inline JvLds jv_bind_split(unsigned char* pd, unsigned char* pa, unsigned char* pb,
+                                      int n) {
+  JvLds w;
+  w.v = (double*)pd;
+  w.d = w.v + n;
+  w.sd = w.d + n;
+  size_t o = 0;
+  auto takeA = [&](int k) { int* q = (int*)(pa + o); o += jv_ints_bytes(k); return q; };
+  w.x = takeA(n);
+  w.y = takeA(n);
+  w.matches = takeA(n);
+  w.freer = takeA(n);
+  w.pred = (int*)pb;
+  w.col = (int*)(pb + jv_ints_bytes(n));
+  w.sc = (int*)(pb + 2 * jv_ints_bytes(n));
+  w.dc = nullptr;
+  return w;
+}
+
 __device__ __forceinline__ double cget(const double* C, int nr, int nc, int i, int j) {
   return (i < nr && j < nc) ? C[i * nc + j] : 0.0;
 }
@@ -83,6 +108,19 @@ struct SyncWaveL {
     __builtin_amdgcn_wave_barrier();
   }
   __device__ void after_atomics() const { (*this)(); }
+};
+// SyncWaveL or SyncWaveG chosen at run time (one instantiation of the solver for both homes of
+// its state: the engine's rare tie path must not add a second inlined copy to its kernel)
+struct SyncWaveLG {
+  bool global;
+  __device__ void operator()() const {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ void after_atomics() const {
+    if (global) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    __builtin_amdgcn_wave_barrier();
+  }
 };
 struct SyncWaveG {
   __device__ void operator()() const {

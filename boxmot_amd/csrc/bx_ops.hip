@@ -156,13 +156,16 @@ __global__ void kf_gate_kernel(int kind, int n, const double* mean, const double
 // One dense problem: CSR of admissible edges (cost < thresh) in LDS, then the wave LAP.  When
 // the optimum is not unique (lap_tied_block) the problem is re-solved by lapx's own lapjv on the
 // (nr+nc)^2 extension (matching.py:54-61: lap.lapjv(extend_cost=True, cost_limit=thresh)), read
-// through an accessor with its state in `jvs` (global memory), so ties resolve as lapx's do.
+// through an accessor, so ties resolve as lapx's do — its state in the kernel's LDS (the sparse
+// solve's CSR and workspace are dead by then) when the launch sized it for that (jv_lds), else in
+// `jvs` (global memory).
 // Outputs: x[i] = column, -1 unmatched, -3 assigned by lapx to a real column above thresh (the
 // reference neither matches nor lists such a row: matching.py:56-61); y likewise.
 __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int nr, int nc,
                                                        double thr, int elds, uint16_t* gcol,
                                                        double* gcost, unsigned char* jvs,
-                                                       int32_t* x, int32_t* y, int32_t* tied) {
+                                                       int jv_lds, int32_t* x, int32_t* y,
+                                                       int32_t* tied) {
   extern __shared__ __align__(16) unsigned char smem[];
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -214,13 +217,17 @@ __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int n
   }
   __syncthreads();
   LapWS W;
-  W.row_ptr = rowptr; W.ecol = ecol; W.ecost = ecost; W.gcol = gcol; W.gcost = gcost;
-  W.elds = elds; W.col4row = c4r; W.row4col = r4c; W.u = u; W.v = v; W.spc = spc;
-  W.path = path; W.colflag = colf; W.touched = touch; W.srlist = srl; W.coldeg = cdeg;
-  W.roots = roots;
-  W.rlab = rlab;
-  W.colaux = caux;
-  W.colmin = cmin;
+  W.row_ptr = lds_ptr<int>(rowptr); W.ecol = lds_ptr<uint16_t>(ecol);
+  W.ecost = lds_ptr<double>(ecost); W.gcol = gcol; W.gcost = gcost;
+  W.elds = elds; W.col4row = lds_ptr<int16_t>(c4r); W.row4col = lds_ptr<int16_t>(r4c);
+  W.u = lds_ptr<double>(u); W.v = lds_ptr<double>(v); W.spc = lds_ptr<double>(spc);
+  W.path = lds_ptr<int16_t>(path); W.colflag = lds_ptr<uint8_t>(colf);
+  W.touched = lds_ptr<uint16_t>(touch); W.srlist = lds_ptr<uint16_t>(srl);
+  W.coldeg = lds_ptr<int>(cdeg);
+  W.roots = lds_ptr<uint16_t>(roots);
+  W.rlab = lds_ptr<int>(rlab);
+  W.colaux = lds_ptr<int>(caux);
+  W.colmin = lds_ptr<int>(cmin);
   lap_solve_block(nr, nc, thr, W, scan_tmp);
   const bool tie = lap_tied_block(nr, nc, thr, W, scan_tmp, pre);
   if (!tie) {
@@ -230,14 +237,15 @@ __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int n
     return;
   }
   const int n = nr + nc;
-  JvLds jw = jv_bind(jvs, n);
+  __syncthreads();  // every wave is done with the CSR before the LDS is rebound
+  JvLds jw = jv_bind(jv_lds ? smem : jvs, n);
   if (wave_id() == 0) {
     const double half = thr / 2.;
-    jv_wave_t([&](int i, int j) {
-                return (i < nr && j < nc) ? cost[(size_t)i * nc + j]
-                                          : (i >= nr && j >= nc) ? 0.0 : half;
-              },
-              n, jw, SyncWaveG{});
+    auto cf = [&](int i, int j) {
+      return (i < nr && j < nc) ? cost[(size_t)i * nc + j] : (i >= nr && j >= nc) ? 0.0 : half;
+    };
+    if (jv_lds) jv_wave_t(cf, n, jw, SyncWaveL{});
+    else jv_wave_t(cf, n, jw, SyncWaveG{});
   }
   __syncthreads();
   for (int i = tid; i < nr; i += WG) {
@@ -427,8 +435,11 @@ int bx_linear_assignment_ex(const double* cost, int nr, int nc, double thresh, i
     return o;
   };
   while (elds > 0 && lds_for(elds) > 160 * 1024) elds /= 2;
-  const size_t lds = lds_for(elds);
+  size_t lds = lds_for(elds);
   if (lds > 160 * 1024) return op_err(BX_ERR_INVALID, "problem too large for LDS");
+  // the tie re-solve's lapjv state in LDS too when it fits (n = nr + nc up to ~4000)
+  const int jv_lds = jv_bytes(nr + nc) <= 160 * 1024;
+  if (jv_lds && jv_bytes(nr + nc) > lds) lds = jv_bytes(nr + nc);
   void* ws = nullptr;
   const size_t ne = (size_t)nr * nc;
   const size_t jvb = (jv_bytes(nr + nc) + 255) & ~size_t(255);
@@ -441,7 +452,7 @@ int bx_linear_assignment_ex(const double* cost, int nr, int nc, double thresh, i
     OPCHK(hipFuncSetAttribute((const void*)lap_dense_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(lap_dense_kernel, dim3(1), dim3(WG), lds, st, cost, nr, nc, thresh, elds,
-                     gcol, gcost, jvs, x, y, tied);
+                     gcol, gcost, jvs, jv_lds, x, y, tied);
   OPCHK(hipGetLastError());
   if (tied_out) OPCHK(hipMemcpyAsync(tied_out, tied, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
   OPCHK(hipFreeAsync(ws, st));

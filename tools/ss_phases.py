@@ -23,9 +23,9 @@ PHASES = ["setup", "crowd", "camera+quality+sort+predict", "lists", "stage1 casc
           "partial_fit", "masks+outputs"]
 COUNTERS = ["cost build cyc", "lsap cyc", "lsap calls", "sum rows (tracks)", "sum cols (dets)",
             "dijkstra steps", "matches", "solver rows R", "solver cols CC", "slow rows",
-            "slow-row cyc", "lsap loop cyc", "fast: wait+relax cyc",
-            "fast: wave min cyc", "fast: ballots cyc", "fast: tie/sink to next row cyc",
-            "table-settled rows"]
+            "slow-row cyc", "lsap loop cyc", "pair: v + wait + relax cyc",
+            "pair: two wave minima cyc", "pair: row 0 decided (fast) cyc",
+            "pair: row 1 decided (fast) cyc"]
 
 
 def build():
