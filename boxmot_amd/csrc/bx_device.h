@@ -575,7 +575,7 @@ __device__ inline float np_sumsq_wave(const XT* x, int n) {
 // ------------------------------------------------------------------------------------------
 // Block (256-thread) helpers.
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 // exclusive prefix of a 0/1 flag over the block in thread order; `tmp` >= 4 ints of LDS.
 __device__ inline int block_scan_flag(bool f, int* tmp, int& total) {
@@ -670,10 +670,29 @@ struct LapWS {
   BX_LDS int* rlab;             // [R] component label (smallest row index of the component)
   BX_LDS int* colaux;           // [C] multi-edge rows per column (star detection)
   BX_LDS int* colmin;           // [C] star components: winning row
-  int* comp_stats = nullptr;  // if set: [0] += components of 17..LAP_LANE_ROWS rows (lane
-                              // solver), [1] += components of more rows (wave solver)
+  // Optional (null: wave 0 solves every component): scratch for the components handed to the
+  // workgroup's other waves, one LDS block hs carved by the accessors below from the row bound
+  // hT (R rounded up to 8) and the touched-list stride tws (C rounded up to 8) — per component
+  // head row its row and column counts (cntr, cntc: [R]), the heads for the wave solver in
+  // ascending order (big: [R], nbig: [1]), and for waves 1..3 their own touched-column and
+  // visited-row lists (wave k: tw + (k-1) * tws, [C]; sw + (k-1) * hT, [R]).  Three fields, not
+  // eight pointers: the association kernel runs at its SGPR limit, and every extra uniform live
+  // across the LAP spilled.  lap_helper_bytes(hT, tws) is the block's size.
+  BX_LDS int* hs = nullptr;
+  int hT = 0, tws = 0;
+  __device__ BX_LDS int* cntr() const { return hs; }
+  __device__ BX_LDS int* cntc() const { return hs + hT; }
+  __device__ BX_LDS int* nbig() const { return hs + 2 * hT; }
+  __device__ BX_LDS uint16_t* big() const { return (BX_LDS uint16_t*)(hs + 2 * hT + 4); }
+  __device__ BX_LDS uint16_t* tw() const { return big() + hT; }
+  __device__ BX_LDS uint16_t* sw() const { return tw() + 3 * tws; }
+  int* comp_stats = nullptr;  // if set: [0] += components solved by the per-lane SSP (past the
+                              // register path), [1] += components on the wave-parallel solver
   unsigned long long* dbg = nullptr;  // diagnostic counters (phase-timing builds only)
 };
+__host__ __device__ inline size_t lap_helper_bytes(int hT, int tws) {
+  return 4 * (2 * (size_t)hT + 4) + 2 * (size_t)hT + 2 * 3 * (size_t)tws + 2 * 3 * (size_t)hT;
+}
 // a generic pointer into LDS (a __shared__ array or the dynamic LDS) as an address-space-3 one
 template <typename T>
 __device__ __forceinline__ BX_LDS T* lds_ptr(void* p) {
@@ -703,6 +722,64 @@ __device__ __forceinline__ void wave_argmin(double& val, int& key) {
     int ok = __shfl_xor(key, d);
     if (ov < val || (ov == val && ok < key)) { val = ov; key = ok; }
   }
+}
+
+// the same (value, key) argmin without LDS traffic: the value's minimum by DPP row rotations
+// and gfx950's row / half swaps, then the smallest key among the lanes holding it (an int
+// minimum the same way).  No NaNs.
+__device__ __forceinline__ double lap_ror_d(double v, int ctrl_sel) {
+  const long long b = __double_as_longlong(v);
+  int lo = (int)(b & 0xffffffffll), hi = (int)(b >> 32);
+  switch (ctrl_sel) {
+    case 8: lo = __builtin_amdgcn_mov_dpp(lo, 0x128, 0xf, 0xf, false);
+            hi = __builtin_amdgcn_mov_dpp(hi, 0x128, 0xf, 0xf, false); break;
+    case 4: lo = __builtin_amdgcn_mov_dpp(lo, 0x124, 0xf, 0xf, false);
+            hi = __builtin_amdgcn_mov_dpp(hi, 0x124, 0xf, 0xf, false); break;
+    case 2: lo = __builtin_amdgcn_mov_dpp(lo, 0x122, 0xf, 0xf, false);
+            hi = __builtin_amdgcn_mov_dpp(hi, 0x122, 0xf, 0xf, false); break;
+    default: lo = __builtin_amdgcn_mov_dpp(lo, 0x121, 0xf, 0xf, false);
+             hi = __builtin_amdgcn_mov_dpp(hi, 0x121, 0xf, 0xf, false); break;
+  }
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double lap_swap_d(double v, bool half) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+  unsigned a0, a1, h0, h1;
+  if (half) {
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a0 = l[0], a1 = l[1], h0 = h[0], h1 = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a0 = l[0], a1 = l[1], h0 = h[0], h1 = h[1];
+  }
+  return fmin(__longlong_as_double(((long long)h0 << 32) | a0),
+              __longlong_as_double(((long long)h1 << 32) | a1));
+}
+__device__ __forceinline__ int lap_swap_i(int v, bool half) {
+  const auto l = half ? __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false)
+                      : __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  return min((int)l[0], (int)l[1]);
+}
+__device__ __forceinline__ void wave_argmin_dpp(double& val, int& key) {
+  double m = val;
+  m = fmin(m, lap_ror_d(m, 8));
+  m = fmin(m, lap_ror_d(m, 4));
+  m = fmin(m, lap_ror_d(m, 2));
+  m = fmin(m, lap_ror_d(m, 1));
+  m = lap_swap_d(m, false);
+  m = lap_swap_d(m, true);  // every lane: the wave minimum
+  int k = val == m ? key : 0x7fffffff;
+  k = min(k, __builtin_amdgcn_mov_dpp(k, 0x128, 0xf, 0xf, false));
+  k = min(k, __builtin_amdgcn_mov_dpp(k, 0x124, 0xf, 0xf, false));
+  k = min(k, __builtin_amdgcn_mov_dpp(k, 0x122, 0xf, 0xf, false));
+  k = min(k, __builtin_amdgcn_mov_dpp(k, 0x121, 0xf, 0xf, false));
+  k = lap_swap_i(k, false);
+  k = lap_swap_i(k, true);
+  val = m;
+  key = k;
 }
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -816,8 +893,10 @@ __device__ __forceinline__ int lap_root_lane(int root, double L, const LapWS& w,
   return steps;
 }
 
-// One SSP root, wave-parallel (called by all 64 lanes).
-__device__ __forceinline__ int lap_root_wave(int root, double L, const LapWS& w) {
+// One SSP root, wave-parallel (called by all 64 lanes); tch / srl: this wave's touched-column and
+// visited-row lists.
+__device__ __forceinline__ int lap_root_wave(int root, double L, const LapWS& w,
+                                             BX_LDS uint16_t* tch, BX_LDS uint16_t* srl) {
   const int lane = lane_id();
   double minVal = 0.0;
   int i = root, ntouched = 0, nsr = 0, steps = 0;
@@ -843,7 +922,7 @@ __device__ __forceinline__ int lap_root_wave(int root, double L, const LapWS& w)
         }
       }
       unsigned long long m = __ballot(newt);
-      if (newt) w.touched[ntouched + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)j;
+      if (newt) tch[ntouched + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)j;
       ntouched += __popcll(m);
     }
     {  // dummy of row i: reduced cost 0 - u_i - 0 (its potential never moves)
@@ -855,19 +934,19 @@ __device__ __forceinline__ int lap_root_wave(int root, double L, const LapWS& w)
     double bv = INF;
     int bk = 0x7fffffff;
     for (int k = lane; k < ntouched; k += WAVE) {
-      int j = w.touched[k];
+      int j = tch[k];
       if (!(w.colflag[j] & 1)) {
         double sv = w.spc[j];
         if (sv < bv) { bv = sv; bk = k; }
       }
     }
-    wave_argmin(bv, bk);
+    wave_argmin_dpp(bv, bk);
     if (dummy_best <= bv) {  // leave dummy_row unmatched (ties: stop early)
       minVal = dummy_best;
       sink = -2;
       break;
     }
-    const int j = w.touched[bk];
+    const int j = tch[bk];
     steps++;
     minVal = bv;
     if (lane == 0) w.colflag[j] |= 1;
@@ -875,24 +954,24 @@ __device__ __forceinline__ int lap_root_wave(int root, double L, const LapWS& w)
     wave_sync_lds();
     if (r4c < 0) { sink = j; break; }
     i = r4c;
-    if (lane == 0) w.srlist[nsr] = (uint16_t)i;
+    if (lane == 0) srl[nsr] = (uint16_t)i;
     nsr++;
   }
   // dual updates
   if (lane == 0) w.u[root] += minVal;
   for (int k = lane; k < nsr; k += WAVE) {
-    int r = w.srlist[k];
+    int r = srl[k];
     w.u[r] += minVal - w.spc[w.col4row[r]];
   }
   wave_sync_lds();
   for (int k = lane; k < ntouched; k += WAVE) {
-    int j = w.touched[k];
+    int j = tch[k];
     if (w.colflag[j] & 1) w.v[j] -= minVal - w.spc[j];
   }
   wave_sync_lds();
   if (lane == 0) lap_augment(w, root, sink, dummy_row);
   for (int k = lane; k < ntouched; k += WAVE) {
-    int j = w.touched[k];
+    int j = tch[k];
     w.spc[j] = INF;
     w.colflag[j] = 0;
   }
@@ -1070,8 +1149,11 @@ __device__ __forceinline__ bool lap_component_regs(const int (&rr)[LAP_RM], int 
   return true;
 }
 
+#ifndef BX_LAP_HELPER_ROOTS
+#define BX_LAP_HELPER_ROOTS 32
+#endif
 #ifndef BX_LAP_LANE_ROWS
-#define BX_LAP_LANE_ROWS 24
+#define BX_LAP_LANE_ROWS 3
 #endif
 constexpr int LAP_LANE_ROWS = BX_LAP_LANE_ROWS;  // components up to this many rows: one lane
 
@@ -1189,13 +1271,59 @@ __device__ __forceinline__ int lap_prepare_block(int R, int C, double L, const L
       [&](int r, int p) { w.roots[p] = (uint16_t)r; }, scan_tmp);
 }
 
-// The searches, called by all 64 lanes of ONE wave after lap_prepare_block.
-__device__ __forceinline__ void lap_solve_roots_wave(int R, int C, int nroots, double L,
-                                                    const LapWS& w) {
+// The components for the wave-parallel solver (its one call site: a second inlined copy pushed
+// the association kernel into scratch): on waves 1..3 from the big list, round-robin, each with
+// its own lists — or, without helper scratch, on wave 0 after its lanes from the nbl heads they
+// left in colaux (dead after lap_prepare_block; a component has a column of its own, so <= C
+// heads).  Each component's roots in ascending order (a ballot over the ascending roots list, 64
+// at a time).  Returns the components solved.
+__device__ __forceinline__ int lap_wave_components(int nroots, double L, const LapWS& w,
+                                                   bool helpers, int wid, int nbl, int& nsteps) {
   const int lane = lane_id();
-  int nsteps = 0, ncomp = 0, maxrows = 0, iters = 0, nlane17 = 0, nwave = 0;
-  if (w.dbg && lane == 0) w.dbg[3] = __builtin_amdgcn_s_memtime();
-  if (nroots > 0) {
+  const int stride = helpers ? 3 : 1;
+  const int nb = helpers ? *w.nbig() : nbl;
+  BX_LDS uint16_t* tch = helpers ? w.tw() + (wid - 1) * w.tws : w.touched;
+  BX_LDS uint16_t* srl = helpers ? w.sw() + (wid - 1) * w.hT : w.srlist;
+  int ncomp = 0;
+  for (int c = helpers ? wid - 1 : 0; c < nb; c += stride) {
+    const int h = helpers ? (int)w.big()[c] : w.colaux[c];
+    for (int k0 = 0; k0 < nroots; k0 += WAVE) {
+      const int k = k0 + lane;
+      unsigned long long m = __ballot(k < nroots && w.rlab[w.roots[k]] == h);
+      while (m) {
+        const int b = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        nsteps += lap_root_wave(w.roots[k0 + b], L, w, tch, srl);
+      }
+    }
+    ncomp++;
+  }
+  return ncomp;
+}
+
+// The searches after lap_prepare_block, called by ALL threads of the workgroup.  Wave 0 labels
+// the components; small ones (<= LAP_LANE_ROWS rows) are solved one lane each on wave 0, the rest
+// by the wave-parallel solver on waves 1..3 (components dealt round-robin in head order, each
+// wave with its own touched / visited lists) when the caller gave the scratch for that (w.cntr),
+// else every component on wave 0's lanes.  Components are disjoint in rows and columns, so the
+// waves share the per-row / per-column arrays without conflict, and every component's result is
+// the same whichever solver takes it.  (One call site per solver: a second inlined copy of the
+// wave solver pushed the association kernel into scratch.)
+__device__ __forceinline__ void lap_solve_roots_block(int R, int C, int nroots, double L,
+                                                      const LapWS& w) {
+  const int lane = lane_id(), wid = wave_id();
+  // (helper waves only past BX_LAP_HELPER_ROOTS roots: the scratch bookkeeping and the two
+  // barriers cost the small LAPs of uncrowded scenes more than the occasional 4+-row component
+  // solved on wave 0 after its lanes)
+#ifdef BX_LAP_NO_HELPERS
+  const bool helpers = false;
+#else
+  const bool helpers = w.hs != nullptr && nroots > BX_LAP_HELPER_ROOTS;
+#endif
+  const int lane_max = LAP_LANE_ROWS;  // rows of a lane-solved component
+  int nsteps = 0, ncomp = 0, maxrows = 0, iters = 0, nlane = 0, nwave = 0, nbl = 0;
+  if (w.dbg && wid == 0 && lane == 0) w.dbg[3] = __builtin_amdgcn_s_memtime();
+  if (wid == 0 && nroots > 0) {
     // component labels by min-label propagation over the roots' finite edges (coldeg reused as
     // the per-column label; columns no root reaches keep "none")
     for (int j = lane; j < C; j += WAVE) w.coldeg[j] = 0x7fffffff;
@@ -1239,29 +1367,53 @@ __device__ __forceinline__ void lap_solve_roots_wave(int R, int C, int nroots, d
       iters++;
       if (!any) break;
     }
+    if (helpers) {
+      // rows and columns per component (by head), then the heads for the wave solver
+      BX_LDS int* cntr = w.cntr();
+      BX_LDS int* cntc = w.cntc();
+      for (int k = lane; k < nroots; k += WAVE) cntr[w.roots[k]] = 0, cntc[w.roots[k]] = 0;
+      wave_sync_lds();
+      for (int k = lane; k < nroots; k += WAVE) lds_add(&cntr[w.rlab[w.roots[k]]], 1);
+      for (int j = lane; j < C; j += WAVE)
+        if (w.coldeg[j] != 0x7fffffff) lds_add(&cntc[w.coldeg[j]], 1);
+      wave_sync_lds();
+      int nb = 0;
+      for (int k0 = 0; k0 < nroots; k0 += WAVE) {
+        const int k = k0 + lane;
+        const int h = k < nroots ? w.roots[k] : 0;
+        const bool bg = k < nroots && w.rlab[h] == h && cntr[h] > lane_max;
+        const unsigned long long m = __ballot(bg);
+        if (bg) w.big()[nb + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)h;
+        nb += __popcll(m);
+      }
+      if (lane == 0) *w.nbig() = nb;
+    }
     if (w.dbg && lane == 0) w.dbg[8] = __builtin_amdgcn_s_memtime();
-    // a component is headed by its smallest row (label == row); its rows are the roots carrying
-    // that label, taken in ascending order.  Small components: one lane each, in parallel.
-    // The lanes take the component heads 64 at a time; a lane solving its component gets a
-    // stretch of touched[] as long as the component's column count (exclusive prefix over the
-    // wave: the components are disjoint, so the stretches fit in C).
-    bool big = false;
+  } else if (helpers && wid == 0 && lane == 0) {
+    *w.nbig() = 0;
+  }
+  if (helpers) __syncthreads();
+  if (wid == 0 && nroots > 0) {
+    // small components: one lane each, in parallel.  The lanes take the component heads 64 at a
+    // time; a lane solving its component gets a stretch of touched[] as long as the component's
+    // column count (exclusive prefix over the wave: the components are disjoint, so the
+    // stretches fit in C).
     for (int k0 = 0; k0 < nroots; k0 += WAVE) {
       const int k = k0 + lane;
       int h = -1, nrows = 0;
-      bool mine = false;
+      bool mine = false, bigh = false;
       if (k < nroots) {
         h = w.roots[k];
         if (w.rlab[h] == h) {
-          for (int q = k; q < nroots; q++) nrows += w.rlab[w.roots[q]] == h;
+          if (helpers) nrows = w.cntr()[h];
+          else
+            for (int q = k; q < nroots; q++) nrows += w.rlab[w.roots[q]] == h;
           ncomp++;
           maxrows = max(maxrows, nrows);
           mine = true;
-          nlane17 += nrows > 16 && nrows <= LAP_LANE_ROWS;
-          nwave += nrows > LAP_LANE_ROWS;
-          if (nrows > LAP_LANE_ROWS) {
-            big = true;
-            mine = false;
+          if (nrows > lane_max) {
+            mine = false;  // the wave solver's
+            bigh = !helpers;
           } else if (nrows <= LAP_RM) {  // register-resident solve when it fits
             int rr[LAP_RM];
             int n = 0;
@@ -1273,11 +1425,15 @@ __device__ __forceinline__ void lap_solve_roots_wave(int R, int C, int nroots, d
             }
             if (lap_component_regs(rr, nrows, L, w, nsteps)) mine = false;
           }
+          nlane += mine;  // (the per-lane SSP: past the register path)
         }
       }
       int ncols = 0;
-      if (mine)
-        for (int j = 0; j < C; j++) ncols += w.coldeg[j] == h;
+      if (mine) {
+        if (helpers) ncols = w.cntc()[h];
+        else
+          for (int j = 0; j < C; j++) ncols += w.coldeg[j] == h;
+      }
       int off = ncols;  // inclusive prefix over the lanes, then exclusive
 #pragma unroll
       for (int d = 1; d < WAVE; d <<= 1) {
@@ -1290,53 +1446,44 @@ __device__ __forceinline__ void lap_solve_roots_wave(int R, int C, int nroots, d
           const int r = w.roots[q];
           if (w.rlab[r] == h) nsteps += lap_root_lane(r, L, w, w.touched + off);
         }
+      const unsigned long long mb = __ballot(bigh);  // (ascending: the heads come in order)
+      if (bigh) w.colaux[nbl + __popcll(mb & ((1ull << lane) - 1ull))] = h;
+      nbl += __popcll(mb);
       wave_sync_lds();
     }
     if (w.dbg && lane == 0) w.dbg[9] = __builtin_amdgcn_s_memtime();
-    // large components: wave-parallel, one after another (components are independent)
-    if (__ballot(big) != 0ull) {
-      for (int k = 0; k < nroots; k++) {
-        const int h = w.roots[k];
-        if (w.rlab[h] != h) continue;
-        int nrows = 0;
-        for (int q = k + lane; q < nroots; q += WAVE) nrows += w.rlab[w.roots[q]] == h;
-        for (int d = 32; d >= 1; d >>= 1) nrows += __shfl_xor(nrows, d);
-        if (nrows <= LAP_LANE_ROWS) continue;
-        for (int q = k; q < nroots; q++) {
-          const int r = w.roots[q];
-          if (w.rlab[r] == h) nsteps += lap_root_wave(r, L, w);
-        }
-      }
-    }
   }
-  for (int r = lane; r < R; r += WAVE)
-    if (w.col4row[r] == -2) w.col4row[r] = -1;
-  wave_sync_lds();
+  if ((helpers ? (wid >= 1 && wid <= 3) : wid == 0) && nroots > 0)
+    nwave += lap_wave_components(nroots, L, w, helpers, wid, nbl, nsteps);
+  if (helpers) __syncthreads();
+  if (wid == 0)
+    for (int r = lane; r < R; r += WAVE)
+      if (w.col4row[r] == -2) w.col4row[r] = -1;
   if (w.comp_stats) {
-    int sa = nlane17, sb = nwave;
+    int sa = nlane;
+    for (int d = 32; d >= 1; d >>= 1) sa += __shfl_xor(sa, d);
+    if (lane == 0 && (sa | nwave)) {  // (nwave is wave-uniform)
+      atomicAdd(&w.comp_stats[0], sa);
+      atomicAdd(&w.comp_stats[1], nwave);
+    }
+  }
+  if (w.dbg && wid == 0) {
     for (int d = 32; d >= 1; d >>= 1) {
-      sa += __shfl_xor(sa, d);
-      sb += __shfl_xor(sb, d);
+      nsteps += __shfl_xor(nsteps, d);
+      ncomp += __shfl_xor(ncomp, d);
+      maxrows = max(maxrows, __shfl_xor(maxrows, d));
     }
-    if (lane == 0 && (sa | sb)) {
-      w.comp_stats[0] += sa;
-      w.comp_stats[1] += sb;
+    if (lane == 0) {
+      w.dbg[0] = nroots;
+      w.dbg[1] = nsteps;  // (wave 0's: the helper waves' steps are not counted)
+      w.dbg[2] = R;
+      w.dbg[4] = ncomp;
+      w.dbg[5] = maxrows;
+      w.dbg[6] = iters;
+      w.dbg[7] = __builtin_amdgcn_s_memtime();  // after labels+solve
     }
   }
-  for (int d = 32; d >= 1; d >>= 1) {
-    nsteps += __shfl_xor(nsteps, d);
-    ncomp += __shfl_xor(ncomp, d);
-    maxrows = max(maxrows, __shfl_xor(maxrows, d));
-  }
-  if (w.dbg && lane == 0) {
-    w.dbg[0] = nroots;
-    w.dbg[1] = nsteps;
-    w.dbg[2] = R;
-    w.dbg[4] = ncomp;
-    w.dbg[5] = maxrows;
-    w.dbg[6] = iters;
-    w.dbg[7] = __builtin_amdgcn_s_memtime();  // after labels+solve
-  }
+  if (!helpers) wave_sync_lds();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1446,7 +1593,7 @@ __device__ inline bool lap_tied_block(int R, int C, double L, const LapWS& w, in
 __device__ __forceinline__ void lap_solve_block(int R, int C, double L, const LapWS& w,
                                                 int* scan_tmp) {
   const int nroots = lap_prepare_block(R, C, L, w, scan_tmp);
-  if (wave_id() == 0) lap_solve_roots_wave(R, C, nroots, L, w);
+  lap_solve_roots_block(R, C, nroots, L, w);
   __syncthreads();
 }
 

@@ -235,7 +235,7 @@ enum {
   SQ_NA = 0, SQ_NL, SQ_FC, SQ_IDC, SQ_STATUS, SQ_NA2, SQ_NL2, SQ_NREC, SQ_SKIP,
   SQ_NHIGH, SQ_NPAIR, SQ_NDET,  // last frame's high dets, gated pairs, dets (statistics)
   SQ_NTIE,                       // associations re-solved by lapx's lapjv (tied optimum), total
-  SQ_NCOMP17, SQ_NCOMPW,         // LAP components of 17..24 rows (lane SSP) / more (wave SSP)
+  SQ_NCOMP17, SQ_NCOMPW,         // LAP components on the per-lane SSP / the wave SSP
   SQ_STRIDE = 16
 };
 // update records: x = slot | kind << 16, y = detection index within the sequence's frame
@@ -934,6 +934,11 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
   W.colaux = lds_ptr<int>(smem + Lo.o_colaux);
   W.colmin = lds_ptr<int>(smem + Lo.o_colmin);
   W.comp_stats = seq + SQ_NCOMP17;
+  // the LAP's helper-wave scratch in the candidate sweep's LDS (tboxf .. dconf: dead while the
+  // LAP runs; lap_helper_bytes(hT, tws) <= 16 T + 18 D, asserted by the host layout check)
+  W.hs = lds_ptr<int>(smem + Lo.o_tboxf);
+  W.hT = (T + 7) & ~7;
+  W.tws = (D + 7) & ~7;
   uint16_t* e_gcol = P.gcol + (size_t)s * T * D;
   double* e_gcost = P.gcost + (size_t)s * T * D;
   auto put_edge = [&](int e, int col, double cost) {
@@ -1136,9 +1141,13 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
       // until the next association rebuilds them (three blocks: see LdsA's take order), when it
       // fits; else in the sequence's global scratch (one wave either way)
       const int n = R + C;
+#ifdef BX_TIE_NO_LDS
+      const bool in_lds = false;
+#else
       const bool in_lds = jv_split_d_bytes(n) <= Lo.o_flags - Lo.o_u &&
                           jv_split_a_bytes(n) <= Lo.o_dconf - Lo.o_tboxf &&
                           jv_split_b_bytes(n) <= Lo.o_ints - Lo.o_rowptr;
+#endif
       JvLds jw = in_lds ? jv_bind_split(smem + Lo.o_u, smem + Lo.o_tboxf, smem + Lo.o_rowptr, n)
                         : jv_bind(P.jvs + (size_t)s * P.jvs_stride, n);
       if (wave_id() == 0) {
@@ -2117,6 +2126,14 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
   HIPCHK(hipMemset(e->arena, 0, bytes));
   e->lds_assoc = LdsA(T, D, d.elds).total;
   e->lds_finish = LdsF(T).total;
+  {
+    const LdsA Lo(T, D, d.elds);  // the LAP helper scratch overlays tboxf .. dconf
+    if (lap_helper_bytes((T + 7) & ~7, (D + 7) & ~7) > Lo.o_dconf - Lo.o_tboxf) {
+      (void)hipFree(e->arena);
+      delete e;
+      return set_err(BX_ERR_INVALID, "LAP helper scratch does not fit its LDS overlay");
+    }
+  }
   if (e->lds_assoc > 160 * 1024 || e->lds_finish > 160 * 1024) {
     (void)hipFree(e->arena);
     delete e;

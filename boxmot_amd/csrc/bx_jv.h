@@ -160,7 +160,7 @@ constexpr int JV_CH = 8;  // 64-position chunks of one relaxation loaded togethe
 // and every cross-lane hand-off through sync() (the whole workgroup when it is one wave, else
 // the calling wave only).
 template <class CF, class SY>
-__device__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync) {
+__device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync) {
   const int lane = threadIdx.x & 63;
   // ---- _ccrrt_dense.  Column minima from LARGE, first row on ties (lane per column) ...
   for (int j = lane; j < n; j += OW) {

@@ -130,12 +130,13 @@ class Engine:
         return int(t.value)
 
     def lap_components(self, seq0: int = 0, nseq: int | None = None) -> dict:
-        """LAP components handed to the per-lane SSP with 17..24 rows and to the wave-parallel
-        SSP (more rows) since creation (bx_engine_lap_components_host), over [seq0, seq0+nseq)."""
+        """LAP components solved by the per-lane SSP (past the register path) and by the
+        wave-parallel SSP (more than 3 rows) since creation (bx_engine_lap_components_host), over
+        [seq0, seq0+nseq)."""
         nseq = self.n_seq - seq0 if nseq is None else nseq
         a = (C.c_int64 * 2)()
         N.check(self._L.bx_engine_lap_components_host(self._h, seq0, nseq, a), "lap_components")
-        return {"lane17_24": int(a[0]), "wave": int(a[1])}
+        return {"lane": int(a[0]), "wave": int(a[1])}
 
     def update_host(self, seq: int, dets: np.ndarray, embs: np.ndarray | None = None,
                     warp: np.ndarray | None = None) -> np.ndarray:

@@ -149,9 +149,10 @@ int bx_engine_probe_read(bx_engine *e, double *total_ms, int *count);
 /* Associations of sequences [seq0, seq0+nseq) whose optimum was tied and that were therefore
  * re-solved by lapx's own lapjv (see bx_linear_assignment), summed since creation / reset. */
 int bx_engine_lap_ties_host(bx_engine *e, int seq0, int nseq, int64_t *total);
-/* Connected components the sparse LAP solver (matching.py:30-108 restated) handed to
- * its per-lane SSP with 17..24 rows (sums[0]) and to its wave-parallel SSP with more rows
- * (sums[1]), over sequences [seq0, seq0+nseq), summed since creation / reset.  Diagnostic: the
+/* Connected components the sparse LAP solver (matching.py:30-108 restated) solved
+ * with its per-lane SSP (small components past the register path, sums[0]) and with its
+ * wave-parallel SSP (components of more than 3 rows, on the association kernel's helper waves:
+ * sums[1]), over sequences [seq0, seq0+nseq), summed since creation / reset.  Diagnostic: the
  * parity tests use it to show a workload exercised both solver paths. */
 int bx_engine_lap_components_host(bx_engine *e, int seq0, int nseq, int64_t *sums);
 
