@@ -187,6 +187,12 @@ __device__ __forceinline__ double wdot(const double* a, const double* b, int n) 
   return s;
 }
 
+// the calling wave's LDS / global writes visible to its other lanes (every user of it runs a whole
+// wave on its own data: one wave per workgroup, or waves with disjoint scratch)
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
 // numpy pairwise sum of x[k]^2 (PW_BLOCKSIZE 128): leaves found by numpy's halving, each leaf
 // summed by 8 lanes (lane j keeps numpy's accumulator r[j]), the leaves folded in the tree's
 // order by lane 0.  Called by all 64 lanes; result valid on every lane.
@@ -282,7 +288,7 @@ __device__ double wpw_norm(const double* x, int n, int* lo, int* ln, double* lea
     const int c = pw_leaves(n, lo, ln);
     ln[PW_MAXLEAF - 1] = c;
   }
-  __syncthreads();
+  wsync();
   const int nl = ln[PW_MAXLEAF - 1];
   for (int base = 0; base < nl; base += 8) {
     const int li = base + (lane >> 3), k = lane & 7;
@@ -312,11 +318,11 @@ __device__ double wpw_norm(const double* x, int n, int* lo, int* ln, double* lea
       leaf[li] = res;
     }
   }
-  __syncthreads();
+  wsync();
   double s = 0.0;
   if (lane == 0) s = pw_fold(n, leaf);
   s = __shfl(s, 0);
-  __syncthreads();
+  wsync();
   return sqrt(s);
 }
 
@@ -516,6 +522,7 @@ struct SsWs {
   int *path, *col4row, *row4col, *rem, *pos, *SR, *SC, *pwlo, *pwln, *sc;
   // doubles
   double *dt, *u, *v, *spc, *meas, *key, *pwleaf, *sd;
+  double* rowbuf = nullptr;  // optional LDS row (64·UQ) for track_update's pairwise norm
 };
 
 // The scratch of one sequence: the LSAP state (3N doubles u v spc, 7N ints path col4row row4col
@@ -579,10 +586,6 @@ __device__ __forceinline__ double bcastd(double v) { return __shfl(v, 0); }
 // loads): what __syncthreads() is in a one-wave workgroup, without waiting for other waves — the
 // match kernel runs its cascade and its solver as two waves of one workgroup, each synchronising
 // only itself.
-__device__ __forceinline__ void wsync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-}
 template <class P, class E>
 __device__ __forceinline__ int wcompact(int n, P pred, E emit) {
   return wave_compact_s(n, pred, emit, SyncWaveG{});
@@ -1825,6 +1828,7 @@ __device__ void kf_update_octet(double* mean, double* cov, const double* z, doub
   double cr[8], mm[8];
   for (int j = 0; j < 8; j++) cr[j] = crow[j];
   for (int q = 0; q < 8; q++) mm[q] = mean[q];
+  const double mr = mean[r];  // (not mm[r]: a run-time index sends the array to scratch)
   double rr[4], S[16], L[16];
   kf_meas_noise(KIND_BYTE, mm, conf, rr);
   for (int i = 0; i < 4; i++)
@@ -1843,7 +1847,7 @@ __device__ void kf_update_octet(double* mean, double* cov, const double* z, doub
   }
   double sm = 0.0;
   for (int k = 0; k < 4; k++) sm += (z[k] - mm[k]) * Kr[k];
-  const double mnew = mm[r] + sm;
+  const double mnew = mr + sm;
   double ks[4];
   for (int j = 0; j < 4; j++) {
     double sv = 0.0;
@@ -1868,37 +1872,42 @@ __device__ void track_update(SsCtx& x, int slot, int di) {
   SsTrk& t = x.trk[slot];
   const double* d = x.det(di);
   const int dk = x.det_in(di);
+  const double* nf = g.nf + ((size_t)x.seq * g.D + dk) * F;
+  const double* pr = g.dprep + ((size_t)x.seq * g.D + dk) * 4;
+  // the register path's two feature rows are loaded before the Kalman update, their latency
+  // under its arithmetic (pool_alloc below changes vmask only: nfeat / feat[] are final here)
+  const int nfeat = t.nfeat;
+  const bool in_regs = nfeat > 0 && F <= 64 * UQ;
+  double rn[UQ], rl[UQ], wl = 0.0;
+  if (in_regs) {
+    const int lv = t.feat[nfeat - 1];
+    const double* last = vecp(g, x.seq, slot, lv);
+    wl = g.vwn[vidx(g, x.seq, slot, lv)];
+#pragma unroll
+    for (int r = 0; r < UQ; r++) {
+      const int q = lane + 64 * r;
+      rn[r] = q < F ? nf[q] : 0.0;
+      rl[r] = q < F ? last[q] : 0.0;
+    }
+  }
   if (lane < 8) {
     double bb[4];
     det_xyah(d, bb);
     kf_update_octet(t.mean, t.cov, bb, d[4], lane);
   }
   if (lane == 0) t.conf = d[4], t.cls = d[5], t.det_ind = d[6];
-  __syncthreads();
-  const double* nf = g.nf + ((size_t)x.seq * g.D + dk) * F;
-  const double* pr = g.dprep + ((size_t)x.seq * g.D + dk) * 4;
+  wsync();
   int v = -1;
   if (lane == 0) v = pool_alloc(t, g.VP);
   v = bcast(v);
-  const int nfeat = t.nfeat;
   if (v < 0) {
     if (lane == 0) atomicExch(g.status, (int)BX_ERR_TRACK_OVERFLOW);
   } else {
     double* dst = vecp(g, x.seq, slot, v);
     const size_t vi = vidx(g, x.seq, slot, v);
-    if (nfeat > 0 && F <= 64 * UQ) {
+    if (in_regs) {
       // the rows in registers (element lane + 64 r in slot r, wdot's order): the EMA vector is
       // written once and its norms come from registers; only numpy's pairwise tree reads it back
-      const int lv = t.feat[nfeat - 1];
-      const double* last = vecp(g, x.seq, slot, lv);
-      const double wl = g.vwn[vidx(g, x.seq, slot, lv)];
-      double rn[UQ], rl[UQ];
-#pragma unroll
-      for (int r = 0; r < UQ; r++) {
-        const int q = lane + 64 * r;
-        rn[r] = q < F ? nf[q] : 0.0;
-        rl[r] = q < F ? last[q] : 0.0;
-      }
       auto rdot = [&](const double* u, const double* v2) {
         double sd = 0.0;
 #pragma unroll
@@ -1922,8 +1931,19 @@ __device__ void track_update(SsCtx& x, int slot, int di) {
         if (q < F) dst[q] = rl[r];
       }
       const double wn = sqrt(rdot(rl, rl));
-      __syncthreads();  // dst visible to the pairwise tree's lane mapping
-      const double pn = wpw_norm(dst, F, x.w.pwlo, x.w.pwln, x.w.pwleaf) + 1e-8;
+      // numpy's pairwise tree reads the row in its own lane mapping: from an LDS copy when the
+      // caller gave one (no store -> load round trip through L2), else from dst
+      const double* prow = dst;
+      if (x.w.rowbuf) {
+#pragma unroll
+        for (int r = 0; r < UQ; r++) {
+          const int q = lane + 64 * r;
+          if (q < F) x.w.rowbuf[q] = rl[r];
+        }
+        prow = x.w.rowbuf;
+      }
+      wsync();  // the row visible to the pairwise tree's lane mapping
+      const double pn = wpw_norm(prow, F, x.w.pwlo, x.w.pwln, x.w.pwleaf) + 1e-8;
       double* dstn = vecnp(g, x.seq, slot, v);
 #pragma unroll
       for (int r = 0; r < UQ; r++) {
@@ -1944,10 +1964,10 @@ __device__ void track_update(SsCtx& x, int slot, int di) {
       const double af = sim > 0.7 ? 1.0 : (sim > 0.4 ? 0.7 : 0.4);
       const double a = clipd(t.base_alpha * cf * af, 0.1, 0.95);
       for (int q = lane; q < F; q += 64) dst[q] = a * last[q] + (1 - a) * nf[q];
-      __syncthreads();
+      wsync();
       const double ns = sqrt(wdot(dst, dst, F)) + 1e-8;
       for (int q = lane; q < F; q += 64) dst[q] = dst[q] / ns;
-      __syncthreads();
+      wsync();
       const double wn = sqrt(wdot(dst, dst, F));
       const double pn = wpw_norm(dst, F, x.w.pwlo, x.w.pwln, x.w.pwleaf) + 1e-8;
       double* dstn = vecnp(g, x.seq, slot, v);
@@ -1978,7 +1998,7 @@ __device__ void track_update(SsCtx& x, int slot, int di) {
     }
   }
   if (lane == 0) track_update_scalars(t, d);
-  __syncthreads();
+  wsync();
 }
 
 // Track.__init__ (track.py:76-131) into a free slot, by one lane (births run lane-parallel).
@@ -2387,20 +2407,28 @@ __global__ void __launch_bounds__(128) SS_MATCH_ATTR
 }
 
 // Track.update for every match of the three stages (tracker.py:139-141): wave per match.
-__global__ void __launch_bounds__(64) ss_update_kernel(SsDev g, int seq0) {
-  __shared__ int lo[PW_MAXLEAF], ln[PW_MAXLEAF];
-  __shared__ double leaf[PW_MAXLEAF];
-  const int b = blockIdx.y, seq = seq0 + b, q = blockIdx.x;
+// SS_UPD_W waves per workgroup, a match each with its own LDS scratch.  (Measured at 256 seq:
+// one wave 0.100 ms, two or four 0.172-0.175 ms.)
+#ifndef SS_UPD_W
+#define SS_UPD_W 1
+#endif
+__global__ void __launch_bounds__(64 * SS_UPD_W) ss_update_kernel(SsDev g, int seq0) {
+  __shared__ int lo[SS_UPD_W][PW_MAXLEAF], ln[SS_UPD_W][PW_MAXLEAF];
+  __shared__ double leaf[SS_UPD_W][PW_MAXLEAF];
+  __shared__ double row[SS_UPD_W][64 * UQ];
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int b = blockIdx.y, seq = seq0 + b, q = blockIdx.x * SS_UPD_W + wv;
   int* sq = g.sq + (size_t)seq * SQS;
-  if (q >= sq[Q_NM]) return;
+  if (q >= sq[Q_NM]) return;  // (wave-uniform; no workgroup barrier below)
   SsWs w{};
   ws_frame(g, seq, w);
   if (w.mt[2 * q] < 0) return;  // a repeated track: ss_post_kernel
-  w.pwlo = lo;
-  w.pwln = ln;
-  w.pwleaf = leaf;
-  SsCtx x{g, w, seq, (int)threadIdx.x, g.trk + (size_t)seq * g.T, sq, g.sqd + (size_t)seq * 2,
-          g.lost + (size_t)seq * LOSTN, 0, 0, 0, 0};
+  w.pwlo = lo[wv];
+  w.pwln = ln[wv];
+  w.pwleaf = leaf[wv];
+  w.rowbuf = row[wv];
+  SsCtx x{g, w, seq, (int)threadIdx.x & 63, g.trk + (size_t)seq * g.T, sq,
+          g.sqd + (size_t)seq * 2, g.lost + (size_t)seq * LOSTN, 0, 0, 0, 0};
   track_update(x, g.order[(size_t)seq * g.T + w.mt[2 * q]], w.mt[2 * q + 1]);
 }
 
@@ -2896,8 +2924,9 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 5, st))) return rc;
   if ((rc = ss_probe_begin(e, 6, st))) return rc;
-  hipLaunchKernelGGL(ss_update_kernel, dim3(d.T < d.D ? d.T : d.D, nseq), dim3(64), 0, st, d,
-                     seq0);
+  hipLaunchKernelGGL(ss_update_kernel,
+                     dim3(((d.T < d.D ? d.T : d.D) + SS_UPD_W - 1) / SS_UPD_W, nseq),
+                     dim3(64 * SS_UPD_W), 0, st, d, seq0);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 6, st))) return rc;
   if ((rc = ss_probe_begin(e, 7, st))) return rc;
