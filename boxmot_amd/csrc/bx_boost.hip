@@ -78,6 +78,11 @@ struct BstDev {
 // sequence, cycles accumulated per phase over all frames [0, 16), event counters [16, 24) and
 // the JV's counters [24, 40).
 constexpr int BST_DBG = 40;
+// lapjv(-cost, extend_cost=True) by the shortest-augmenting-path solve + uniqueness test, lapjv
+// itself only for a tied optimum (legacy_lap_ssp); 0: lapjv always
+#ifndef BX_BOOST_SSP
+#define BX_BOOST_SSP 1
+#endif
 #ifdef BX_PHASE_TIMING
 #define BSTAMP(k)                                                                    \
   do {                                                                               \
@@ -725,7 +730,13 @@ __global__ void __launch_bounds__(BW)
         if (wid == 0) {
           // (generic cost loads: LDS-typed ones, legacy_lap's cas = 3, measured slower at C5,
           // frame kernel 0.413 vs 0.393 ms)
+#if BX_BOOST_SSP
+          bool jv_ran;
+          nmi = legacy_lap_ssp(C, nk, nt, L.jv, L.mi, SyncWaveL{}, jv_ran);
+          BCOUNT(6, jv_ran ? 1 : 0);
+#else
           nmi = legacy_lap(C, nk, nt, L.jv, L.mi, SyncWaveL{});
+#endif
           if (lane == 0) L.u[0] = nmi;
         }
         __syncthreads();

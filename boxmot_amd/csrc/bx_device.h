@@ -1318,7 +1318,7 @@ __device__ __forceinline__ void lap_solve_roots_block(int R, int C, int nroots, 
 #ifdef BX_LAP_NO_HELPERS
   const bool helpers = false;
 #else
-  const bool helpers = w.hs != nullptr && nroots > BX_LAP_HELPER_ROOTS;
+  const bool helpers = w.hT > 0 && nroots > BX_LAP_HELPER_ROOTS;
 #endif
   const int lane_max = LAP_LANE_ROWS;  // rows of a lane-solved component
   int nsteps = 0, ncomp = 0, maxrows = 0, iters = 0, nlane = 0, nwave = 0, nbl = 0;

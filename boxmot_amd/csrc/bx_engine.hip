@@ -1141,7 +1141,9 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
       // until the next association rebuilds them (three blocks: see LdsA's take order), when it
       // fits; else in the sequence's global scratch (one wave either way)
       const int n = R + C;
-#ifdef BX_TIE_NO_LDS
+#if defined(BX_TIE_NO_LDS) || defined(BX_PHASE_TIMING)
+      // (the diagnostic timing build keeps lapjv's state in global scratch: with the stamps added,
+      // the LDS/global pointer select hits an instruction-selection error in this compiler)
       const bool in_lds = false;
 #else
       const bool in_lds = jv_split_d_bytes(n) <= Lo.o_flags - Lo.o_u &&

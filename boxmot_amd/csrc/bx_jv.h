@@ -996,6 +996,127 @@ __device__ void jv_wave64(const double* C, int nr, int nc, JvLds& w, SY sync = S
 #undef JCNT
 }
 
+// lapx's lapjv(extend_cost=True) answer on the real rows when that answer is the ONLY optimum,
+// found without lapjv: scipy's shortest-augmenting-path LSAP (Crouse; rows in order, a Dijkstra
+// over the columns per row, column j on lane j, row i's duals on lane i) on the zero-padded
+// n x n problem lapx solves (n = max(nr, nc) <= 64), then a uniqueness test.  Any optimal
+// assignment uses only edges that are tight (zero reduced cost) under ANY optimal duals, so a
+// second optimum exists iff the tight graph (row i -> the row matched to a tight column of i)
+// has a cycle; one through a real row could change lapx's pairs.  Tight = reduced cost <=
+// LSAP_TIE_TOL, far above the two solvers' rounding (n * eps * |C| ~ 1e-14 at these costs), so a
+// near-tie is treated as a tie.  Returns true with w.x (row -> column, >= nc: unmatched) when
+// the real rows' optimum is unique; false when tied or degenerate (NaN / infinite costs, a
+// dual infeasibility) — the caller then runs lapjv itself.  One wave; sync as jv_wave64's.
+constexpr double LSAP_TIE_TOL = 1e-9;
+template <class SY = SyncBlock, int AS = 0>
+__device__ bool lsap_unique64(const double* C, int nr, int nc, JvLds& w, SY sync = SY{}) {
+  const int n = nr > nc ? nr : nc;
+  const int lane = threadIdx.x & 63;
+  const bool own = lane < n;
+  auto crow_at = [&](int i, int j) -> double {  // row i uniform, column j per lane
+    double c = 0.0;
+    if (i < nr && nc > 0) {
+      const double t = cget_as<AS>(C, nr, nc, i, j < nc ? j : nc - 1);
+      c = j < nc ? t : 0.0;
+    }
+    return c;
+  };
+  double u = 0.0, v = 0.0, spc = INF;
+  int r4c = -1, c4r = -1, path = -1;  // column lane: its row; row lane: its column
+  bool bad = false;
+  for (int cur = 0; cur < n && !bad; cur++) {
+    spc = INF;
+    path = -1;
+    bool sc = false, sr = false;
+    int i = cur, sink = -1;
+    double minv = 0.0;
+    while (sink < 0) {
+      if (lane == i) sr = true;
+      const double ui = rl_d(u, i);
+      const double r = minv + crow_at(i, lane) - ui - v;
+      if (own && !sc && r < spc) {
+        spc = r;
+        path = i;
+      }
+      const double lowest = wave_min_bfly(own && !sc ? spc : INF);
+      if (!(lowest < INF)) {  // NaN / infinite costs: lapjv's own handling
+        bad = true;
+        break;
+      }
+      const bool cand = own && !sc && spc == lowest;
+      int j = first_lane(cand && r4c < 0);  // scipy's tie rule: an unassigned column first
+      if (j < 0) j = first_lane(cand);
+      minv = lowest;
+      if (lane == j) sc = true;
+      const int r4 = rl_i(r4c, j);
+      if (r4 < 0) sink = j;
+      else i = r4;
+    }
+    if (bad) break;
+    // duals: u[cur] += minv; the other rows of SR u[i] += minv - spc[col4row[i]]; SC columns
+    // v[j] -= minv - spc[j]
+    const double sp4 = __shfl(spc, c4r >= 0 ? c4r : 0);
+    if (lane == cur) u += minv;
+    else if (sr) u += minv - sp4;
+    if (sc) v -= minv - spc;
+    // augment along path[] from the sink back to cur
+    int j = sink;
+    while (true) {
+      const int pi = rl_i(path, j);
+      if (lane == j) r4c = pi;
+      const int old = rl_i(c4r, pi);
+      if (lane == pi) c4r = j;
+      if (pi == cur) break;
+      j = old;
+    }
+  }
+  if (bad) return false;
+  // the tight graph: row lane i's successors (the rows matched to its tight unmatched columns)
+  if (own) {
+    w.v[lane] = v;
+    w.y[lane] = r4c;
+  }
+  sync();
+  unsigned long long A = 0;
+  bool infeasible = false;
+  if (own)
+    for (int j = 0; j < n; j++) {
+      double c = 0.0;
+      if (lane < nr && j < nc) c = cget_as<AS>(C, nr, nc, lane, j);
+      const double rc = c - u - w.v[j];
+      if (!(rc >= -LSAP_TIE_TOL)) infeasible = true;  // (NaN included)
+      if (j != c4r && rc <= LSAP_TIE_TOL) A |= 1ull << w.y[j];
+    }
+  if (__any(infeasible)) return false;
+  // cycle test: reachability closure by repeated squaring (masks in w.d), then a real row on a
+  // cycle is a tie
+  unsigned long long* M = (unsigned long long*)w.d;
+  bool tied = false;
+  if (__any(A != 0ull)) {
+    unsigned long long R = A;
+    for (int it = 0; it < 7; it++) {
+      sync();
+      if (own) M[lane] = R;
+      sync();
+      unsigned long long nR = R, m = R;
+      while (m) {
+        const int k = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        nR |= M[k];
+      }
+      const bool grew = __any(nR != R);
+      R = nR;
+      if (!grew) break;
+    }
+    tied = __any(own && lane < nr && ((R >> lane) & 1ull));
+  }
+  if (tied) return false;
+  sync();
+  if (own) w.x[lane] = c4r;
+  sync();
+  return true;
+}
+
 // legacy linear_assignment of the nr x nc matrix C: pairs (row, col) in row order into out
 // (interleaved), returns the count (uniform).  SY: the whole one-wave workgroup, or SyncWaveL
 // when one wave of a larger workgroup solves alone.
@@ -1019,4 +1140,23 @@ __device__ int legacy_lap(const double* C, int nr, int nc, JvLds& jv, int* out, 
         out[2 * p + 1] = jv.x[i];
       },
       sync);
+}
+
+// legacy_lap with the shortest-augmenting-path solve first (lsap_unique64): lapjv itself only
+// when the real rows' optimum is tied (or n > 64).  `jv_ran` tells the caller which it was.
+template <class SY = SyncBlock>
+__device__ int legacy_lap_ssp(const double* C, int nr, int nc, JvLds& jv, int* out, SY sync,
+                              bool& jv_ran) {
+  if ((nr > nc ? nr : nc) <= OW && lsap_unique64<SY, 0>(C, nr, nc, jv, sync)) {
+    jv_ran = false;
+    return wave_compact_s(
+        nr, [&](int i) { return jv.x[i] < nc; },
+        [&](int i, int p) {
+          out[2 * p] = i;
+          out[2 * p + 1] = jv.x[i];
+        },
+        sync);
+  }
+  jv_ran = true;
+  return legacy_lap(C, nr, nc, jv, out, sync);
 }

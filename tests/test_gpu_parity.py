@@ -1040,6 +1040,41 @@ def test_boosttrack_engines_of_different_lds_sizes(torch_cuda):
     assert big.status() == 0
 
 
+class _DupScene:
+    """A scene whose detections are each listed twice (same box, score and embedding): every
+    association with both copies in play has a tied optimum, so the frame kernel's
+    shortest-augmenting-path solve must hand it to lapjv (lapx's own order decides)."""
+
+    def __init__(self, sc, every=1):
+        self.sc, self.every, self.emb_dim = sc, every, sc.emb_dim
+
+    def frame(self, t):
+        d, e = self.sc.frame(t)[:2]
+        k = np.arange(0, d.shape[0], self.every)
+        dd = np.concatenate([d, d[k]], 0)
+        ee = np.concatenate([e, e[k]], 0) if e is not None and e.size else e
+        return dd, ee
+
+
+@pytest.mark.parametrize("variant", ["reid", "noreid"])
+def test_boosttrack_tied_assignments_vs_oracle(torch_cuda, variant):
+    """Tied LAP optima (duplicated detections; without ReID also exactly-zero costs of
+    non-overlapping pairs, tied with lapjv's zero padding): the tie test must send them to lapjv,
+    outputs and Kalman state bitwise against the oracle (lapjv_restated order)."""
+    from boxmot_amd.synth import SyntheticScene
+
+    args = dict(BOOST_ARGS)
+    emb = 48
+    if variant == "noreid":
+        args.update(with_reid=False, use_sb=False, use_vt=False, use_rich_s=False)
+        emb = 0
+    scenes = [_DupScene(SyntheticScene(n_obj=10 + 6 * s, seed=1300 + s, emb_dim=emb,
+                                       emb_dtype=np.float64, layout="crowded" if s % 2 else "grid",
+                                       p_det=0.6, conf_lo=0.3), every=1 + s)
+              for s in range(4)]
+    run_boost_batched(torch_cuda, scenes, 30, args, emb)
+
+
 def test_boosttrack_large_scene_vs_oracle(torch_cuda):
     """A crowded 160-object sequence with 512-d ReID: cost matrices past the LDS budget (HBM
     path), several MFMA output tiles per sequence, LAP solves."""

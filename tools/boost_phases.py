@@ -19,7 +19,7 @@ sys.path.insert(0, str(ROOT))
 LIB = ROOT / "boxmot_amd" / "lib" / "libbxassoc_timing.so"
 PHASES = ["load", "warp+predict", "DLO", "DUO", "keep+colsum", "cost", "fastpath/LAP",
           "validate", "updates", "births", "outputs+deaths"]
-COUNTERS = ["LAP calls", "LAP n", "kept dets", "tracks", "frames", "LAP calls n > 64", "-", "-",
+COUNTERS = ["LAP calls", "LAP n", "kept dets", "tracks", "frames", "LAP calls n > 64", "LAP tied (lapjv ran)", "-",
             "JV free rows", "JV scans", "JV relax steps", "JV sequential scans",
             "JV64 setup (ccrrt+ARR) cyc", "JV64 find cyc", "JV64 scan cyc", "JV64 writeout cyc",
             "JV64 find events", "JV64 scan events", "JV64 path steps", "JV64 ARR iterations",
