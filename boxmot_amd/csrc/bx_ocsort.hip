@@ -473,6 +473,21 @@ size_t lds_bytes(int D, int T, int N, int cost_lds) {
          2 * dI(T) + 2 * dI(2 * N) + 2 * dI(D + T) + 4 * dI(N) + dI(16) + 6 * dI(N) + dI(8);
 }
 
+// lapjv(-cost, extend_cost=True): the shortest-augmenting-path solve + uniqueness test first,
+// lapjv itself for a tied optimum (legacy_lap_ssp; the IoU-only BYTE / OCR rounds tie more often:
+// non-overlapping pairs cost exactly 0, like lapjv's padding).  BX_OCS_SSP=0: lapjv always.
+#ifndef BX_OCS_SSP
+#define BX_OCS_SSP 1
+#endif
+__device__ __forceinline__ int ocs_lap(const double* C, int nr, int nc, JvLds& jv, int* out) {
+#if BX_OCS_SSP
+  bool jv_ran;
+  return legacy_lap_ssp(C, nr, nc, jv, out, SyncBlock{}, jv_ran);
+#else
+  return legacy_lap(C, nr, nc, jv, out);
+#endif
+}
+
 __global__ void __launch_bounds__(OW)
     ocsort_frame_kernel(OcsDev g, int seq0, const float* __restrict__ dets,
                         const int* __restrict__ det_off, double* __restrict__ out,
@@ -659,7 +674,7 @@ __global__ void __launch_bounds__(OW)
           }
         }
         __syncthreads();
-        nmi = legacy_lap(C, nh, nt, L.jv, L.mi);
+        nmi = ocs_lap(C, nh, nt, L.jv, L.mi);
         OCOUNT(0, 1);
         OCOUNT(1, nh > nt ? nh : nt);
       }
@@ -760,7 +775,7 @@ __global__ void __launch_bounds__(OW)
     if (mx > thr) {
       double* C = (nl * nut <= g.cost_lds) ? L.cost : cost;
       iou_fill(C, nl, L.lo, nullptr, nut, L.ut, 0);
-      const int np_ = legacy_lap(C, nl, nut, L.jv, L.mi);
+      const int np_ = ocs_lap(C, nl, nut, L.jv, L.mi);
       for (int k = lane; k < g.N; k += OW) L.fl[k] = 0;
       __syncthreads();
       for (int c = 0; c < np_; c += 8) {
@@ -792,7 +807,7 @@ __global__ void __launch_bounds__(OW)
     if (mx > thr) {
       double* C = (nud * nut <= g.cost_lds) ? L.cost : cost;
       iou_fill(C, nud, L.hi, L.ud, nut, L.ut, 9);
-      const int np_ = legacy_lap(C, nud, nut, L.jv, L.mi);
+      const int np_ = ocs_lap(C, nud, nut, L.jv, L.mi);
       OCOUNT(3, 1);
       OCOUNT(4, nud > nut ? nud : nut);
       for (int k = lane; k < g.N; k += OW) L.rowcnt[k] = L.fl[k] = 0;
