@@ -182,7 +182,7 @@ EXPORTS = [
     "bx_engine_probe", "bx_engine_probe_read", "bx_engine_set_overlap", "bx_engine_frame_stats_host",
     "bx_iou_batch", "bx_pairwise_cost", "bx_aw_max_metric", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
     "bx_kf_multi_predict", "bx_kf_update", "bx_kf_gating_distance", "bx_linear_assignment", "bx_lapjv",
-    "bx_linear_assignment_ex", "bx_engine_lap_ties_host", "bx_engine_lap_components_host",
+    "bx_linear_assignment_ex", "bx_engine_lap_ties_host", "bx_engine_lap_components_host", "bx_engine_set_lap_stats",
     "bx_engine_inputs_released",
     "bx_engine_copy_state", "bx_engine_slots_used_host", "bx_ocsort_copy_state",
     "bx_boost_copy_state", "bx_ss_copy_state",
@@ -242,6 +242,7 @@ _SIGS = {
     "bx_linear_assignment_ex": ([_vp, C.c_int, C.c_int, C.c_double, _vp, _vp, _vp, _vp], C.c_int),
     "bx_engine_lap_ties_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_engine_lap_components_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
+    "bx_engine_set_lap_stats": ([_vp, C.c_int], C.c_int),
     "bx_engine_inputs_released": ([_vp, _vp], C.c_int),
     "bx_engine_copy_state": ([_vp, _vp], C.c_int),
     "bx_ocsort_copy_state": ([_vp, _vp], C.c_int),
@@ -326,7 +327,11 @@ def load(path: Path | None = None):
             "as g; g.build()' or boxmot_amd._native.build())")
     L = C.CDLL(str(p))
     for name, (args, res) in _SIGS.items():
-        fn = getattr(L, name)
+        fn = getattr(L, name, None)
+        if fn is None and not path and "BX_LIB_PATH" in os.environ:
+            continue  # (an older diagnostic build for an A/B: entry points it predates stay unset)
+        if fn is None:
+            raise NativeUnavailable(f"{p} does not export {name}: rebuild the HIP extension")
         fn.argtypes = args
         fn.restype = res
     _lib = L

@@ -686,6 +686,11 @@ struct LapWS {
   __device__ BX_LDS uint16_t* big() const { return (BX_LDS uint16_t*)(hs + 2 * hT + 4); }
   __device__ BX_LDS uint16_t* tw() const { return big() + hT; }
   __device__ BX_LDS uint16_t* sw() const { return tw() + 3 * tws; }
+  // if set: `stamp` stored (system scope: host-visible) whenever this LAP had a component for
+  // the wave solver among more than BX_LAP_HELPER_ROOTS roots — the host's cue to launch the
+  // helper-wave build of the association kernel (the two builds give identical results)
+  int* bigmark = nullptr;
+  int stamp = 0;
   int* comp_stats = nullptr;  // if set: [0] += components solved by the per-lane SSP (past the
                               // register path), [1] += components on the wave-parallel solver
   unsigned long long* dbg = nullptr;  // diagnostic counters (phase-timing builds only)
@@ -1149,6 +1154,9 @@ __device__ __forceinline__ bool lap_component_regs(const int (&rr)[LAP_RM], int 
   return true;
 }
 
+#ifndef BX_HELP_MIN_BIG  // components for the wave solver in one LAP that cue the helper build
+#define BX_HELP_MIN_BIG 1
+#endif
 #ifndef BX_LAP_HELPER_ROOTS
 #define BX_LAP_HELPER_ROOTS 32
 #endif
@@ -1452,6 +1460,9 @@ __device__ __forceinline__ void lap_solve_roots_block(int R, int C, int nroots, 
       wave_sync_lds();
     }
     if (w.dbg && lane == 0) w.dbg[9] = __builtin_amdgcn_s_memtime();
+    if (w.bigmark && lane == 0 && nroots > BX_LAP_HELPER_ROOTS &&
+        (helpers ? *w.nbig() : nbl) >= BX_HELP_MIN_BIG)
+      __hip_atomic_store(w.bigmark, w.stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if ((helpers ? (wid >= 1 && wid <= 3) : wid == 0) && nroots > 0)
     nwave += lap_wave_components(nroots, L, w, helpers, wid, nbl, nsteps);

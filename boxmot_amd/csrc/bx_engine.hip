@@ -184,6 +184,9 @@ int set_err(int code, const std::string& msg) {
 // Device-side view of an engine (passed by value to every kernel).
 struct Dev {
   int S, T, D, F, kind, emb_f64, with_reid, fuse_first, max_time_lost, elds;
+  int lap_stats;  // count LAP components per solver path (bx_engine_set_lap_stats; default off)
+  int* lapmark;   // host-mapped: the launch stamp of the last LAP that wanted the helper waves
+  int lapstamp;   // this launch's stamp
   double low, high, new_thresh, match_thresh, prox, app;
   int* seq;           // [S][SQ_STRIDE] per-sequence scalars (SQ_*)
   uint16_t* act;      // [S][T] active list (slots)
@@ -805,7 +808,10 @@ __global__ __launch_bounds__(WG) void materialize_kernel(Dev P, int s) {
 // K3: the sequential heart of a frame, one workgroup per sequence: detection split, track lists,
 // the three assignments (candidate CSR, exact fp64 costs, lapx-semantics LAP), state/list
 // bookkeeping, id allocation.  Kalman/feature work is emitted as update records for K4/K5.
-template <int KIND>
+// HELP: the LAP's wave solver on the helper waves 1..3 (crowded scenes); without it the
+// components for the wave solver run on wave 0 after its lanes (the host picks the build from the
+// LAPs' marks, DESIGN §2.3: the helper machinery costs an uncrowded frame ~2.5 us of K3)
+template <int KIND, bool HELP>
 __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float* __restrict__ dets,
                                                    const int* __restrict__ det_off) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -933,12 +939,14 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
   W.rlab = lds_ptr<int>(smem + Lo.o_rlab);
   W.colaux = lds_ptr<int>(smem + Lo.o_colaux);
   W.colmin = lds_ptr<int>(smem + Lo.o_colmin);
-  W.comp_stats = seq + SQ_NCOMP17;
+  W.comp_stats = P.lap_stats ? seq + SQ_NCOMP17 : nullptr;  // (off: no reductions, no atomics)
   // the LAP's helper-wave scratch in the candidate sweep's LDS (tboxf .. dconf: dead while the
   // LAP runs; lap_helper_bytes(hT, tws) <= 16 T + 18 D, asserted by the host layout check)
   W.hs = lds_ptr<int>(smem + Lo.o_tboxf);
-  W.hT = (T + 7) & ~7;
+  W.hT = HELP ? (T + 7) & ~7 : 0;
   W.tws = (D + 7) & ~7;
+  W.bigmark = P.lapmark;
+  W.stamp = P.lapstamp;
   uint16_t* e_gcol = P.gcol + (size_t)s * T * D;
   double* e_gcost = P.gcost + (size_t)s * T * D;
   auto put_edge = [&](int e, int col, double cost) {
@@ -1782,6 +1790,8 @@ struct bx_engine {
   int* p_cnt = nullptr;
   int* p_seq = nullptr;     // the sequence's counters row after the last update_host
   int cache_seq = -1;       // sequence whose counters p_seq holds (-1: none / stale)
+  int* h_lapmark = nullptr;  // host-mapped helper-wave cue (Dev::lapmark)
+  int nlaunch = 0;           // association launches so far (the cue's clock)
   // side stream of the frame's fork-join (launch_frame): the ReID feature kernels K1 and K5 run
   // there beside the Kalman/list kernels they share no data with
   hipStream_t side = nullptr;
@@ -1943,7 +1953,13 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
                 hipLaunchKernelGGL(cosine_kernel_any<FT>, dim3(nseq, COS_BLOCKS), dim3(WG), 0, st,
                                    d, seq0, det_off, (const FT*)embs));
   }
-  auto assoc = assoc_kernel<KIND>;
+  // the helper-wave build while LAPs that want it were seen in the last BX_HELP_WINDOW launches
+#ifndef BX_HELP_WINDOW
+#define BX_HELP_WINDOW 64
+#endif
+  e->dev.lapstamp = ++e->nlaunch;
+  const bool help = e->h_lapmark && e->nlaunch - *(volatile int*)e->h_lapmark <= BX_HELP_WINDOW;
+  auto assoc = help ? assoc_kernel<KIND, true> : assoc_kernel<KIND, false>;
   if (int rc = lds_attr((const void*)assoc, e->lds_assoc)) return rc;
   BX_PROBED(BX_STAGE_ASSOC, hipLaunchKernelGGL(assoc, dim3(nseq), dim3(WG), e->lds_assoc, st, d,
                                                seq0, dets, det_off));
@@ -2066,6 +2082,7 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
   d.S = S; d.T = T; d.D = D; d.F = F; d.kind = cfg->kind; d.emb_f64 = cfg->emb_f64;
   d.with_reid = reid; d.fuse_first = cfg->fuse_first_associate;
   d.elds = ELDS_DEFAULT;
+  d.lap_stats = 0;
   d.jvs_stride = (jv_bytes(T + D) + 255) & ~size_t(255);
   d.match_thresh = cfg->match_thresh;
   d.max_time_lost = (int)(cfg->frame_rate / 30.0 * cfg->track_buffer);
@@ -2155,6 +2172,10 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
   HIPCHK(hipHostMalloc(&e->p_out, sizeof(double) * 8 * D));
   HIPCHK(hipHostMalloc(&e->p_cnt, sizeof(int) * 2));
   HIPCHK(hipHostMalloc(&e->p_seq, sizeof(int) * SQ_STRIDE));
+  // the LAPs' helper-wave cue, written by the association kernel, read by the host at launch
+  HIPCHK(hipHostMalloc(&e->h_lapmark, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+  *e->h_lapmark = -(1 << 30);
+  HIPCHK(hipHostGetDevicePointer((void**)&e->dev.lapmark, e->h_lapmark, 0));
   *out = e;
   return BX_OK;
 }
@@ -2181,6 +2202,7 @@ int bx_engine_destroy(bx_engine* e) {
   (void)hipFree(e->h_cnt);
   (void)hipFree(e->h_warp);
   (void)hipHostFree(e->p_dets);
+  if (e->h_lapmark) (void)hipHostFree(e->h_lapmark);
   (void)hipHostFree(e->p_embs);
   (void)hipHostFree(e->p_off);
   (void)hipHostFree(e->p_warp);
@@ -2633,6 +2655,13 @@ int bx_engine_state_set_host(bx_engine* e, int seq, int n, const int32_t* ids, c
     if (cov) HIPCHK(hipMemcpy(kf + 8, cov + 64 * j, 64 * 8, hipMemcpyHostToDevice));
   }
   HIPCHK(hipDeviceSynchronize());
+  return BX_OK;
+}
+
+int bx_engine_set_lap_stats(bx_engine* e, int on) {
+  if (!e) return set_err(BX_ERR_INVALID, "null engine");
+  if (int rc = settle(e)) return rc;
+  e->dev.lap_stats = on != 0;
   return BX_OK;
 }
 

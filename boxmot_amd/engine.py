@@ -138,6 +138,10 @@ class Engine:
         N.check(self._L.bx_engine_lap_components_host(self._h, seq0, nseq, a), "lap_components")
         return {"lane": int(a[0]), "wave": int(a[1])}
 
+    def set_lap_stats(self, on: bool = True) -> None:
+        """Count LAP components for lap_components (bx_engine_set_lap_stats; off by default)."""
+        N.check(self._L.bx_engine_set_lap_stats(self._h, int(bool(on))), "bx_engine_set_lap_stats")
+
     def update_host(self, seq: int, dets: np.ndarray, embs: np.ndarray | None = None,
                     warp: np.ndarray | None = None) -> np.ndarray:
         """One frame of one sequence from host arrays; returns float64 [M, 8]."""

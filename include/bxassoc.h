@@ -155,6 +155,9 @@ int bx_engine_lap_ties_host(bx_engine *e, int seq0, int nseq, int64_t *total);
  * sums[1]), over sequences [seq0, seq0+nseq), summed since creation / reset.  Diagnostic: the
  * parity tests use it to show a workload exercised both solver paths. */
 int bx_engine_lap_components_host(bx_engine *e, int seq0, int nseq, int64_t *sums);
+/* Turn the component counting of bx_engine_lap_components_host on (off by default: it costs the
+ * association kernel reductions and atomics per LAP).  Diagnostic; settles overlap mode first. */
+int bx_engine_set_lap_stats(bx_engine *e, int on);
 
 /* Capacity growth (the reference's track lists are unbounded: bytetrack.py:272-346): copy every
  * sequence's tracker state of `src` into `dst`, a fresh engine with the same kind, sequences and

@@ -35,7 +35,8 @@ def torch_cuda():
     return torch
 
 
-def drive_bench(torch, config, n_seq, n_frames, warmup=10, track_cap=512, det_cap=256):
+def drive_bench(torch, config, n_seq, n_frames, warmup=10, track_cap=512, det_cap=256,
+                lap_stats=False):
     """Run `n_frames` steps of bench.py's workload for `config` the way bench.py runs them (probe
     schedule included, one launch per frame over every sequence, no host sync in between).
     Returns (engine, frames on device, per-frame (out, cnt) on device)."""
@@ -45,6 +46,8 @@ def drive_bench(torch, config, n_seq, n_frames, warmup=10, track_cap=512, det_ca
     dev = torch.device("cuda", 0)
     src = BenchFrames(config, n_seq, dev)
     eng, stages = bench_engine(config, src.n_seq, track_cap, det_cap, overlap=True)
+    if lap_stats:
+        eng.set_lap_stats(True)
     S = src.n_seq
     stream = torch.cuda.current_stream()
     width = 10 if kind == "strongsort" else 8
@@ -205,7 +208,7 @@ def test_botsort_crowded_bench_workload_vs_oracle(torch_cuda):
 
     kind, _, F, params = CONFIGS["botsort_crowded"]
     n_frames = 60
-    eng, frames, outs = drive_bench(torch_cuda, "botsort_crowded", 1024, n_frames)
+    eng, frames, outs = drive_bench(torch_cuda, "botsort_crowded", 1024, n_frames, lap_stats=True)
     tot = eng.lap_components()
     assert tot["lane"] > 0 and tot["wave"] > 0, tot
     per = [eng.lap_components(s, 1) for s in range(1024)]
