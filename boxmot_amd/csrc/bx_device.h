@@ -1323,11 +1323,7 @@ __device__ __forceinline__ void lap_solve_roots_block(int R, int C, int nroots, 
   // (helper waves only past BX_LAP_HELPER_ROOTS roots: the scratch bookkeeping and the two
   // barriers cost the small LAPs of uncrowded scenes more than the occasional 4+-row component
   // solved on wave 0 after its lanes)
-#ifdef BX_LAP_NO_HELPERS
-  const bool helpers = false;
-#else
   const bool helpers = w.hT > 0 && nroots > BX_LAP_HELPER_ROOTS;
-#endif
   const int lane_max = LAP_LANE_ROWS;  // rows of a lane-solved component
   int nsteps = 0, ncomp = 0, maxrows = 0, iters = 0, nlane = 0, nwave = 0, nbl = 0;
   if (w.dbg && wid == 0 && lane == 0) w.dbg[3] = __builtin_amdgcn_s_memtime();

@@ -1149,7 +1149,7 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
       // until the next association rebuilds them (three blocks: see LdsA's take order), when it
       // fits; else in the sequence's global scratch (one wave either way)
       const int n = R + C;
-#if defined(BX_TIE_NO_LDS) || defined(BX_PHASE_TIMING)
+#ifdef BX_PHASE_TIMING
       // (the diagnostic timing build keeps lapjv's state in global scratch: with the stamps added,
       // the LDS/global pointer select hits an instruction-selection error in this compiler)
       const bool in_lds = false;
