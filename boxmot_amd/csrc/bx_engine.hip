@@ -363,9 +363,11 @@ __device__ __forceinline__ void det_measurement(const float* r, double* meas) {
 // Grid (n_seq, ceil(D/K1_DETS)); each wave walks its block's detections with stride 4 (no
 // prefetch of the next row: the lower VGPR count buys more resident waves, which hide more).
 #ifndef BX_K1_DETS
-#define BX_K1_DETS 8
+#define BX_K1_DETS 16
 #endif
-constexpr int K1_DETS = BX_K1_DETS;  // detections per K1 block (2 per wave)
+// detections per K1 block (4 per wave; round 5, interleaved A/Bs at C3: 16 per block 0.5975 /
+// 0.5997 ms per step against 0.6003 / 0.6011 with 8, 32 no better, 64 and 4 worse)
+constexpr int K1_DETS = BX_K1_DETS;
 // FC: the feature width when it is a compile-time constant (REG_F: bounds tests and per-element
 // addressing fold away, measured ~1/3 of the row's VALU instructions), else 0 (P.F).
 template <typename FT, bool NPF, int FC>
