@@ -503,7 +503,10 @@ __global__ __launch_bounds__(WG) void gate_kernel(Dev P, int seq0, const float* 
 // COS_CH = 32-element chunks (one whole 128-B line of each row per chunk: 8 lanes x 16 B), the
 // elementwise divisions done by the loading lane, the next chunk's loads in flight meanwhile.
 // Grid (n_seq, COS_BLOCKS).
-constexpr int COS_BLOCKS = 2;
+#ifndef BX_COS_BLOCKS
+#define BX_COS_BLOCKS 2
+#endif
+constexpr int COS_BLOCKS = BX_COS_BLOCKS;
 constexpr int COS_CH = 32;
 #ifndef BX_COS_P
 #define BX_COS_P 16
