@@ -374,15 +374,16 @@ size_t lds_bytes(int D, int T, int N, int cost_lds, int tb_lds) {
          dI(8);
 }
 
-// One workgroup of 2-4 waves per sequence (frame_threads: four for up to 256 sequences in the
+// One workgroup of 2-6 waves per sequence (frame_threads: six for up to 256 sequences in the
 // launch, three up to 511, two from 512 on — at 1024 sequences two waves each measured 5% faster
-// than one (C2 1.39 -> 1.46 M frames/s) and four 20% slower).  Work over pairs, detections or tracks
+// than one (C2 1.39 -> 1.46 M frames/s) and four 20% slower; at C5, since the LAP no longer runs
+// lapjv, six waves 55.1 k frames/s against 52.5 k with four, 54.6 k with eight, 54.5 k with twelve).  Work over pairs, detections or tracks
 // is spread over all the waves; the order-dependent steps (compactions, the validation's ballots)
 // run in every wave at once on the same LDS data — each wave derives the same counts and writes the
 // same values — except the JV, which wave 0 solves alone (SyncWaveL) while the others wait at the
 // barrier after it.
 #ifndef BX_BOOST_MAX_THREADS
-#define BX_BOOST_MAX_THREADS 256
+#define BX_BOOST_MAX_THREADS 384
 #endif
 constexpr int BW = BX_BOOST_MAX_THREADS > 256 ? BX_BOOST_MAX_THREADS : 256;  // the most threads per sequence
 #ifndef BX_BOOST_THREADS_1024
