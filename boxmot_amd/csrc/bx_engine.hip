@@ -38,7 +38,10 @@ namespace {
 #include "bx_jv.h"
 
 constexpr int CLS_HIST = 8;  // BoT-SORT per-track class-history entries (update_cls)
-constexpr int ELDS_DEFAULT = 1024;  // LAP edges kept in LDS; the rest spill to global scratch
+#ifndef BX_ELDS
+#define BX_ELDS 1024
+#endif
+constexpr int ELDS_DEFAULT = BX_ELDS;  // LAP edges kept in LDS; the rest spill to global scratch
 constexpr int REG_F = 512;   // feature rows up to this width live in registers: 8 per lane
 constexpr int REG_EPL = REG_F / 64;
 constexpr int REG_FP = REG_F + REG_F / 16;  // LDS row stride: 8 pad floats per 128 (np_dn)
