@@ -2048,9 +2048,18 @@ __device__ void track_birth(SsCtx& x, int slot, int di, int id) {
 // detect_crowd_situations' pair test (utils/occlusion_handler.py:45-87; the fork passes tlwh
 // boxes that it reads as xyxy): the track pairs whose intersection exceeds 30 % of either box,
 // counted over the whole grid (block per slice of rows, threads over partners) into Q_CROWDN.
+// Blocks per sequence: 16 for a few sequences (C4's 1024 tracks), 2 for many (each block loads
+// every box of its sequence: at 256 sequences 16 blocks each spent 154 us mostly on those loads);
+// the boxes in dynamic LDS sized to the track capacity.
 constexpr int CROWD_BLOCKS = 16;
+#ifndef BX_CROWD_BLOCKS_MANY
+#define BX_CROWD_BLOCKS_MANY 2
+#endif
+__host__ __device__ constexpr int crowd_blocks(int nseq) {
+  return nseq >= 64 ? BX_CROWD_BLOCKS_MANY : CROWD_BLOCKS;
+}
 __global__ void __launch_bounds__(256) ss_crowd_kernel(SsDev g, int seq0) {
-  __shared__ double box[4 * 1024];
+  extern __shared__ __align__(16) double box[];  // [4 * T]
   const int b = blockIdx.y, seq = seq0 + b;
   int* sq = g.sq + (size_t)seq * SQS;
   const int nn = sq[Q_NTR];
@@ -2060,7 +2069,7 @@ __global__ void __launch_bounds__(256) ss_crowd_kernel(SsDev g, int seq0) {
   for (int k = threadIdx.x; k < nn; k += 256) to_tlwh(trk[order[k]], box + 4 * k);
   __syncthreads();
   int high = 0;
-  for (int i = blockIdx.x; i < nn; i += CROWD_BLOCKS) {
+  for (int i = blockIdx.x; i < nn; i += gridDim.x) {
     const double* bi = box + 4 * i;
     for (int j = i + 1 + threadIdx.x; j < nn; j += 256) {
       const double* bj = box + 4 * j;
@@ -2874,7 +2883,8 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   }
   if ((rc = ss_probe_begin(e, 3, sm))) return rc;
   if (d.crowd)
-    hipLaunchKernelGGL(ss_crowd_kernel, dim3(CROWD_BLOCKS, nseq), dim3(256), 0, sm, d, seq0);
+    hipLaunchKernelGGL(ss_crowd_kernel, dim3(crowd_blocks(nseq), nseq), dim3(256),
+                       sizeof(double) * 4 * d.T, sm, d, seq0);
   hipLaunchKernelGGL(ss_motion_kernel, dim3(d.T, nseq), dim3(64), 0, sm, d, seq0, warps);
   SCHK(hipGetLastError());
   if (!side_all) {
