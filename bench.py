@@ -16,8 +16,10 @@ that stage's launch, `Engine.probe`); the slowest stage is the dominant kernel a
 every timed step.  Its algorithmic bytes per launch (DESIGN.md §4 per-stage model, priced with
 the engine's own per-frame unit counts) over its measured average launch time is `achieved`.
 
-Single process: `python bench.py`.  Multi-GPU: `torch.distributed.run --nproc-per-node N
-bench.py --gpus N` (RCCL only gathers the per-sequence records once, at the end).
+Single process: `python bench.py`.  Multi-GPU: `python bench.py --gpus N` starts N child ranks
+itself (one per GPU, `launch_ranks`), or `torch.distributed.run --nproc-per-node N bench.py
+--gpus N` sets RANK/WORLD_SIZE for it; either way RCCL only gathers the per-sequence records
+once, at the end.
 """
 from __future__ import annotations
 
@@ -338,6 +340,45 @@ def run_dropin(args):
     print(json.dumps(line), flush=True)
 
 
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a torch.distributed launcher: start N child processes of
+    this script, one per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT
+    in their environment; the reference's one-process-per-sequence-pool model, val.py:389-392),
+    wait for all of them and print rank 0's JSON line.  This parent never imports torch.cuda or
+    touches a GPU, and never execs: the children are ordinary subprocesses.  A failing rank ends
+    the run: the others are killed (by their own Popen handles) and the exit code is non-zero."""
+    import subprocess
+
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    argv = [sys.executable, "-u", str(Path(__file__).resolve())] + sys.argv[1:]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen(argv, env=env, stdout=subprocess.PIPE if r == 0 else None))
+    out0 = procs[0].communicate()[0].decode()
+    rc0 = procs[0].returncode
+    rcs = [rc0]
+    for p in procs[1:]:
+        if rc0 != 0 and p.poll() is None:
+            p.kill()
+        rcs.append(p.wait())
+    bad = [(r, c) for r, c in enumerate(rcs) if c != 0]
+    sys.stdout.write(out0)
+    sys.stdout.flush()
+    if bad:
+        sys.stderr.write(f"bench.py --gpus {n}: rank(s) failed {bad}\n")
+        raise SystemExit(1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -368,19 +409,34 @@ def main():
         return
     if args.dropin:
         return run_dropin(args)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus)  # this process stays off the GPU
 
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting {world} ranks",
+              file=sys.stderr)
     dist = None
     backend = os.environ.get("BX_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI on ROCm
     if world > 1:
         import torch.distributed as dist
 
+        ndev = torch.cuda.device_count()  # counts devices without initialising one
+        if backend == "nccl" and world > ndev:
+            # RCCL: one rank per GPU, no oversubscription (gloo keeps the 1-GPU modulo rehearsal)
+            print(f"bench.py: {world} ranks over RCCL need {world} GPUs, {ndev} visible",
+                  file=sys.stderr)
+            raise SystemExit(3)
+        if ndev == 0:
+            raise SystemExit("bench.py: no HIP device visible")
         # one process per GPU; modulo only so a 1-GPU rehearsal (gloo) can run 2 ranks
-        torch.cuda.set_device(local % torch.cuda.device_count())
+        torch.cuda.set_device(local % ndev)
         dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
@@ -551,6 +607,11 @@ def main():
                        "n_dets_mean": round(mean_d, 1), "feat_dim": F,
                        "emb_dtype": "f64" if emb_bytes == 8 else "f32",
                        "parallelism": f"seq-sharded x{world}",
+                       "sequences_gathered": int(allrec.shape[0]),
+                       **({"last_frame_checksums": {str(int(g)): c for g, c in
+                                                    sorted(zip(allrec[:, 0], allrec[:, 4]))}}
+                          if c5 else {}),
+                       "dist_backend": backend if world > 1 else None,
                        "timed_frames": [t_first + 1, total],
                        **({"feature_overlap": not args.no_overlap}
                           if kind == "botsort" and F else {})},

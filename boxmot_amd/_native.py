@@ -77,7 +77,9 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     objdir = LIB_DIR / "obj"
     objdir.mkdir(parents=True, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    flags = [f for f in HIPCC_FLAGS if f != "-shared"]
+    # BX_HIPCC_EXTRA: extra compile flags for a debug build (e.g. -DBX_CHECK: device-side bounds
+    # checks latched as engine errors); part of the toolchain stamp, so switching rebuilds
+    flags = [f for f in HIPCC_FLAGS if f != "-shared"] + os.environ.get("BX_HIPCC_EXTRA", "").split()
     link_flags = [f for f in HIPCC_FLAGS if f.startswith("--offload-arch")] + ["-shared", "-fPIC"]
     stamp_file = objdir / "toolchain.stamp"
     stamp = _toolchain_stamp(hipcc, flags)
@@ -183,6 +185,7 @@ EXPORTS = [
     "bx_iou_batch", "bx_pairwise_cost", "bx_aw_max_metric", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
     "bx_kf_multi_predict", "bx_kf_update", "bx_kf_gating_distance", "bx_linear_assignment", "bx_lapjv",
     "bx_linear_assignment_ex", "bx_engine_lap_ties_host", "bx_engine_lap_components_host", "bx_engine_set_lap_stats",
+    "bx_engine_force_assoc_build", "bx_legacy_lap_pair",
     "bx_engine_inputs_released",
     "bx_engine_copy_state", "bx_engine_slots_used_host", "bx_ocsort_copy_state",
     "bx_boost_copy_state", "bx_ss_copy_state",
@@ -243,6 +246,8 @@ _SIGS = {
     "bx_engine_lap_ties_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_engine_lap_components_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_engine_set_lap_stats": ([_vp, C.c_int], C.c_int),
+    "bx_engine_force_assoc_build": ([_vp, C.c_int], C.c_int),
+    "bx_legacy_lap_pair": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "bx_engine_inputs_released": ([_vp, _vp], C.c_int),
     "bx_engine_copy_state": ([_vp, _vp], C.c_int),
     "bx_ocsort_copy_state": ([_vp, _vp], C.c_int),

@@ -692,7 +692,8 @@ struct LapWS {
   int* bigmark = nullptr;
   int stamp = 0;
   int* comp_stats = nullptr;  // if set: [0] += components solved by the per-lane SSP (past the
-                              // register path), [1] += components on the wave-parallel solver
+                              // register path), [1] += components on the wave-parallel solver,
+                              // [2] += those of [1] solved on the helper waves 1..3
   unsigned long long* dbg = nullptr;  // diagnostic counters (phase-timing builds only)
 };
 __host__ __device__ inline size_t lap_helper_bytes(int hT, int tws) {
@@ -1472,6 +1473,7 @@ __device__ __forceinline__ void lap_solve_roots_block(int R, int C, int nroots, 
     if (lane == 0 && (sa | nwave)) {  // (nwave is wave-uniform)
       atomicAdd(&w.comp_stats[0], sa);
       atomicAdd(&w.comp_stats[1], nwave);
+      if (helpers) atomicAdd(&w.comp_stats[2], nwave);
     }
   }
   if (w.dbg && wid == 0) {

@@ -242,6 +242,7 @@ enum {
   SQ_NHIGH, SQ_NPAIR, SQ_NDET,  // last frame's high dets, gated pairs, dets (statistics)
   SQ_NTIE,                       // associations re-solved by lapx's lapjv (tied optimum), total
   SQ_NCOMP17, SQ_NCOMPW,         // LAP components on the per-lane SSP / the wave SSP
+  SQ_NCOMPH,                     // ... of which on the helper waves 1..3 (helper build)
   SQ_STRIDE = 16
 };
 // update records: x = slot | kind << 16, y = detection index within the sequence's frame
@@ -1799,7 +1800,8 @@ struct bx_engine {
   int* p_seq = nullptr;     // the sequence's counters row after the last update_host
   int cache_seq = -1;       // sequence whose counters p_seq holds (-1: none / stale)
   int* h_lapmark = nullptr;  // host-mapped helper-wave cue (Dev::lapmark)
-  int nlaunch = 0;           // association launches so far (the cue's clock)
+  uint32_t nlaunch = 0;      // association launches so far (the cue's clock; wraps, compared mod 2^32)
+  int force_help = -1;       // bx_engine_force_assoc_build: -1 cue-driven, 0 / 1 that build always
   // side stream of the frame's fork-join (launch_frame): the ReID feature kernels K1 and K5 run
   // there beside the Kalman/list kernels they share no data with
   hipStream_t side = nullptr;
@@ -1822,6 +1824,8 @@ struct bx_engine {
   double* h_cwarp = nullptr;  // [C][6] the class calls' warps
 };
 
+hipError_t bx_lds_attr(const void* kern, size_t bytes);  // below (never lowers a limit)
+
 namespace {
 
 template <typename T>
@@ -1832,16 +1836,10 @@ T* carve(char*& p, size_t n) {
   return r;
 }
 
-// hipFuncSetAttribute once per (kernel, size) for > 64 KiB dynamic LDS
+// the dynamic-LDS limit for > 64 KiB, per device and never lowered (bx_lds_attr, below)
 int lds_attr(const void* kern, size_t bytes) {
-  static std::mutex mu;
-  static std::vector<std::pair<const void*, size_t>> done;
   if (bytes <= 65536) return BX_OK;
-  std::lock_guard<std::mutex> lk(mu);
-  for (auto& d : done)
-    if (d.first == kern && d.second >= bytes) return BX_OK;
-  HIPCHK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-  done.emplace_back(kern, bytes);
+  HIPCHK(bx_lds_attr(kern, bytes));
   return BX_OK;
 }
 
@@ -1965,8 +1963,11 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
 #ifndef BX_HELP_WINDOW
 #define BX_HELP_WINDOW 64
 #endif
-  e->dev.lapstamp = ++e->nlaunch;
-  const bool help = e->h_lapmark && e->nlaunch - *(volatile int*)e->h_lapmark <= BX_HELP_WINDOW;
+  e->dev.lapstamp = (int)++e->nlaunch;
+  const bool help = e->force_help >= 0
+                        ? e->force_help != 0
+                        : e->h_lapmark && (uint32_t)(e->nlaunch - (uint32_t)*(volatile int*)
+                                                         e->h_lapmark) <= BX_HELP_WINDOW;
   auto assoc = help ? assoc_kernel<KIND, true> : assoc_kernel<KIND, false>;
   if (int rc = lds_attr((const void*)assoc, e->lds_assoc)) return rc;
   BX_PROBED(BX_STAGE_ASSOC, hipLaunchKernelGGL(assoc, dim3(nseq), dim3(WG), e->lds_assoc, st, d,
@@ -2182,7 +2183,7 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
   HIPCHK(hipHostMalloc(&e->p_seq, sizeof(int) * SQ_STRIDE));
   // the LAPs' helper-wave cue, written by the association kernel, read by the host at launch
   HIPCHK(hipHostMalloc(&e->h_lapmark, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
-  *e->h_lapmark = -(1 << 30);
+  *e->h_lapmark = (int)(0u - (BX_HELP_WINDOW + 1u));  // "long ago" on the wrapping clock
   HIPCHK(hipHostGetDevicePointer((void**)&e->dev.lapmark, e->h_lapmark, 0));
   *out = e;
   return BX_OK;
@@ -2464,10 +2465,11 @@ int bx_engine_lap_components_host(bx_engine* e, int seq0, int nseq, int64_t* sum
   std::vector<int> v((size_t)nseq * SQ_STRIDE);
   HIPCHK(hipMemcpy(v.data(), e->dev.seq + (size_t)seq0 * SQ_STRIDE, sizeof(int) * v.size(),
                    hipMemcpyDeviceToHost));
-  sums[0] = sums[1] = 0;
+  sums[0] = sums[1] = sums[2] = 0;
   for (int q = 0; q < nseq; q++) {
     sums[0] += v[(size_t)q * SQ_STRIDE + SQ_NCOMP17];
     sums[1] += v[(size_t)q * SQ_STRIDE + SQ_NCOMPW];
+    sums[2] += v[(size_t)q * SQ_STRIDE + SQ_NCOMPH];
   }
   return BX_OK;
 }
@@ -2670,6 +2672,13 @@ int bx_engine_set_lap_stats(bx_engine* e, int on) {
   if (!e) return set_err(BX_ERR_INVALID, "null engine");
   if (int rc = settle(e)) return rc;
   e->dev.lap_stats = on != 0;
+  return BX_OK;
+}
+
+int bx_engine_force_assoc_build(bx_engine* e, int mode) {
+  if (!e || mode < -1 || mode > 1) return set_err(BX_ERR_INVALID, "bad assoc build mode");
+  if (int rc = settle(e)) return rc;
+  e->force_help = mode;
   return BX_OK;
 }
 

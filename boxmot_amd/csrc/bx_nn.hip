@@ -20,6 +20,7 @@
 #include "bx_device.h"
 
 int bx_record_error(int code, const char* msg);  // bx_engine.hip (shared bx_last_error)
+hipError_t bx_lds_attr(const void* kern, size_t bytes);  // bx_engine.hip (never lowers a limit)
 
 namespace {
 
@@ -295,13 +296,9 @@ int nn_launch(const double* S, int G, const double* Dm, int D, int F, const int*
               unsigned long long* keys, hipStream_t st) {
   using P = NnTile<RT, CT, WR, WC>;
   const size_t lds = sizeof(double) * 2 * P::STAGE;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)nn_cosine_mfma_kernel<RT, CT, WR, WC>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return bx_record_error(BX_ERR_HIP, "hipFuncSetAttribute(nn_cosine_mfma_kernel)");
-    attr = true;
-  }
+  // (per device, never lowered: bx_lds_attr)
+  if (bx_lds_attr((const void*)nn_cosine_mfma_kernel<RT, CT, WR, WC>, lds) != hipSuccess)
+    return bx_record_error(BX_ERR_HIP, "hipFuncSetAttribute(nn_cosine_mfma_kernel)");
   const int nrb = (G + P::BM - 1) / P::BM, ncb = (D + P::BN - 1) / P::BN;
   hipLaunchKernelGGL((nn_cosine_mfma_kernel<RT, CT, WR, WC>), dim3(nrb * ncb), dim3(P::NT), lds,
                      st, S, G, Dm, D, F, tgt, keys);

@@ -8,6 +8,8 @@
 #include "../../include/bxassoc.h"
 #include "bx_device.h"
 
+hipError_t bx_lds_attr(const void* kern, size_t bytes);  // bx_engine.hip (never lowers a limit)
+
 using namespace bx;
 
 int bx_record_error(int code, const char* msg);  // bx_engine.hip (shared bx_last_error)
@@ -268,6 +270,21 @@ int grid_for(size_t n) {
 // 1 = extend_cost (zero padding to max(nr, nc), read through cget), 2 = cost_limit (the
 // (nr+nc)^2 extension with cost_limit / 2 off the diagonal blocks, read through an accessor).
 // State in LDS when gst is null, else in global memory at gst.
+// The legacy association.linear_assignment both ways on one matrix (n <= 64): lapx's lapjv
+// (legacy_lap) and the shortest-augmenting-path solve with its uniqueness certificate
+// (legacy_lap_ssp, lapjv only on a tie), for the op-level test that they agree.
+__global__ __launch_bounds__(OW) void legacy_lap_pair_kernel(const double* cost, int nr, int nc,
+                                                             int32_t* a, int32_t* b,
+                                                             int32_t* info) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  JvLds w = jv_bind(smem, nr > nc ? nr : nc);
+  const int na = legacy_lap(cost, nr, nc, w, a);
+  __syncthreads();
+  bool ran = false;
+  const int nb = legacy_lap_ssp(cost, nr, nc, w, b, SyncBlock{}, ran);
+  if (threadIdx.x == 0) info[0] = na, info[1] = nb, info[2] = ran ? 1 : 0;
+}
+
 __global__ __launch_bounds__(OW) void lapjv_kernel(const double* cost, int nr, int nc, int mode,
                                                    double lim, unsigned char* gst, int32_t* x,
                                                    int32_t* y) {
@@ -448,14 +465,30 @@ int bx_linear_assignment_ex(const double* cost, int nr, int nc, double thresh, i
   int32_t* tied = (int32_t*)(jvs + jvb);
   double* gcost = (double*)(jvs + jvb + 64);
   uint16_t* gcol = (uint16_t*)(gcost + ne);
-  if (lds > 65536)
-    OPCHK(hipFuncSetAttribute((const void*)lap_dense_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  // (never lowers the limit a concurrent call on another thread or stream launches with)
+  if (lds > 65536) OPCHK(bx_lds_attr((const void*)lap_dense_kernel, lds));
   hipLaunchKernelGGL(lap_dense_kernel, dim3(1), dim3(WG), lds, st, cost, nr, nc, thresh, elds,
                      gcol, gcost, jvs, jv_lds, x, y, tied);
   OPCHK(hipGetLastError());
   if (tied_out) OPCHK(hipMemcpyAsync(tied_out, tied, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
   OPCHK(hipFreeAsync(ws, st));
+  return BX_OK;
+}
+
+int bx_legacy_lap_pair(const double* cost, int nr, int nc, int32_t* pairs_jv, int32_t* pairs_ssp,
+                       int32_t* info, void* stream) {
+  if (nr < 0 || nc < 0 || (nr > nc ? nr : nc) > OW || !info)
+    return op_err(BX_ERR_INVALID, "bx_legacy_lap_pair: 0 <= nr, nc <= 64");
+  hipStream_t st = (hipStream_t)stream;
+  if (!nr || !nc) {
+    const int32_t z[3] = {0, 0, 0};
+    OPCHK(hipMemcpyAsync(info, z, sizeof(z), hipMemcpyHostToDevice, st));
+    return BX_OK;
+  }
+  const size_t lds = jv_bytes(nr > nc ? nr : nc);
+  hipLaunchKernelGGL(legacy_lap_pair_kernel, dim3(1), dim3(OW), lds, st, cost, nr, nc, pairs_jv,
+                     pairs_ssp, info);
+  OPCHK(hipGetLastError());
   return BX_OK;
 }
 
@@ -480,9 +513,7 @@ int bx_lapjv(const double* cost, int nr, int nc, int extend_cost, double cost_li
   unsigned char* gst = nullptr;
   if (lds > 160 * 1024) OPCHK(hipMallocAsync((void**)&gst, lds, st));
   const size_t dyn = gst ? 0 : lds;
-  if (dyn > 65536)
-    OPCHK(hipFuncSetAttribute((const void*)lapjv_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+  if (dyn > 65536) OPCHK(bx_lds_attr((const void*)lapjv_kernel, dyn));
   hipLaunchKernelGGL(lapjv_kernel, dim3(1), dim3(OW), dyn, st, cost, nr, nc, mode, cost_limit,
                      gst, x, y);
   OPCHK(hipGetLastError());

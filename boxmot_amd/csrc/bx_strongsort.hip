@@ -1006,6 +1006,7 @@ struct LsapJob {
   double max_d;
   int R, CC, tr, kind, np;
   int flag;
+  int abort;  // set by either wave on a timeout: both stop handing over, nobody writes np / flag
 };
 struct SsCtx {
   const SsDev& g;
@@ -1049,15 +1050,22 @@ __device__ __forceinline__ const double* lsap_mat(const SsDev& g, int seq, int k
 #define SS_SPIN_TICKS 200000000ull
 #endif
 // wait until *flag != v (want_ne) or == v (!want_ne); returns the value seen, or v after a timeout
+// or once the other wave has aborted (*abort set; a timeout here sets it): after that neither
+// wave waits again, so one fault costs one SS_SPIN_TICKS, not one per remaining hand-off
 __device__ __forceinline__ int lds_flag_wait(int* flag, int v, bool want_ne, int* status,
-                                             bool& timed_out) {
+                                             int* abort, bool& timed_out) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     const int f = (int)__builtin_amdgcn_readfirstlane(
         (unsigned)__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
     if ((f != v) == want_ne) return f;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > SS_SPIN_TICKS) {
-      if ((threadIdx.x & 63) == 0) atomicExch(status, (int)BX_ERR_INVALID);
+    const bool ab = __builtin_amdgcn_readfirstlane((unsigned)__hip_atomic_load(
+                        abort, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
+    if (ab || __builtin_amdgcn_s_memrealtime() - t0 > SS_SPIN_TICKS) {
+      if ((threadIdx.x & 63) == 0) {
+        atomicExch(status, (int)BX_ERR_INVALID);
+        __hip_atomic_store(abort, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       timed_out = true;
       return v;
     }
@@ -1124,6 +1132,12 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       (void*)pbu, (short)0, (int)__builtin_amdgcn_readfirstlane((unsigned)(8 * x.g.T * x.g.D)),
       0x00020000);
   auto ld_elem = [&](int roff_r, int q) {  // row element offset roff_r (wave-uniform), slot q
+#ifdef BX_CHECK
+    // debug builds: a raw buffer load past num_records reads 0 instead of faulting, so an
+    // indexing slip would become a silent wrong cost; latch it as an engine error instead
+    if ((unsigned long long)cb[q] + 8ull * (unsigned)roff_r >= 8ull * x.g.T * x.g.D)
+      atomicExch(x.g.status, (int)BX_ERR_INVALID);
+#endif
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
                                           rsrc, cb[q], __builtin_amdgcn_readfirstlane(8 * roff_r), 0));
   };
@@ -1417,6 +1431,17 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
 
 enum { M_GATED = 0, M_IOU = 1 };
 
+// max_distance of the matching_cascade a detection takes part in (tracker.py:206-233): stage 1
+// (confidence >= conf_thresh_high) matching_threshold * 0.8, stage 2 (medium confidence) the
+// threshold itself.  The one definition both ss_cost_kernel's clamp and ss_match_kernel's stage
+// loop use, so stage membership and the stored clamp can never disagree.
+__device__ __forceinline__ double ss_stage_max_d(double thr, int stage) {
+  return stage == 0 ? thr * 0.8 : thr;
+}
+__device__ __forceinline__ double ss_det_max_d(double conf, double thi, double thr) {
+  return ss_stage_max_d(thr, conf >= thi ? 0 : 1);
+}
+
 // _enhance_cost_matrix (linear_assignment.py:251-273) of one entry, unclamped
 __device__ __forceinline__ double enhance_v(double tq, double tcls, double tconf, const double* d,
                                             double e) {
@@ -1578,7 +1603,7 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
     if (ls) v *= 1.05;
     if (g.idw > 0) v *= (1.0 - pb);
     double e = enhance(t, d, v);
-    const double md = d[4] >= g.thi ? thr * 0.8 : thr;
+    const double md = ss_det_max_d(d[4], g.thi, thr);
     if (e > md) e = md + 1e-5;
     out[c] = e;
     outT[(size_t)c * g.T] = e;
@@ -1593,8 +1618,8 @@ __device__ __forceinline__ void lsap_server(SsCtx& x, LsapJob* jb, const int* ro
                                             const int* cidx) {
   for (;;) {
     bool to = false;
-    const int f = lds_flag_wait(&jb->flag, 0, true, x.g.status, to);
-    if (f < 0 || to) return;  // exit posted (the cascade always posts it last), or a timeout
+    const int f = lds_flag_wait(&jb->flag, 0, true, x.g.status, &jb->abort, to);
+    if (f < 0 || to) return;  // exit posted (the cascade always posts it last), or aborted
     const double mx = jb->max_d;
     const int R = jb->R, CC = jb->CC, kind = jb->kind;
     const bool tr = jb->tr != 0;
@@ -1604,6 +1629,11 @@ __device__ __forceinline__ void lsap_server(SsCtx& x, LsapJob* jb, const int* ro
         : CC <= 512  ? lsap_wave<8, true>(x, P, roff, cidx, mx, R, CC, tr)
         : CC <= 1024 ? lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr)
                      : lsap_wave<32, true>(x, P, roff, cidx, mx, R, CC, tr);
+    // the cascade gave up on this job (timeout): it may have posted another one since, which
+    // this answer must not overwrite
+    if (__builtin_amdgcn_readfirstlane((unsigned)__hip_atomic_load(
+            &jb->abort, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0)
+      return;
     if (x.lane == 0) jb->np = np;
     wsync();
     if (x.lane == 0) __hip_atomic_store(&jb->flag, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1692,10 +1722,14 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
       jb->kind = kind;
     }
     wsync();
-    if (lane == 0) __hip_atomic_store(&jb->flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    bool to = false;
-    lds_flag_wait(&jb->flag, 0, false, g.status, to);
-    np_ = to ? 0 : jb->np;  // (a timeout latched BX_ERR_INVALID: the frame is void)
+    bool to = __builtin_amdgcn_readfirstlane((unsigned)__hip_atomic_load(
+                  &jb->abort, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
+    if (!to) {  // (after an abort nothing is posted: the frame is void, BX_ERR_INVALID latched)
+      if (lane == 0)
+        __hip_atomic_store(&jb->flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      lds_flag_wait(&jb->flag, 0, false, g.status, &jb->abort, to);
+    }
+    np_ = to ? 0 : jb->np;
   }
 #ifdef BX_PHASE_TIMING
   wsync();
@@ -2262,7 +2296,7 @@ __global__ void __launch_bounds__(128) SS_MATCH_ATTR
   const int lane = threadIdx.x & 63, b = blockIdx.x, seq = seq0 + b;
   SsWs w;
   ws_carve(g, seq, w, ss_lds);
-  if (threadIdx.x == 0) job.flag = 0;
+  if (threadIdx.x == 0) job.flag = 0, job.abort = 0;
   __syncthreads();  // the only barrier of both waves; from here each synchronises itself
   // the LSAP's rows' offsets and columns' indices (written by the cascade wave, read by the
   // solver wave): sage and flt
@@ -2335,7 +2369,7 @@ __global__ void __launch_bounds__(128) SS_MATCH_ATTR
     const int* ti = w.conf_t;
     const int* di = w.hi;
     int nt = ncf, nd = nhi;
-    double md = thr * 0.8;
+    double md = ss_stage_max_d(thr, 0);
     int kind = M_GATED;
     if (st == 1) {
       // the unmatched tracks are all confirmed (a subset of conf_t)
@@ -2349,7 +2383,7 @@ __global__ void __launch_bounds__(128) SS_MATCH_ATTR
       ti = w.ti2;
       nt = naut;
       di = w.rd;
-      md = thr;
+      md = ss_stage_max_d(thr, 1);
     } else if (st == 2) {
       ncand = nun;
       for (int k = lane; k < nun; k += 64) w.cand[k] = w.unconf_t[k];

@@ -134,9 +134,14 @@ class Engine:
         wave-parallel SSP (more than 3 rows) since creation (bx_engine_lap_components_host), over
         [seq0, seq0+nseq)."""
         nseq = self.n_seq - seq0 if nseq is None else nseq
-        a = (C.c_int64 * 2)()
+        a = (C.c_int64 * 3)()
         N.check(self._L.bx_engine_lap_components_host(self._h, seq0, nseq, a), "lap_components")
-        return {"lane": int(a[0]), "wave": int(a[1])}
+        return {"lane": int(a[0]), "wave": int(a[1]), "helper": int(a[2])}
+
+    def force_assoc_build(self, mode: int) -> None:
+        """-1: the association kernel build is picked per launch from the helper-wave cue
+        (default); 0 / 1: always the wave-0-only / helper-wave build (bx_engine_force_assoc_build)."""
+        N.check(self._L.bx_engine_force_assoc_build(self._h, int(mode)), "force_assoc_build")
 
     def set_lap_stats(self, on: bool = True) -> None:
         """Count LAP components for lap_components (bx_engine_set_lap_stats; off by default)."""

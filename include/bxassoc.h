@@ -150,11 +150,17 @@ int bx_engine_probe_read(bx_engine *e, double *total_ms, int *count);
  * re-solved by lapx's own lapjv (see bx_linear_assignment), summed since creation / reset. */
 int bx_engine_lap_ties_host(bx_engine *e, int seq0, int nseq, int64_t *total);
 /* Connected components the sparse LAP solver (matching.py:30-108 restated) solved
- * with its per-lane SSP (small components past the register path, sums[0]) and with its
- * wave-parallel SSP (components of more than 3 rows, on the association kernel's helper waves:
- * sums[1]), over sequences [seq0, seq0+nseq), summed since creation / reset.  Diagnostic: the
- * parity tests use it to show a workload exercised both solver paths. */
+ * with its per-lane SSP (small components past the register path, sums[0]), with its
+ * wave-parallel SSP (components of more than 3 rows: sums[1]) and, of those, on the association
+ * kernel's helper waves 1..3 (sums[2]), over sequences [seq0, seq0+nseq), summed since creation
+ * / reset.  sums has 3 entries.  Diagnostic: the parity tests use it to show a workload
+ * exercised every solver path. */
 int bx_engine_lap_components_host(bx_engine *e, int seq0, int nseq, int64_t *sums);
+/* Which build of the association kernel runs (BoT-SORT / ByteTrack engines): -1 (default) the
+ * host picks per launch from the device's helper-wave cue; 0 always the wave-0-only build; 1
+ * always the helper-wave build.  Both builds give identical results; tests force each to prove
+ * it.  Settles overlap mode first. */
+int bx_engine_force_assoc_build(bx_engine *e, int mode);
 /* Turn the component counting of bx_engine_lap_components_host on (off by default: it costs the
  * association kernel reductions and atomics per LAP).  Diagnostic; settles overlap mode first. */
 int bx_engine_set_lap_stats(bx_engine *e, int on);
@@ -255,6 +261,14 @@ int bx_linear_assignment_ex(const double *cost, int nr, int nc, double thresh, i
  * ValueError text for a non-square cost without extend_cost. */
 int bx_lapjv(const double *cost, int nr, int nc, int extend_cost, double cost_limit, int32_t *x,
              int32_t *y, void *stream);
+/* Test entry point of the legacy association.linear_assignment (association.py:109; OCSort /
+ * BoostTrack) for a dense [nr][nc] float64 cost, nr, nc <= 64: lapx's lapjv order (the engines'
+ * legacy_lap) into pairs_jv and the shortest-augmenting-path solve with its uniqueness
+ * certificate (legacy_lap_ssp, which runs lapjv itself on a tie) into pairs_ssp, both
+ * [min(nr,nc)][2] (row, col) in row order.  info[3] (device) = {pairs_jv count, pairs_ssp count,
+ * 1 if legacy_lap_ssp fell back to lapjv}.  The two must always agree. */
+int bx_legacy_lap_pair(const double *cost, int nr, int nc, int32_t *pairs_jv, int32_t *pairs_ssp,
+                       int32_t *info, void *stream);
 
 #ifdef __cplusplus
 }

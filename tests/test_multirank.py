@@ -212,3 +212,46 @@ def test_gather_records_over_rccl_single_gpu():
         torch.cuda.synchronize()
     finally:
         dist.destroy_process_group()
+
+
+def _bench(args, backend, timeout=900):
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["BX_DIST_BACKEND"] = backend
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_gpus_n_refuses_more_ranks_than_gpus_over_rccl():
+    """`bench.py --gpus 2` without a launcher starts two ranks itself; over RCCL each rank refuses
+    a world larger than the visible device count (none here), and the launcher exits non-zero
+    instead of timing one GPU and reporting it as two."""
+    r = _bench(["--gpus", "2", "--config", "boosttrack_mot8", "--steps", "1", "--warmup", "1",
+                "--no-cpu-baseline"], "nccl", timeout=300)
+    assert r.returncode != 0
+    assert "need 2 GPUs" in r.stderr, r.stderr[-2000:]
+    assert "rank(s) failed" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_launches_two_ranks():
+    """`python bench.py --gpus 2` (no torch.distributed launcher) on the one-GPU box with gloo:
+    two ranks share the card (modulo rehearsal), C5's eight sequences are LPT-sharded over them,
+    the line reports n_gpus 2 with all eight gathered, and every sequence's last-frame checksum
+    equals the one-rank run's (sharding never changes a sequence's outputs)."""
+    args = ["--config", "boosttrack_mot8", "--steps", "3", "--warmup", "2", "--no-cpu-baseline"]
+    two = _bench(["--gpus", "2"] + args, "gloo")
+    assert two.returncode == 0, two.stderr[-3000:]
+    l2 = json.loads(two.stdout.strip().splitlines()[-1])
+    assert l2["n_gpus"] == 2
+    assert l2["config"]["sequences_gathered"] == 8
+    assert sorted(map(int, l2["config"]["last_frame_checksums"])) == list(range(8))
+    one = _bench(["--gpus", "1"] + args, "gloo")
+    assert one.returncode == 0, one.stderr[-3000:]
+    l1 = json.loads(one.stdout.strip().splitlines()[-1])
+    assert l1["n_gpus"] == 1
+    assert l1["config"]["last_frame_checksums"] == l2["config"]["last_frame_checksums"]
