@@ -394,6 +394,13 @@ def main():
     ap.add_argument("--det-cap", type=int, default=256,
                     help="BoT-SORT/ByteTrack engine detection slots per sequence")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--with-d2h", action="store_true",
+                    help="deliver every frame's output rows to pinned host memory inside the "
+                         "timed region (a side-stream copy per frame, overlapped with the next "
+                         "frame), as motio.run_sequences users receive them")
+    ap.add_argument("--lsap-exact", action="store_true",
+                    help="StrongSort: solve every LSAP in scipy's row order (bx_ss_set_lsap_mode "
+                         "0) instead of solve + certify")
     ap.add_argument("--no-overlap", action="store_true",
                     help="join each step's feature EMA before it returns (bx_engine_set_overlap off)")
     ap.add_argument("--start-frame", type=int, default=0,
@@ -459,6 +466,8 @@ def main():
     eng, stages = bench_engine(args.config, S, args.track_cap, args.det_cap,
                                overlap=not args.no_overlap)
     layout = src.layout
+    if sss and args.lsap_exact:
+        eng.set_lsap_mode(False)
     # W warm-up steps (at least start_frame - 1 - probes: the first timed frame), then one
     # untimed probe step per pipeline stage (each stage timed once whatever W is), then the K
     # timed steps
@@ -473,9 +482,26 @@ def main():
         raise SystemExit("boosttrack_mot8: warmup + probes + steps exceed the shortest "
                          "sequence (600 frames)")
     frames = [src.frame(t) for t in range(1, n_frames + 1)]  # resident in HBM before timing
-    max_n = max(int(f[1][-1].item()) for f in frames)
-    out = torch.empty((max_n, 10 if kind == "strongsort" else 8), dtype=torch.float64, device=dev)
+    n_rows = [int(f[1][-1].item()) for f in frames]  # detections per frame (host, pre-timing)
+    max_n = max(n_rows)
+    width = 10 if kind == "strongsort" else 8
+    out = torch.empty((max_n, width), dtype=torch.float64, device=dev)
     cnt = torch.empty(S, dtype=torch.int32, device=dev)
+    # --with-d2h: a ring of output buffers, each frame's rows (and per-sequence counts) copied to
+    # pinned host memory on a side stream while the next frame computes; a buffer is rewritten
+    # only after its copy completed (event), so no frame's rows are lost or torn
+    RING = 3
+    d2h = None
+    if args.with_d2h:
+        d2h = dict(
+            outs=[torch.empty((max_n, width), dtype=torch.float64, device=dev)
+                  for _ in range(RING)],
+            cnts=[torch.empty(S, dtype=torch.int32, device=dev) for _ in range(RING)],
+            host=[torch.empty((max_n, width), dtype=torch.float64, pin_memory=True)
+                  for _ in range(RING)],
+            hcnt=[torch.empty(S, dtype=torch.int32, pin_memory=True) for _ in range(RING)],
+            side=torch.cuda.Stream(device=dev),
+            done=[None] * RING, bytes=0)
     stream = torch.cuda.current_stream()
     torch.cuda.synchronize()
 
@@ -486,6 +512,8 @@ def main():
     bounds = [(c0, min(c0 + chunk, S)) for c0 in range(0, S, chunk)]
 
     def step(k):
+        if d2h is not None:
+            return step_d2h(k)
         d, off, e = frames[k]
         if ocs:
             eng.step(d, off, out, cnt, stream=stream.cuda_stream)
@@ -495,6 +523,34 @@ def main():
             for c0, c1 in bounds:
                 eng.step(d, off[c0:c1 + 1], e, None, out, cnt[c0:c1], seq0=c0, nseq=c1 - c0,
                          stream=stream.cuda_stream)
+
+    def step_d2h(k):
+        nonlocal out, cnt
+        slot = k % RING
+        if d2h["done"][slot] is not None:
+            stream.wait_event(d2h["done"][slot])  # this buffer's previous copy has landed
+        out, cnt = d2h["outs"][slot], d2h["cnts"][slot]
+        d, off, e = frames[k]
+        if ocs:
+            eng.step(d, off, out, cnt, stream=stream.cuda_stream)
+        elif bst or sss:
+            eng.step(d, off, e, None, out, cnt, stream=stream.cuda_stream)
+        else:
+            for c0, c1 in bounds:
+                eng.step(d, off[c0:c1 + 1], e, None, out, cnt[c0:c1], seq0=c0, nseq=c1 - c0,
+                         stream=stream.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        side = d2h["side"]
+        side.wait_event(ev)
+        n = n_rows[k]
+        with torch.cuda.stream(side):
+            d2h["host"][slot][:n].copy_(out[:n], non_blocking=True)
+            d2h["hcnt"][slot].copy_(cnt, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(side)
+        d2h["done"][slot] = done
+        d2h["bytes"] += n * width * 8 + S * 4
 
     # warm-up, then the probe steps: each times one stage to find the dominant kernel
     stage_ms = {}
@@ -515,14 +571,17 @@ def main():
     torch.cuda.synchronize()
     # two event records per step around the dominant stage's launch (OCSort: its one kernel)
     eng.probe(True if ocs else dominant)
+    if d2h is not None:
+        d2h["bytes"] = 0
     t0 = time.perf_counter()
     for k in range(t_first, total):
         step(k)
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()  # (every stream of the device: the side-stream copies included)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    d2h_bytes = d2h["bytes"] if d2h is not None else 0
     dom_ms, dom_n = eng.probe_read()
     eng.probe(False if ocs else None)
     dom_ms /= args.steps  # per step: the dominant stage's launches over all chunks
@@ -536,6 +595,9 @@ def main():
         units["seqs"] = S
         # distinct gallery samples compared per queried track at the last timed frame
         units["rows_per_queried_track"] = round(units["rows"] / max(units["queried"], 1), 2)
+        # LSAPs solved (all frames of this rank): certified unique / unique up to rejected pairs
+        # / ties re-solved in scipy's order / cascade stages restarted
+        units["lsap_all_frames"] = eng.lsap_stats()
     if kind in ("bytetrack", "botsort"):
         # associations whose optimum was tied, re-solved in lapx's JV order, summed
         # over all frames of this rank
@@ -614,7 +676,13 @@ def main():
                        "dist_backend": backend if world > 1 else None,
                        "timed_frames": [t_first + 1, total],
                        **({"feature_overlap": not args.no_overlap}
-                          if kind == "botsort" and F else {})},
+                          if kind == "botsort" and F else {}),
+                       **({"outputs_to_host": {
+                           "what": "every frame's output rows + per-sequence counts copied to "
+                                   "pinned host memory on a side stream inside the timed region",
+                           "bytes_per_step": round(d2h_bytes / args.steps),
+                           "GB_s": round(d2h_bytes / t_max / 1e9, 2)}} if d2h is not None else
+                          {})},
             "roofline": {**roof, "kernel": dominant,
                          "kernel_ms": round(dom_ms, 4), "probe_steps": n_probe,
                          "launches_per_step": len(bounds),

@@ -198,6 +198,7 @@ EXPORTS = [
     "bx_boost_probe", "bx_boost_probe_read", "bx_ss_create", "bx_ss_destroy", "bx_ss_reset",
     "bx_ss_step", "bx_ss_update_host", "bx_ss_status", "bx_ss_counters_host",
     "bx_ss_tracks_host", "bx_ss_frame_stats_host", "bx_ss_probe", "bx_ss_probe_read",
+    "bx_ss_set_lsap_mode", "bx_ss_lsap_stats_host", "bx_ss_lsap_op",
     "bx_txt_shape", "bx_txt_read", "bx_mot_format", "bx_mot_write",
     "bx_engine_update_classes_host", "bx_ocsort_update_classes_host",
     "bx_boost_update_classes_host", "bx_kf_xysr_initiate", "bx_kf_xysr_predict",
@@ -295,6 +296,10 @@ _SIGS = {
     "bx_boost_state_set_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
     "bx_ss_state_set_host": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
     "bx_ss_frame_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
+    "bx_ss_set_lsap_mode": ([_vp, C.c_int], C.c_int),
+    "bx_ss_lsap_op": ([_vp, C.c_int, C.c_int, C.c_double, C.c_int, _vp, _vp, _vp, _vp, _vp],
+                      C.c_int),
+    "bx_ss_lsap_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_ss_probe": ([_vp, C.c_int], C.c_int),
     "bx_ss_probe_read": ([_vp, _dp, _ip], C.c_int),
     "bx_engine_update_classes_host": ([_vp, C.c_int, _vp, C.c_int, _vp, _vp, C.c_int, _vp, _ip,

@@ -1158,25 +1158,30 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
       // until the next association rebuilds them (three blocks: see LdsA's take order), when it
       // fits; else in the sequence's global scratch (one wave either way)
       const int n = R + C;
-#ifdef BX_PHASE_TIMING
-      // (the diagnostic timing build keeps lapjv's state in global scratch: with the stamps added,
-      // the LDS/global pointer select hits an instruction-selection error in this compiler)
-      const bool in_lds = false;
-#else
       const bool in_lds = jv_split_d_bytes(n) <= Lo.o_flags - Lo.o_u &&
                           jv_split_a_bytes(n) <= Lo.o_dconf - Lo.o_tboxf &&
                           jv_split_b_bytes(n) <= Lo.o_ints - Lo.o_rowptr;
-#endif
+      const double half = L / 2.;
+      auto ext = [&](int i, int j) {
+        return (i < R && j < C) ? M[(size_t)i * C + j] : (i >= R && j >= C) ? 0.0 : half;
+      };
+#ifdef BX_PHASE_TIMING
+      // (the diagnostic timing build solves in the same state layout through two call sites,
+      // one per layout: with the stamps added, one call over a selected LDS-or-global state
+      // pointer hits an instruction-selection error in this compiler — a generic-pointer
+      // aperture compare given an SGPR operand)
+      JvLds jw_l = jv_bind_split(smem + Lo.o_u, smem + Lo.o_tboxf, smem + Lo.o_rowptr, n);
+      JvLds jw_g = jv_bind(P.jvs + (size_t)s * P.jvs_stride, n);
+      if (wave_id() == 0) {
+        if (in_lds) jv_wave_t(ext, n, jw_l, SyncWaveLG{false});
+        else jv_wave_t(ext, n, jw_g, SyncWaveLG{true});
+      }
+      JvLds& jw = in_lds ? jw_l : jw_g;
+#else
       JvLds jw = in_lds ? jv_bind_split(smem + Lo.o_u, smem + Lo.o_tboxf, smem + Lo.o_rowptr, n)
                         : jv_bind(P.jvs + (size_t)s * P.jvs_stride, n);
-      if (wave_id() == 0) {
-        const double half = L / 2.;
-        jv_wave_t([&](int i, int j) {
-                    return (i < R && j < C) ? M[(size_t)i * C + j]
-                                            : (i >= R && j >= C) ? 0.0 : half;
-                  },
-                  n, jw, SyncWaveLG{!in_lds});
-      }
+      if (wave_id() == 0) jv_wave_t(ext, n, jw, SyncWaveLG{!in_lds});
+#endif
       __syncthreads();
       // x >= C: unmatched (-1); a real partner above L is neither matched nor listed (-3)
       for (int i = tid; i < R; i += WG) {

@@ -80,6 +80,10 @@ enum {
   Q_BUDGET, Q_HIST, Q_NNL, Q_NK, Q_NT0, Q_NOUT, Q_ROWS, Q_ROWSL,
   Q_NM, Q_NAUD, Q_FID, Q_ANYF, Q_NFUT, Q_NDUP,
   Q_CROWDN,  // high-overlap track pairs counted by ss_crowd_kernel for this frame  // handed from ss_match_kernel / ss_post_kernel to the next launch
+  // LSAP statistics since creation (bx_ss_lsap_stats_host): solves; certified unique; certified
+  // up to rejected (clamped) pairs; real ties re-solved in scipy's order; stages restarted in
+  // scipy's order (a real tie after a level whose unmatched order was not certified)
+  Q_LCALL, Q_LUNIQ, Q_LCLAMP, Q_LTIE, Q_LRESTART,
   SQS
 };
 
@@ -110,6 +114,8 @@ struct SsDev {
   double* cost;   // [S][2T*D] scratch cost matrices
   double* cfull;  // [S][T][D] stage 1/2 cost by (cascade rank, sorted detection)
   double* cfullT; // [S][D][T] the same, detection-major
+  int16_t* tlist; // [S][T][SS_TL] by cascade rank: the sorted detections of its real entries
+  int* tcnt;      // [S][T] their count (-1: more than SS_TL, or a NaN cost in the row)
   int* crank;     // [S][T] cascade rank of a list position (confirmed tracks), else -1
   double* ckey;   // [S][T] quality + stability by list position
   int* ctsu;      // [S][T] time_since_update by list position (confirmed), else -1
@@ -124,6 +130,7 @@ struct SsDev {
   double* wsd;    // [S][WSD] double scratch
   int wsi_n, wsd_n;
   int ws_lds;     // 1: the whole frame-kernel workspace in LDS, 2: its LSAP state only
+  int lsap_fast;  // 1: LSAPs solved then certified (scipy's order only on a tie); 0: scipy's order
   int* status;
   unsigned long long* dbg;  // [S][SS_DBG] phase stamps (diagnostic builds only, else null)
 };
@@ -131,6 +138,7 @@ struct SsDev {
 // Diagnostic phase stamps and counters (build with -DBX_PHASE_TIMING; never shipped): per
 // sequence, cycles accumulated per phase [0, 16), sub-phase cycles / counters [16, 32).
 constexpr int SS_DBG = 48;
+constexpr int SS_TL = 16;  // real entries listed per track for the LSAP's sparse first step
 #ifdef BX_PHASE_TIMING
 #define SSTAMP(k)                                                                    \
   do {                                                                               \
@@ -1005,6 +1013,9 @@ __global__ void __launch_bounds__(256)
 struct LsapJob {
   double max_d;
   int R, CC, tr, kind, np;
+  int mode;  // 0 scipy's order; 1 solve + certify, a tie re-solved in scipy's order; 2 ... a tie
+             // reported (stat 3) instead: the columns' order is not certified to be scipy's
+  int stat;  // 0 unique, 1 unique up to rejected pairs, 2 tie re-solved, 3 tie not solved
   int flag;
   int abort;  // set by either wave on a timeout: both stop handing over, nobody writes np / flag
 };
@@ -1027,6 +1038,7 @@ struct SsCtx {
   double* ks;   // match kernel: sort-key scratch (LDS)
   int* cidx;    // match kernel: the solver's column indices (LDS, 2048 ints)
   struct LsapJob* job;  // match kernel: the hand-off to its solver wave
+  int lmode = 0, lstat = 0;  // match kernel: the next LSAP's LsapJob::mode, the last one's stat
   __device__ const double* det(int i) const { return w.dt + (size_t)w.dord[i] * DTW; }
   __device__ int det_in(int i) const { return (int)det(i)[6]; }
 };
@@ -1098,9 +1110,28 @@ __device__ __forceinline__ int lds_flag_wait(int* flag, int v, bool want_ne, int
 // decided in order; when the first row's search goes on (v changes), the second is reloaded and
 // relaxed again first: every row is decided exactly as the sequential solver decides it.  The
 // next pair's costs are in flight meanwhile.
+//
+// fast (solve, then certify; LQ <= 16): the same optimum without scipy's row order.  (A) every
+// row's minimum and its lowest argmin column with v = 0, rows streamed two at a time with the
+// next pair's loads in flight — no row waits for the one before; u[r] = the minimum, and a row
+// whose argmin column is still free takes it (a feasible dual solution, tight on this partial
+// matching).  (C) the rows that lost their column ("contested") run Crouse's search from there
+// (finish_row, the same code as the exact path), in any order: the result is an optimum.  (D)
+// certify it: the reduced costs c - u - v of every unmatched entry against LSAP_SS_TOL (far above
+// both solvers' rounding).  Any optimum uses tight entries only, so an entry (r, j) that is not
+// tight means no optimum assigns j to r.  If no unmatched entry is tight the optimum is unique
+// and equals scipy's, pairs and all (fstat 0).  If the only tight unmatched entries are in rows
+// whose matched entry and the tight one are both clamped (> max_d, min_cost_matching rejects
+// them), every other optimum differs from this one in rejected pairs only: the same matches, the
+// same unmatched sets, but possibly another ORDER of min_cost_matching's unmatched lists (fstat
+// 1).  Otherwise a real pair could change: returns -1 (fstat 2) and the caller re-solves in
+// scipy's order.  NaN costs (a failed Cholesky) also go back to the exact path.
+constexpr double LSAP_SS_TOL = 1e-9;
 template <int LQ, bool IDX>
 __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P, const int* roff,
-                                         const int* cidx, double max_d, int R, int CC, bool tr) {
+                                         const int* cidx, double max_d, int R, int CC, bool tr,
+                                         bool fast, int& fstat, const int16_t* tl = nullptr,
+                                         const int* tc = nullptr) {
   SsWs& w = x.w;
   const int lane = x.lane;
 #ifdef BX_PHASE_TIMING
@@ -1108,6 +1139,10 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
   const int seq = x.seq;
   SCOUNT(7, R);
   SCOUNT(8, CC);
+  SCOUNT(16, (unsigned long long)R * CC);
+  const bool big_call = (size_t)R * CC * 8 > 65536;
+  SCOUNT(17, big_call ? 1 : 0);
+  SCOUNT(18, big_call ? R : 0);
   unsigned long long t_slow = 0, t_all = SS_NOW();
 #endif
   for (int i = lane; i < R; i += 64) w.u[i] = 0.0, w.col4row[i] = -1;
@@ -1159,10 +1194,15 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     return lmin;
   };
   bool bad = false;
+  // fast mode's per-row flags (w.v, unused by the exact path): bit 0 = more than one entry
+  // within LSAP_SS_TOL of the row's minimum at its claim, bit 1 = touched by a search (its u, or
+  // its column, changed after the claim)
+  int* rfl = (int*)w.v;
   // Row cur from its first step (rv, wave minimum m0): assigned when the step ends on an
   // unassigned column, else Crouse's search continued.  Returns true when v changed (the search
   // went on).
   auto finish_row = [&](int cur, double* rv, double m0) -> bool {
+    if (fast && lane == 0) rfl[cur] |= 2;
     if (!(m0 < INF)) {  // infeasible (cannot happen with finite costs)
       bad = true;
       return false;
@@ -1322,6 +1362,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     for (int k = lane; k < nvis; k += 64) {
       const int r = w.SR[k];
       w.u[r] += minVal - w.spc[k];
+      if (fast) rfl[r] |= 2;
     }
     if (lane == 0) w.u[cur] = 0.0 + minVal;
 #pragma unroll
@@ -1346,7 +1387,469 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
 #endif
     return true;
   };
+  fstat = 0;
   if constexpr (LQ <= 16) {
+   if (fast) {
+    const int rlast = R - 1;
+    auto roff_c = [&](int r) { return roff[r < rlast ? r : rlast]; };
+    double A0[LQ], A1[LQ], B0[LQ], B1[LQ];
+    bool nan_l = false;  // a NaN cost in a real column (lane-local)
+    int ncont = 0;       // contested rows, listed in w.SC
+    // (A) row r's minimum m over v = 0 (vr: 0, -INF past CC); it takes the lowest column at
+    // the minimum that is still free (a row of rejected entries only — most of a cascade
+    // level's detections — finds one), else it is contested
+    auto claim = [&](int r, const double* a, double m) {
+      if (!(m < INF)) {  // no finite entry: the exact path's business
+        bad = true;
+        return;
+      }
+      int j0 = -1, ntie = 0;
+      const double mt = m + LSAP_SS_TOL;
+#pragma unroll
+      for (int q = 0; q < LQ; q++) {
+        const double h = a[q] - vr[q];
+        const unsigned long long e = __ballot(h == m && !((asg >> q) & 1u));
+        if (j0 < 0 && e) j0 = 64 * q + __ffsll((long long)e) - 1;
+        ntie += __popcll(__ballot(h <= mt));
+      }
+      if (j0 >= 0) {
+        if (lane == (j0 & 63)) asg |= 1u << (j0 >> 6);
+        if (lane == 0) {
+          w.u[r] = m;
+          w.col4row[r] = j0;
+          w.row4col[j0] = r;
+          rfl[r] = ntie > 1 ? 1 : 0;
+        }
+      } else {
+        if (lane == 0) w.SC[ncont] = r, rfl[r] = 3;
+        ncont++;
+      }
+    };
+    auto minpair = [&](int r, const double* a0, const double* a1) {
+      double m0 = INF, m1 = INF;
+#pragma unroll
+      for (int q = 0; q < LQ; q++) {
+        m0 = fmin(m0, a0[q] - vr[q]);
+        m1 = fmin(m1, a1[q] - vr[q]);
+        nan_l |= (lane + 64 * q < CC) && (a0[q] != a0[q] || a1[q] != a1[q]);
+      }
+      wave_min_bfly2(m0, m1);
+      claim(r, a0, m0);
+      if (r + 1 < R && !bad) claim(r + 1, a1, m1);
+    };
+#ifdef BX_PHASE_TIMING
+    unsigned long long tA = SS_NOW();
+#endif
+    // The sparse form of (A) for the cascade levels (tl: ss_cost_kernel's lists of each track's
+    // real entries): every other entry of the matrix is the clamp K = max_d + 1e-5, so a row's
+    // minimum is its least real entry in this LSAP's columns, or K.  Rows with a real minimum
+    // bid for its column (the lowest row wins; the others are contested); the rows without
+    // one take the columns left free, in order (there are enough: R <= CC).  Lane per row (per
+    // column, scattering into the rows, when the rows are the detections).  Any track with an
+    // overflowing or NaN list sends the LSAP through the dense form below.
+    bool sparse = false;
+    if (tl != nullptr) {
+      const int T = x.g.T, D = x.g.D;
+#ifdef BX_PHASE_TIMING
+      unsigned long long tS = SS_NOW();
+#endif
+      bool ovf = false;
+      if (!tr)
+        for (int r = lane; r < R; r += 64) ovf |= tc[roff[r] / D] < 0;
+      else
+        for (int c = lane; c < CC; c += 64) ovf |= tc[cidx[c]] < 0;
+      sparse = !__any(ovf);
+#ifdef BX_PHASE_TIMING
+      SCOUNT(27, SS_NOW() - tS);
+      tS = SS_NOW();
+#endif
+      if (sparse) {
+        const double K = max_d + 1e-5;
+        auto ordb = [](double v) -> unsigned long long {  // order-preserving bits
+          const unsigned long long bb = (unsigned long long)__double_as_longlong(v);
+          return (bb >> 63) ? ~bb : (bb | 0x8000000000000000ull);
+        };
+        auto unord = [](unsigned long long bb) -> double {
+          return __longlong_as_double(
+              (long long)((bb >> 63) ? (bb & 0x7fffffffffffffffull) : ~bb));
+        };
+        int* pos = w.rem;  // sorted detection -> this LSAP's column (!tr) / row (tr), or -1
+        // row minima (order-preserving bits) in w.v's upper half: rfl takes its first R ints and
+        // R <= N/2 (R = min(tracks, detections) <= T, N >= 2T)
+        unsigned long long* rmin = (unsigned long long*)w.v + x.g.N / 2;
+        int* rcol = w.path;  // row -> lowest column at its real minimum
+        int* rtie = w.pos;   // row -> real entries within LSAP_SS_TOL of it
+        int* own = w.SR;     // column -> lowest bidding row
+        for (int e = lane; e < D; e += 64) pos[e] = -1;
+        for (int r = lane; r < R; r += 64)
+          rmin[r] = ordb(INF), rcol[r] = 0x7fffffff, rtie[r] = 0;
+        for (int c = lane; c < CC; c += 64) own[c] = 0x7fffffff;
+        wsync();
+        if (!tr)
+          for (int c = lane; c < CC; c += 64) pos[cidx[c]] = c;
+        else
+          for (int r = lane; r < R; r += 64) pos[roff[r] / T] = r;
+        wsync();
+#ifdef BX_PHASE_TIMING
+        SCOUNT(28, SS_NOW() - tS);
+        tS = SS_NOW();
+#endif
+        if (!tr) {
+          for (int r = lane; r < R; r += 64) {
+            const int rank = roff[r] / D, n = tc[rank];
+            const int16_t* L = tl + (size_t)rank * SS_TL;
+            double m = INF;
+            int jm = 0x7fffffff, nin = 0;
+            for (int k = 0; k < n; k++) {
+              const int e = L[k], c = pos[e];
+              if (c < 0) continue;
+              const double val = P[roff[r] + e];
+              nin++;
+              if (val < m || (val == m && c < jm)) m = val, jm = c;
+            }
+            int nt = nin;  // (one entry: itself)
+            if (nin > 1) {
+              nt = 0;
+              for (int k = 0; k < n; k++) {
+                const int e = L[k];
+                nt += pos[e] >= 0 && P[roff[r] + e] <= m + LSAP_SS_TOL;
+              }
+            }
+            rmin[r] = ordb(m);
+            rcol[r] = jm;
+            rtie[r] = nt;
+          }
+        } else {
+          // lane per column (track): its real entries dealt into two LDS slots per row (w.spc
+          // values, w.row4col columns — reset after: 2R <= N), counted in rtie; a row with more
+          // than two in this LSAP (rare: a detection gated to three tracks of one cascade
+          // level) sends the LSAP through the dense form
+          double* sv = w.spc;
+          int* sc2 = w.row4col;
+          for (int c = lane; c < CC; c += 64) {
+            const int rank = cidx[c], n = tc[rank];
+            const int16_t* L = tl + (size_t)rank * SS_TL;
+            for (int k = 0; k < n; k++) {
+              const int r = pos[L[k]];
+              if (r < 0) continue;
+              const double val = P[roff[r] + rank];
+              const int sl = atomicAdd(&rtie[r], 1);
+              if (sl < 2) sv[2 * r + sl] = val, sc2[2 * r + sl] = c;
+            }
+          }
+          wsync();
+          bool many = false;
+          for (int r = lane; r < R; r += 64) {
+            const int n = rtie[r];
+            many |= n > 2;
+            double m = INF;
+            int jm = 0x7fffffff, nt = 0;
+            if (n >= 1 && n <= 2) {
+              const double a0 = sv[2 * r], a1 = n == 2 ? sv[2 * r + 1] : INF;
+              const int c0 = sc2[2 * r], c1 = n == 2 ? sc2[2 * r + 1] : 0x7fffffff;
+              m = fmin(a0, a1);
+              const int k0 = a0 == m ? c0 : 0x7fffffff, k1 = a1 == m ? c1 : 0x7fffffff;
+              jm = k0 < k1 ? k0 : k1;
+              nt = (a0 <= m + LSAP_SS_TOL) + (n == 2 && a1 <= m + LSAP_SS_TOL);
+            }
+            rmin[r] = ordb(m);
+            rcol[r] = jm;
+            rtie[r] = nt;
+          }
+          if (__any(many)) bad = true;  // (-> the exact path: rare)
+          wsync();
+          for (int j = lane; j < 2 * R || j < CC; j += 64) sc2[j] = -1;
+        }
+#ifdef BX_PHASE_TIMING
+        wsync();
+        SCOUNT(29, SS_NOW() - tS);
+        tS = SS_NOW();
+#endif
+        wsync();
+        for (int r = lane; r < R; r += 64)
+          if (rcol[r] != 0x7fffffff) atomicMin(&own[rcol[r]], r);
+        wsync();
+        int* fcol = w.rem;  // the columns no row bid for, in order (pos is done)
+        const int nfree = wcompact(CC, [&](int c) { return own[c] == 0x7fffffff; },
+                                   [&](int c, int p) { fcol[p] = c; });
+        int ncl = 0;
+        for (int r0 = 0; r0 < R; r0 += 64) {
+          const int r = r0 + lane;
+          const bool in = r < R;
+          const int jc = in ? rcol[r] : 0;
+          const bool clampr = in && jc == 0x7fffffff;
+          const bool wins = in && !clampr && own[jc] == r;
+          const bool lost = in && !clampr && !wins;
+          const unsigned long long mc = __ballot(clampr), ml = __ballot(lost);
+          const unsigned long long below = (1ull << lane) - 1ull;
+          if (clampr) {
+            const int k = ncl + __popcll(mc & below);
+            const int j = fcol[k < nfree ? k : nfree - 1];
+            w.u[r] = K;
+            w.col4row[r] = j;
+            w.row4col[j] = r;
+            rfl[r] = CC > 1 ? 1 : 0;
+          } else if (wins) {
+            w.u[r] = unord(rmin[r]);
+            w.col4row[r] = jc;
+            w.row4col[jc] = r;
+            rfl[r] = rtie[r] > 1 ? 1 : 0;
+          } else if (lost) {
+            w.SC[ncont + __popcll(ml & below)] = r;
+            rfl[r] = 3;
+          }
+          ncl += __popcll(mc);
+          ncont += __popcll(ml);
+        }
+        if (ncl > nfree) bad = true;  // (cannot happen: R <= CC)
+        wsync();
+#ifdef BX_PHASE_TIMING
+        SCOUNT(30, SS_NOW() - tS);
+#endif
+        asg = 0u;
+#pragma unroll
+        for (int q = 0; q < LQ; q++) {
+          const int j = lane + 64 * q;
+          if (j < CC) {
+            w.path[j] = -1;
+            if (w.row4col[j] >= 0) asg |= 1u << q;
+          }
+        }
+        wsync();
+      }
+    }
+    if (!sparse) {
+      load_row(roff_c(0), A0);
+      load_row(roff_c(1), A1);
+      for (int r = 0; r < R && !bad;) {
+        load_row(roff_c(r + 2), B0);
+        load_row(roff_c(r + 3), B1);
+        minpair(r, A0, A1);
+        r += 2;
+        if (r >= R || bad) break;
+        load_row(roff_c(r + 2), A0);
+        load_row(roff_c(r + 3), A1);
+        minpair(r, B0, B1);
+        r += 2;
+      }
+      if (__any(nan_l)) bad = true;
+    }
+#ifdef BX_PHASE_TIMING
+    SCOUNT(20, ncont);
+    wsync();
+    SCOUNT(23, SS_NOW() - tA);
+    tA = SS_NOW();
+#endif
+    wsync();
+    // (C) the contested rows: Crouse's search from the partial matching (the next one's costs in
+    // flight meanwhile; v changes between them, so each is relaxed when its turn comes)
+    auto croff = [&](int k) {
+      return roff[(int)__builtin_amdgcn_readfirstlane((unsigned)w.SC[k < ncont ? k : ncont - 1])];
+    };
+    auto contested = [&](int k, double* a) {
+      const int cur = (int)__builtin_amdgcn_readfirstlane((unsigned)w.SC[k]);
+      const double m0 = wave_min_bfly(relax(a, a));
+      finish_row(cur, a, m0);
+    };
+    if (ncont > 0 && !bad) load_row(croff(0), A0);
+    for (int k = 0; k < ncont && !bad;) {
+      load_row(croff(k + 1), B0);
+      contested(k, A0);
+      if (++k >= ncont || bad) break;
+      load_row(croff(k + 1), A0);
+      contested(k, B0);
+      ++k;
+    }
+    wsync();
+#ifdef BX_PHASE_TIMING
+    wsync();
+    SCOUNT(24, SS_NOW() - tA);
+    tA = SS_NOW();
+#endif
+    // (D) the certificate, rows streamed as in (A).  Per row r: its tight unmatched entries
+    // (reduced cost <= LSAP_SS_TOL; a reduced cost below -LSAP_SS_TOL would mean broken duals:
+    // back to the exact path), whether its column is free-priced (v >= -LSAP_SS_TOL: w.SR, the
+    // "sources" below) and whether it is a candidate: a row with tight unmatched entries whose
+    // matched entry or one of those tight entries is real (<= max_d) — only a candidate on a
+    // cycle can change a real pair (w.SC, up to R of them; w.SR bit 1: matched entry real).
+    constexpr int SS_CERT_ROUNDS = 4, SS_CERT_BUDGET = 256;
+    bool infeas = false, tight_l = false;
+    int ncand = 0;
+    auto cert = [&](int r, const double* a) {
+      const int cr = (int)__builtin_amdgcn_readfirstlane((unsigned)w.col4row[r]);
+      if (cr < 0 || cr >= CC) {
+        infeas = true;
+        return;
+      }
+      const double ur = w.u[r];
+      double mv = a[0], mvv = vr[0];
+#pragma unroll
+      for (int q = 1; q < LQ; q++) {
+        mv = q == (cr >> 6) ? a[q] : mv;
+        mvv = q == (cr >> 6) ? vr[q] : mvv;
+      }
+      const bool realm = rl_d(mv, cr & 63) <= max_d;
+      const bool src = rl_d(mvv, cr & 63) >= -LSAP_SS_TOL;
+      bool t_r = false, rt_r = false;
+#pragma unroll
+      for (int q = 0; q < LQ; q++) {
+        const int j = lane + 64 * q;
+        if (j < CC && j != cr) {
+          const double rc = (a[q] - ur) - vr[q];
+          infeas |= !(rc >= -LSAP_SS_TOL);
+          if (rc <= LSAP_SS_TOL) {
+            t_r = true;
+            rt_r |= a[q] <= max_d;
+          }
+        }
+      }
+      const bool any_t = __any(t_r);
+      tight_l |= any_t;
+      const bool cand = any_t && (realm || __any(rt_r));
+      if (lane == 0) {
+        w.SR[r] = (src ? 1 : 0) | (realm ? 2 : 0);
+        if (cand) w.SC[ncand] = r;
+      }
+      ncand += cand;
+    };
+    // A row no search touched kept its claim (column at its minimum m = u) and its u; v only
+    // decreases, so its reduced costs only grew since the claim: its tight entries are among
+    // those within LSAP_SS_TOL of m then.  With one such entry (its own) it has no tight
+    // unmatched entry; with more but m > max_d they are all rejected entries (no candidate,
+    // the order is not certified).  Neither needs its costs reloaded; the rest are rescanned.
+    if (!bad) {
+      for (int r0 = 0; r0 < R; r0 += 64) {
+        const int r = r0 + lane;
+        bool scan = false;
+        if (r < R) {
+          const int fl = rfl[r];
+          const double ur = w.u[r];
+          scan = (fl & 2) || ((fl & 1) && ur <= max_d);
+          tight_l |= !scan && (fl & 1);
+          w.SR[r] = ur <= max_d ? 2 : 0;  // (untouched: matched entry = m = u)
+        }
+        unsigned long long todo = __ballot(scan);
+#ifdef BX_PHASE_TIMING
+        SCOUNT(26, __popcll(todo));
+#endif
+        while (todo) {
+          const int l = __ffsll((long long)todo) - 1;
+          todo &= todo - 1ull;
+          load_row(roff[r0 + l], A0);
+          cert(r0 + l, A0);
+        }
+      }
+      // sources: rows whose column is free-priced (v >= -LSAP_SS_TOL; v staged in w.spc)
+#pragma unroll
+      for (int q = 0; q < LQ; q++)
+        if (lane + 64 * q < CC) w.spc[lane + 64 * q] = vr[q];
+      wsync();
+      for (int r = lane; r < R; r += 64) {
+        const int cr = w.col4row[r];
+        if (cr < 0 || cr >= CC) infeas = true;
+        else if (w.spc[cr] >= -LSAP_SS_TOL) w.SR[r] |= 1;
+      }
+      wsync();
+    }
+    bool tie = bad || __any(infeas) || ncand > 64 * SS_CERT_ROUNDS;
+    // Another optimum exists iff the tight digraph has a cycle: rows, plus a node Z for "a free
+    // column"; row x -> the owner of each of x's tight unmatched columns (x could take it), or
+    // -> Z for a free one; Z -> every source row (its column may be left free: v = 0).  An
+    // optimum that changes a real pair needs a cycle through a real-matched candidate (it
+    // leaves its real partner) or through a real tight edge of a candidate (a new real pair; a
+    // cycle through a rejected-matched row over rejected entries only changes rejected pairs).
+    // Up to 64 candidates at a time: candidate k's bit is seeded into its successors (all of
+    // them when its matched entry is real, else those over real entries) and pushed along the tight
+    // edges (each row expanded once per new bit set: its costs reloaded, its tight successors
+    // OR-ed) until nothing changes; candidate k is on a cycle iff its own mask gets bit k.  Past
+    // SS_CERT_BUDGET row expansions per LSAP: counted as a tie (scipy's order decides).
+    if (!tie && ncand > 0) {
+      unsigned long long* msk = (unsigned long long*)w.spc;  // reached-by bits per row
+      unsigned long long* exm = (unsigned long long*)w.v;    // bits already pushed on per row
+      int budget = SS_CERT_BUDGET;
+      for (int c0 = 0; c0 < ncand && !tie; c0 += 64) {
+        const int nc = ncand - c0 < 64 ? ncand - c0 : 64;
+        wsync();
+        for (int r = lane; r < R; r += 64) msk[r] = 0ull, exm[r] = 0ull;
+        wsync();
+        unsigned long long mz = 0ull, ez = 0ull;  // Z's
+        // row x's tight successors (over real entries only: `ronly`) get `bits` (costs in `a`)
+        auto push = [&](int x, const double* a, unsigned long long bits, bool ronly) {
+          const int cx = (int)__builtin_amdgcn_readfirstlane((unsigned)w.col4row[x]);
+          const double ux = w.u[x];
+          bool zl = false;
+#pragma unroll
+          for (int q = 0; q < LQ; q++) {
+            const int j = lane + 64 * q;
+            if (j < CC && j != cx && (a[q] - ux) - vr[q] <= LSAP_SS_TOL &&
+                (!ronly || a[q] <= max_d)) {
+              const int y = w.row4col[j];
+              if (y < 0) zl = true;
+              else msk[y] |= bits;  // (distinct columns, distinct owners: no two lanes collide)
+            }
+          }
+          if (__any(zl)) mz |= bits;
+          wsync();
+        };
+        for (int k = 0; k < nc && !tie; k++) {
+          const int cand = (int)__builtin_amdgcn_readfirstlane((unsigned)w.SC[c0 + k]);
+          load_row(roff[cand], A0);
+          push(cand, A0, 1ull << k, !(w.SR[cand] & 2));
+          tie = --budget < 0;
+        }
+        bool changed = true;
+        while (changed && !tie) {
+          changed = false;
+          for (int r0 = 0; r0 < R && !tie; r0 += 64) {
+            const int r = r0 + lane;
+            const unsigned long long nw = r < R ? msk[r] & ~exm[r] : 0ull;
+            unsigned long long todo = __ballot(nw != 0ull);
+            while (todo && !tie) {
+              const int l = __ffsll((long long)todo) - 1;
+              todo &= todo - 1ull;
+              const int x = r0 + l;
+              const unsigned long long bx =
+                  (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(nw >> 32), l) << 32 |
+                  (unsigned)__builtin_amdgcn_readlane((int)nw, l);
+              if (lane == 0) exm[x] |= bx;
+              load_row(roff[x], A0);
+              push(x, A0, bx, false);
+              changed = true;
+              tie = --budget < 0;
+            }
+          }
+          const unsigned long long nz = mz & ~ez;
+          if (nz && !tie) {  // Z -> every source
+            ez |= nz;
+            for (int r = lane; r < R; r += 64)
+              if (w.SR[r] & 1) msk[r] |= nz;
+            wsync();
+            changed = true;
+          }
+        }
+        if (!tie) {
+          bool hit = false;
+          for (int k = lane; k < nc; k += 64)
+            hit |= (msk[w.SC[c0 + k]] >> k) & 1ull;
+          tie = __any(hit);
+        }
+      }
+#ifdef BX_PHASE_TIMING
+      SCOUNT(21, SS_CERT_BUDGET - budget);
+#endif
+    }
+#ifdef BX_PHASE_TIMING
+    SCOUNT(22, ncand);
+    wsync();
+    SCOUNT(25, SS_NOW() - tA);
+#endif
+    if (tie) {
+      fstat = 2;
+      wsync();
+      return -1;  // (bad latched nothing: the exact path decides)
+    }
+    fstat = __any(tight_l) ? 1 : 0;
+   } else {
     // Rows in pairs: the pair's two rows relaxed against the same v and their wave minima taken
     // together (two independent chains), then decided in order — the second one after the first
     // one's assignment, or relaxed again (its costs reloaded) when the first one's search changed
@@ -1384,6 +1887,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
       pair(cur, B0, B1);
       cur += 2;
     }
+   }
   } else {  // LQ = 32 (IoU stage of more than 1024 candidates, rare): one row at a time
     double A[LQ], C[LQ];
     for (int cur = 0; cur < R && !bad; cur++) {
@@ -1400,6 +1904,7 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
 #ifdef BX_PHASE_TIMING
   SCOUNT(10, t_slow);
   SCOUNT(11, SS_NOW() - t_all);
+  SCOUNT(19, big_call ? SS_NOW() - t_all : 0);
 #endif
   // every row is assigned a column in [0, CC) by now; a value outside it would be an engine
   // fault: latched as an error instead of indexing with it
@@ -1411,14 +1916,17 @@ __device__ __forceinline__ int lsap_wave(SsCtx& x, const double* __restrict__ P,
     }
   }
   wsync();
-  if (tr) {  // argsort(col4row): pairs ordered by the original row
-    for (int q = lane; q < R; q += 64) {
-      const int orow = w.col4row[q];
-      int rank = 0;
-      for (int k = 0; k < R; k++) rank += w.col4row[k] < orow;
-      w.rows[rank] = orow;
-      w.cols[rank] = q;
-    }
+  if (tr) {  // argsort(col4row): pairs ordered by the original row — col4row is injective
+    // into [0, CC), so a table over the columns read in order sorts it (w.rem: free by now)
+    int* t = w.rem;
+    for (int j = lane; j < CC; j += 64) t[j] = -1;
+    wsync();
+    for (int q = lane; q < R; q += 64) t[w.col4row[q]] = q;
+    wsync();
+    wcompact(CC, [&](int j) { return t[j] >= 0; }, [&](int j, int p) {
+      w.rows[p] = j;
+      w.cols[p] = t[j];
+    });
   } else {
     for (int q = lane; q < R; q += 64) {
       w.rows[q] = q;
@@ -1571,7 +2079,16 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
   // one cascade a detection takes part in: stage 1 (high confidence) thr * 0.8, stage 2 (medium)
   // thr (tracker.py:206-233; thr after ss_pre_kernel's crowd-mode adjustment)
   const double thr = g.sqd[(size_t)seq * 2];
-  for (int c = lane; c < nk; c += 64) {
+  // the track's real entries (<= its detections' max_distance: not clamped) as a list of sorted
+  // detection indices for the solver's sparse first step; -1 when more than SS_TL, or when a
+  // cost is NaN (only the dense path handles those)
+  int16_t* tl = g.tlist + ((size_t)seq * g.T + rk) * SS_TL;
+  int nreal = 0;
+  bool nan_l = false;
+  for (int c0 = 0; c0 < nk; c0 += 64) {
+   const int c = c0 + lane;
+   bool real = false;
+   if (c < nk) {
     const double* d = dt + (size_t)dord[c] * DTW;
     double z[4];
     det_xyah(d, z);
@@ -1604,10 +2121,18 @@ __global__ void __launch_bounds__(64) ss_cost_kernel(SsDev g, int seq0) {
     if (g.idw > 0) v *= (1.0 - pb);
     double e = enhance(t, d, v);
     const double md = ss_det_max_d(d[4], g.thi, thr);
+    real = e <= md;
+    nan_l |= e != e;
     if (e > md) e = md + 1e-5;
     out[c] = e;
     outT[(size_t)c * g.T] = e;
+   }
+   const unsigned long long m = __ballot(real);
+   const int p = nreal + __popcll(m & ((1ull << lane) - 1ull));
+   if (real && p < SS_TL) tl[p] = (int16_t)c;
+   nreal += __popcll(m);
   }
+  if (lane == 0) g.tcnt[(size_t)seq * g.T + rk] = (__any(nan_l) || nreal > SS_TL) ? -1 : nreal;
 }
 
 // The match kernel's solver wave: runs each posted LSAP (column slots per lane sized to CC: every
@@ -1621,20 +2146,40 @@ __device__ __forceinline__ void lsap_server(SsCtx& x, LsapJob* jb, const int* ro
     const int f = lds_flag_wait(&jb->flag, 0, true, x.g.status, &jb->abort, to);
     if (f < 0 || to) return;  // exit posted (the cascade always posts it last), or aborted
     const double mx = jb->max_d;
-    const int R = jb->R, CC = jb->CC, kind = jb->kind;
+    const int R = jb->R, CC = jb->CC, kind = jb->kind, mode = jb->mode;
     const bool tr = jb->tr != 0;
     const double* P = lsap_mat(x.g, x.seq, kind, tr);
-    const int np =
-        CC <= 256    ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr)
-        : CC <= 512  ? lsap_wave<8, true>(x, P, roff, cidx, mx, R, CC, tr)
-        : CC <= 1024 ? lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr)
-                     : lsap_wave<32, true>(x, P, roff, cidx, mx, R, CC, tr);
+    // solve + certify first (mode 1, 2); on a tie scipy's order (mode 1) or a report (mode 2).
+    // One call site per width: every inlined copy grows the kernel's register allocation.
+    bool fast = mode != 0;
+    int np = 0, st = 0;
+    for (;;) {
+      int fs = 0;
+      // the cascade levels' matrices come with ss_cost_kernel's real-entry lists
+      const int16_t* tl = kind == 0 ? x.g.tlist + (size_t)x.seq * x.g.T * SS_TL : nullptr;
+      const int* tc = x.g.tcnt + (size_t)x.seq * x.g.T;
+      np = CC <= 256    ? lsap_wave<4, true>(x, P, roff, cidx, mx, R, CC, tr, fast, fs, tl, tc)
+           : CC <= 512  ? lsap_wave<8, true>(x, P, roff, cidx, mx, R, CC, tr, fast, fs, tl, tc)
+           : CC <= 1024 ? lsap_wave<16, true>(x, P, roff, cidx, mx, R, CC, tr, fast, fs, tl, tc)
+                        : lsap_wave<32, true>(x, P, roff, cidx, mx, R, CC, tr, fast, fs, tl, tc);
+      if (np >= 0) {
+        if (fast) st = fs;
+        break;
+      }
+      if (mode == 2) {
+        st = 3;
+        np = 0;
+        break;
+      }
+      fast = false;
+      st = 2;
+    }
     // the cascade gave up on this job (timeout): it may have posted another one since, which
     // this answer must not overwrite
     if (__builtin_amdgcn_readfirstlane((unsigned)__hip_atomic_load(
             &jb->abort, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0)
       return;
-    if (x.lane == 0) jb->np = np;
+    if (x.lane == 0) jb->np = np, jb->stat = st;
     wsync();
     if (x.lane == 0) __hip_atomic_store(&jb->flag, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
@@ -1650,6 +2195,7 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
   const SsDev& g = x.g;
   SsWs& w = x.w;
   const int lane = x.lane;
+  x.lstat = 0;
   if (nd == 0 || nt == 0) {
     for (int k = lane; k < nt; k += 64)
       if (ut_out) ut_out[k] = ti[k];
@@ -1720,6 +2266,7 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
       jb->CC = CC;
       jb->tr = tr;
       jb->kind = kind;
+      jb->mode = x.lmode;
     }
     wsync();
     bool to = __builtin_amdgcn_readfirstlane((unsigned)__hip_atomic_load(
@@ -1730,6 +2277,11 @@ __device__ __forceinline__ void min_cost_matching(SsCtx& x, int kind, double max
       lds_flag_wait(&jb->flag, 0, false, g.status, &jb->abort, to);
     }
     np_ = to ? 0 : jb->np;
+    x.lstat = to ? 0 : jb->stat;
+    if (lane == 0 && !to) {
+      x.sq[Q_LCALL]++;
+      x.sq[x.lstat == 0 ? Q_LUNIQ : x.lstat == 1 ? Q_LCLAMP : Q_LTIE] += x.lstat <= 2;
+    }
   }
 #ifdef BX_PHASE_TIMING
   wsync();
@@ -1830,6 +2382,10 @@ __device__ void match_stage(SsCtx& x, int kind, double max_d, const int* ti, int
     for (int k = lane; k < nt; k += 64) x.inset[ti[k]] = 1;
     wsync();
   }
+  // LSAPs solved then certified; the columns' order (the previous level's unmatched detections)
+  // is scipy's while every level so far was unique outright or tie-re-solved in scipy's order
+  const int nm0 = x.nm;
+  x.lmode = x.g.lsap_fast ? 1 : 0;
   for (int q = 0; q < na; q++) {
     const int* lt = ti;
     int nl = nt;
@@ -1845,6 +2401,19 @@ __device__ void match_stage(SsCtx& x, int kind, double max_d, const int* ti, int
     int nud2 = 0, nut_l = 0;
     min_cost_matching(x, kind, max_d, lt, nl, w.ud, nud, kind == M_IOU ? ut_out : nullptr, nut_l,
                       w.ud2, nud2);
+    if (x.lstat == 3) {
+      // a real tie at a level whose columns' order may not be scipy's (an earlier level was only
+      // unique up to rejected pairs): the whole stage again, every level in scipy's order
+      x.nm = nm0;
+      nud = nd;
+      for (int k = lane; k < nd; k += 64) w.ud[k] = di[k];
+      if (lane == 0) x.sq[Q_LRESTART]++;
+      x.lmode = 0;
+      q = -1;
+      wsync();
+      continue;
+    }
+    if (x.lstat == 1 && x.lmode == 1) x.lmode = 2;
     if (kind == M_IOU) nut = nut_l;
     for (int k = lane; k < nud2; k += 64) w.ud[k] = w.ud2[k];
     nud = nud2;
@@ -2833,6 +3402,42 @@ __global__ void __launch_bounds__(64) ss_feat_set_kernel(SsDev g, int seq, const
   }
 }
 
+// Test entry point of the match kernel's LSAP (lsap_wave) on a dense row-major R x CC matrix,
+// R <= CC <= 1024, one wave: mode 0 scipy's row order, 1 solve + certify (a tie answered -1).
+__global__ void __launch_bounds__(64) ss_lsap_op_kernel(const double* C, int R, int CC,
+                                                        double max_d, int fast, int32_t* rows,
+                                                        int32_t* cols, int32_t* info,
+                                                        int* status) {
+  extern __shared__ __align__(16) char ss_lds[];
+  const int N = CC;
+  SsDev g{};
+  g.T = R;
+  g.D = CC;
+  g.N = N;
+  g.status = status;
+  SsWs w{};
+  double* ld = (double*)ss_lds;
+  int* li = (int*)(ss_lds + (size_t)3 * N * 8);
+  w.u = ld; w.v = ld + N; w.spc = ld + 2 * N;
+  w.path = li; w.col4row = li + N; w.row4col = li + 2 * N; w.rem = li + 3 * N;
+  w.pos = li + 4 * N; w.SR = li + 5 * N; w.SC = li + 6 * N;
+  w.rows = li + 7 * N; w.cols = li + 8 * N;
+  int* roff = li + 9 * N;
+  int* cidx = li + 10 * N;
+  const int lane = threadIdx.x;
+  for (int r = lane; r < R; r += 64) roff[r] = r * CC;
+  for (int j = lane; j < CC; j += 64) cidx[j] = j;
+  __syncthreads();
+  SsCtx x{g, w, 0, lane, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0};
+  int fs = 0;
+  const bool f = fast != 0;
+  const int np = CC <= 256   ? lsap_wave<4, true>(x, C, roff, cidx, max_d, R, CC, false, f, fs)
+                 : CC <= 512 ? lsap_wave<8, true>(x, C, roff, cidx, max_d, R, CC, false, f, fs)
+                             : lsap_wave<16, true>(x, C, roff, cidx, max_d, R, CC, false, f, fs);
+  for (int q = lane; q < np; q += 64) rows[q] = w.rows[q], cols[q] = w.cols[q];
+  if (lane == 0) info[0] = np, info[1] = fs;
+}
+
 }  // namespace
 
 struct bx_ss {
@@ -3029,6 +3634,7 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   // all of it in LDS when it fits beside ~3 other workgroups per CU; else the LSAP state alone
   // (the solver's inner loops; track_cap, det_cap <= 1024 keep it within 106 KB)
   d.ws_lds = ws_bytes <= 48 * 1024 ? 1 : 2;
+  d.lsap_fast = 1;
   const size_t S = d.S, T = d.T, D = d.D, F = d.F, VP = d.VP, GB = d.GB;
   size_t off = 0;
   auto cb = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
@@ -3054,6 +3660,8 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   const size_t o_cost = cb(S * 4 * T * D * sizeof(double));
   const size_t o_cfull = cb(S * T * D * sizeof(double));
   const size_t o_cfullT = cb(S * T * D * sizeof(double));
+  const size_t o_tlist = cb(S * T * SS_TL * sizeof(int16_t));
+  const size_t o_tcnt = cb(S * T * sizeof(int));
   const size_t o_crank = cb(S * T * sizeof(int));
   const size_t o_ckey = cb(S * T * sizeof(double));
   const size_t o_ctsu = cb(S * T * sizeof(int));
@@ -3098,6 +3706,8 @@ int bx_ss_create(const bx_ss_config* c, bx_ss** out) {
   d.cost = (double*)(base + o_cost);
   d.cfull = (double*)(base + o_cfull);
   d.cfullT = (double*)(base + o_cfullT);
+  d.tlist = (int16_t*)(base + o_tlist);
+  d.tcnt = (int*)(base + o_tcnt);
   d.crank = (int*)(base + o_crank);
   d.ckey = (double*)(base + o_ckey);
   d.ctsu = (int*)(base + o_ctsu);
@@ -3456,6 +4066,45 @@ int bx_ss_state_set_host(bx_ss* e, int seq, int n, const int32_t* ids, const dou
     if (mean) memcpy(t.mean, mean + 8 * j, sizeof(t.mean));
     if (cov) memcpy(t.cov, cov + 64 * j, sizeof(t.cov));
     SCHK(hipMemcpy(dt, &t, sizeof(SsTrk), hipMemcpyHostToDevice));
+  }
+  return BX_OK;
+}
+
+int bx_ss_lsap_op(const double* cost, int R, int CC, double max_d, int fast, int32_t* rows,
+                  int32_t* cols, int32_t* info, int32_t* status, void* stream) {
+  if (R < 1 || R > CC || CC > 1024 || !info || !status)
+    return bx_record_error(BX_ERR_INVALID, "bx_ss_lsap_op: 1 <= R <= CC <= 1024");
+  const size_t lds = (size_t)3 * CC * 8 + (size_t)11 * CC * 4;
+  SCHK(bx_lds_attr((const void*)ss_lsap_op_kernel, lds));
+  hipLaunchKernelGGL(ss_lsap_op_kernel, dim3(1), dim3(64), lds, (hipStream_t)stream, cost, R, CC,
+                     max_d, fast, rows, cols, info, status);
+  SCHK(hipGetLastError());
+  return BX_OK;
+}
+
+int bx_ss_set_lsap_mode(bx_ss* e, int fast) {
+  if (!e || fast < 0 || fast > 1) return bx_record_error(BX_ERR_INVALID, "bad lsap mode");
+  SCHK(hipDeviceSynchronize());
+  e->dev.lsap_fast = fast;
+  return BX_OK;
+}
+
+int bx_ss_lsap_stats_host(bx_ss* e, int seq0, int nseq, int64_t* sums) {
+  if (!e || !sums || seq0 < 0 || nseq < 0 || seq0 + nseq > e->dev.S)
+    return bx_record_error(BX_ERR_INVALID, "bad arguments to bx_ss_lsap_stats_host");
+  std::vector<int> s((size_t)nseq * SQS);
+  SCHK(hipDeviceSynchronize());
+  if (nseq)
+    SCHK(hipMemcpy(s.data(), e->dev.sq + (size_t)seq0 * SQS, sizeof(int) * s.size(),
+                   hipMemcpyDeviceToHost));
+  for (int k = 0; k < 5; k++) sums[k] = 0;
+  for (int k = 0; k < nseq; k++) {
+    const int* q = s.data() + (size_t)k * SQS;
+    sums[0] += q[Q_LCALL];
+    sums[1] += q[Q_LUNIQ];
+    sums[2] += q[Q_LCLAMP];
+    sums[3] += q[Q_LTIE];
+    sums[4] += q[Q_LRESTART];
   }
   return BX_OK;
 }

@@ -833,6 +833,20 @@ class SsEngine:
         return dict(zip(["dets", "tracks", "queried", "rows", "outputs", "frame", "matches"],
                         [int(x) for x in a]))
 
+    def set_lsap_mode(self, fast: bool) -> None:
+        """Solve + certify the cascade LSAPs (default) or always solve them in scipy's row order
+        (bx_ss_set_lsap_mode)."""
+        N.check(self._L.bx_ss_set_lsap_mode(self._h, int(bool(fast))), "bx_ss_set_lsap_mode")
+
+    def lsap_stats(self, seq0: int = 0, nseq: int | None = None) -> dict:
+        """LSAP counters since creation (bx_ss_lsap_stats_host): solves, certified unique,
+        unique up to rejected pairs, ties re-solved in scipy's order, stages restarted."""
+        nseq = self.n_seq - seq0 if nseq is None else nseq
+        a = (C.c_int64 * 5)()
+        N.check(self._L.bx_ss_lsap_stats_host(self._h, seq0, nseq, a), "lsap_stats")
+        return dict(zip(["solves", "unique", "unique_up_to_rejected", "ties", "restarts"],
+                        [int(x) for x in a]))
+
     def probe(self, stage) -> None:
         idx = -1 if stage is None else (self.STAGES.index(stage) if isinstance(stage, str)
                                         else int(stage))

@@ -123,6 +123,25 @@ int bx_ss_last_feature_set_host(bx_ss *e, int seq, int n, const int32_t *ids, co
  * tracks entering the frame, confirmed tracks queried next frame, gallery sample rows compared,
  * output rows, max frame counter, matches} — bench.py's unit counts. */
 int bx_ss_frame_stats_host(bx_ss *e, int seq0, int nseq, int64_t *sums);
+/* How the cascade / IoU LSAPs (linear_assignment.py:14-93's linear_sum_assignment) are solved:
+ * fast = 1 (default) solve + certify — rows' minima in parallel, Crouse's search for the
+ * contested ones, then a reduced-cost certificate that the optimum is unique up to pairs
+ * min_cost_matching rejects; scipy's own row order only for a tied level (and a whole cascade
+ * stage in scipy's order when a tie follows a level whose unmatched order was not certified).
+ * fast = 0: scipy's row order always.  Both give the reference's matches.  Synchronous. */
+int bx_ss_set_lsap_mode(bx_ss *e, int fast);
+/* LSAP counters of sequences [seq0, seq0+nseq) since creation: sums[5] = {solves, certified
+ * unique, certified unique up to rejected pairs, ties re-solved in scipy's order, cascade stages
+ * restarted in scipy's order}.  Synchronous. */
+int bx_ss_lsap_stats_host(bx_ss *e, int seq0, int nseq, int64_t *sums);
+/* Test entry point of the match kernel's LSAP on a dense row-major [R][CC] float64 cost (device),
+ * 1 <= R <= CC <= 1024: fast = 0 scipy's linear_sum_assignment row order, 1 solve + certify
+ * against max_d (min_cost_matching's rejection threshold).  rows / cols [R] (device) get the
+ * pairs in row order; info[2] (device) = {pairs, or -1 when fast found a tie that could change a
+ * real (<= max_d) pair; 0 unique, 1 unique up to rejected pairs, 2 tie}; status (device) is
+ * latched BX_ERR_INVALID on an engine fault. */
+int bx_ss_lsap_op(const double *cost, int R, int CC, double max_d, int fast, int32_t *rows,
+                  int32_t *cols, int32_t *info, int32_t *status, void *stream);
 /* Timing probe: stage 0 = detection features, 1 = gallery distance, 2 = recovery similarities,
  * 3 = pre-match (crowd, warp, quality, predict), 4 = stage 1/2 costs, 5 = matching, 6 = track
  * updates, 7 = post-match, 8 = partial_fit; -1 = off (see bx_boost_probe). */

@@ -130,6 +130,9 @@ def test_strongsort_c4_bench_workload_vs_oracle(torch_cuda):
     eng, frames, outs = drive_bench(torch_cuda, "strongsort_c4", 1, n_frames)
     st = eng.frame_stats()
     assert st["dets"] > 450 and st["tracks"] > 900, st
+    ls = eng.lsap_stats()
+    print(f"C4 LSAPs over {n_frames} frames: {ls}")
+    assert ls["unique"] + ls["unique_up_to_rejected"] > 0, ls  # solve + certify really ran
     orc = po.OracleTracker("strongsort", **params)
     for t in range(1, n_frames + 1):
         dets, embs, rows = host_rows(frames, outs, 0, t)

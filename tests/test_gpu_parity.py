@@ -1136,7 +1136,7 @@ SS_ARGS = dict(min_conf=0.1, max_cos_dist=0.15, max_iou_dist=0.7, max_age=50, n_
 
 
 def run_ss_batched(torch, scenes, n_frames, args, emb_dim, track_cap=256, det_cap=256,
-                   warps=None, vec_cap=32):
+                   warps=None, vec_cap=32, lsap_fast=True):
     """SsEngine with len(scenes) sequences per launch vs one oracle per sequence: outputs and
     Kalman state bitwise."""
     from boxmot_amd.engine import SsEngine, SsParams
@@ -1144,6 +1144,8 @@ def run_ss_batched(torch, scenes, n_frames, args, emb_dim, track_cap=256, det_ca
     S = len(scenes)
     eng = SsEngine(n_seq=S, track_cap=track_cap, det_cap=det_cap, emb_dim=emb_dim,
                    vec_cap=vec_cap, params=SsParams(**args))
+    if not lsap_fast:
+        eng.set_lsap_mode(False)
     orcs = [po.OracleTracker("strongsort", **args) for _ in range(S)]
     for t in range(1, n_frames + 1):
         frames = [sc.frame(t) for sc in scenes]
@@ -1204,6 +1206,43 @@ def test_strongsort_batched_vs_oracle(torch_cuda, variant):
         run_ss_batched(torch_cuda, scenes, 30, args, 48, track_cap=512)
         return
     run_ss_batched(torch_cuda, scenes, 50, args, 48)
+
+
+class DupScene:
+    """A scene whose every `every`-th detection is repeated (same box, confidence, class and
+    embedding) at the end of the frame: the cascade's LSAPs get exactly tied optima."""
+
+    def __init__(self, sc, every):
+        self.sc, self.every = sc, every
+
+    def frame(self, t):
+        d, e, x = self.sc.frame(t)
+        k = np.arange(0, d.shape[0], self.every)
+        return np.concatenate([d, d[k]], 0), np.concatenate([e, e[k]], 0), x
+
+
+@pytest.mark.parametrize("lsap_fast", [True, False])
+def test_strongsort_tied_lsaps_vs_oracle(torch_cuda, lsap_fast):
+    """Duplicated detections make min_cost_matching's optimum tie between the copies: solve +
+    certify must detect every such tie and re-solve it in scipy's order (or restart its cascade
+    stage in scipy's order when an earlier level's unmatched order was only certified up to
+    rejected pairs), and give the oracle's outputs and Kalman state bit for bit; scipy's order
+    throughout (lsap_fast False) too."""
+    from boxmot_amd.synth import SyntheticScene
+
+    args = dict(SS_ARGS)
+    args.update(max_age=8)
+    scenes = [DupScene(SyntheticScene(n_obj=24 + 12 * s, seed=870 + s, emb_dim=48,
+                                      emb_dtype=np.float64, conf_lo=0.15,
+                                      layout="crowded" if s % 2 else "grid"), 2 + s)
+              for s in range(4)]
+    eng = run_ss_batched(torch_cuda, scenes, 40, args, 48, lsap_fast=lsap_fast)
+    st = eng.lsap_stats()
+    print(f"lsap_fast={lsap_fast}: {st}")
+    if lsap_fast:
+        assert st["ties"] > 0 and st["unique"] + st["unique_up_to_rejected"] > 0, st
+    else:
+        assert st["ties"] == 0 and st["unique"] == st["solves"], st
 
 
 def test_strongsort_large_scene_vs_oracle(torch_cuda):
@@ -1452,3 +1491,72 @@ def test_legacy_lap_ssp_equals_lapjv_op_level(torch_cuda):
     print(f"certified {certified}/{eligible}, duplicates fell back {fell_back}")
     assert certified >= 0.8 * eligible and eligible >= 10, (certified, eligible)
     assert fell_back >= 1, fell_back
+
+
+def gpu_ss_lsap(torch, cost, max_d, fast):
+    from boxmot_amd import _native as N
+
+    R, CC = cost.shape
+    c = dev(torch, np.ascontiguousarray(cost, np.float64))
+    rows = torch.full((R,), -7, dtype=torch.int32, device="cuda")
+    cols = torch.full((R,), -7, dtype=torch.int32, device="cuda")
+    info = torch.zeros(2, dtype=torch.int32, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    N.check(N.load().bx_ss_lsap_op(c.data_ptr(), R, CC, float(max_d), int(fast), rows.data_ptr(),
+                                   cols.data_ptr(), info.data_ptr(), st.data_ptr(), None),
+            "bx_ss_lsap_op")
+    torch.cuda.synchronize()
+    assert int(host(st)[0]) == 0
+    np_, fs = (int(v) for v in host(info))
+    if np_ < 0:
+        return None, fs
+    return np.stack([host(rows)[:np_], host(cols)[:np_]], 1), fs
+
+
+@pytest.mark.gpu
+def test_strongsort_lsap_solve_certify_vs_scipy(torch_cuda):
+    """The match kernel's LSAP op-level (bx_ss_lsap_op) on min_cost_matching-shaped costs
+    (linear_assignment.py:62-70: entries above max_distance clamped to max_distance + 1e-5,
+    then linear_sum_assignment): scipy's row order (fast = 0) returns the oracle's pairs
+    (scipy restated, pinned by test_oracle) bit for bit on every matrix, ties included.  Solve +
+    certify (fast = 1) must either return the same pairs (stat 0: unique), the same pairs where
+    the cost is <= max_distance (stat 1: other optima differ in rejected pairs only), or report a
+    tie (-1) — never a different accepted match.  Random, sparse-real (most entries clamped:
+    the cascade's shape), duplicated rows and coarse-grid (tie-heavy) matrices, R <= CC up to
+    1024 columns."""
+    rng = np.random.default_rng(2024)
+    stats = {0: 0, 1: 0, 2: 0}
+    for t in range(150):
+        R = int(rng.integers(1, 200))
+        CC = int(min(1024, R + rng.integers(0, 300)))
+        if t % 25 == 0:
+            R, CC = int(rng.integers(300, 700)), 1024
+        max_d = 0.2 + 0.3 * rng.random()
+        kind = t % 5
+        c = rng.uniform(0.0, 1.0, (R, CC))
+        if kind == 1:  # sparse real entries: a few candidates per row
+            c = np.full((R, CC), 5.0)
+            for r in range(R):
+                k = int(rng.integers(0, 4))
+                c[r, rng.choice(CC, k, replace=False)] = rng.uniform(0, max_d, k)
+        elif kind == 2 and R > 1:
+            c[R // 2] = c[0]
+        elif kind == 3:
+            c = np.round(c * 4) / 4
+        c = np.where(c > max_d, max_d + 1e-5, c)
+        rr, kk = po.lsap(c)
+        ref = np.stack([rr, kk], 1).astype(np.int64)
+        ex, fs0 = gpu_ss_lsap(torch_cuda, c, max_d, False)
+        np.testing.assert_array_equal(ex, ref, err_msg=f"exact t={t} kind={kind} {R}x{CC}")
+        assert fs0 == 0
+        got, fs = gpu_ss_lsap(torch_cuda, c, max_d, True)
+        stats[fs] += 1
+        if fs == 2:
+            assert got is None
+            continue
+        if fs == 0:
+            np.testing.assert_array_equal(got, ref, err_msg=f"fast t={t} kind={kind}")
+        real = lambda p: p[c[p[:, 0], p[:, 1]] <= max_d]  # noqa: E731
+        np.testing.assert_array_equal(real(got), real(ref), err_msg=f"fast real t={t} k={kind}")
+    print(f"solve + certify outcomes: {stats}")
+    assert stats[0] + stats[1] >= 75 and stats[2] >= 3, stats

@@ -25,7 +25,13 @@ COUNTERS = ["cost build cyc", "lsap cyc", "lsap calls", "sum rows (tracks)", "su
             "dijkstra steps", "matches", "solver rows R", "solver cols CC", "slow rows",
             "slow-row cyc", "lsap loop cyc", "pair: v + wait + relax cyc",
             "pair: two wave minima cyc", "pair: row 0 decided (fast) cyc",
-            "pair: row 1 decided (fast) cyc"]
+            "pair: row 1 decided (fast) cyc", "sum R x CC", "calls R*CC*8 > 64 KiB",
+            "rows in those calls", "lsap cyc in those calls", "fast: contested rows",
+            "fast: certificate row expansions", "fast: certificate candidates",
+            "fast: (A) minima + claims cyc", "fast: (C) contested searches cyc",
+            "fast: (D) certificate cyc", "fast: (D) rows rescanned",
+            "sparse (A): list check cyc", "sparse (A): tables cyc", "sparse (A): minima cyc",
+            "sparse (A): claims cyc"]
 
 
 def build():
