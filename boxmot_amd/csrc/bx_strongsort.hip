@@ -84,6 +84,7 @@ enum {
   // up to rejected (clamped) pairs; real ties re-solved in scipy's order; stages restarted in
   // scipy's order (a real tie after a level whose unmatched order was not certified)
   Q_LCALL, Q_LUNIQ, Q_LCLAMP, Q_LTIE, Q_LRESTART,
+  Q_NNCTR,  // ss_nn_kernel's work counter (zeroed by ss_prep_kernel's pack block each frame)
   SQS
 };
 
@@ -729,6 +730,7 @@ __global__ void __launch_bounds__(64)
       pk[np] = nl;
       pk[g.T + 1] = np;
       pk[g.T + 2] = keep;
+      g.sq[(size_t)seq * SQS + Q_NNCTR] = 0;
     }
     return;
   }
@@ -859,6 +861,11 @@ __device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT],
 // detections in blocks of NDT 16-detection tiles; out = 1 - clip(max over the track's rows), the
 // max taken per track over its row range by wave shuffles.  Each output's k-chain is the oracle's
 // ascending fma chain whatever the tiling.
+// Work items (pack, detection block) of the frame's actual sizes — packs x ceil(dets / DB) —
+// are handed out by a per-sequence atomic counter to a fixed set of waves (blockIdx.x), each
+// looping until the counter passes the last item (every wave reaches that exit): the launch is
+// sized by capacities, the work by this frame's packs and detections, so no wave sits on an
+// empty (pack, block) slot while another runs two.
 template <int NDT>
 __global__ void __launch_bounds__(64)
     ss_nn_kernel(SsDev g, int seq0, const int* __restrict__ det_off) {
@@ -866,16 +873,22 @@ __global__ void __launch_bounds__(64)
   const int b = blockIdx.y, seq = seq0 + b, lane = threadIdx.x;
   const int* pk = g.pk + (size_t)seq * (g.T + 3);
   const int np = pk[g.T + 1];
-  if ((int)blockIdx.x >= np) return;
   const int r0 = det_off[b];
   int n = det_off[b + 1] - r0;
   if (n > g.D) n = g.D;
-  if (n <= 0) return;
+  if (n <= 0 || np <= 0) return;
   const int F = g.F;
   const double* dnb = g.dn + (size_t)seq * g.D * F;
   const int kl = lane >> 4, cl = lane & 15;
   constexpr int DB = 16 * NDT;  // detections per block
-  for (int p = blockIdx.x; p < np; p += gridDim.x) {
+  const int nb = (n + DB - 1) / DB, total = np * nb;
+  int* ctr = g.sq + (size_t)seq * SQS + Q_NNCTR;
+  for (;;) {
+    int item = 0;
+    if (lane == 0) item = atomicAdd(ctr, 1);
+    item = __shfl(item, 0);
+    if (item >= total) break;
+    const int p = item / nb, blk = item - p * nb;
     const int t0 = pk[p], nq = pk[p + 1] - t0;  // this pack's tracks (<= 64)
     int slot = 0, c = 0;
     unsigned long long m = 0;
@@ -902,7 +915,7 @@ __global__ void __launch_bounds__(64)
         r++;
         m &= m - 1;
       }
-      if (blockIdx.z == 0) atomicAdd(g.sq + (size_t)seq * SQS + Q_ROWS, c);  // a statistic
+      if (blk == 0) atomicAdd(g.sq + (size_t)seq * SQS + Q_ROWS, c);  // a statistic
     }
     if (lane == 0) qoff[nq] = nrows;
     __syncthreads();
@@ -914,7 +927,8 @@ __global__ void __launch_bounds__(64)
       const int row = 16 * rt + cl, rr = row < nrows ? row : 0;
       ap[rt] = vecnp(g, seq, qslot[rowq[rr]], rowv[rr]);
     }
-    for (int db = DB * blockIdx.z; db < n; db += DB * gridDim.z) {  // this wave's blocks
+    {  // this item's detection block
+      const int db = blk * DB;
       const int ndt = n - db >= DB ? NDT : (n - db + 15) / 16;
       const double* bp[NDT];
 #pragma unroll
@@ -2806,6 +2820,9 @@ __global__ void __launch_bounds__(64)
       __syncthreads();
     }
     SSTAMP(1);
+#ifdef BX_PHASE_TIMING
+    unsigned long long tq = SS_NOW();
+#endif
     const int crowd_mode = sq[Q_CROWD];
     for (int i = lane; i < x.nk; i += 64) {  // _compute_detection_quality
       double* d = w.dt + (size_t)i * DTW;
@@ -2821,8 +2838,10 @@ __global__ void __launch_bounds__(64)
       d[7] = q;
     }
     __syncthreads();
-    stable_sort_desc(w.dord, x.nk, [&](int r) { return w.dt[(size_t)r * DTW + 7]; }, w.tmp, sbox);
-    __syncthreads();
+#ifdef BX_PHASE_TIMING
+    SCOUNT(12, SS_NOW() - tq);
+#endif
+    // (the stable sort by quality is ss_sort_kernel's, next on this stream)
   }
   if (!fid) fid = sq[Q_HIST];
   // the cascade order of the confirmed tracks: time_since_update ascending, then -(quality +
@@ -2848,6 +2867,30 @@ __global__ void __launch_bounds__(64)
     sq[Q_CROWDN] = 0;  // the next frame's ss_crowd_kernel counts from zero
   }
   SSTAMP(2);
+}
+
+// The detections' stable sort by quality, descending (tracker.py's sorted(..., reverse=True) of
+// _compute_detection_quality): rank(i) = #{j : q_j > q_i} + #{j < i : q_j == q_i}, a thread per
+// detection against all keys in LDS; dord[rank(i)] = i.  (In ss_pre_kernel's one wave this was
+// 0.4 ms at C4 — ~514 keys, 16 per lane, beside the gallery distance's MFMA waves.)
+__global__ void __launch_bounds__(256) ss_sort_kernel(SsDev g, int seq0) {
+  __shared__ double ks[1024];
+  const int seq = seq0 + blockIdx.y;
+  const int nk = g.sq[(size_t)seq * SQS + Q_NK];
+  if ((int)blockIdx.x * 256 >= nk) return;
+  const double* dt = g.fdt + (size_t)seq * g.D * DTW;
+  int* dord = g.fdord + (size_t)seq * g.D;
+  for (int i = threadIdx.x; i < nk; i += 256) ks[i] = dt[(size_t)i * DTW + 7];
+  __syncthreads();
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= nk) return;
+  const double ki = ks[i];
+  int r = 0;
+  for (int j = 0; j < nk; j++) {
+    const double kj = ks[j];
+    r += (kj > ki) || (kj == ki && j < i);
+  }
+  dord[r] = i;
 }
 
 // ss_match_kernel (one two-wave workgroup per sequence): the three matching stages of
@@ -3535,28 +3578,35 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   hipLaunchKernelGGL(ss_pre_kernel, dim3(nseq), dim3(64), lds, e->side, d, seq0, dets, off,
                      warps);
   SCHK(hipGetLastError());
+  hipLaunchKernelGGL(ss_sort_kernel, dim3((d.D + 255) / 256, nseq), dim3(256), 0, e->side, d,
+                     seq0);
+  SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 3, e->side))) return rc;
   SCHK(hipEventRecord(e->ev_join, e->side));
   if ((rc = ss_probe_begin(e, 1, st))) return rc;
-  // packs per sequence <= listed tracks; a wave per (pack, detection-block split), waves looping
-  // over packs past the grid; the detection blocks split over waves for ~4k waves in all
-  const int gx = d.T < 4 ? d.T : (d.T + 3) / 4;
-  // detection tiles per wave: 4 when the detection capacity is large (C4: 1024 slots, ~510
-  // dets; 0.68 -> 0.64 ms and fewer waves beside ss_pre_kernel on the side stream, step 2.44 ->
-  // 2.38 ms), 2 otherwise (256 x ~24 dets: 4 tiles pad 0.19 -> 0.25 ms)
+  // a fixed set of waves per sequence pulls (pack, 16 NDT-detection block) items off the
+  // sequence's counter (ss_nn_kernel): ~BX_SS_NN_WAVES in all (two per SIMD), at least one per
+  // sequence and no more than its largest item count (packs <= listed tracks)
+  // detection tiles per item: 4 when the detection capacity is large (C4: 578 us per launch vs
+  // 711 with 2 and 1024 waves 661 — profiles/r06/ab_ss_nn_work_counter.txt), 2 otherwise (the
+  // 256-sequence config, ~24 detections: 417 k vs 412 k frames/s)
 #ifndef BX_SS_NDT
 #define BX_SS_NDT 4
 #endif
+#ifndef BX_SS_NN_WAVES
+#define BX_SS_NN_WAVES 2048
+#endif
   const int ndt = d.D >= 256 ? BX_SS_NDT : 2;
-  const int nblk = (d.D + 16 * ndt - 1) / (16 * ndt);
-  int zb = (int)((4096 + (long)gx * nseq - 1) / ((long)gx * nseq));
-  zb = zb < 1 ? 1 : (zb > nblk ? nblk : zb);
+  const long items_max = (long)d.T * ((d.D + 16 * ndt - 1) / (16 * ndt));
+  long gw = (BX_SS_NN_WAVES + nseq - 1) / nseq;
+  gw = gw < 1 ? 1 : (gw > items_max ? items_max : gw);
+  const int gx = (int)gw;
   if (ndt == 4)
-    hipLaunchKernelGGL((ss_nn_kernel<4>), dim3(gx, nseq, zb), dim3(64), 0, st, d, seq0, off);
+    hipLaunchKernelGGL((ss_nn_kernel<4>), dim3(gx, nseq, 1), dim3(64), 0, st, d, seq0, off);
   else if (ndt == 3)
-    hipLaunchKernelGGL((ss_nn_kernel<3>), dim3(gx, nseq, zb), dim3(64), 0, st, d, seq0, off);
+    hipLaunchKernelGGL((ss_nn_kernel<3>), dim3(gx, nseq, 1), dim3(64), 0, st, d, seq0, off);
   else
-    hipLaunchKernelGGL((ss_nn_kernel<2>), dim3(gx, nseq, zb), dim3(64), 0, st, d, seq0, off);
+    hipLaunchKernelGGL((ss_nn_kernel<2>), dim3(gx, nseq, 1), dim3(64), 0, st, d, seq0, off);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 1, st))) return rc;
   if ((rc = ss_probe_begin(e, 2, st))) return rc;

@@ -1,0 +1,6 @@
+# StrongSort parity subset, then an interleaved A/B of library variants on C4 and the 256 config
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_bench_workload.py -k "strongsort or ss_ or nn_ or lsap" > gpurun_out/r6_ssab_tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/r6_ssab_tests.log; exit 1; }
+tail -1 gpurun_out/r6_ssab_tests.log
+bash tools/ab_bench.sh strongsort_c4 2 "$@" && bash tools/ab_bench.sh strongsort 1 "$@"

@@ -23,9 +23,8 @@ PHASES = ["setup", "crowd", "camera+quality+sort+predict", "lists", "stage1 casc
           "partial_fit", "masks+outputs"]
 COUNTERS = ["cost build cyc", "lsap cyc", "lsap calls", "sum rows (tracks)", "sum cols (dets)",
             "dijkstra steps", "matches", "solver rows R", "solver cols CC", "slow rows",
-            "slow-row cyc", "lsap loop cyc", "pair: v + wait + relax cyc",
-            "pair: two wave minima cyc", "pair: row 0 decided (fast) cyc",
-            "pair: row 1 decided (fast) cyc", "sum R x CC", "calls R*CC*8 > 64 KiB",
+            "slow-row cyc", "lsap loop cyc", "pre: detection quality cyc",
+            "pre: detection sort cyc", "(unused)", "(unused)", "sum R x CC", "calls R*CC*8 > 64 KiB",
             "rows in those calls", "lsap cyc in those calls", "fast: contested rows",
             "fast: certificate row expansions", "fast: certificate candidates",
             "fast: (A) minima + claims cyc", "fast: (C) contested searches cyc",
