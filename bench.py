@@ -398,6 +398,10 @@ def main():
                     help="deliver every frame's output rows to pinned host memory inside the "
                          "timed region (a side-stream copy per frame, overlapped with the next "
                          "frame), as motio.run_sequences users receive them")
+    ap.add_argument("--early-features", action="store_true",
+                    help="BoT-SORT: each frame's detection-feature kernel starts on its own "
+                         "stream beside the previous frame's tail (bx_engine_set_early_features; "
+                         "the frames are resident before timing)")
     ap.add_argument("--lsap-exact", action="store_true",
                     help="StrongSort: solve every LSAP in scipy's row order (bx_ss_set_lsap_mode "
                          "0) instead of solve + certify")
@@ -464,7 +468,7 @@ def main():
     bst = kind == "boosttrack"
     sss = kind == "strongsort"
     eng, stages = bench_engine(args.config, S, args.track_cap, args.det_cap,
-                               overlap=not args.no_overlap)
+                               overlap=not args.no_overlap, early=args.early_features)
     layout = src.layout
     if sss and args.lsap_exact:
         eng.set_lsap_mode(False)
@@ -675,7 +679,8 @@ def main():
                           if c5 else {}),
                        "dist_backend": backend if world > 1 else None,
                        "timed_frames": [t_first + 1, total],
-                       **({"feature_overlap": not args.no_overlap}
+                       **({"feature_overlap": not args.no_overlap,
+                           "early_features": bool(args.early_features)}
                           if kind == "botsort" and F else {}),
                        **({"outputs_to_host": {
                            "what": "every frame's output rows + per-sequence counts copied to "

@@ -185,7 +185,7 @@ EXPORTS = [
     "bx_iou_batch", "bx_pairwise_cost", "bx_aw_max_metric", "bx_fuse_score", "bx_embedding_distance", "bx_kf_initiate",
     "bx_kf_multi_predict", "bx_kf_update", "bx_kf_gating_distance", "bx_linear_assignment", "bx_lapjv",
     "bx_linear_assignment_ex", "bx_engine_lap_ties_host", "bx_engine_lap_components_host", "bx_engine_set_lap_stats",
-    "bx_engine_force_assoc_build", "bx_legacy_lap_pair",
+    "bx_engine_force_assoc_build", "bx_legacy_lap_pair", "bx_engine_set_early_features",
     "bx_engine_inputs_released",
     "bx_engine_copy_state", "bx_engine_slots_used_host", "bx_ocsort_copy_state",
     "bx_boost_copy_state", "bx_ss_copy_state",
@@ -220,6 +220,7 @@ _SIGS = {
     "bx_engine_status": ([_vp, _ip], C.c_int),
     "bx_engine_probe": ([_vp, C.c_int], C.c_int),
     "bx_engine_set_overlap": ([_vp, C.c_int], C.c_int),
+    "bx_engine_set_early_features": ([_vp, C.c_int], C.c_int),
     "bx_engine_probe_read": ([_vp, _dp, _ip], C.c_int),
     "bx_engine_frame_stats_host": ([_vp, C.c_int, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "bx_engine_counters_host": ([_vp, C.c_int, _ip, _ip, _ip, _ip], C.c_int),

@@ -211,7 +211,10 @@ struct Dev {
   uint16_t* gcol;     // [S][T*D] LAP edge overflow
   double* gcost;      // [S][T*D]
   int2* rec;          // [S][D] frame scratch: update records (K3 → K4/K5)
-  double* dnrm;       // [S][D][4] frame scratch: n1, n2 (update_features), dn (embedding_distance)
+  double* dnrm;       // [2][S][D][4] frame scratch: n1, n2 (update_features), dn
+                      // (embedding_distance), by launch parity (early-features mode: K1 of the
+                      // next frame writes the other half while this frame's K1c / K5 read)
+  int dpar;           // this launch's half of dnrm
   float* tdn;         // [S][T] numpy float32 norm (+1e-8) of each track's smooth_feat (K5 keeps it)
   uint32_t* pairs;    // [S][T*D] frame scratch: gated (slot << 16 | det) pairs
   int* npair;         // [S] gated pair count (zeroed by K6 for the next frame)
@@ -400,7 +403,7 @@ __global__ __launch_bounds__(WG) void det_feature_kernel(Dev P, int seq0,
   };
   auto put_norms = [&](int k, FT n1, FT n2, float dn) {
     if (lane == 0) {
-      double* o = P.dnrm + ((size_t)s * D + k) * 4;
+      double* o = P.dnrm + ((size_t)P.dpar * P.S * D + (size_t)s * D + k) * 4;
       o[0] = (double)n1;
       o[1] = (double)n2;
       o[2] = (double)dn;
@@ -562,7 +565,7 @@ __global__ __launch_bounds__(WG) void cosine_kernel(Dev P, int seq0, const int* 
       arow[k] = (const FT*)P.feat + ((size_t)s * T + slot) * F + col;
       brow[k] = embs + (size_t)(d0 + dk) * F + col;
       da[k] = Div32(P.tdn[(size_t)s * T + slot]);
-      const double* nr = P.dnrm + ((size_t)s * D + dk) * 4;
+      const double* nr = P.dnrm + ((size_t)P.dpar * P.S * D + (size_t)s * D + dk) * 4;
       d1[k] = DivBy<FT>((FT)nr[0]);
       d2[k] = DivBy<FT>((FT)nr[1]);
       db[k] = Div32((float)nr[2]);
@@ -627,7 +630,7 @@ __global__ __launch_bounds__(WG) void cosine_kernel_any(Dev P, int seq0,
     const FT* a = (const FT*)P.feat + ((size_t)s * T + slot) * F;
     const FT* f = embs + (size_t)(det_off[b] + dk) * F;
     const float dn = P.tdn[(size_t)s * T + slot];
-    const double* nr = P.dnrm + ((size_t)s * D + dk) * 4;
+    const double* nr = P.dnrm + ((size_t)P.dpar * P.S * D + (size_t)s * D + dk) * 4;
     const FT n1 = (FT)nr[0], n2 = (FT)nr[1];
     const float bdn = (float)nr[2];
     auto A = [&](int q) { return (double)((float)a[q] / dn); };
@@ -1572,8 +1575,8 @@ __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
       g.load(fembs + (size_t)dk * F, F);
       FT* sm = feat + (size_t)slot * F;
       if ((kind & 3) != R_NEW) m.load(sm, F);
-      const FT n1 = (FT)P.dnrm[((size_t)s * D + dk) * 4];
-      const FT n2 = (FT)P.dnrm[((size_t)s * D + dk) * 4 + 1];
+      const FT n1 = (FT)P.dnrm[((size_t)P.dpar * P.S * D + (size_t)s * D + dk) * 4];
+      const FT n2 = (FT)P.dnrm[((size_t)P.dpar * P.S * D + (size_t)s * D + dk) * 4 + 1];
       g.div(n1);
       g.div(n2);
       float dn;
@@ -1597,8 +1600,8 @@ __global__ __launch_bounds__(WG) void feature_kernel(Dev P, int seq0,
     const int slot = rc.x & 0xffff, kind = rc.x >> 16, dk = rc.y;
     FT* sm = feat + (size_t)slot * F;
     const FT* f = fembs + (size_t)dk * F;
-    const FT n1 = (FT)P.dnrm[((size_t)s * D + dk) * 4];
-    const FT n2 = (FT)P.dnrm[((size_t)s * D + dk) * 4 + 1];
+    const FT n1 = (FT)P.dnrm[((size_t)P.dpar * P.S * D + (size_t)s * D + dk) * 4];
+    const FT n2 = (FT)P.dnrm[((size_t)P.dpar * P.S * D + (size_t)s * D + dk) * 4 + 1];
     FT* f2 = (FT*)P.fscr + ((size_t)s * D + dk) * F;  // this wave's scratch row
     for (int q = lane; q < F; q += WAVE) f2[q] = (f[q] / n1) / n2;
     if ((kind & 3) == R_NEW) {
@@ -1815,6 +1818,14 @@ struct bx_engine {
   // step's K1 queues behind it there and its K1c join covers both, every other entry point
   // settles it first (side_pending)
   bool overlap = false, side_pending = false;
+  // early-features mode (bx_engine_set_early_features): K1 on its own stream `k1s`, waiting only
+  // for the K5 that last read its half of dnrm (ev_k5[parity]), not for the previous frame —
+  // the caller guarantees each step's inputs are complete when the step is called
+  bool early = false;
+  hipStream_t k1s = nullptr;
+  hipEvent_t ev_k1 = nullptr, ev_k5[2] = {nullptr, nullptr};
+  bool k5_rec[2] = {false, false};
+  int par = 0;  // the next full launch's dnrm half
   // serialises every entry point that touches side_pending / the host staging buffers
   // (recursive: the host paths call bx_engine_step while holding it)
   std::recursive_mutex mu;
@@ -1858,8 +1869,13 @@ template <int KIND, typename FT, bool NPF>
 int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int* det_off,
                  const void* embs, const double* warps, double* out, int* out_count,
                  hipStream_t st) {
+  const bool reid = KIND == KIND_BOT && e->dev.with_reid;
+  // early features: full launches only (a chunked frame's launches would share the parity)
+  const bool early = reid && e->early && seq0 == 0 && nseq == e->dev.S;
+  const int par = early ? e->par : 0;
+  if (early) e->par ^= 1;
+  e->dev.dpar = par;
   const Dev& d = e->dev;
-  const bool reid = KIND == KIND_BOT && d.with_reid;
   // Fork-join: K1 (detection norms) only feeds K1c, and K5 (feature EMA) only reads K3's records
   // and K1's norms and writes smooth_feat / tdn, which nothing else in the frame touches — so K1
   // runs on the side stream beside K2/K1b, and K5 beside K4/K4b/K6.  Both joins land on `st`
@@ -1913,7 +1929,17 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
   } while (0)
 #define BX_PROBED(stage, ...) BX_PROBED_ON(stage, st, __VA_ARGS__)
   const int gy_det64 = (d.D + K1_DETS - 1) / K1_DETS, gy_slot = (d.T + WG - 1) / WG;
-  if (reid)
+  if (early && !e->k1s) {
+    HIPCHK(hipStreamCreateWithFlags(&e->k1s, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&e->ev_k1, hipEventDisableTiming | hipEventDisableSystemFence));
+    for (int k = 0; k < 2; k++)
+      HIPCHK(hipEventCreateWithFlags(&e->ev_k5[k], hipEventDisableTiming | hipEventDisableSystemFence));
+  }
+  // early features: K1 on k1s after only the K5 two launches back (the last reader of this
+  // dnrm half; K1c of that launch came before that K5); else on the side stream, forked here
+  if (early && e->k5_rec[par]) HIPCHK(hipStreamWaitEvent(e->k1s, e->ev_k5[par], 0));
+  hipStream_t k1st = early ? e->k1s : side;
+  if (reid && !early)
     if (int rc = fork(0)) return rc;
   const bool gmc = KIND == KIND_BOT && warps;
   // K1 on the side stream, submitted first (measured: 0.644 ms/step; submitted after K2/K1b
@@ -1929,14 +1955,15 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
   const bool fc = NPF && d.F == REG_F && (BX_FC_MASK & 1);
   const bool fc5 = NPF && d.F == REG_F && (BX_FC_MASK & 2);
   if (reid && fc)
-    BX_PROBED_ON(BX_STAGE_DET_FEATURES, side,
+    BX_PROBED_ON(BX_STAGE_DET_FEATURES, k1st,
                  hipLaunchKernelGGL((det_feature_kernel<FT, NPF, (NPF ? REG_F : 0)>),
-                                    dim3(nseq, gy_det64), dim3(WG), 0, side, d, seq0, dets,
+                                    dim3(nseq, gy_det64), dim3(WG), 0, k1st, d, seq0, dets,
                                     det_off, (const FT*)embs));
   else if (reid)
-    BX_PROBED_ON(BX_STAGE_DET_FEATURES, side,
+    BX_PROBED_ON(BX_STAGE_DET_FEATURES, k1st,
                  hipLaunchKernelGGL((det_feature_kernel<FT, NPF, 0>), dim3(nseq, gy_det64),
-                                    dim3(WG), 0, side, d, seq0, dets, det_off, (const FT*)embs));
+                                    dim3(WG), 0, k1st, d, seq0, dets, det_off, (const FT*)embs));
+  if (early) HIPCHK(hipEventRecord(e->ev_k1, e->k1s));
   if (gmc)
     BX_PROBED(BX_STAGE_PREDICT,
               hipLaunchKernelGGL((predict_kernel<KIND, true>), dim3(nseq, gy_slot), dim3(WG), 0,
@@ -1950,7 +1977,10 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
     BX_PROBED(BX_STAGE_GATE,
               hipLaunchKernelGGL(gate_kernel<KIND>, dim3(nseq, GATE_BLOCKS), dim3(WG), glds, st,
                                  d, seq0, dets, det_off));
-    if (int rc = join(0)) return rc;
+    // K1c reads K1's norms and the smooth features the last K5 wrote (overlap mode: unjoined)
+    if (early) HIPCHK(hipStreamWaitEvent(st, e->ev_k1, 0));
+    if (!early || e->side_pending)
+      if (int rc = join(0)) return rc;
     if (d.F == REG_F && (BX_FC_MASK & 4))
       BX_PROBED(BX_STAGE_COSINE,
                 hipLaunchKernelGGL((cosine_kernel<FT, REG_F>), dim3(nseq, COS_BLOCKS), dim3(WG), 0,
@@ -1993,6 +2023,10 @@ int launch_frame(bx_engine* e, int seq0, int nseq, const float* dets, const int*
   if (reid) {
     if (int rc = fork(1)) return rc;
     if (int rc = launch_k5()) return rc;
+    if (early) {  // the last reader of this dnrm half: the launch after next's K1 waits for it
+      HIPCHK(hipEventRecord(e->ev_k5[par], side));
+      e->k5_rec[par] = true;
+    }
   }
   BX_PROBED(BX_STAGE_UPDATE,
             hipLaunchKernelGGL(update_kernel<KIND>,
@@ -2134,7 +2168,7 @@ int bx_engine_create(const bx_config* cfg, bx_engine** out) {
     d.gcol = carve<uint16_t>(p, ST * D);
     d.gcost = carve<double>(p, ST * D);
     d.rec = carve<int2>(p, SD);
-    d.dnrm = carve<double>(p, SD * 4);
+    d.dnrm = carve<double>(p, 2 * SD * 4);
     d.tdn = carve<float>(p, reid ? ST : 1);
     d.pairs = carve<uint32_t>(p, reid ? ST * D : 1);
     d.npair = carve<int>(p, S);
@@ -2203,6 +2237,12 @@ int bx_engine_destroy(bx_engine* e) {
       (void)hipEventDestroy(e->ev_fork[k]);
       (void)hipEventDestroy(e->ev_join[k]);
     }
+  }
+  if (e->k1s) {
+    (void)hipStreamSynchronize(e->k1s);
+    (void)hipStreamDestroy(e->k1s);
+    (void)hipEventDestroy(e->ev_k1);
+    for (int k = 0; k < 2; k++) (void)hipEventDestroy(e->ev_k5[k]);
   }
   for (auto& ev : e->probe_ev) {
     (void)hipEventDestroy(ev.first);
@@ -2684,6 +2724,15 @@ int bx_engine_force_assoc_build(bx_engine* e, int mode) {
   if (!e || mode < -1 || mode > 1) return set_err(BX_ERR_INVALID, "bad assoc build mode");
   if (int rc = settle(e)) return rc;
   e->force_help = mode;
+  return BX_OK;
+}
+
+int bx_engine_set_early_features(bx_engine* e, int on) {
+  if (!e) return set_err(BX_ERR_INVALID, "null engine");
+  if (int rc = settle(e)) return rc;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  if (e->k1s) HIPCHK(hipStreamSynchronize(e->k1s));
+  e->early = on != 0;
   return BX_OK;
 }
 

@@ -208,6 +208,13 @@ class Engine:
         k = -1 if stage is None else (self.STAGES.index(stage) if isinstance(stage, str) else stage)
         N.check(self._L.bx_engine_probe(self._h, k), "bx_engine_probe")
 
+    def set_early_features(self, on: bool = True) -> None:
+        """Start each full step's detection-feature kernel at once on a stream of its own
+        (bx_engine_set_early_features): the caller guarantees a step's inputs are complete when
+        the step is called."""
+        N.check(self._L.bx_engine_set_early_features(self._h, int(bool(on))),
+                "bx_engine_set_early_features")
+
     def set_overlap(self, on: bool = True) -> None:
         """Leave each step's feature EMA (K5) unjoined on the side stream (bx_engine_set_overlap):
         the caller keeps a step's input tensors unmodified until the next step is enqueued."""

@@ -74,7 +74,7 @@ def ss_caps(config, n_obj):
 OCS_CONF_LO = 0.3  # OCSort / BoostTrack scenes: confidences U(0.3, 1) -> ~40% below det_thresh
 
 
-def bench_engine(config, n_seq, track_cap=512, det_cap=256, overlap=True):
+def bench_engine(config, n_seq, track_cap=512, det_cap=256, overlap=True, early=False):
     """The engine bench.py times for ``config`` with ``n_seq`` sequences per launch, and its
     pipeline stages (the probe targets).  BoT-SORT / ByteTrack: ``track_cap`` / ``det_cap`` slots
     and overlap mode (each step's feature EMA left unjoined: the caller keeps a step's inputs
@@ -98,6 +98,8 @@ def bench_engine(config, n_seq, track_cap=512, det_cap=256, overlap=True):
     eng = Engine(kind, n_seq=n_seq, track_cap=track_cap, det_cap=det_cap, emb_dim=F,
                  params=EngineParams(**params))
     eng.set_overlap(overlap)
+    if early and F:
+        eng.set_early_features(True)
     return eng, [s for s in Engine.STAGES
                  if F or s not in ("det_features", "gate", "cosine", "features")]
 

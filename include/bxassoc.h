@@ -107,6 +107,15 @@ int bx_engine_step(bx_engine *e, int seq0, int nseq, const float *dets, const in
  * hipDeviceSynchronize covers it.  Saves the join and lets the next frame's K1 start as soon as
  * K5 ends instead of after the caller's stream drains. */
 int bx_engine_set_overlap(bx_engine *e, int on);
+/* Early-features mode (default off; BoT-SORT with ReID): the caller guarantees that the inputs
+ * (dets, det_off, embs) of every bx_engine_step are complete in device memory when the step is
+ * CALLED (not merely enqueued before it on `stream`) — e.g. produced before a host
+ * synchronisation, as bench.py's resident frames are.  The detection-feature kernel (K1) of a
+ * full launch (seq0 0, all sequences) then runs on a stream of its own that waits only for the
+ * feature EMA (K5) two launches back (the last reader of the norms half it writes), so it starts
+ * beside the previous frame's tail instead of after it.  Results are unchanged.  Chunked
+ * launches keep the normal order.  Synchronises the engine's streams. */
+int bx_engine_set_early_features(bx_engine *e, int on);
 /* Overlap mode: make `stream` wait (stream-ordered, no host sync) until the last step's inputs
  * are no longer read — call it before refilling a reused dets / det_off / embs buffer on
  * `stream`.  A no-op when nothing is pending. */

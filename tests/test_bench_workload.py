@@ -36,7 +36,7 @@ def torch_cuda():
 
 
 def drive_bench(torch, config, n_seq, n_frames, warmup=10, track_cap=512, det_cap=256,
-                lap_stats=False, assoc_build=-1):
+                lap_stats=False, assoc_build=-1, early=False):
     """Run `n_frames` steps of bench.py's workload for `config` the way bench.py runs them (probe
     schedule included, one launch per frame over every sequence, no host sync in between).
     Returns (engine, frames on device, per-frame (out, cnt) on device)."""
@@ -45,7 +45,7 @@ def drive_bench(torch, config, n_seq, n_frames, warmup=10, track_cap=512, det_ca
     kind = CONFIGS[config][0]
     dev = torch.device("cuda", 0)
     src = BenchFrames(config, n_seq, dev)
-    eng, stages = bench_engine(config, src.n_seq, track_cap, det_cap, overlap=True)
+    eng, stages = bench_engine(config, src.n_seq, track_cap, det_cap, overlap=True, early=early)
     if lap_stats:
         eng.set_lap_stats(True)
     if assoc_build != -1:
@@ -55,8 +55,11 @@ def drive_bench(torch, config, n_seq, n_frames, warmup=10, track_cap=512, det_ca
     width = 10 if kind == "strongsort" else 8
     frames, outs = [], []
     dominant = stages[-1] if stages else None
+    if early:  # the early-features contract: inputs complete when each step is called
+        pre = [src.frame(t) for t in range(1, n_frames + 1)]
+        torch.cuda.synchronize()
     for t in range(1, n_frames + 1):
-        d, off, e = src.frame(t)
+        d, off, e = pre[t - 1] if early else src.frame(t)
         frames.append((d, off, e))
         j = t - 1 - warmup
         probed = None
@@ -95,15 +98,18 @@ def host_rows(frames, outs, s, t):
     return dets, embs, rows
 
 
-def test_botsort_c3_bench_workload_vs_oracle(torch_cuda):
+@pytest.mark.parametrize("early", [False, True])
+def test_botsort_c3_bench_workload_vs_oracle(torch_cuda, early):
     """The driver-timed line (BASELINE configs[2]): 1024 sequences in one launch per frame at
-    bench capacities in overlap mode; 8 sequences spread over the batch (first, last, both
-    halves' edges) bitwise against the oracle every frame, and their Kalman state at the end."""
+    bench capacities in overlap mode (and in early-features mode: each frame's K1 on its own
+    stream beside the previous frame's tail, the norms double-buffered); 8 sequences spread over
+    the batch (first, last, both halves' edges) bitwise against the oracle every frame, and their
+    Kalman state at the end."""
     from boxmot_amd.workloads import CONFIGS
 
     _, _, F, params = CONFIGS["botsort"]
     n_frames = 60
-    eng, frames, outs = drive_bench(torch_cuda, "botsort", 1024, n_frames)
+    eng, frames, outs = drive_bench(torch_cuda, "botsort", 1024, n_frames, early=early)
     st = eng.frame_stats()
     assert st["dets"] > 1024 * 100 and st["active"] > 1024 * 100, st  # the C3 shape, really
     for s in (0, 1, 255, 511, 512, 700, 1022, 1023):
