@@ -84,8 +84,8 @@ enum {
   // up to rejected (clamped) pairs; real ties re-solved in scipy's order; stages restarted in
   // scipy's order (a real tie after a level whose unmatched order was not certified)
   Q_LCALL, Q_LUNIQ, Q_LCLAMP, Q_LTIE, Q_LRESTART,
-  Q_NNCTR,  // ss_nn_kernel's work counter (zeroed by ss_prep_kernel's pack block each frame)
-  SQS
+  Q_NNCTR,  // ss_nn_kernel's work counters, one per XCD (zeroed by ss_prep_kernel's pack block)
+  SQS = Q_NNCTR + 8
 };
 
 struct SsDev {
@@ -730,7 +730,7 @@ __global__ void __launch_bounds__(64)
       pk[np] = nl;
       pk[g.T + 1] = np;
       pk[g.T + 2] = keep;
-      g.sq[(size_t)seq * SQS + Q_NNCTR] = 0;
+      for (int x = 0; x < 8; x++) g.sq[(size_t)seq * SQS + Q_NNCTR + x] = 0;
     }
     return;
   }
@@ -865,7 +865,11 @@ __device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT],
 // are handed out by a per-sequence atomic counter to a fixed set of waves (blockIdx.x), each
 // looping until the counter passes the last item (every wave reaches that exit): the launch is
 // sized by capacities, the work by this frame's packs and detections, so no wave sits on an
-// empty (pack, block) slot while another runs two.
+// empty (pack, block) slot while another runs two.  With many waves per sequence (C4) the items
+// are split by XCD: workgroups are dealt to the 8 XCDs round robin, so wave blockIdx.x runs on
+// XCD blockIdx.x % 8 (gridDim.x a multiple of 8) and takes only packs p = xcd (mod 8) from that
+// XCD's counter — every item of a pack reads its gallery rows through one XCD's L2 (HBM/MALL
+// traffic per launch 881 -> see profiles/r06) instead of all eight.
 template <int NDT>
 __global__ void __launch_bounds__(64)
     ss_nn_kernel(SsDev g, int seq0, const int* __restrict__ det_off) {
@@ -881,14 +885,19 @@ __global__ void __launch_bounds__(64)
   const double* dnb = g.dn + (size_t)seq * g.D * F;
   const int kl = lane >> 4, cl = lane & 15;
   constexpr int DB = 16 * NDT;  // detections per block
-  const int nb = (n + DB - 1) / DB, total = np * nb;
-  int* ctr = g.sq + (size_t)seq * SQS + Q_NNCTR;
+  const int nb = (n + DB - 1) / DB;
+  const bool byx = gridDim.x >= 64;  // split by XCD
+  const int xcd = byx ? (int)(blockIdx.x & 7) : 0;
+  const int npx = byx ? (np > xcd ? (np - xcd + 7) / 8 : 0) : np;  // this XCD's packs
+  const int total = npx * nb;
+  int* ctr = g.sq + (size_t)seq * SQS + Q_NNCTR + xcd;
   for (;;) {
     int item = 0;
     if (lane == 0) item = atomicAdd(ctr, 1);
     item = __shfl(item, 0);
     if (item >= total) break;
-    const int p = item / nb, blk = item - p * nb;
+    const int pi = item / nb, blk = item - pi * nb;
+    const int p = byx ? xcd + 8 * pi : pi;
     const int t0 = pk[p], nq = pk[p + 1] - t0;  // this pack's tracks (<= 64)
     int slot = 0, c = 0;
     unsigned long long m = 0;
@@ -3600,13 +3609,16 @@ static int ss_launch(bx_ss* e, int seq0, int nseq, const double* dets, const int
   const long items_max = (long)d.T * ((d.D + 16 * ndt - 1) / (16 * ndt));
   long gw = (BX_SS_NN_WAVES + nseq - 1) / nseq;
   gw = gw < 1 ? 1 : (gw > items_max ? items_max : gw);
+  if (gw >= 64) gw = (gw + 7) / 8 * 8;  // (the kernel's XCD split needs a multiple of 8)
   const int gx = (int)gw;
   if (ndt == 4)
     hipLaunchKernelGGL((ss_nn_kernel<4>), dim3(gx, nseq, 1), dim3(64), 0, st, d, seq0, off);
   else if (ndt == 3)
     hipLaunchKernelGGL((ss_nn_kernel<3>), dim3(gx, nseq, 1), dim3(64), 0, st, d, seq0, off);
-  else
+  else if (ndt == 2)
     hipLaunchKernelGGL((ss_nn_kernel<2>), dim3(gx, nseq, 1), dim3(64), 0, st, d, seq0, off);
+  else
+    hipLaunchKernelGGL((ss_nn_kernel<1>), dim3(gx, nseq, 1), dim3(64), 0, st, d, seq0, off);
   SCHK(hipGetLastError());
   if ((rc = ss_probe_end(e, 1, st))) return rc;
   if ((rc = ss_probe_begin(e, 2, st))) return rc;

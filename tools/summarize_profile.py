@@ -22,7 +22,7 @@ STAGE_OF = {"det_feature_kernel": "det_features", "predict_kernel": "predict",
             "ocsort_frame_kernel": "ocsort_frame", "boost_embcost_kernel": "embcost",
             "boost_frame_kernel": "frame", "boost_feature_kernel": "feature",
             "ss_prep_kernel": "prep", "ss_nn_kernel": "nn", "ss_rec_kernel": "recovery",
-            "ss_pre_kernel": "pre", "ss_cost_kernel": "cost", "ss_match_kernel": "match",
+            "ss_pre_kernel": "pre", "ss_sort_kernel": "sort", "ss_cost_kernel": "cost", "ss_match_kernel": "match",
             "ss_update_kernel": "update", "ss_post_kernel": "post", "ss_fit_kernel": "fit"}
 
 
