@@ -567,7 +567,11 @@ def main():
             ms, n = eng.probe_read()
             stage_ms[stages[j]] = ms  # the stage's launches of one step (one per chunk)
             eng.probe(None)
-    dominant = max(stage_ms, key=stage_ms.get) if stage_ms else (
+    # (StrongSort's "pre" probe spans its side-stream branch — crowd test, pre kernel, detection
+    # sort — from events that also wait for the gallery distance's waves beside it: 0.15-0.18 ms
+    # probed against ~45 us of kernels in the trace at 256 sequences, so it is not a candidate)
+    cand = {k: v for k, v in stage_ms.items() if not (sss and k == "pre")}
+    dominant = max(cand, key=cand.get) if cand else (
         "ocsort_frame" if ocs else ("features" if F else "assoc"))
     torch.cuda.synchronize()
     if dist:
