@@ -809,19 +809,20 @@ __device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT],
                                          d4 (&acc)[RT][NA]) {
   const int FB = (F & 1) ? 0 : F - F % 8;  // 16-byte loads need even rows
   if (FB > 0) {
-    double2 a[RT], bb[NDT];
+    // two operand buffers alternate (no register copies), the next block's loads issued before
+    // this block's MFMAs and pinned there by scheduling barriers: left to itself the compiler
+    // sank the loads to their MFMAs, so every block waited a full load round trip
+    // (profiles/r06/nn_prefetch.txt)
+    double2 a0[RT], b0[NDT], a1[RT], b1[NDT];
+    auto ld = [&](double2* a, double2* bb, int k) {
+      const int kk = k < FB ? k : FB - 8;  // past the end: re-read the last block
 #pragma unroll
-    for (int rt = 0; rt < RT; rt++) a[rt] = *(const double2*)(ap[rt] + 2 * kl);
+      for (int rt = 0; rt < RT; rt++) a[rt] = *(const double2*)(ap[rt] + kk + 2 * kl);
 #pragma unroll
-    for (int dt = 0; dt < NDT; dt++) bb[dt] = *(const double2*)(bp[dt] + 2 * kl);
-    for (int k = 0; k < FB; k += 8) {
-      const int kn = k + 8 < FB ? k + 8 : k;  // the last block re-reads its own operands
-      double2 na[RT], nb[NDT];
-#pragma unroll
-      for (int rt = 0; rt < RT; rt++) na[rt] = *(const double2*)(ap[rt] + kn + 2 * kl);
-#pragma unroll
-      for (int dt = 0; dt < NDT; dt++) nb[dt] = *(const double2*)(bp[dt] + kn + 2 * kl);
-      // (rows stored in MFMA order, nn_pos: .x is k-slot k + kl, .y is k + 4 + kl)
+      for (int dt = 0; dt < NDT; dt++) bb[dt] = *(const double2*)(bp[dt] + kk + 2 * kl);
+    };
+    // (rows stored in MFMA order, nn_pos: .x is k-slot k + kl, .y is k + 4 + kl)
+    auto mm = [&](const double2* a, const double2* bb) {
 #pragma unroll
       for (int rt = 0; rt < RT; rt++)
 #pragma unroll
@@ -832,10 +833,18 @@ __device__ __forceinline__ void nn_kloop(const double* const (&ap)[RT],
 #pragma unroll
         for (int dt = 0; dt < NDT; dt++)
           acc[rt][dt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[rt].y, bb[dt].y, acc[rt][dt], 0, 0, 0);
-#pragma unroll
-      for (int rt = 0; rt < RT; rt++) a[rt] = na[rt];
-#pragma unroll
-      for (int dt = 0; dt < NDT; dt++) bb[dt] = nb[dt];
+    };
+    ld(a0, b0, 0);
+    for (int k = 0; k < FB; k += 16) {
+      ld(a1, b1, k + 8);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (k + 8 >= FB) break;
+      ld(a0, b0, k + 16);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   for (int k = FB; k < F; k += 4) {  // tail: lanes past F multiply zeros (a clamped read)
