@@ -472,12 +472,12 @@ def main():
     layout = src.layout
     if sss and args.lsap_exact:
         eng.set_lsap_mode(False)
-    # W warm-up steps (at least start_frame - 1 - probes: the first timed frame), then one
-    # untimed probe step per pipeline stage (each stage timed once whatever W is), then the K
-    # timed steps
+    # W warm-up steps (at least start_frame - 1 - probes: the first timed frame), then two
+    # untimed probe steps per pipeline stage (each stage timed twice whatever W is, the larger
+    # kept: one event pair beside a concurrent side stream can read short), then the K timed steps
     n_probe = len(stages)
-    warmup = max(args.warmup, args.start_frame - 1 - n_probe)
-    t_first = warmup + n_probe
+    warmup = max(args.warmup, args.start_frame - 1 - 2 * n_probe)
+    t_first = warmup + 2 * n_probe
     total = t_first + args.steps
     # after the timed steps, one more probe step per stage: the stages at the timed frames' state
     # (StrongSort's galleries, for one, are still filling during the early probes)
@@ -561,11 +561,12 @@ def main():
     for k in range(t_first):
         j = k - warmup
         if j >= 0:
-            eng.probe(stages[j])
+            eng.probe(stages[j % n_probe])
         step(k)
         if j >= 0:
             ms, n = eng.probe_read()
-            stage_ms[stages[j]] = ms  # the stage's launches of one step (one per chunk)
+            # the stage's launches of one step (one per chunk), the larger of its two probes
+            stage_ms[stages[j % n_probe]] = max(ms, stage_ms.get(stages[j % n_probe], 0.0))
             eng.probe(None)
     # (StrongSort's "pre" probe spans its side-stream branch — crowd test, pre kernel, detection
     # sort — from events that also wait for the gallery distance's waves beside it: 0.15-0.18 ms
@@ -693,7 +694,7 @@ def main():
                            "GB_s": round(d2h_bytes / t_max / 1e9, 2)}} if d2h is not None else
                           {})},
             "roofline": {**roof, "kernel": dominant,
-                         "kernel_ms": round(dom_ms, 4), "probe_steps": n_probe,
+                         "kernel_ms": round(dom_ms, 4), "probe_steps": 2 * n_probe,
                          "launches_per_step": len(bounds),
                          "algorithmic_bytes_per_launch": int(per_launch),
                          "units_last_frame": units,

@@ -334,7 +334,7 @@ struct LdsF {
 // mark bits (per slot, per frame)
 enum : uint8_t { M_POOL = 1, M_ACT2 = 2, M_REMNOW = 4, M_TMP = 32 };
 // ints[] scratch slots
-enum { I_NA = 0, I_NL, I_FC, I_IDC, I_ERR, I_XMIN, I_XMAX, I_W, I_SCAN = 32 };
+enum { I_NA = 0, I_NL, I_FC, I_IDC, I_ERR, I_XMIN, I_XMAX, I_W, I_CLS0, I_SCAN = 32 };
 
 // STrack.xyxy of a track (mean-based): KF mean (x, y, a|w, h) → xyxy
 template <int KIND>
@@ -1157,6 +1157,30 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
         M[k] = pair_cost(tb, rows[i], cols[j]);
       }
       __syncthreads();
+      // row classes for the solver's scan skip (jv_wave_t): the dummy rows (0), and the real rows
+      // whose every cost equals the first constant row's (1: a track with no candidate pair, all
+      // 1.0 — most rows of a crowded scene); in the SSP's root list, dead until the next solve
+      uint16_t* s_cls = (uint16_t*)(smem + Lo.o_roots);
+      for (int i = tid; i < R; i += WG) {
+        const double c0 = M[(size_t)i * C];
+        bool cst = isfinite(c0);
+        for (int j = 1; j < C && cst; j++) cst = M[(size_t)i * C + j] == c0;
+        s_cls[i] = cst ? 1 : 0;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int i0 = 0;
+        while (i0 < R && !s_cls[i0]) i0++;
+        I[I_CLS0] = i0;
+      }
+      __syncthreads();
+      {
+        const int i0 = I[I_CLS0];
+        const double K = i0 < R ? M[(size_t)i0 * C] : 0.0;
+        for (int i = tid; i < R; i += WG) s_cls[i] = s_cls[i] && M[(size_t)i * C] == K ? 1 : 0;
+      }
+      __syncthreads();
+      auto rk = [&](int i) { return i >= R ? 0 : (s_cls[i] ? 1 : -1); };
       // lapx's state in this association's LAP workspace and candidate-sweep LDS, which are dead
       // until the next association rebuilds them (three blocks: see LdsA's take order), when it
       // fits; else in the sequence's global scratch (one wave either way)
@@ -1165,9 +1189,7 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
                           jv_split_a_bytes(n) <= Lo.o_dconf - Lo.o_tboxf &&
                           jv_split_b_bytes(n) <= Lo.o_ints - Lo.o_rowptr;
       const double half = L / 2.;
-      auto ext = [&](int i, int j) {
-        return (i < R && j < C) ? M[(size_t)i * C + j] : (i >= R && j >= C) ? 0.0 : half;
-      };
+      const JvExt ext{M, R, C, half};
 #ifdef BX_PHASE_TIMING
       // (the diagnostic timing build solves in the same state layout through two call sites,
       // one per layout: with the stamps added, one call over a selected LDS-or-global state
@@ -1176,14 +1198,14 @@ __global__ __launch_bounds__(WG) void assoc_kernel(Dev P, int seq0, const float*
       JvLds jw_l = jv_bind_split(smem + Lo.o_u, smem + Lo.o_tboxf, smem + Lo.o_rowptr, n);
       JvLds jw_g = jv_bind(P.jvs + (size_t)s * P.jvs_stride, n);
       if (wave_id() == 0) {
-        if (in_lds) jv_wave_t(ext, n, jw_l, SyncWaveLG{false});
-        else jv_wave_t(ext, n, jw_g, SyncWaveLG{true});
+        if (in_lds) jv_wave_t(ext, n, jw_l, SyncWaveLG{false}, rk);
+        else jv_wave_t(ext, n, jw_g, SyncWaveLG{true}, rk);
       }
       JvLds& jw = in_lds ? jw_l : jw_g;
 #else
       JvLds jw = in_lds ? jv_bind_split(smem + Lo.o_u, smem + Lo.o_tboxf, smem + Lo.o_rowptr, n)
                         : jv_bind(P.jvs + (size_t)s * P.jvs_stride, n);
-      if (wave_id() == 0) jv_wave_t(ext, n, jw, SyncWaveLG{!in_lds});
+      if (wave_id() == 0) jv_wave_t(ext, n, jw, SyncWaveLG{!in_lds}, rk);
 #endif
       __syncthreads();
       // x >= C: unmatched (-1); a real partner above L is neither matched nor listed (-3)

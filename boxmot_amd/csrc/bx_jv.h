@@ -72,7 +72,7 @@ __device__ __forceinline__ double cget(const double* C, int nr, int nc, int i, i
   return (i < nr && j < nc) ? C[i * nc + j] : 0.0;
 }
 
-__device__ double wave_min_d(double a) {
+__device__ __forceinline__ double wave_min_d(double a) {
   for (int o = 32; o >= 1; o >>= 1) a = fmin(a, __shfl_xor(a, o));
   return a;
 }
@@ -135,7 +135,7 @@ struct SyncWaveG {
 
 // Wave-order-preserving compaction: emit(k, pos) for k < n with pred(k); returns the count.
 template <class P, class E, class SY>
-__device__ int wave_compact_s(int n, P pred, E emit, SY sync) {
+__device__ __forceinline__ int wave_compact_s(int n, P pred, E emit, SY sync) {
   const int lane = threadIdx.x & 63;
   int base = 0;
   for (int c = 0; c < n; c += OW) {
@@ -155,13 +155,74 @@ __device__ int wave_compact(int n, P pred, E emit) {
 
 constexpr int JV_CH = 8;  // 64-position chunks of one relaxation loaded together
 
+__device__ __forceinline__ int rl_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+__device__ __forceinline__ double rl_d(double v, int k) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// a value every lane holds alike (an LDS word all lanes read), made wave-uniform for the compiler
+// (scalar registers: branches on it are scalar, not exec-mask juggling)
+__device__ __forceinline__ int ufl_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ double ufl_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// BX_JV_CLOCK (diagnostic builds only, tools/dbg/jv_clock.hip): wall-clock ticks per phase of
+// jv_wave_t added to w.dc[8..15] by lane 0 (8 ccrrt, 9 carr, 10 find, 11 scan, 12 augment,
+// 13 scan steps, 14 scans of a row below w.dc[7] (the caller stores R there), 15 skipped scans)
+#ifdef BX_JV_CLOCK
+#define JV_T0(t) unsigned long long t = wall_clock64()
+#define JV_ACC(q, t) do { if (lane == 0 && w.dc) w.dc[q] += wall_clock64() - t; } while (0)
+#define JV_CNT(q, k) do { if (lane == 0 && w.dc) w.dc[q] += (k); } while (0)
+#else
+#define JV_T0(t) do {} while (0)
+#define JV_ACC(q, t) do {} while (0)
+#define JV_CNT(q, k) do {} while (0)
+#endif
+
+// lapx's cost_limit extension of a row-major nr x nc cost (matching.py:54-61): the real block,
+// limit / 2 off the diagonal blocks, 0 in the dummy block — read with the row index uniform (a
+// scalar branch) and the column clamped into the row, so a chunk's lanes load without masking.
+struct JvExt {
+  const double* M;
+  int nr, nc;
+  double half;
+  __device__ __forceinline__ double operator()(int i, int j) const {
+    if (i < nr) {
+      const double c = M[(size_t)i * nc + min(max(j, 0), nc - 1)];
+      return j < nc ? c : half;
+    }
+    return j < nc ? half : 0.0;
+  }
+};
+
+// Row classes for the scan skip of jv_wave_t: rk(i) = 0 or 1 when row i belongs to that class of
+// rows with IDENTICAL finite cost rows (the cost_limit extension's dummy rows; real rows whose
+// every real cost equals one constant), -1 otherwise.
+struct JvNoClass {
+  __device__ int operator()(int) const { return -1; }
+};
+
 // ------------------------------------------------------------------------------------------
 // Any n, state in `w` (LDS, or global memory with a SyncWaveG); the cost of (i, j) from cf(i, j)
 // and every cross-lane hand-off through sync() (the whole workgroup when it is one wave, else
 // the calling wave only).
-template <class CF, class SY>
-__device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync) {
+//
+// Scan skip (exact): within one shortest-path search v is fixed, d only falls and the TODO set
+// only shrinks, so after a row of class c was scanned with h = c(i, j1) - v[j1] - mind every
+// TODO column has d[j] <= c(i, j) - v[j] - h.  A later scan of a row i' of the same class (the
+// same cost row) with h' <= h computes c(i, j) - v[j] - h' >= d[j] everywhere: no update, no
+// swap, no end of path — it is skipped.  (lapx scans it to no effect.)  Only finite h count.
+template <class CF, class SY, class RK = JvNoClass>
+__device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync,
+                                          const RK& rk = RK{}) {
   const int lane = threadIdx.x & 63;
+  JV_T0(tc0);
   // ---- _ccrrt_dense.  Column minima from LARGE, first row on ties (lane per column) ...
   for (int j = lane; j < n; j += OW) {
     double mn = LAPX_LARGE;
@@ -191,8 +252,8 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
   // reduction transfer, uniquely-assigned rows in order (each lowers v[x[i]], which the rows
   // after it read)
   for (int i = 0; i < n; i++) {
-    const int j1 = w.x[i];
-    if (j1 < 0 || w.matches[i] != 1) continue;
+    const int j1 = ufl_i(w.x[i]);
+    if (j1 < 0 || ufl_i(w.matches[i]) != 1) continue;
     double mn = LAPX_LARGE;
     for (int j = lane; j < n; j += OW) {
       const double h = cf(i, j) - w.v[j];
@@ -203,13 +264,15 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
     if (lane == 0) w.v[j1] = w.v[j1] - mn;
     sync();
   }
+  JV_ACC(8, tc0);
+  JV_T0(tc1);
   // ---- _carr_dense, at most two passes over the free rows (lapjv_internal)
   for (int pass = 0; pass < 2 && nfree > 0; pass++) {
     unsigned current = 0, rr_cnt = 0;
     int nnew = 0;
     while (current < (unsigned)nfree) {
       rr_cnt++;
-      const int fi = w.freer[current++];
+      const int fi = ufl_i(w.freer[current++]);
       // the cheapest column j1 (first on ties) and the cheapest other one j2 (first on ties):
       // exactly lapx's running pair whenever every reduced cost is below LARGE
       double m1 = INF;
@@ -224,7 +287,7 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
       double v1, v2;
       if (!__any(odd)) {
         wave_argmin(m1, k1);
-        j1 = k1;
+        j1 = ufl_i(k1);
         double m2 = INF;
         int k2 = JV_IMAX;
         for (int j = lane; j < n; j += OW) {
@@ -232,10 +295,10 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
           if (j != j1 && h < m2) m2 = h, k2 = j;
         }
         wave_argmin(m2, k2);
-        v1 = cf(fi, j1) - w.v[j1];
+        v1 = ufl_d(cf(fi, j1) - w.v[j1]);
         if (n >= 2) {
-          j2 = k2;
-          v2 = cf(fi, j2) - w.v[j2];
+          j2 = ufl_i(k2);
+          v2 = ufl_d(cf(fi, j2) - w.v[j2]);
         } else {
           j2 = -1;
           v2 = LAPX_LARGE;
@@ -260,8 +323,8 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
           }
         }
       }
-      int i0 = w.y[j1];
-      const double vj1 = w.v[j1];
+      int i0 = ufl_i(w.y[j1]);
+      const double vj1 = ufl_d(w.v[j1]);
       const double v1_new = vj1 - (v2 - v1);
       const bool lowers = v1_new < vj1;
       if (rr_cnt < current * (unsigned)n) {
@@ -269,7 +332,7 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
           if (lane == 0) w.v[j1] = v1_new;
         } else if (i0 >= 0 && j2 >= 0) {
           j1 = j2;
-          i0 = w.y[j2];
+          i0 = ufl_i(w.y[j2]);
         }
         if (i0 >= 0) {
           if (lowers) {
@@ -296,9 +359,10 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
 #ifdef BX_PHASE_TIMING
   if (lane == 0 && w.dc) w.dc[0] += nfree;
 #endif
+  JV_ACC(9, tc1);
   // ---- _ca_dense: one shortest augmenting path per remaining free row
   for (int f = 0; f < nfree; f++) {
-    const int start = w.freer[f];
+    const int start = ufl_i(w.freer[f]);
     for (int j = lane; j < n; j += OW) {
       w.d[j] = cf(start, j) - w.v[j];
       w.pred[j] = start;
@@ -307,83 +371,180 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
     sync();
     int low = 0, up = 0, last = 0, endofpath = -1, found = 0;
     double mn = 0.0;
+    double hmax0 = -INF, hmax1 = -INF;  // the largest finite h scanned per row class
     do {
 #ifdef BX_PHASE_TIMING
       if (lane == 0 && w.dc) w.dc[up == low ? 1 : 2] += 1;
 #endif
       if (up == low) {
+        JV_T0(tf);
         // _find_dense.  It gathers, in position order, every TODO column at the minimum into
         // col[low..up) and the path ends at the LAST unassigned one.  When one exists the search
         // ends here and the rest of the permutation is never read again (col is rebuilt for the
         // next free row), so the lane-parallel path finds it directly; otherwise (or with NaN
-        // distances) the scan runs as written.
-        double m = INF;
-        bool bad = false;
-        for (int k = low + lane; k < n; k += OW) {
-          const double h = w.d[w.col[k]];
-          m = fmin(m, h);
-          bad |= isnan(h);
-        }
-        m = wave_min_d(m);
-        bad = __any(bad) || !(m < INF);
-        int kg = -1, ke = -1;
-        if (!bad) {
-          for (int base = low; base < n; base += OW) {
-            const int k = base + lane;
-            bool G = false, E = false;
+        // distances) the scan runs as written — over a register copy of the positions when at
+        // most JV_CH * 64 remain, else over LDS on lane 0.
+        if (n - low <= JV_CH * OW) {
+          int cq[JV_CH];
+          double dq[JV_CH];
+          double m = INF;
+          bool bad = false;
+#pragma unroll
+          for (int q = 0; q < JV_CH; q++) {
+            const int k = low + q * OW + lane;
+            cq[q] = -1;
+            dq[q] = INF;
             if (k < n) {
-              const int j = w.col[k];
-              G = w.d[j] == m;
-              E = G && w.y[j] < 0;
+              cq[q] = w.col[k];
+              dq[q] = w.d[cq[q]];
+              m = fmin(m, dq[q]);
+              bad |= isnan(dq[q]);
             }
-            const unsigned long long gm = __ballot(G), em = __ballot(E);
-            if (kg < 0 && gm) kg = base + __ffsll((long long)gm) - 1;
-            if (em) ke = base + 63 - __clzll((long long)em);
           }
-        }
+          m = wave_min_d(m);
+          bad = __any(bad) || !(m < INF);
+          int kg = -1, ke = -1;
+          if (!bad) {
+#pragma unroll
+            for (int q = 0; q < JV_CH; q++) {
+              const int base = low + q * OW;
+              if (base >= n) break;
+              const bool G = base + lane < n && dq[q] == m;
+              const bool E = G && w.y[cq[q]] < 0;
+              const unsigned long long gm = __ballot(G), em = __ballot(E);
+              if (kg < 0 && gm) kg = base + __ffsll((long long)gm) - 1;
+              if (em) ke = base + 63 - __clzll((long long)em);
+            }
+          }
 #ifdef BX_PHASE_TIMING
-        if (lane == 0 && w.dc && ke < 0) w.dc[3] += 1;
+          if (lane == 0 && w.dc && ke < 0) w.dc[3] += 1;
 #endif
-        if (ke >= 0) {
-          last = low - 1;
-          mn = w.d[w.col[kg]];  // d[cols[lo]] after the scan: the first column at the minimum
-          endofpath = w.col[ke];
-          found = 1;
-        } else {
-          if (lane == 0) {
+          if (ke >= 0) {
             last = low - 1;
-            mn = w.d[w.col[up++]];
-            for (int k = up; k < n; k++) {
-              const int j = w.col[k];
-              const double h = w.d[j];
-              if (h <= mn) {
-                if (h < mn) {
-                  up = low;
-                  mn = h;
+            mn = m;  // d[cols[lo]] after the scan: the first column at the minimum
+            endofpath = w.col[ke];
+            found = 1;
+          } else {
+            // lapx's sequential loop, every lane in step: position k's own entry is read before
+            // any swap writes it (a swap writes positions <= k), so the registers hold what the
+            // loop reads there; col[up] is read back from LDS (lane 0 swaps in place).  Only
+            // positions at or below the running minimum when their chunk starts can act (the
+            // minimum only falls), so each chunk visits its ballot's lanes.
+            last = low - 1;
+            double mnv = rl_d(dq[0], 0);
+            int upl = low + 1;
+#pragma unroll
+            for (int q = 0; q < JV_CH; q++) {
+              const int base = low + q * OW;
+              if (base >= n) break;
+              unsigned long long cm = __ballot(base + lane < n && dq[q] <= mnv);
+              if (q == 0) cm &= ~1ull;
+              while (cm) {
+                const int t = __ffsll((long long)cm) - 1;
+                cm &= cm - 1;
+                const double h = rl_d(dq[q], t);
+                if (h <= mnv) {
+                  if (h < mnv) {
+                    upl = low;
+                    mnv = h;
+                  }
+                  const int j = rl_i(cq[q], t);
+                  if (lane == 0) {
+                    w.col[base + t] = w.col[upl];
+                    w.col[upl] = j;
+                  }
+                  upl++;
                 }
-                w.col[k] = w.col[up];
-                w.col[up++] = j;
               }
             }
-            for (int k = low; k < up; k++)
-              if (w.y[w.col[k]] < 0) {
-                endofpath = w.col[k];
+            sync();
+            for (int base = low; base < upl; base += OW) {
+              const int k = base + lane;
+              int j = -1;
+              bool E = false;
+              if (k < upl) {
+                j = w.col[k];
+                E = w.y[j] < 0;
+              }
+              const unsigned long long em = __ballot(E);
+              if (em) {
+                endofpath = __shfl(j, 63 - __clzll((long long)em));
                 found = 1;
               }
-            w.sc[0] = last;
-            w.sc[1] = up;
-            w.sc[2] = endofpath;
-            w.sc[3] = found;
-            w.sd[0] = mn;
+            }
+            up = upl;
+            mn = mnv;
           }
-          sync();
-          last = w.sc[0];
-          up = w.sc[1];
-          endofpath = w.sc[2];
-          found = w.sc[3];
-          mn = w.sd[0];
-          sync();
+        } else {
+          double m = INF;
+          bool bad = false;
+          for (int k = low + lane; k < n; k += OW) {
+            const double h = w.d[w.col[k]];
+            m = fmin(m, h);
+            bad |= isnan(h);
+          }
+          m = wave_min_d(m);
+          bad = __any(bad) || !(m < INF);
+          int kg = -1, ke = -1;
+          if (!bad) {
+            for (int base = low; base < n; base += OW) {
+              const int k = base + lane;
+              bool G = false, E = false;
+              if (k < n) {
+                const int j = w.col[k];
+                G = w.d[j] == m;
+                E = G && w.y[j] < 0;
+              }
+              const unsigned long long gm = __ballot(G), em = __ballot(E);
+              if (kg < 0 && gm) kg = base + __ffsll((long long)gm) - 1;
+              if (em) ke = base + 63 - __clzll((long long)em);
+            }
+          }
+#ifdef BX_PHASE_TIMING
+          if (lane == 0 && w.dc && ke < 0) w.dc[3] += 1;
+#endif
+          if (ke >= 0) {
+            last = low - 1;
+            mn = w.d[w.col[kg]];
+            endofpath = w.col[ke];
+            found = 1;
+          } else {
+            if (lane == 0) {
+              last = low - 1;
+              mn = w.d[w.col[up++]];
+              for (int k = up; k < n; k++) {
+                const int j = w.col[k];
+                const double h = w.d[j];
+                if (h <= mn) {
+                  if (h < mn) {
+                    up = low;
+                    mn = h;
+                  }
+                  w.col[k] = w.col[up];
+                  w.col[up++] = j;
+                }
+              }
+              for (int k = low; k < up; k++)
+                if (w.y[w.col[k]] < 0) {
+                  endofpath = w.col[k];
+                  found = 1;
+                }
+              w.sc[0] = last;
+              w.sc[1] = up;
+              w.sc[2] = endofpath;
+              w.sc[3] = found;
+              w.sd[0] = mn;
+            }
+            sync();
+            last = w.sc[0];
+            up = w.sc[1];
+            endofpath = w.sc[2];
+            found = w.sc[3];
+            mn = w.sd[0];
+            sync();
+          }
         }
+        JV_ACC(10, tf);
       }
       if (!found) {
         // _scan_dense from SCAN column j1 = col[low]: relax the TODO columns col[up..n) in
@@ -391,13 +552,24 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
         // ends the path.  Every operand of every chunk is loaded up front: a swap writes only
         // positions up to the chunk in flight, and each column appears once, so later chunks
         // read what the sequential loop would.
-        const int j1 = w.col[low++];
-        const int i = w.y[j1];
-        const double mind = w.d[j1];
+        JV_T0(ts);
+        const int j1 = ufl_i(w.col[low++]);
+        const int i = ufl_i(w.y[j1]);
+        JV_CNT(13, 1);
+        JV_CNT(14, i < (int)w.dc[7] ? 1 : 0);
+        const double mind = ufl_d(w.d[j1]);
         const double h = cf(i, j1) - w.v[j1] - mind;
+        const int cls = rk(i);
+        bool skip = false;
+        if (cls >= 0 && isfinite(h)) {
+          double& hm = cls == 0 ? hmax0 : hmax1;
+          skip = h <= hm;
+          if (!skip) hm = h;
+        }
+        JV_CNT(15, skip ? 1 : 0);
         // groups of JV_CH chunks (a swap only writes positions up to the chunk in flight, so a
         // later group's operands are still the sequential loop's)
-        for (int g0 = up; g0 < n && !found; g0 += JV_CH * OW) {
+        for (int g0 = up; g0 < n && !found && !skip; g0 += JV_CH * OW) {
           int jc[JV_CH];
           double v2c[JV_CH], dc[JV_CH];
           bool yc[JV_CH];
@@ -452,8 +624,10 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
           }
         }
         sync();
+        JV_ACC(11, ts);
       }
     } while (!found);
+    JV_T0(ta);
     for (int k = lane; k <= last; k += OW) {
       const int j1 = w.col[k];
       w.v[j1] = w.v[j1] + (w.d[j1] - mn);  // lapx: v[j] += d[j] - mind
@@ -470,6 +644,7 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
       } while (i != start);
     }
     sync();
+    JV_ACC(12, ta);
   }
 }
 
@@ -524,13 +699,6 @@ __device__ __forceinline__ int scan_min_i(int r) {
   return r;
 }
 __device__ __forceinline__ int wave_min_i(int a) { return __builtin_amdgcn_readlane(scan_min_i(a), 63); }
-__device__ __forceinline__ int rl_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
-__device__ __forceinline__ double rl_d(double v, int k) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 __device__ __forceinline__ int first_lane(bool p) {
   const unsigned long long m = __ballot(p);
   return m ? __ffsll((long long)m) - 1 : -1;

@@ -166,8 +166,8 @@ __global__ void kf_gate_kernel(int kind, int n, const double* mean, const double
 __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int nr, int nc,
                                                        double thr, int elds, uint16_t* gcol,
                                                        double* gcost, unsigned char* jvs,
-                                                       int jv_lds, int32_t* x, int32_t* y,
-                                                       int32_t* tied) {
+                                                       int jv_lds, int cls_lds, int32_t* x,
+                                                       int32_t* y, int32_t* tied) {
   extern __shared__ __align__(16) unsigned char smem[];
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -241,13 +241,30 @@ __global__ __launch_bounds__(WG) void lap_dense_kernel(const double* cost, int n
   const int n = nr + nc;
   __syncthreads();  // every wave is done with the CSR before the LDS is rebound
   JvLds jw = jv_bind(jv_lds ? smem : jvs, n);
+  // row classes for the solver's scan skip (jv_wave_t): dummy rows 0; real rows whose every cost
+  // equals the first constant row's 1 (flags in the LDS past the state when the launch sized it)
+  unsigned char* cls = cls_lds ? smem + ((jv_bytes(n) + 15) & ~size_t(15)) : nullptr;
+  if (cls) {
+    for (int i = tid; i < nr; i += WG) {
+      const double c0 = cost[(size_t)i * nc];
+      bool cst = isfinite(c0);
+      for (int j = 1; j < nc && cst; j++) cst = cost[(size_t)i * nc + j] == c0;
+      cls[i] = cst ? 1 : 0;
+    }
+    __syncthreads();
+    int i0 = 0;
+    while (i0 < nr && !cls[i0]) i0++;
+    const double K = i0 < nr ? cost[(size_t)i0 * nc] : 0.0;
+    __syncthreads();
+    for (int i = tid; i < nr; i += WG) cls[i] = cls[i] && cost[(size_t)i * nc] == K ? 1 : 0;
+    __syncthreads();
+  }
   if (wave_id() == 0) {
     const double half = thr / 2.;
-    auto cf = [&](int i, int j) {
-      return (i < nr && j < nc) ? cost[(size_t)i * nc + j] : (i >= nr && j >= nc) ? 0.0 : half;
-    };
-    if (jv_lds) jv_wave_t(cf, n, jw, SyncWaveL{});
-    else jv_wave_t(cf, n, jw, SyncWaveG{});
+    const JvExt cf{cost, nr, nc, half};
+    auto rk = [&](int i) { return i >= nr ? 0 : (cls && cls[i] ? 1 : -1); };
+    if (jv_lds) jv_wave_t(cf, n, jw, SyncWaveL{}, rk);
+    else jv_wave_t(cf, n, jw, SyncWaveG{}, rk);
   }
   __syncthreads();
   for (int i = tid; i < nr; i += WG) {
@@ -296,11 +313,8 @@ __global__ __launch_bounds__(OW) void lapjv_kernel(const double* cost, int nr, i
   auto solve = [&](auto sync) {
     if (mode == 2) {
       const double half = lim / 2.;
-      jv_wave_t([&](int i, int j) {
-                  return (i < nr && j < nc) ? cost[(size_t)i * nc + j]
-                                            : (i >= nr && j >= nc) ? 0.0 : half;
-                },
-                n, w, sync);
+      jv_wave_t(JvExt{cost, nr, nc, half}, n, w, sync,
+                [&](int i) { return i >= nr ? 0 : -1; });  // dummy rows: one class
     } else if (n <= OW) {
       jv_wave64(cost, nr, nc, w);
     } else {
@@ -457,6 +471,10 @@ int bx_linear_assignment_ex(const double* cost, int nr, int nc, double thresh, i
   // the tie re-solve's lapjv state in LDS too when it fits (n = nr + nc up to ~4000)
   const int jv_lds = jv_bytes(nr + nc) <= 160 * 1024;
   if (jv_lds && jv_bytes(nr + nc) > lds) lds = jv_bytes(nr + nc);
+  // and the row-class flags of its scan skip past that state
+  const size_t jvc = ((jv_bytes(nr + nc) + 15) & ~size_t(15)) + (size_t)nr;
+  const int cls_lds = jv_lds && jvc <= 160 * 1024;
+  if (cls_lds && jvc > lds) lds = jvc;
   void* ws = nullptr;
   const size_t ne = (size_t)nr * nc;
   const size_t jvb = (jv_bytes(nr + nc) + 255) & ~size_t(255);
@@ -468,7 +486,7 @@ int bx_linear_assignment_ex(const double* cost, int nr, int nc, double thresh, i
   // (never lowers the limit a concurrent call on another thread or stream launches with)
   if (lds > 65536) OPCHK(bx_lds_attr((const void*)lap_dense_kernel, lds));
   hipLaunchKernelGGL(lap_dense_kernel, dim3(1), dim3(WG), lds, st, cost, nr, nc, thresh, elds,
-                     gcol, gcost, jvs, jv_lds, x, y, tied);
+                     gcol, gcost, jvs, jv_lds, cls_lds, x, y, tied);
   OPCHK(hipGetLastError());
   if (tied_out) OPCHK(hipMemcpyAsync(tied_out, tied, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
   OPCHK(hipFreeAsync(ws, st));

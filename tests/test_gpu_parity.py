@@ -337,6 +337,62 @@ def test_linear_assignment_sparse_components_vs_oracle(torch_cuda, shape, densit
         np.testing.assert_array_equal(gub, oub)
 
 
+def crowd_dup_costs(rng, nt, nd, dup_every=3):
+    """1 - IoU of nt track boxes against nd detections near some of them, every dup_every-th
+    detection emitted twice (a detector without NMS): duplicate columns, and most rows all 1.0 —
+    the tie path's row classes (jv_wave_t's scan skip)."""
+    def boxes(k):
+        xy = rng.uniform(0, 1000, (k, 2))
+        return np.hstack([xy, xy + rng.uniform(30, 80, (k, 2))])
+
+    T = boxes(nt)
+    D = T[rng.choice(nt, nd, replace=nd > nt)] + rng.normal(0, 5, (nd, 4))
+    D = np.vstack([np.repeat(D[i:i + 1], 2 if i % dup_every == 0 else 1, 0) for i in range(nd)])
+    x1 = np.maximum(T[:, None, 0], D[None, :, 0])
+    y1 = np.maximum(T[:, None, 1], D[None, :, 1])
+    x2 = np.minimum(T[:, None, 2], D[None, :, 2])
+    y2 = np.minimum(T[:, None, 3], D[None, :, 3])
+    inter = np.clip(x2 - x1, 0, None) * np.clip(y2 - y1, 0, None)
+    area = lambda z: (z[:, 2] - z[:, 0]) * (z[:, 3] - z[:, 1])  # noqa: E731
+    return np.ascontiguousarray(1.0 - inter / (area(T)[:, None] + area(D)[None, :] - inter))
+
+
+@pytest.mark.gpu
+def test_linear_assignment_equivalent_rows_vs_oracle(torch_cuda):
+    """The tie re-solve skips a scan of a row whose cost row equals an already-scanned row's
+    (dummy rows; real rows constant at the first constant row's value) when it provably changes
+    nothing (jv_wave_t).  Problems made of such rows: crowded IoU with duplicated detections,
+    all-equal costs, and mixed constant rows (some at the class value, some at another, some
+    above the limit) — bx_linear_assignment_ex and bx_lapjv(cost_limit) == the oracle's lapx."""
+    rng = np.random.default_rng(4242)
+    cases = [crowd_dup_costs(rng, nt, nd, de) for nt, nd, de in
+             [(64, 32, 3), (128, 64, 3), (256, 128, 3), (96, 80, 2), (40, 90, 3)]]
+    cases += [np.full((n, m), 0.5) for n, m in [(64, 64), (100, 37), (30, 120)]]
+    for t in range(4):
+        nr, nc = [(80, 60), (60, 80), (150, 90), (33, 33)][t]
+        c = crowd_dup_costs(rng, nr, max(1, nc * 2 // 3))[:, :nc]
+        c = np.hstack([c, np.ones((nr, nc - c.shape[1]))]) if c.shape[1] < nc else c
+        rows = rng.choice(nr, nr // 3, replace=False)
+        c[rows[: len(rows) // 3]] = 0.5  # constant rows at another value (the first may set K)
+        c[rows[len(rows) // 3: 2 * len(rows) // 3]] = 0.9  # constant above the limit
+        cases.append(np.ascontiguousarray(c))
+    n_tied = 0
+    for k, c in enumerate(cases):
+        thr = 0.8
+        om, oua, oub = po.linear_assignment(c, thr)
+        tied = []
+        gm, gua, gub = gpu_linear_assignment(torch_cuda, c, thr, tied)
+        np.testing.assert_array_equal(gm, om, err_msg=f"case {k} {c.shape}")
+        np.testing.assert_array_equal(gua, oua, err_msg=f"case {k}")
+        np.testing.assert_array_equal(gub, oub, err_msg=f"case {k}")
+        n_tied += tied[0]
+        ox, oy = po.lapjv(c, extend_cost=True, cost_limit=thr)
+        gx, gy = gpu_lapjv(torch_cuda, c, extend_cost=True, cost_limit=thr)
+        np.testing.assert_array_equal(gx, ox, err_msg=f"lapjv x case {k}")
+        np.testing.assert_array_equal(gy, oy, err_msg=f"lapjv y case {k}")
+    assert n_tied >= len(cases) // 2
+
+
 def gpu_lapjv(torch, cost, extend_cost=False, cost_limit=float("inf")):
     from boxmot_amd import _native as N
 
