@@ -472,12 +472,14 @@ def main():
     layout = src.layout
     if sss and args.lsap_exact:
         eng.set_lsap_mode(False)
-    # W warm-up steps (at least start_frame - 1 - probes: the first timed frame), then two
-    # untimed probe steps per pipeline stage (each stage timed twice whatever W is, the larger
-    # kept: one event pair beside a concurrent side stream can read short), then the K timed steps
+    # W warm-up steps (at least start_frame - 1 - probes: the first timed frame), then one
+    # untimed probe step per pipeline stage, then the K timed steps.  The stages are probed on
+    # the last 2 x stages untimed steps (warm-up ones included), each twice, the larger kept: one
+    # event pair beside a concurrent side stream can read short
     n_probe = len(stages)
-    warmup = max(args.warmup, args.start_frame - 1 - 2 * n_probe)
-    t_first = warmup + 2 * n_probe
+    warmup = max(args.warmup, args.start_frame - 1 - n_probe)
+    t_first = warmup + n_probe
+    n_pr = min(2 * n_probe, t_first)
     total = t_first + args.steps
     # after the timed steps, one more probe step per stage: the stages at the timed frames' state
     # (StrongSort's galleries, for one, are still filling during the early probes)
@@ -559,7 +561,7 @@ def main():
     # warm-up, then the probe steps: each times one stage to find the dominant kernel
     stage_ms = {}
     for k in range(t_first):
-        j = k - warmup
+        j = k - (t_first - n_pr)
         if j >= 0:
             eng.probe(stages[j % n_probe])
         step(k)
@@ -694,7 +696,7 @@ def main():
                            "GB_s": round(d2h_bytes / t_max / 1e9, 2)}} if d2h is not None else
                           {})},
             "roofline": {**roof, "kernel": dominant,
-                         "kernel_ms": round(dom_ms, 4), "probe_steps": 2 * n_probe,
+                         "kernel_ms": round(dom_ms, 4), "probe_steps": n_pr,
                          "launches_per_step": len(bounds),
                          "algorithmic_bytes_per_launch": int(per_launch),
                          "units_last_frame": units,
