@@ -275,26 +275,36 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
       const int fi = ufl_i(w.freer[current++]);
       // the cheapest column j1 (first on ties) and the cheapest other one j2 (first on ties):
       // exactly lapx's running pair whenever every reduced cost is below LARGE
-      double m1 = INF;
-      int k1 = JV_IMAX;
+      // (one pass: each lane's two smallest (value, index) pairs, merged over the wave)
+      double m1 = INF, m2 = INF;
+      int k1 = JV_IMAX, k2 = JV_IMAX;
       bool odd = false;
       for (int j = lane; j < n; j += OW) {
         const double h = cf(fi, j) - w.v[j];
         odd |= !(h < LAPX_LARGE);
-        if (h < m1) m1 = h, k1 = j;
+        if (h < m1) {
+          m2 = m1, k2 = k1;
+          m1 = h, k1 = j;
+        } else if (h < m2) {
+          m2 = h, k2 = j;
+        }
       }
       int j1, j2;
       double v1, v2;
       if (!__any(odd)) {
-        wave_argmin(m1, k1);
-        j1 = ufl_i(k1);
-        double m2 = INF;
-        int k2 = JV_IMAX;
-        for (int j = lane; j < n; j += OW) {
-          const double h = cf(fi, j) - w.v[j];
-          if (j != j1 && h < m2) m2 = h, k2 = j;
+        auto lt = [](double a, int ia, double b, int ib) { return a < b || (a == b && ia < ib); };
+        for (int o = 32; o >= 1; o >>= 1) {
+          const double b1 = __shfl_xor(m1, o), b2 = __shfl_xor(m2, o);
+          const int c1 = __shfl_xor(k1, o), c2 = __shfl_xor(k2, o);
+          if (lt(b1, c1, m1, k1)) {  // partner's first leads: second = min(own first, its second)
+            if (lt(m1, k1, b2, c2)) m2 = m1, k2 = k1;
+            else m2 = b2, k2 = c2;
+            m1 = b1, k1 = c1;
+          } else if (lt(b1, c1, m2, k2)) {
+            m2 = b1, k2 = c1;
+          }
         }
-        wave_argmin(m2, k2);
+        j1 = ufl_i(k1);
         v1 = ufl_d(cf(fi, j1) - w.v[j1]);
         if (n >= 2) {
           j2 = ufl_i(k2);
@@ -547,6 +557,28 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
         JV_ACC(10, tf);
       }
       if (!found) {
+        // batch skip: the SCAN positions from low on whose scans the skip rule below passes over
+        // (with the class maxima as they stand — a skipped scan changes nothing, so they stand up
+        // to the first position that is scanned) are passed over 64 at a time
+        while (low < up) {
+          const int p = low + lane;
+          bool sk = false;
+          if (p < up) {
+            const int j = w.col[p];
+            const int ii = w.y[j];
+            const int c = rk(ii);
+            if (c >= 0) {
+              const double hh = cf(ii, j) - w.v[j] - w.d[j];
+              sk = isfinite(hh) && hh <= (c == 0 ? hmax0 : hmax1);
+            }
+          }
+          const unsigned long long ns = __ballot(p < up && !sk);
+          const int adv = ns ? __ffsll((long long)ns) - 1 : min(OW, up - low);
+          JV_CNT(15, adv);
+          low += adv;
+          if (ns) break;
+        }
+        if (low < up) {
         // _scan_dense from SCAN column j1 = col[low]: relax the TODO columns col[up..n) in
         // chunks of 64 positions; the first column lowered to the minimum that is unassigned
         // ends the path.  Every operand of every chunk is loaded up front: a swap writes only
@@ -625,6 +657,7 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
         }
         sync();
         JV_ACC(11, ts);
+        }
       }
     } while (!found);
     JV_T0(ta);
