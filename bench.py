@@ -576,6 +576,12 @@ def main():
     cand = {k: v for k, v in stage_ms.items() if not (sss and k == "pre")}
     dominant = max(cand, key=cand.get) if cand else (
         "ocsort_frame" if ocs else ("features" if F else "assoc"))
+    # StrongSort: the roofline kernel is the gallery distance, its one matrix-core kernel and the
+    # largest at the timed frames (stage_ms_after_timed); the probes run on the first frames,
+    # while the galleries are still filling (C4 at frames 11-19: nn 0.36 ms against the match's
+    # 0.38; at frames 20-69 0.56-0.58 ms)
+    if sss and "nn" in stage_ms:
+        dominant = "nn"
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
