@@ -153,7 +153,15 @@ __device__ int wave_compact(int n, P pred, E emit) {
   return wave_compact_s(n, pred, emit, SyncBlock{});
 }
 
-constexpr int JV_CH = 8;  // 64-position chunks of one relaxation loaded together
+// 64-position chunks of one scan's relaxation loaded together (two: a scan's TODO range is
+// usually one or two chunks, and the unrolled group is issued whole — 8 measured 25 % slower on
+// the crowd solve, profiles/r06/tie_path_r06.txt), and the find's register copy of at most
+// JV_FR chunks
+#ifndef BX_JV_CH
+#define BX_JV_CH 2
+#endif
+constexpr int JV_CH = BX_JV_CH;
+constexpr int JV_FR = 8;
 
 __device__ __forceinline__ int rl_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 __device__ __forceinline__ double rl_d(double v, int k) {
@@ -393,14 +401,14 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
         // ends here and the rest of the permutation is never read again (col is rebuilt for the
         // next free row), so the lane-parallel path finds it directly; otherwise (or with NaN
         // distances) the scan runs as written — over a register copy of the positions when at
-        // most JV_CH * 64 remain, else over LDS on lane 0.
-        if (n - low <= JV_CH * OW) {
-          int cq[JV_CH];
-          double dq[JV_CH];
+        // most JV_FR * 64 remain, else over LDS on lane 0.
+        if (n - low <= JV_FR * OW) {
+          int cq[JV_FR];
+          double dq[JV_FR];
           double m = INF;
           bool bad = false;
 #pragma unroll
-          for (int q = 0; q < JV_CH; q++) {
+          for (int q = 0; q < JV_FR; q++) {
             const int k = low + q * OW + lane;
             cq[q] = -1;
             dq[q] = INF;
@@ -416,7 +424,7 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
           int kg = -1, ke = -1;
           if (!bad) {
 #pragma unroll
-            for (int q = 0; q < JV_CH; q++) {
+            for (int q = 0; q < JV_FR; q++) {
               const int base = low + q * OW;
               if (base >= n) break;
               const bool G = base + lane < n && dq[q] == m;
@@ -444,7 +452,7 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
             double mnv = rl_d(dq[0], 0);
             int upl = low + 1;
 #pragma unroll
-            for (int q = 0; q < JV_CH; q++) {
+            for (int q = 0; q < JV_FR; q++) {
               const int base = low + q * OW;
               if (base >= n) break;
               unsigned long long cm = __ballot(base + lane < n && dq[q] <= mnv);
