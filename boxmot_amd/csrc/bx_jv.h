@@ -235,6 +235,7 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
   for (int j = lane; j < n; j += OW) {
     double mn = LAPX_LARGE;
     int im = 0;
+#pragma unroll 8
     for (int i = 0; i < n; i++) {
       const double c = cf(i, j);
       if (c < mn) mn = c, im = i;
@@ -263,6 +264,7 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
     const int j1 = ufl_i(w.x[i]);
     if (j1 < 0 || ufl_i(w.matches[i]) != 1) continue;
     double mn = LAPX_LARGE;
+#pragma unroll 4
     for (int j = lane; j < n; j += OW) {
       const double h = cf(i, j) - w.v[j];
       if (j != j1 && h < mn) mn = h;
@@ -287,6 +289,7 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
       double m1 = INF, m2 = INF;
       int k1 = JV_IMAX, k2 = JV_IMAX;
       bool odd = false;
+#pragma unroll 4
       for (int j = lane; j < n; j += OW) {
         const double h = cf(fi, j) - w.v[j];
         odd |= !(h < LAPX_LARGE);
@@ -381,6 +384,7 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
   // ---- _ca_dense: one shortest augmenting path per remaining free row
   for (int f = 0; f < nfree; f++) {
     const int start = ufl_i(w.freer[f]);
+#pragma unroll 4
     for (int j = lane; j < n; j += OW) {
       w.d[j] = cf(start, j) - w.v[j];
       w.pred[j] = start;
@@ -567,8 +571,19 @@ __device__ __forceinline__ void jv_wave_t(const CF& cf, int n, JvLds& w, SY sync
       if (!found) {
         // batch skip: the SCAN positions from low on whose scans the skip rule below passes over
         // (with the class maxima as they stand — a skipped scan changes nothing, so they stand up
-        // to the first position that is scanned) are passed over 64 at a time
-        while (low < up) {
+        // to the first position that is scanned) are passed over 64 at a time — entered only
+        // when position low itself skips (a scanned row pays one test, not a batch)
+        bool skip0 = false;
+        {
+          const int j = ufl_i(w.col[low]);
+          const int ii = ufl_i(w.y[j]);
+          const int c = rk(ii);
+          if (c >= 0) {
+            const double hh = cf(ii, j) - w.v[j] - w.d[j];
+            skip0 = isfinite(hh) && hh <= (c == 0 ? hmax0 : hmax1);
+          }
+        }
+        while (skip0 && low < up) {
           const int p = low + lane;
           bool sk = false;
           if (p < up) {
