@@ -72,10 +72,71 @@ __device__ __forceinline__ double cget(const double* C, int nr, int nc, int i, i
   return (i < nr && j < nc) ? C[i * nc + j] : 0.0;
 }
 
-__device__ __forceinline__ double wave_min_d(double a) {
-  for (int o = 32; o >= 1; o >>= 1) a = fmin(a, __shfl_xor(a, o));
-  return a;
+__device__ __forceinline__ int rl_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+__device__ __forceinline__ double rl_d(double v, int k) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int dpp_i(int src, int old) {
+  return __builtin_amdgcn_update_dpp(old, src, CTRL, RM, BM, false);
+}
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ double dpp_d(double src, double old) {
+  const long long s = __double_as_longlong(src), o = __double_as_longlong(old);
+  const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffffll), (int)(s & 0xffffffffll),
+                                             CTRL, RM, BM, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(s >> 32), CTRL, RM, BM, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double scan_min_d(double r) {  // no NaNs
+  r = fmin(r, dpp_d<0x111, 0xf, 0xf>(r, INF));
+  r = fmin(r, dpp_d<0x112, 0xf, 0xf>(r, INF));
+  r = fmin(r, dpp_d<0x114, 0xf, 0xf>(r, INF));
+  r = fmin(r, dpp_d<0x118, 0xf, 0xf>(r, INF));
+  r = fmin(r, dpp_d<0x142, 0xa, 0xf>(r, INF));
+  r = fmin(r, dpp_d<0x143, 0xc, 0xf>(r, INF));
+  return r;
+}
+__device__ __forceinline__ int scan_min_i(int r) {
+  constexpr int BIG = 0x7fffffff;
+  r = min(r, dpp_i<0x111, 0xf, 0xf>(r, BIG));
+  r = min(r, dpp_i<0x112, 0xf, 0xf>(r, BIG));
+  r = min(r, dpp_i<0x114, 0xf, 0xf>(r, BIG));
+  r = min(r, dpp_i<0x118, 0xf, 0xf>(r, BIG));
+  r = min(r, dpp_i<0x142, 0xa, 0xf>(r, BIG));
+  r = min(r, dpp_i<0x143, 0xc, 0xf>(r, BIG));
+  return r;
+}
+__device__ __forceinline__ int wave_min_i(int a) { return __builtin_amdgcn_readlane(scan_min_i(a), 63); }
+__device__ __forceinline__ int first_lane(bool p) {
+  const unsigned long long m = __ballot(p);
+  return m ? __ffsll((long long)m) - 1 : -1;
+}
+__device__ __forceinline__ int last_lane(bool p) {
+  const unsigned long long m = __ballot(p);
+  return m ? 63 - __clzll((long long)m) : -1;
+}
+// send each lane's value to lane `dst` (a permutation)
+__device__ __forceinline__ int perm_i(int v, int dst) {
+  return __builtin_amdgcn_ds_permute(dst << 2, v);
+}
+__device__ __forceinline__ double perm_d(double v, int dst) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_permute(dst << 2, (int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_ds_permute(dst << 2, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// (compare-select steps instead of fmin measured slower: C5 22.4 vs 23.0 k frames/s)
+__device__ __forceinline__ double wave_min_dpp(double a) {  // no NaNs (fmin drops them anyway)
+  return rl_d(scan_min_d(a), 63);
+}
+// the wave minimum in every lane (DPP row shifts and a readlane, no LDS permutes); NaNs dropped
+// as fmin drops them (no caller feeds one: their running minima start from INF / LARGE)
+__device__ __forceinline__ double wave_min_d(double a) { return wave_min_dpp(a); }
 
 // (value, index) argmin across the wave: the smallest value, the smallest index among equal
 // values — what a sequential ascending `<` scan keeps.  No NaNs.
@@ -163,13 +224,6 @@ __device__ int wave_compact(int n, P pred, E emit) {
 constexpr int JV_CH = BX_JV_CH;
 constexpr int JV_FR = 8;
 
-__device__ __forceinline__ int rl_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
-__device__ __forceinline__ double rl_d(double v, int k) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 // a value every lane holds alike (an LDS word all lanes read), made wave-uniform for the compiler
 // (scalar registers: branches on it are scalar, not exec-mask juggling)
 __device__ __forceinline__ int ufl_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -723,61 +777,6 @@ __device__ void jv_wave(const double* C, int nr, int nc, JvLds& w, SY sync = SY{
 // DPP inclusive min-scan across the wave (row_shr 1/2/4/8 within rows of 16, then row_bcast 15
 // and 31 — the gfx9 wave64 scan sequence); lanes whose source is outside the row keep the
 // identity.  Lane 63 holds the wave minimum.
-template <int CTRL, int RM, int BM>
-__device__ __forceinline__ int dpp_i(int src, int old) {
-  return __builtin_amdgcn_update_dpp(old, src, CTRL, RM, BM, false);
-}
-template <int CTRL, int RM, int BM>
-__device__ __forceinline__ double dpp_d(double src, double old) {
-  const long long s = __double_as_longlong(src), o = __double_as_longlong(old);
-  const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffffll), (int)(s & 0xffffffffll),
-                                             CTRL, RM, BM, false);
-  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(s >> 32), CTRL, RM, BM, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-__device__ __forceinline__ double scan_min_d(double r) {  // no NaNs
-  r = fmin(r, dpp_d<0x111, 0xf, 0xf>(r, INF));
-  r = fmin(r, dpp_d<0x112, 0xf, 0xf>(r, INF));
-  r = fmin(r, dpp_d<0x114, 0xf, 0xf>(r, INF));
-  r = fmin(r, dpp_d<0x118, 0xf, 0xf>(r, INF));
-  r = fmin(r, dpp_d<0x142, 0xa, 0xf>(r, INF));
-  r = fmin(r, dpp_d<0x143, 0xc, 0xf>(r, INF));
-  return r;
-}
-__device__ __forceinline__ int scan_min_i(int r) {
-  constexpr int BIG = 0x7fffffff;
-  r = min(r, dpp_i<0x111, 0xf, 0xf>(r, BIG));
-  r = min(r, dpp_i<0x112, 0xf, 0xf>(r, BIG));
-  r = min(r, dpp_i<0x114, 0xf, 0xf>(r, BIG));
-  r = min(r, dpp_i<0x118, 0xf, 0xf>(r, BIG));
-  r = min(r, dpp_i<0x142, 0xa, 0xf>(r, BIG));
-  r = min(r, dpp_i<0x143, 0xc, 0xf>(r, BIG));
-  return r;
-}
-__device__ __forceinline__ int wave_min_i(int a) { return __builtin_amdgcn_readlane(scan_min_i(a), 63); }
-__device__ __forceinline__ int first_lane(bool p) {
-  const unsigned long long m = __ballot(p);
-  return m ? __ffsll((long long)m) - 1 : -1;
-}
-__device__ __forceinline__ int last_lane(bool p) {
-  const unsigned long long m = __ballot(p);
-  return m ? 63 - __clzll((long long)m) : -1;
-}
-// send each lane's value to lane `dst` (a permutation)
-__device__ __forceinline__ int perm_i(int v, int dst) {
-  return __builtin_amdgcn_ds_permute(dst << 2, v);
-}
-__device__ __forceinline__ double perm_d(double v, int dst) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_ds_permute(dst << 2, (int)(b & 0xffffffffll));
-  const int hi = __builtin_amdgcn_ds_permute(dst << 2, (int)(b >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// (compare-select steps instead of fmin measured slower: C5 22.4 vs 23.0 k frames/s)
-__device__ __forceinline__ double wave_min_dpp(double a) {  // no NaNs (fmin drops them anyway)
-  return rl_d(scan_min_d(a), 63);
-}
 // at least three bits set (scalar ops only: a popcount compare became a VALU 64-bit compare)
 __device__ __forceinline__ bool ge3(unsigned long long m) {
   const unsigned long long a = m & (m - 1);
